@@ -1,0 +1,173 @@
+"""ctypes mirror of include/hipbatch.h (records, enums, constants).
+
+Shared by the product bindings (etcd_amd.hipbatch) and the test harness.
+tests/test_abi.py checks every constant and record layout here against the
+header text, so the two cannot drift apart.
+"""
+import ctypes as C
+
+import numpy as np
+
+HB_ABI_VERSION = 1
+
+HB_OK = 0
+HB_EINVAL = -1
+HB_ENOMEM = -2
+HB_EDEVICE = -3
+HB_EINVARIANT = -4
+
+HB_MAX_REPLICAS = 7
+HB_MAX_INFLIGHT = 1024
+HB_NO_LIMIT = (1 << 64) - 1
+HB_NO_INDEX = (1 << 64) - 1
+
+# StateType raft/raft.go:35-39
+HB_STATE_FOLLOWER = 0
+HB_STATE_CANDIDATE = 1
+HB_STATE_LEADER = 2
+# ProgressStateType raft/progress.go:19-23
+HB_PR_PROBE = 0
+HB_PR_REPLICATE = 1
+HB_PR_SNAPSHOT = 2
+# MessageType raft/raftpb/raft.proto:34-47
+HB_MSG_HUP = 0
+HB_MSG_BEAT = 1
+HB_MSG_PROP = 2
+HB_MSG_APP = 3
+HB_MSG_APP_RESP = 4
+HB_MSG_VOTE = 5
+HB_MSG_VOTE_RESP = 6
+HB_MSG_SNAP = 7
+HB_MSG_HEARTBEAT = 8
+HB_MSG_HEARTBEAT_RESP = 9
+HB_MSG_UNREACHABLE = 10
+HB_MSG_SNAP_STATUS = 11
+
+HB_REF_SLOT_MAX = 6
+HB_REF_OTHER = 0xD
+HB_REF_SELF = 0xE
+HB_REF_NONE = 0xF
+HB_SLOT_NONE = 0xF
+
+HB_STEP_HOST_PTRS = 0x1
+HB_STEP_PROFILE = 0x2
+
+HB_FAULT_NONE = 0
+HB_FAULT_LEADER_CAMPAIGN = 1
+HB_FAULT_EMPTY_PROP = 2
+HB_FAULT_EMPTY_SNAPSHOT = 3
+HB_FAULT_INFLIGHTS_FULL = 4
+HB_FAULT_NIL_PROGRESS = 5
+HB_FAULT_COMMIT_RANGE = 6
+HB_FAULT_NO_SELF = 7
+HB_FAULT_FOLLOWER_LEADER = 8
+
+HB_EV_TERM = 1
+HB_EV_STATE = 2
+HB_EV_COMMIT = 3
+HB_EV_LAST = 4
+HB_EV_APP = 5
+HB_EV_SNAP = 6
+HB_EV_HEARTBEAT = 7
+HB_EV_VOTE = 8
+HB_EV_PROP_FWD = 9
+HB_EV_PROP_DROP = 10
+HB_EV_FAULT = 11
+
+HB_STAT_MSGS = 0
+HB_STAT_APPRESP = 1
+HB_STAT_VOTERESP = 2
+HB_STAT_DROPPED = 3
+HB_STAT_COMMITS = 4
+HB_STAT_WON = 5
+HB_STAT_LOST = 6
+HB_STAT_EVENTS = 7
+HB_STAT_FAULTS = 8
+HB_STAT_ENTRIES = 9
+HB_STAT_COUNT = 10
+
+HB_PHASE_PARTITION = 0
+HB_PHASE_APPLY = 1
+HB_PHASE_FINISH = 2
+HB_PHASE_COUNT = 3
+
+STAT_NAMES = ["msgs", "appresp", "voteresp", "dropped", "commits", "won", "lost",
+              "events", "faults", "entries"]
+
+
+def hb_info(mtype, from_slot, reject=False):
+    return (mtype & 0xF) | ((from_slot & 0xF) << 4) | ((1 if reject else 0) << 8)
+
+
+class hb_progress(C.Structure):
+    _fields_ = [
+        ("match", C.c_uint64),
+        ("next", C.c_uint64),
+        ("pending_snapshot", C.c_uint64),
+        ("state", C.c_uint32),
+        ("paused", C.c_uint32),
+        ("ins_start", C.c_uint32),
+        ("ins_count", C.c_uint32),
+    ]
+
+
+class hb_group(C.Structure):
+    _fields_ = [
+        ("term", C.c_uint64),
+        ("committed", C.c_uint64),
+        ("first_index", C.c_uint64),
+        ("last_index", C.c_uint64),
+        ("term_first", C.c_uint64),
+        ("term_last", C.c_uint64),
+        ("snap_index", C.c_uint64),
+        ("state", C.c_uint32),
+        ("n", C.c_uint32),
+        ("self_slot", C.c_uint32),
+        ("lead", C.c_uint32),
+        ("vote", C.c_uint32),
+        ("votes_resp", C.c_uint32),
+        ("votes_grant", C.c_uint32),
+        ("fault", C.c_uint32),
+        ("pr", hb_progress * HB_MAX_REPLICAS),
+    ]
+
+
+class hb_event(C.Structure):
+    _fields_ = [
+        ("x", C.c_uint64),
+        ("group", C.c_uint32),
+        ("type", C.c_uint8),
+        ("to", C.c_uint8),
+        ("aux", C.c_uint16),
+    ]
+
+
+class hb_batch(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64),
+        ("group", C.c_void_p),
+        ("info", C.c_void_p),
+        ("term", C.c_void_p),
+        ("index", C.c_void_p),
+        ("hint", C.c_void_p),
+        ("props", C.c_void_p),
+    ]
+
+
+# numpy views of the records (same layout as the ctypes structs)
+PROGRESS_DTYPE = np.dtype([
+    ("match", "<u8"), ("next", "<u8"), ("pending_snapshot", "<u8"),
+    ("state", "<u4"), ("paused", "<u4"), ("ins_start", "<u4"), ("ins_count", "<u4"),
+])
+GROUP_DTYPE = np.dtype([
+    ("term", "<u8"), ("committed", "<u8"), ("first_index", "<u8"), ("last_index", "<u8"),
+    ("term_first", "<u8"), ("term_last", "<u8"), ("snap_index", "<u8"),
+    ("state", "<u4"), ("n", "<u4"), ("self_slot", "<u4"), ("lead", "<u4"), ("vote", "<u4"),
+    ("votes_resp", "<u4"), ("votes_grant", "<u4"), ("fault", "<u4"),
+    ("pr", PROGRESS_DTYPE, (HB_MAX_REPLICAS,)),
+])
+EVENT_DTYPE = np.dtype([("x", "<u8"), ("group", "<u4"), ("type", "u1"), ("to", "u1"), ("aux", "<u2")])
+
+assert GROUP_DTYPE.itemsize == C.sizeof(hb_group)
+assert EVENT_DTYPE.itemsize == C.sizeof(hb_event) == 16
+assert PROGRESS_DTYPE.itemsize == C.sizeof(hb_progress)

@@ -1,0 +1,304 @@
+/*
+ * hipbatch.h — C ABI of the MI355X batched Raft leader-bookkeeping engine.
+ *
+ * This is the drop-in boundary that a Go `raft/hipbatch` package binds through
+ * cgo.  It replaces the per-group CPU loop that
+ * `raft.MultiNode` runs in its single `run` goroutine
+ * (reference: raft/multinode.go:166-322) for the leader-side bookkeeping:
+ *
+ *   - MsgAppResp progress updates    raft/raft.go:514-546, raft/progress.go:100-166
+ *   - inflight flow control          raft/progress.go:172-237
+ *   - quorum commit                  raft/raft.go:323-332, raft/log.go:241-247
+ *   - vote tally / campaign          raft/raft.go:429-460, 585-614
+ *   - the Step term gate             raft/raft.go:462-490
+ *   - MultiNode dispatch filters     raft/multinode.go:233-237, raft/util.go:49-55
+ *
+ * Design rules:
+ *   - Group state lives on the device as structure-of-arrays in HBM; one
+ *     handle owns one GPU's shard of groups.  A handle is single-owner and not
+ *     thread-safe, mirroring the single `run` goroutine that owns all group
+ *     state in the reference (raft/multinode.go:166-168).
+ *   - Every export returns an int: 0 = OK, negative = HB_E*.  Invariant
+ *     violations that make the reference panic are reported per group as an
+ *     HB_EV_FAULT event (the host then panics with the reference message); they
+ *     never unwind across this ABI.
+ *   - No torch types, no C++ types: plain pointers and sizes only.
+ */
+#ifndef HIPBATCH_H_
+#define HIPBATCH_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HB_ABI_VERSION 1
+
+/* ---- error codes -------------------------------------------------------- */
+#define HB_OK          0
+#define HB_EINVAL     -1   /* bad argument (range, size, unsupported config)   */
+#define HB_ENOMEM     -2   /* device or pinned allocation failed               */
+#define HB_EDEVICE    -3   /* HIP runtime error / no device                    */
+#define HB_EINVARIANT -4   /* a device-side capacity invariant was violated    */
+
+/* ---- limits -------------------------------------------------------------- */
+#define HB_MAX_REPLICAS   7      /* n = len(r.prs) per group, 1..7 (north star: 3/5/7) */
+#define HB_MAX_INFLIGHT   1024   /* Config.MaxInflightMsgs upper bound on device       */
+#define HB_NO_LIMIT       UINT64_MAX  /* raft noLimit (raft/raft.go:30)                */
+#define HB_NO_INDEX       UINT64_MAX
+
+/* ---- raft enums (values equal the reference's) --------------------------- */
+/* StateType raft/raft.go:35-39 */
+#define HB_STATE_FOLLOWER  0
+#define HB_STATE_CANDIDATE 1
+#define HB_STATE_LEADER    2
+/* ProgressStateType raft/progress.go:19-23 */
+#define HB_PR_PROBE     0
+#define HB_PR_REPLICATE 1
+#define HB_PR_SNAPSHOT  2
+/* MessageType raft/raftpb/raft.proto:34-47 */
+#define HB_MSG_HUP            0
+#define HB_MSG_BEAT           1
+#define HB_MSG_PROP           2
+#define HB_MSG_APP            3
+#define HB_MSG_APP_RESP       4
+#define HB_MSG_VOTE           5
+#define HB_MSG_VOTE_RESP      6
+#define HB_MSG_SNAP           7
+#define HB_MSG_HEARTBEAT      8
+#define HB_MSG_HEARTBEAT_RESP 9
+#define HB_MSG_UNREACHABLE    10
+#define HB_MSG_SNAP_STATUS    11
+
+/* ---- node references ------------------------------------------------------
+ * Peers of a group are addressed by their slot in the group's peer list
+ * (the host keeps slot -> node id).  lead / vote are encoded as:           */
+#define HB_REF_SLOT_MAX   6      /* 0..6 = slot in the peer list              */
+#define HB_REF_OTHER      0xD    /* an id that is not in prs (host keeps it)   */
+#define HB_REF_SELF       0xE    /* r.id while r.id is not in prs              */
+#define HB_REF_NONE       0xF    /* raft.None (raft/raft.go:29)                */
+#define HB_SLOT_NONE      0xF    /* from_slot of a non-member / self not in prs*/
+
+/* ---- messages (structure-of-arrays batch) --------------------------------
+ * One batch = messages in arrival order, as the `run` goroutine would receive
+ * them on recvc/propc.  Only the relative order of messages of the same group
+ * is significant (groups are independent, raft/multinode.go:125-131).
+ *
+ * info[i] = type | from_slot << 4 | reject << 8
+ *   type      : HB_MSG_* of m.Type.  Device types: HUP, BEAT, PROP, APP_RESP,
+ *               VOTE_RESP, HEARTBEAT_RESP, UNREACHABLE, SNAP_STATUS.
+ *   from_slot : slot of m.From in the group's prs, HB_SLOT_NONE if absent.
+ *   reject    : m.Reject.
+ * term[i]  = m.Term (0 = local message, no term gate, raft/raft.go:471-472)
+ * index[i] = m.Index; for HB_MSG_PROP the number of entries (>0).
+ * hint[i]  = m.RejectHint; read only for rejected MsgAppResp (may be NULL when
+ *            the batch holds none).
+ * props    = optional dense [capacity] entry counts: group g first steps one
+ *            MsgProp carrying props[g] entries (if > 0), before its messages
+ *            in this batch.  NULL = none.
+ */
+#define HB_INFO(type, from_slot, reject) \
+  ((uint32_t)(type) | ((uint32_t)(from_slot) << 4) | ((uint32_t)((reject) ? 1 : 0) << 8))
+
+typedef struct hb_batch {
+  uint64_t        n;
+  const uint32_t* group;
+  const uint32_t* info;
+  const uint64_t* term;
+  const uint64_t* index;
+  const uint64_t* hint;
+  const uint32_t* props;
+} hb_batch;
+
+/* hb_step flags */
+#define HB_STEP_HOST_PTRS 0x1u   /* batch arrays are host pointers (copied H2D) */
+#define HB_STEP_PROFILE   0x2u   /* record per-phase HIP events (hb_phase_ms)   */
+
+/* ---- per-group state (host view, array-of-structures) --------------------
+ * Device keeps this as SoA.  Field meanings follow the reference:
+ *   term/vote/commit : pb.HardState (raft/raft.go:126; vote is a node ref)
+ *   lead, state      : SoftState (raft/node.go:40-43)
+ *   committed        : raftLog.committed (== HardState.Commit between Steps)
+ *   first_index      : raftLog.firstIndex()   (raft/log.go:150-159)
+ *   last_index       : raftLog.lastIndex()    (raft/log.go:161-170)
+ *   term_first..term_last : the maximal run of indices i in
+ *        [first_index-1, last_index] with raftLog.term(i) == term.  Exact
+ *        because log terms never decrease with the index and never exceed the
+ *        current Term.  Empty run: term_first = HB_NO_INDEX, term_last = 0.
+ *   snap_index       : raftLog.snapshot().Metadata.Index (0 = empty snapshot)
+ *   votes_resp/grant : r.votes (raft/raft.go:139) as slot bitmasks; bit 7 =
+ *                      r.id when r.id is not in prs.
+ *   fault            : non-zero once the group hit a reference panic; the
+ *                      device ignores the group until it is reloaded.
+ */
+typedef struct hb_progress {
+  uint64_t match;
+  uint64_t next;
+  uint64_t pending_snapshot;  /* valid in HB_PR_SNAPSHOT, else 0 */
+  uint32_t state;             /* HB_PR_* */
+  uint32_t paused;
+  uint32_t ins_start;         /* inflights.start */
+  uint32_t ins_count;         /* inflights.count */
+} hb_progress;
+
+typedef struct hb_group {
+  uint64_t term;
+  uint64_t committed;
+  uint64_t first_index;
+  uint64_t last_index;
+  uint64_t term_first;
+  uint64_t term_last;
+  uint64_t snap_index;
+  uint32_t state;
+  uint32_t n;
+  uint32_t self_slot;         /* slot of r.id or HB_SLOT_NONE */
+  uint32_t lead;              /* node ref */
+  uint32_t vote;              /* node ref */
+  uint32_t votes_resp;
+  uint32_t votes_grant;
+  uint32_t fault;             /* HB_FAULT_* */
+  hb_progress pr[HB_MAX_REPLICAS];
+} hb_group;
+
+/* fault codes: the reference panic each one stands for */
+#define HB_FAULT_NONE            0
+#define HB_FAULT_LEADER_CAMPAIGN 1  /* "invalid transition [leader -> candidate]" raft/raft.go:396 */
+#define HB_FAULT_EMPTY_PROP      2  /* "%x stepped empty MsgProp" raft/raft.go:502               */
+#define HB_FAULT_EMPTY_SNAPSHOT  3  /* "need non-empty snapshot" raft/raft.go:252-254            */
+#define HB_FAULT_INFLIGHTS_FULL  4  /* "cannot add into a full inflights" raft/progress.go:192  */
+#define HB_FAULT_NIL_PROGRESS    5  /* nil *Progress dereference (local msg from non-member)    */
+#define HB_FAULT_COMMIT_RANGE    6  /* "tocommit(%d) is out of range" raft/log.go:175-177       */
+#define HB_FAULT_NO_SELF         7  /* appendEntry with r.id not in prs (nil deref raft.go:358) */
+#define HB_FAULT_FOLLOWER_LEADER 8  /* "invalid transition [follower -> leader]" raft/raft.go:409 (oracle KATs only) */
+
+/* ---- events (the sparse delta list) ---------------------------------------
+ * One ordered stream of 16-byte records per group describes everything the
+ * host needs to build `Ready` (raft/node.go:447-463) for the groups that
+ * changed: HardState/SoftState marks and the messages raft.send appended to
+ * r.msgs (raft/raft.go:227-236), in the order the reference produced them.
+ * Groups with no event did not change.  Marks are emitted eagerly at the
+ * point the reference changes the value.
+ *
+ *   HB_EV_TERM      x = new Term                   (raft.reset, raft/raft.go:334-338)
+ *   HB_EV_STATE     x = state | lead<<8 | vote<<16 (becomeFollower/Candidate/Leader)
+ *   HB_EV_COMMIT    x = new committed              (raftLog.commitTo, raft/log.go:172-180)
+ *   HB_EV_LAST      x = new lastIndex, aux = 1 for the becomeLeader noop entry,
+ *                   0 for proposal entries        (raft.appendEntry, raft/raft.go:351-360)
+ *   HB_EV_APP       to, x = m.Index (= Next-1).  Entries are (x, L] where L is
+ *                   the current lastIndex (max_msg_size noLimit) or x+1
+ *                   (max_msg_size 0); none if x+1 > L.  m.Commit = current
+ *                   committed, m.Term = current term, m.LogTerm = term(x).
+ *                   (raft.sendAppend, raft/raft.go:261-281)
+ *   HB_EV_SNAP      to, x = snapshot index         (raft/raft.go:246-260)
+ *   HB_EV_HEARTBEAT to, x = m.Commit              (raft.sendHeartbeat, raft/raft.go:285-299)
+ *   HB_EV_VOTE      to, x = m.Index (lastIndex); m.LogTerm = lastTerm (raft/raft.go:435-442)
+ *   HB_EV_PROP_FWD  to = lead ref, x = arrival index of the MsgProp (HB_NO_INDEX
+ *                   for a dense props[] proposal)  (stepFollower, raft/raft.go:618-624)
+ *   HB_EV_PROP_DROP x = arrival index (HB_NO_INDEX for props[]): proposal dropped
+ *                   (raft/raft.go:587-589, 619-621)
+ *   HB_EV_FAULT     aux = HB_FAULT_*, x = arrival index of the message
+ */
+#define HB_EV_TERM      1
+#define HB_EV_STATE     2
+#define HB_EV_COMMIT    3
+#define HB_EV_LAST      4
+#define HB_EV_APP       5
+#define HB_EV_SNAP      6
+#define HB_EV_HEARTBEAT 7
+#define HB_EV_VOTE      8
+#define HB_EV_PROP_FWD  9
+#define HB_EV_PROP_DROP 10
+#define HB_EV_FAULT     11
+
+typedef struct hb_event {
+  uint64_t x;
+  uint32_t group;
+  uint8_t  type;
+  uint8_t  to;
+  uint16_t aux;
+} hb_event;
+
+/* ---- step statistics (reduced over the batch; RCCL-reducible u64s) ------- */
+#define HB_STAT_MSGS       0  /* messages stepped (after the membership filter)     */
+#define HB_STAT_APPRESP    1  /* MsgAppResp stepped (incl. stale / ignored ones)     */
+#define HB_STAT_VOTERESP   2  /* MsgVoteResp stepped                                 */
+#define HB_STAT_DROPPED    3  /* responses from non-members (raft/multinode.go:235)  */
+#define HB_STAT_COMMITS    4  /* groups whose committed advanced in this batch       */
+#define HB_STAT_WON        5  /* elections won (candidate -> leader)                 */
+#define HB_STAT_LOST       6  /* elections lost by poll (candidate -> follower)      */
+#define HB_STAT_EVENTS     7  /* events emitted                                      */
+#define HB_STAT_FAULTS     8  /* groups that faulted in this batch                   */
+#define HB_STAT_ENTRIES    9  /* log entries appended (proposals + noops)            */
+#define HB_STAT_COUNT      10
+
+/* ---- phases (HB_STEP_PROFILE) -------------------------------------------- */
+#define HB_PHASE_PARTITION 0  /* histogram + scan + stable scatter by partition */
+#define HB_PHASE_APPLY     1  /* per-group apply (the dominant kernel)          */
+#define HB_PHASE_FINISH    2  /* stats reduction + event chunk bookkeeping      */
+#define HB_PHASE_COUNT     3
+
+typedef struct hb_handle hb_handle;
+
+/* ---- lifecycle ------------------------------------------------------------ */
+/* Create a handle on `device` holding up to `capacity` groups of at most
+ * `max_replicas` peers, MaxInflightMsgs = max_inflight (Config.MaxInflightMsgs,
+ * raft/raft.go:98) and MaxSizePerMsg = max_msg_size (HB_NO_LIMIT or 0 on the
+ * device; raft/raft.go:93).  `max_batch` bounds hb_step's n. */
+int  hb_create(int device, uint32_t capacity, uint32_t max_replicas,
+               uint32_t max_inflight, uint64_t max_msg_size, uint64_t max_batch,
+               hb_handle** out);
+int  hb_destroy(hb_handle* h);
+/* Launch on this HIP stream (hipStream_t as void*); NULL = the null stream. */
+int  hb_set_stream(hb_handle* h, void* hip_stream);
+int  hb_sync(hb_handle* h);
+int  hb_abi_version(void);
+const char* hb_strerror(int code);
+
+/* ---- group state (CreateGroup / RemoveGroup / Status) ---------------------
+ * Load `count` groups into slots [first, first+count) from host records
+ * (CreateGroup, raft/multinode.go:181-217; inflight windows start empty
+ * unless set with hb_set_inflights).  Gather them back for Status
+ * (raft/status.go:34-49). */
+int  hb_load_groups(hb_handle* h, uint32_t first, uint32_t count, const hb_group* groups);
+int  hb_get_groups(hb_handle* h, uint32_t first, uint32_t count, hb_group* out);
+/* RemoveGroup (raft/multinode.go:219-222): mark slots empty (all messages to
+ * them are ignored until reloaded). */
+int  hb_remove_groups(hb_handle* h, uint32_t first, uint32_t count);
+/* Inflight window of (group, slot): buffer[(start + i) % max_inflight] = vals[i]. */
+int  hb_set_inflights(hb_handle* h, uint32_t group, uint32_t slot,
+                      uint32_t start, uint32_t count, const uint64_t* vals);
+int  hb_get_inflights(hb_handle* h, uint32_t group, uint32_t slot,
+                      uint32_t* start, uint32_t* count, uint64_t* vals /* [max_inflight] */);
+
+/* ---- the hot path ----------------------------------------------------------
+ * Step one batch (all messages of the batch, per group in arrival order).
+ * Asynchronous on the handle's stream.  Events and statistics of the step
+ * are read with the functions below. */
+int  hb_step(hb_handle* h, const hb_batch* b, uint32_t flags);
+
+/* Events of the last step: `n_chunks` chunks, chunk c holds counts[c] events
+ * at base + c * chunk_cap; per group, events appear in order across chunks
+ * taken in index order.  Device pointers; valid until the next hb_step. */
+int  hb_events_device(hb_handle* h, const hb_event** base, const uint32_t** counts,
+                      uint32_t* n_chunks, uint32_t* chunk_cap);
+/* Gather the last step's events densely into host memory (synchronizes).
+ * *n = number of events; returns HB_EINVAL if cap is too small. */
+int  hb_copy_events(hb_handle* h, hb_event* out, uint64_t cap, uint64_t* n);
+/* Statistics of the last step: device pointer to HB_STAT_COUNT u64 (for an
+ * RCCL all-reduce on the same stream) or a synchronous host copy. */
+int  hb_stats_device(hb_handle* h, uint64_t** dev_stats);
+int  hb_stats(hb_handle* h, uint64_t* out);
+/* Per-phase device time in ms of the last HB_STEP_PROFILE step. */
+int  hb_phase_ms(hb_handle* h, float* out /* [HB_PHASE_COUNT] */);
+
+/* ---- pinned host memory for cgo callers (Go must not hand Go memory to C
+ * that C retains; raft/hipbatch packs batches into these buffers). -------- */
+int  hb_alloc_pinned(size_t bytes, void** out);
+int  hb_free_pinned(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HIPBATCH_H_ */

@@ -1,0 +1,435 @@
+"""ctypes bindings of the C parity oracle (oracle/raft_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, never by the product package (etcd_amd).
+
+`Raft` wraps one orc_raft with the method names of the reference's Go `raft`
+struct so the transcribed known-answer tests read like raft/raft_test.go.
+`OracleGroups` drives many groups through orc_step_batch in the engine's batch
+format for GPU parity tests and the CPU baseline.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from etcd_amd import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+ORC_MAX_PEERS = 8
+NO_LIMIT = abi.HB_NO_LIMIT
+
+
+class orc_inflights(C.Structure):
+    _fields_ = [("start", C.c_int), ("count", C.c_int), ("size", C.c_int),
+                ("buffer", C.POINTER(C.c_uint64))]
+
+    @property
+    def buf(self):
+        return [self.buffer[i] for i in range(self.size)]
+
+
+class orc_progress(C.Structure):
+    _fields_ = [("Match", C.c_uint64), ("Next", C.c_uint64), ("State", C.c_int),
+                ("Paused", C.c_int), ("PendingSnapshot", C.c_uint64), ("ins", orc_inflights)]
+
+
+class orc_run(C.Structure):
+    _fields_ = [("index", C.c_uint64), ("term", C.c_uint64)]
+
+
+class orc_log(C.Structure):
+    _fields_ = [("first_index", C.c_uint64), ("last_index", C.c_uint64),
+                ("committed", C.c_uint64), ("applied", C.c_uint64), ("snap_index", C.c_uint64),
+                ("nruns", C.c_int), ("cap", C.c_int), ("runs", C.POINTER(orc_run))]
+
+
+class orc_msg(C.Structure):
+    _fields_ = [("Type", C.c_int), ("To", C.c_uint64), ("From", C.c_uint64), ("Term", C.c_uint64),
+                ("LogTerm", C.c_uint64), ("Index", C.c_uint64), ("Commit", C.c_uint64),
+                ("Reject", C.c_int), ("RejectHint", C.c_uint64), ("nents", C.c_uint64),
+                ("ent_lo", C.c_uint64), ("snap_index", C.c_uint64)]
+
+    def __repr__(self):
+        return (f"Msg(type={self.Type}, to={self.To}, from={self.From}, term={self.Term}, "
+                f"logterm={self.LogTerm}, index={self.Index}, commit={self.Commit}, "
+                f"reject={self.Reject}, nents={self.nents}, ent_lo={self.ent_lo})")
+
+
+class orc_raft(C.Structure):
+    _fields_ = [
+        ("id", C.c_uint64), ("Term", C.c_uint64), ("Vote", C.c_uint64), ("Commit", C.c_uint64),
+        ("log", orc_log), ("max_inflight", C.c_int), ("max_msg_size", C.c_uint64),
+        ("n", C.c_int), ("ids", C.c_uint64 * ORC_MAX_PEERS), ("prs_", orc_progress * ORC_MAX_PEERS),
+        ("state", C.c_int), ("lead", C.c_uint64), ("pending_conf", C.c_int), ("elapsed", C.c_int),
+        ("nvotes", C.c_int), ("vote_ids", C.c_uint64 * (ORC_MAX_PEERS + 1)),
+        ("vote_vals", C.c_int * (ORC_MAX_PEERS + 1)),
+        ("msgs", C.POINTER(orc_msg)), ("nmsgs", C.c_int), ("msgs_cap", C.c_int),
+        ("ev", C.c_void_p), ("nev", C.c_uint64), ("ev_cap", C.c_uint64), ("group", C.c_uint32),
+        ("arrival", C.c_uint64), ("fault", C.c_int), ("n_won", C.c_uint64), ("n_lost", C.c_uint64),
+    ]
+
+
+def build():
+    """Compile the oracle with its Makefile (gcc)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        P = C.POINTER
+        R = P(orc_raft)
+        sig = {
+            "orc_sizeof_raft": (C.c_size_t, []),
+            "orc_ins_init": (None, [P(orc_inflights), C.c_int]),
+            "orc_ins_free": (None, [P(orc_inflights)]),
+            "orc_ins_add": (C.c_int, [P(orc_inflights), C.c_uint64]),
+            "orc_ins_free_to": (None, [P(orc_inflights), C.c_uint64]),
+            "orc_ins_free_first_one": (None, [P(orc_inflights)]),
+            "orc_ins_full": (C.c_int, [P(orc_inflights)]),
+            "orc_pr_become_probe": (None, [P(orc_progress)]),
+            "orc_pr_become_replicate": (None, [P(orc_progress)]),
+            "orc_pr_become_snapshot": (None, [P(orc_progress), C.c_uint64]),
+            "orc_pr_maybe_update": (C.c_int, [P(orc_progress), C.c_uint64]),
+            "orc_pr_optimistic_update": (None, [P(orc_progress), C.c_uint64]),
+            "orc_pr_maybe_decr_to": (C.c_int, [P(orc_progress), C.c_uint64, C.c_uint64]),
+            "orc_pr_is_paused": (C.c_int, [P(orc_progress)]),
+            "orc_log_init": (None, [P(orc_log), C.c_uint64, C.c_uint64]),
+            "orc_log_push": (None, [P(orc_log), C.c_uint64, C.c_uint64]),
+            "orc_log_term": (C.c_uint64, [P(orc_log), C.c_uint64]),
+            "orc_raft_init": (None, [R, C.c_uint64, P(C.c_uint64), C.c_int, C.c_int, C.c_uint64]),
+            "orc_raft_free": (None, [R]),
+            "orc_raft_pr": (P(orc_progress), [R, C.c_uint64]),
+            "orc_raft_set_progress": (None, [R, C.c_uint64, C.c_uint64, C.c_uint64]),
+            "orc_raft_load_state": (None, [R, C.c_uint64, C.c_uint64, C.c_uint64]),
+            "orc_raft_q": (C.c_int, [R]),
+            "orc_raft_reset": (None, [R, C.c_uint64]),
+            "orc_raft_send_append": (None, [R, C.c_uint64]),
+            "orc_raft_bcast_append": (None, [R]),
+            "orc_raft_bcast_heartbeat": (None, [R]),
+            "orc_raft_maybe_commit": (C.c_int, [R]),
+            "orc_raft_append_entry": (None, [R, C.c_uint64, C.c_int]),
+            "orc_raft_become_follower": (None, [R, C.c_uint64, C.c_uint64]),
+            "orc_raft_become_candidate": (None, [R]),
+            "orc_raft_become_leader": (None, [R]),
+            "orc_raft_campaign": (None, [R]),
+            "orc_raft_poll": (C.c_int, [R, C.c_uint64, C.c_int]),
+            "orc_raft_step": (None, [R, P(orc_msg)]),
+            "orc_raft_commit_to": (None, [R, C.c_uint64]),
+            "orc_raft_read_messages": (C.c_int, [R, P(orc_msg), C.c_int]),
+            "orc_raft_from_group": (C.c_int, [R, P(abi.hb_group), P(orc_run), C.c_int, C.c_int, C.c_uint64]),
+            "orc_raft_to_group": (None, [R, P(abi.hb_group)]),
+            "orc_raft_set_inflights": (C.c_int, [R, C.c_int, C.c_int, C.c_int, P(C.c_uint64)]),
+            "orc_raft_get_inflights": (C.c_int, [R, C.c_int, P(C.c_uint64)]),
+            "orc_step_batch": (C.c_int, [R, C.c_uint32, P(abi.hb_batch), C.c_void_p, C.c_uint64,
+                                         P(C.c_uint64), P(C.c_uint64)]),
+            "orc_groups_new": (R, [C.c_uint32]),
+            "orc_groups_free": (None, [R, C.c_uint32]),
+            "orc_groups_at": (R, [R, C.c_uint32]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        assert L.orc_sizeof_raft() == C.sizeof(orc_raft), "orc_raft layout drift"
+        _lib = L
+    return _lib
+
+
+# ---------------------------------------------------------------------------
+# Go-shaped wrappers for the known-answer tests
+# ---------------------------------------------------------------------------
+class Inflights:
+    """newInflights(size) (raft/progress.go:183-188)."""
+
+    def __init__(self, size, start=0):
+        self.s = orc_inflights()
+        lib().orc_ins_init(C.byref(self.s), size)
+        self.s.start = start
+
+    def __del__(self):
+        try:
+            lib().orc_ins_free(C.byref(self.s))
+        except Exception:
+            pass
+
+    def add(self, v):
+        if lib().orc_ins_add(C.byref(self.s), v) != 0:
+            raise RuntimeError("cannot add into a full inflights")
+
+    def freeTo(self, to):
+        lib().orc_ins_free_to(C.byref(self.s), to)
+
+    def freeFirstOne(self):
+        lib().orc_ins_free_first_one(C.byref(self.s))
+
+    def full(self):
+        return bool(lib().orc_ins_full(C.byref(self.s)))
+
+    def as_tuple(self):
+        return (self.s.start, self.s.count, self.s.size, self.s.buf)
+
+
+class Progress:
+    """A free-standing Progress (raft/progress.go:37-67) for the table tests."""
+
+    def __init__(self, State=abi.HB_PR_PROBE, Match=0, Next=0, Paused=False, PendingSnapshot=0, ins=256):
+        self.p = orc_progress()
+        self.p.State, self.p.Match, self.p.Next = State, Match, Next
+        self.p.Paused, self.p.PendingSnapshot = int(Paused), PendingSnapshot
+        lib().orc_ins_init(C.byref(self.p.ins), ins)
+
+    def __getattr__(self, k):
+        if k in ("State", "Match", "Next", "PendingSnapshot"):
+            return getattr(self.p, k)
+        if k == "Paused":
+            return bool(self.p.Paused)
+        raise AttributeError(k)
+
+    def becomeProbe(self):
+        lib().orc_pr_become_probe(C.byref(self.p))
+
+    def becomeReplicate(self):
+        lib().orc_pr_become_replicate(C.byref(self.p))
+
+    def becomeSnapshot(self, i):
+        lib().orc_pr_become_snapshot(C.byref(self.p), i)
+
+    def maybeUpdate(self, n):
+        return bool(lib().orc_pr_maybe_update(C.byref(self.p), n))
+
+    def maybeDecrTo(self, rejected, last):
+        return bool(lib().orc_pr_maybe_decr_to(C.byref(self.p), rejected, last))
+
+    def isPaused(self):
+        return bool(lib().orc_pr_is_paused(C.byref(self.p)))
+
+
+def Msg(Type, From=0, To=0, Term=0, Index=0, LogTerm=0, Commit=0, Reject=False, RejectHint=0, Entries=0):
+    m = orc_msg()
+    m.Type, m.From, m.To, m.Term, m.Index = Type, From, To, Term, Index
+    m.LogTerm, m.Commit, m.Reject, m.RejectHint, m.nents = LogTerm, Commit, int(Reject), RejectHint, Entries
+    return m
+
+
+class Raft:
+    """newTestRaft(id, peers, election, heartbeat, storage) (raft/raft_test.go:1884-1898).
+
+    `ents` = list of (index, term) entries appended to a MemoryStorage, `snapshot` =
+    (index, term) applied first, `hard` = (term, vote, commit) HardState.
+    """
+
+    def __init__(self, id, peers, ents=(), snapshot=None, hard=None, max_inflight=256,
+                 max_msg_size=NO_LIMIT):
+        L = lib()
+        self.r = orc_raft()
+        if snapshot:
+            L.orc_log_init(C.byref(self.r.log), snapshot[0] + 1, snapshot[1])
+            self.r.log.snap_index = snapshot[0]
+        else:
+            L.orc_log_init(C.byref(self.r.log), 1, 0)
+        for idx, term in ents:
+            assert idx == self.r.log.last_index + 1
+            L.orc_log_push(C.byref(self.r.log), term, 1)
+        arr = (C.c_uint64 * max(1, len(peers)))(*peers)
+        L.orc_raft_init(C.byref(self.r), id, arr, len(peers), max_inflight, max_msg_size)
+        if hard and any(hard):
+            L.orc_raft_load_state(C.byref(self.r), *hard)
+
+    def __del__(self):
+        try:
+            lib().orc_raft_free(C.byref(self.r))
+        except Exception:
+            pass
+
+    # -- fields ------------------------------------------------------------
+    @property
+    def Term(self):
+        return self.r.Term
+
+    @Term.setter
+    def Term(self, v):
+        self.r.Term = v
+
+    @property
+    def Commit(self):
+        return self.r.Commit
+
+    @property
+    def state(self):
+        return self.r.state
+
+    @property
+    def lead(self):
+        return self.r.lead
+
+    @property
+    def Vote(self):
+        return self.r.Vote
+
+    @property
+    def committed(self):
+        return self.r.log.committed
+
+    @property
+    def lastIndex(self):
+        return self.r.log.last_index
+
+    @property
+    def firstIndex(self):
+        return self.r.log.first_index
+
+    @property
+    def fault(self):
+        return self.r.fault
+
+    def pr(self, id):
+        p = lib().orc_raft_pr(C.byref(self.r), id)
+        if not p:
+            return None
+        return p.contents
+
+    def nodes(self):
+        return sorted(self.r.ids[i] for i in range(self.r.n))
+
+    def term(self, i):
+        return lib().orc_log_term(C.byref(self.r.log), i)
+
+    # -- methods -----------------------------------------------------------
+    def Step(self, m):
+        lib().orc_raft_step(C.byref(self.r), C.byref(m))
+
+    def readMessages(self):
+        n = self.r.nmsgs
+        out = (orc_msg * max(1, n))()
+        lib().orc_raft_read_messages(C.byref(self.r), out, n)
+        return [out[i] for i in range(n)]
+
+    def becomeFollower(self, term, lead):
+        lib().orc_raft_become_follower(C.byref(self.r), term, lead)
+
+    def becomeCandidate(self):
+        lib().orc_raft_become_candidate(C.byref(self.r))
+
+    def becomeLeader(self):
+        lib().orc_raft_become_leader(C.byref(self.r))
+
+    def setProgress(self, id, match, next):
+        lib().orc_raft_set_progress(C.byref(self.r), id, match, next)
+
+    def maybeCommit(self):
+        return bool(lib().orc_raft_maybe_commit(C.byref(self.r)))
+
+    def appendEntry(self, k=1):
+        lib().orc_raft_append_entry(C.byref(self.r), k, 0)
+
+    def sendAppend(self, to):
+        lib().orc_raft_send_append(C.byref(self.r), to)
+
+    def bcastAppend(self):
+        lib().orc_raft_bcast_append(C.byref(self.r))
+
+    def bcastHeartbeat(self):
+        lib().orc_raft_bcast_heartbeat(C.byref(self.r))
+
+    def commitTo(self, i):
+        lib().orc_raft_commit_to(C.byref(self.r), i)
+
+    def reset(self, term):
+        lib().orc_raft_reset(C.byref(self.r), term)
+
+    def q(self):
+        return lib().orc_raft_q(C.byref(self.r))
+
+    def to_group(self):
+        g = abi.hb_group()
+        lib().orc_raft_to_group(C.byref(self.r), C.byref(g))
+        return g
+
+
+# ---------------------------------------------------------------------------
+# batch driver (engine format)
+# ---------------------------------------------------------------------------
+class OracleGroups:
+    """ngroups oracle rafts stepped with orc_step_batch (the engine's batch format)."""
+
+    def __init__(self, groups, runs, max_inflight, max_msg_size=NO_LIMIT, inflights=None):
+        """groups: numpy GROUP_DTYPE [G]; runs: list of [(index, term), ...] per group;
+        inflights: optional dict {(g, slot): np.uint64 array of the live window}."""
+        L = lib()
+        self.G = len(groups)
+        self.max_inflight = max_inflight
+        self.ptr = L.orc_groups_new(self.G)
+        gbuf = np.ascontiguousarray(groups)
+        for g in range(self.G):
+            rs = runs[g]
+            rr = (orc_run * len(rs))(*[orc_run(int(a), int(b)) for a, b in rs])
+            rec = abi.hb_group.from_buffer_copy(gbuf[g].tobytes())
+            rc = L.orc_raft_from_group(L.orc_groups_at(self.ptr, g), C.byref(rec), rr, len(rs),
+                                       max_inflight, max_msg_size)
+            if rc != 0:
+                raise ValueError(f"orc_raft_from_group({g}) = {rc}")
+        for (g, s), vals in (inflights or {}).items():
+            v = np.ascontiguousarray(vals, dtype=np.uint64)
+            start = int(gbuf[g]["pr"][s]["ins_start"])
+            L.orc_raft_set_inflights(L.orc_groups_at(self.ptr, g), s, start, len(v),
+                                     v.ctypes.data_as(C.POINTER(C.c_uint64)))
+
+    def __del__(self):
+        try:
+            lib().orc_groups_free(self.ptr, self.G)
+        except Exception:
+            pass
+
+    def step(self, batch_arrays, ev_cap=None):
+        """batch_arrays: dict of numpy arrays group/info/term/index/hint/props.
+        Returns (events ndarray EVENT_DTYPE, stats ndarray u64)."""
+        L = lib()
+        b = abi.hb_batch()
+        n = len(batch_arrays["group"])
+        keep = {}
+        for k, dt in (("group", np.uint32), ("info", np.uint32), ("term", np.uint64),
+                      ("index", np.uint64), ("hint", np.uint64), ("props", np.uint32)):
+            a = batch_arrays.get(k)
+            if a is None:
+                setattr(b, k, None)
+                continue
+            a = np.ascontiguousarray(a, dtype=dt)
+            keep[k] = a
+            setattr(b, k, a.ctypes.data)
+        b.n = n
+        if ev_cap is None:
+            ev_cap = (n + self.G) * (abi.HB_MAX_REPLICAS + 6) + 64
+        ev = np.zeros(ev_cap, dtype=abi.EVENT_DTYPE)
+        nev = C.c_uint64()
+        stats = (C.c_uint64 * abi.HB_STAT_COUNT)()
+        rc = L.orc_step_batch(self.ptr, self.G, C.byref(b), ev.ctypes.data, ev_cap, C.byref(nev), stats)
+        if rc != 0:
+            raise RuntimeError("oracle event buffer too small")
+        return ev[: nev.value].copy(), np.array(stats[:], dtype=np.uint64)
+
+    def groups(self):
+        L = lib()
+        out = np.zeros(self.G, dtype=abi.GROUP_DTYPE)
+        g = abi.hb_group()
+        for i in range(self.G):
+            L.orc_raft_to_group(L.orc_groups_at(self.ptr, i), C.byref(g))
+            out[i] = np.frombuffer(bytes(g), dtype=abi.GROUP_DTYPE)[0]
+        return out
+
+    def inflights(self, g, slot):
+        L = lib()
+        buf = (C.c_uint64 * max(1, self.max_inflight))()
+        n = L.orc_raft_get_inflights(L.orc_groups_at(self.ptr, g), slot, buf)
+        return np.array(buf[: max(n, 0)], dtype=np.uint64)
+
+    def raft(self, g):
+        return lib().orc_groups_at(self.ptr, g).contents

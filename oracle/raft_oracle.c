@@ -1,0 +1,897 @@
+/*
+ * raft_oracle.c — CPU restatement of the reference raft leader bookkeeping.
+ * TEST INFRASTRUCTURE ONLY (see raft_oracle.h).  Every function cites the
+ * reference Go it restates (paths relative to holandes22/etcd).
+ */
+#include "raft_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+static inline uint64_t umin(uint64_t a, uint64_t b) { return a > b ? b : a; }  /* raft/util.go:35-40 */
+static inline uint64_t umax(uint64_t a, uint64_t b) { return a > b ? a : b; }  /* raft/util.go:42-47 */
+
+/* ========================================================================
+ * inflights — raft/progress.go:172-237
+ * ======================================================================== */
+void orc_ins_init(orc_inflights* in, int size) {          /* newInflights :183-188 */
+  in->start = 0;
+  in->count = 0;
+  in->size = size;
+  in->buffer = (uint64_t*)calloc((size_t)(size > 0 ? size : 1), sizeof(uint64_t));
+}
+
+void orc_ins_free(orc_inflights* in) {
+  free(in->buffer);
+  in->buffer = NULL;
+}
+
+int orc_ins_full(const orc_inflights* in) { return in->count == in->size; }  /* :229-231 */
+
+int orc_ins_add(orc_inflights* in, uint64_t inflight) {   /* add :191-201 */
+  if (orc_ins_full(in)) return -1;                        /* panic "cannot add into a full inflights" */
+  int next = in->start + in->count;
+  if (next >= in->size) next -= in->size;
+  in->buffer[next] = inflight;
+  in->count++;
+  return 0;
+}
+
+void orc_ins_free_to(orc_inflights* in, uint64_t to) {    /* freeTo :204-224 */
+  if (in->count == 0 || to < in->buffer[in->start]) return;
+  int i, idx = in->start;
+  for (i = 0; i < in->count; i++) {
+    if (to < in->buffer[idx]) break;
+    if (++idx >= in->size) idx -= in->size;
+  }
+  in->count -= i;
+  in->start = idx;
+}
+
+void orc_ins_free_first_one(orc_inflights* in) {          /* :226 */
+  orc_ins_free_to(in, in->buffer[in->start]);
+}
+
+void orc_ins_reset(orc_inflights* in) {                   /* :234-237 */
+  in->count = 0;
+  in->start = 0;
+}
+
+/* ========================================================================
+ * Progress — raft/progress.go:69-166
+ * ======================================================================== */
+void orc_pr_reset_state(orc_progress* pr, int state) {    /* resetState :69-74 */
+  pr->paused = 0;
+  pr->pending_snapshot = 0;
+  pr->state = state;
+  orc_ins_reset(&pr->ins);
+}
+
+void orc_pr_become_probe(orc_progress* pr) {              /* :76-88 */
+  if (pr->state == HB_PR_SNAPSHOT) {
+    uint64_t pending = pr->pending_snapshot;
+    orc_pr_reset_state(pr, HB_PR_PROBE);
+    pr->next = umax(pr->match + 1, pending + 1);
+  } else {
+    orc_pr_reset_state(pr, HB_PR_PROBE);
+    pr->next = pr->match + 1;
+  }
+}
+
+void orc_pr_become_replicate(orc_progress* pr) {          /* :90-93 */
+  orc_pr_reset_state(pr, HB_PR_REPLICATE);
+  pr->next = pr->match + 1;
+}
+
+void orc_pr_become_snapshot(orc_progress* pr, uint64_t snapshoti) {  /* :95-98 */
+  orc_pr_reset_state(pr, HB_PR_SNAPSHOT);
+  pr->pending_snapshot = snapshoti;
+}
+
+void orc_pr_pause(orc_progress* pr) { pr->paused = 1; }   /* :143 */
+void orc_pr_resume(orc_progress* pr) { pr->paused = 0; }  /* :144 */
+
+int orc_pr_maybe_update(orc_progress* pr, uint64_t n) {   /* :102-113 */
+  int updated = 0;
+  if (pr->match < n) {
+    pr->match = n;
+    updated = 1;
+    orc_pr_resume(pr);
+  }
+  if (pr->next < n + 1) pr->next = n + 1;
+  return updated;
+}
+
+void orc_pr_optimistic_update(orc_progress* pr, uint64_t n) { pr->next = n + 1; }  /* :115 */
+
+int orc_pr_maybe_decr_to(orc_progress* pr, uint64_t rejected, uint64_t last) {  /* :119-141 */
+  if (pr->state == HB_PR_REPLICATE) {
+    if (rejected <= pr->match) return 0;
+    pr->next = pr->match + 1;
+    return 1;
+  }
+  if (pr->next - 1 != rejected) return 0;
+  pr->next = umin(rejected, last + 1);
+  if (pr->next < 1) pr->next = 1;
+  orc_pr_resume(pr);
+  return 1;
+}
+
+int orc_pr_is_paused(const orc_progress* pr) {            /* :147-158 */
+  switch (pr->state) {
+    case HB_PR_PROBE: return pr->paused;
+    case HB_PR_REPLICATE: return orc_ins_full(&pr->ins);
+    default: return 1;                                    /* ProgressStateSnapshot */
+  }
+}
+
+void orc_pr_snapshot_failure(orc_progress* pr) { pr->pending_snapshot = 0; }  /* :160 */
+
+int orc_pr_maybe_snapshot_abort(const orc_progress* pr) { /* :164-166 */
+  return pr->state == HB_PR_SNAPSHOT && pr->match >= pr->pending_snapshot;
+}
+
+/* ========================================================================
+ * log metadata — raft/log.go, raft/log_unstable.go
+ * ======================================================================== */
+void orc_log_init(orc_log* l, uint64_t first_index, uint64_t dummy_term) {
+  /* newLog (raft/log.go:43-64): committed = applied = firstIndex-1 */
+  memset(l, 0, sizeof(*l));
+  l->first_index = first_index;
+  l->last_index = first_index - 1;
+  l->committed = first_index - 1;
+  l->applied = first_index - 1;
+  l->cap = 4;
+  l->runs = (orc_run*)malloc(sizeof(orc_run) * (size_t)l->cap);
+  l->runs[0].index = first_index - 1;  /* dummy entry (snapshot index) */
+  l->runs[0].term = dummy_term;
+  l->nruns = 1;
+}
+
+void orc_log_free(orc_log* l) {
+  free(l->runs);
+  l->runs = NULL;
+  l->nruns = l->cap = 0;
+}
+
+void orc_log_push(orc_log* l, uint64_t term, uint64_t k) {
+  if (k == 0) return;
+  if (l->runs[l->nruns - 1].term != term) {
+    if (l->nruns == l->cap) {
+      l->cap *= 2;
+      l->runs = (orc_run*)realloc(l->runs, sizeof(orc_run) * (size_t)l->cap);
+    }
+    l->runs[l->nruns].index = l->last_index + 1;
+    l->runs[l->nruns].term = term;
+    l->nruns++;
+  }
+  l->last_index += k;
+}
+
+uint64_t orc_log_term(const orc_log* l, uint64_t i) {     /* term raft/log.go:198-217 */
+  uint64_t dummy = l->first_index - 1;
+  if (i < dummy || i > l->last_index) return 0;
+  int lo = 0, hi = l->nruns - 1;                          /* last run with index <= i */
+  while (lo < hi) {
+    int mid = (lo + hi + 1) / 2;
+    if (l->runs[mid].index <= i) lo = mid; else hi = mid - 1;
+  }
+  return l->runs[lo].term;
+}
+
+uint64_t orc_log_last_term(const orc_log* l) {            /* lastTerm raft/log.go:196 */
+  return orc_log_term(l, l->last_index);
+}
+
+/* ========================================================================
+ * raft — raft/raft.go
+ * ======================================================================== */
+static void fault(orc_raft* r, int code);
+
+static void emit(orc_raft* r, int type, int to, uint64_t x, int aux) {
+  if (r->ev) {
+    if (r->nev < r->ev_cap) {
+      hb_event* e = &r->ev[r->nev];
+      e->x = x;
+      e->group = r->group;
+      e->type = (uint8_t)type;
+      e->to = (uint8_t)to;
+      e->aux = (uint16_t)aux;
+    }
+    r->nev++;
+  }
+}
+
+static void fault(orc_raft* r, int code) {
+  if (r->fault) return;
+  r->fault = code;
+  emit(r, HB_EV_FAULT, 0, r->arrival, code);
+}
+
+int orc_raft_slot(const orc_raft* r, uint64_t id) {
+  for (int i = 0; i < r->n; i++)
+    if (r->ids[i] == id) return i;
+  return -1;
+}
+
+orc_progress* orc_raft_pr(orc_raft* r, uint64_t id) {
+  int s = orc_raft_slot(r, id);
+  return s < 0 ? NULL : &r->prs[s];
+}
+
+uint32_t orc_raft_ref(const orc_raft* r, uint64_t id) {
+  if (id == ORC_NONE) return HB_REF_NONE;
+  int s = orc_raft_slot(r, id);
+  if (s >= 0) return (uint32_t)s;
+  if (id == r->id) return HB_REF_SELF;
+  return HB_REF_OTHER;
+}
+
+static uint64_t soft_pack(const orc_raft* r) {
+  return (uint64_t)r->state | ((uint64_t)orc_raft_ref(r, r->lead) << 8) |
+         ((uint64_t)orc_raft_ref(r, r->vote) << 16);
+}
+
+orc_log* orc_raft_log(orc_raft* r) { return &r->log; }
+
+void orc_raft_init(orc_raft* r, uint64_t id, const uint64_t* peers, int npeers,
+                   int max_inflight, uint64_t max_msg_size) {
+  /* newRaft (raft/raft.go:157-209).  The caller set up r->log beforehand
+   * (zeroed struct => empty MemoryStorage: firstIndex 1, lastIndex 0). */
+  orc_log saved = r->log;
+  memset(r, 0, sizeof(*r));
+  if (saved.runs) r->log = saved; else orc_log_init(&r->log, 1, 0);
+  r->id = id;
+  r->max_inflight = max_inflight;
+  r->max_msg_size = max_msg_size;
+  r->n = 0;
+  for (int i = 0; i < npeers && i < ORC_MAX_PEERS; i++) {
+    r->ids[r->n] = peers[i];
+    memset(&r->prs[r->n], 0, sizeof(orc_progress));
+    r->prs[r->n].next = 1;                                /* :190-192 */
+    orc_ins_init(&r->prs[r->n].ins, max_inflight);
+    r->n++;
+  }
+  r->state = HB_STATE_FOLLOWER;
+  orc_raft_become_follower(r, r->term, ORC_NONE);         /* :199 */
+}
+
+void orc_raft_free(orc_raft* r) {
+  for (int i = 0; i < r->n; i++) orc_ins_free(&r->prs[i].ins);
+  orc_log_free(&r->log);
+  free(r->msgs);
+  r->msgs = NULL;
+  r->n = 0;
+}
+
+void orc_raft_set_progress(orc_raft* r, uint64_t id, uint64_t match, uint64_t next) {
+  /* setProgress raft/raft.go:744-746 (adds the id when absent) */
+  int s = orc_raft_slot(r, id);
+  if (s < 0) {
+    if (r->n >= ORC_MAX_PEERS) return;
+    s = r->n++;
+    r->ids[s] = id;
+  } else {
+    orc_ins_free(&r->prs[s].ins);
+  }
+  memset(&r->prs[s], 0, sizeof(orc_progress));
+  r->prs[s].match = match;
+  r->prs[s].next = next;
+  orc_ins_init(&r->prs[s].ins, r->max_inflight);
+}
+
+void orc_raft_load_state(orc_raft* r, uint64_t term, uint64_t vote, uint64_t commit) {
+  /* loadState raft/raft.go:752-760 */
+  r->log.committed = commit;
+  r->term = term;
+  r->vote = vote;
+  r->commit = commit;
+}
+
+int orc_raft_q(const orc_raft* r) { return r->n / 2 + 1; }  /* q raft/raft.go:215 */
+
+static void send(orc_raft* r, orc_msg m) {                /* send raft/raft.go:227-236 */
+  m.from = r->id;
+  if (m.type != HB_MSG_PROP) m.term = r->term;
+  if (r->nmsgs == r->msgs_cap) {
+    r->msgs_cap = r->msgs_cap ? r->msgs_cap * 2 : 8;
+    r->msgs = (orc_msg*)realloc(r->msgs, sizeof(orc_msg) * (size_t)r->msgs_cap);
+  }
+  r->msgs[r->nmsgs++] = m;
+  int to = (int)orc_raft_ref(r, m.to);
+  switch (m.type) {
+    case HB_MSG_APP: emit(r, HB_EV_APP, to, m.index, 0); break;
+    case HB_MSG_SNAP: emit(r, HB_EV_SNAP, to, m.snap_index, 0); break;
+    case HB_MSG_HEARTBEAT: emit(r, HB_EV_HEARTBEAT, to, m.commit, 0); break;
+    case HB_MSG_VOTE: emit(r, HB_EV_VOTE, to, m.index, 0); break;
+    case HB_MSG_PROP: emit(r, HB_EV_PROP_FWD, to, r->arrival, 0); break;
+    default: break;  /* MsgVoteResp etc.: off the engine's path */
+  }
+}
+
+int orc_raft_read_messages(orc_raft* r, orc_msg* out, int cap) {
+  int n = r->nmsgs;
+  if (out) memcpy(out, r->msgs, sizeof(orc_msg) * (size_t)(n < cap ? n : cap));
+  r->nmsgs = 0;
+  return n;
+}
+
+void orc_raft_commit_to(orc_raft* r, uint64_t tocommit) { /* commitTo raft/log.go:172-180 */
+  if (r->log.committed < tocommit) {
+    if (r->log.last_index < tocommit) {
+      fault(r, HB_FAULT_COMMIT_RANGE);
+      return;
+    }
+    r->log.committed = tocommit;
+    emit(r, HB_EV_COMMIT, 0, tocommit, 0);
+  }
+}
+
+void orc_raft_send_append(orc_raft* r, uint64_t to) {     /* sendAppend raft/raft.go:239-282 */
+  orc_progress* pr = orc_raft_pr(r, to);
+  if (!pr) { fault(r, HB_FAULT_NIL_PROGRESS); return; }
+  if (orc_pr_is_paused(pr)) return;
+  orc_msg m;
+  memset(&m, 0, sizeof(m));
+  m.to = to;
+  if (pr->next < r->log.first_index) {                    /* needSnapshot :715-717 */
+    m.type = HB_MSG_SNAP;
+    if (r->log.snap_index == 0) { fault(r, HB_FAULT_EMPTY_SNAPSHOT); return; }  /* :252-254 */
+    m.snap_index = r->log.snap_index;
+    orc_pr_become_snapshot(pr, r->log.snap_index);
+  } else {
+    m.type = HB_MSG_APP;
+    m.index = pr->next - 1;
+    m.log_term = orc_log_term(&r->log, pr->next - 1);
+    /* entries(Next, maxMsgSize) raft/log.go:219-224 + limitSize raft/util.go:97-110:
+     * noLimit -> through lastIndex; 0 -> exactly one entry. */
+    if (pr->next <= r->log.last_index) {
+      uint64_t last = r->max_msg_size == 0 ? pr->next : r->log.last_index;
+      m.nents = last - pr->next + 1;
+      m.ent_lo = pr->next;
+    }
+    m.commit = r->log.committed;
+    if (m.nents != 0) {
+      uint64_t last = m.ent_lo + m.nents - 1;
+      switch (pr->state) {
+        case HB_PR_REPLICATE:
+          orc_pr_optimistic_update(pr, last);
+          if (orc_ins_add(&pr->ins, last) < 0) { fault(r, HB_FAULT_INFLIGHTS_FULL); return; }
+          break;
+        case HB_PR_PROBE:
+          orc_pr_pause(pr);
+          break;
+        default:
+          break;  /* unreachable: isPaused() is true in Snapshot */
+      }
+    }
+  }
+  send(r, m);
+}
+
+static void send_heartbeat(orc_raft* r, int slot) {       /* sendHeartbeat raft/raft.go:285-299 */
+  orc_msg m;
+  memset(&m, 0, sizeof(m));
+  m.to = r->ids[slot];
+  m.type = HB_MSG_HEARTBEAT;
+  m.commit = umin(r->prs[slot].match, r->log.committed);
+  send(r, m);
+}
+
+void orc_raft_bcast_append(orc_raft* r) {                 /* bcastAppend raft/raft.go:303-310 */
+  for (int i = 0; i < r->n && !r->fault; i++) {
+    if (r->ids[i] == r->id) continue;
+    orc_raft_send_append(r, r->ids[i]);
+  }
+}
+
+void orc_raft_bcast_heartbeat(orc_raft* r) {              /* bcastHeartbeat raft/raft.go:313-321 */
+  for (int i = 0; i < r->n; i++) {
+    if (r->ids[i] == r->id) continue;
+    send_heartbeat(r, i);
+    orc_pr_resume(&r->prs[i]);
+  }
+}
+
+static int cmp_desc(const void* a, const void* b) {
+  uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+  return x < y ? 1 : (x > y ? -1 : 0);
+}
+
+int orc_raft_maybe_commit(orc_raft* r) {                  /* maybeCommit raft/raft.go:323-332 */
+  uint64_t mis[ORC_MAX_PEERS];
+  for (int i = 0; i < r->n; i++) mis[i] = r->prs[i].match;
+  qsort(mis, (size_t)r->n, sizeof(uint64_t), cmp_desc);   /* sort.Sort(sort.Reverse(mis)) */
+  uint64_t mci = mis[orc_raft_q(r) - 1];
+  /* raftLog.maybeCommit raft/log.go:241-247 */
+  if (mci > r->log.committed && orc_log_term(&r->log, mci) == r->term) {
+    orc_raft_commit_to(r, mci);
+    return !r->fault;
+  }
+  return 0;
+}
+
+void orc_raft_reset(orc_raft* r, uint64_t term) {         /* reset raft/raft.go:334-349 */
+  if (r->term != term) {
+    r->term = term;
+    r->vote = ORC_NONE;
+    emit(r, HB_EV_TERM, 0, term, 0);
+  }
+  r->lead = ORC_NONE;
+  r->elapsed = 0;
+  r->nvotes = 0;
+  for (int i = 0; i < r->n; i++) {
+    orc_progress* pr = &r->prs[i];
+    orc_ins_free(&pr->ins);
+    memset(pr, 0, sizeof(*pr));
+    pr->next = r->log.last_index + 1;
+    orc_ins_init(&pr->ins, r->max_inflight);
+    if (r->ids[i] == r->id) pr->match = r->log.last_index;
+  }
+  r->pending_conf = 0;
+}
+
+void orc_raft_append_entry(orc_raft* r, uint64_t k, int noop) {  /* appendEntry raft/raft.go:351-360 */
+  /* entries get Term = r.Term, Index = li+1..; raftLog.append (raft/log.go:90-99) */
+  orc_log_push(&r->log, r->term, k);
+  emit(r, HB_EV_LAST, 0, r->log.last_index, noop);
+  orc_progress* self = orc_raft_pr(r, r->id);
+  if (!self) { fault(r, HB_FAULT_NO_SELF); return; }     /* r.prs[r.id] is nil */
+  orc_pr_maybe_update(self, r->log.last_index);
+  orc_raft_maybe_commit(r);
+}
+
+static void emit_state_if_changed(orc_raft* r, uint64_t before) {
+  uint64_t now = soft_pack(r);
+  if (now != before) emit(r, HB_EV_STATE, 0, now, 0);
+}
+
+void orc_raft_become_follower(orc_raft* r, uint64_t term, uint64_t lead) {  /* :384-391 */
+  uint64_t before = soft_pack(r);
+  orc_raft_reset(r, term);
+  r->lead = lead;
+  r->state = HB_STATE_FOLLOWER;
+  emit_state_if_changed(r, before);
+}
+
+void orc_raft_become_candidate(orc_raft* r) {             /* :393-404 */
+  if (r->state == HB_STATE_LEADER) { fault(r, HB_FAULT_LEADER_CAMPAIGN); return; }
+  uint64_t before = soft_pack(r);
+  orc_raft_reset(r, r->term + 1);
+  r->vote = r->id;
+  r->state = HB_STATE_CANDIDATE;
+  emit_state_if_changed(r, before);
+}
+
+void orc_raft_become_leader(orc_raft* r) {                /* :406-427 */
+  /* unreachable on the engine's paths (only poll/campaign promote, both from
+   * candidate); kept for the TestStateTransition KAT. */
+  if (r->state == HB_STATE_FOLLOWER) { fault(r, HB_FAULT_FOLLOWER_LEADER); return; }
+  uint64_t before = soft_pack(r);
+  orc_raft_reset(r, r->term);
+  r->lead = r->id;
+  r->state = HB_STATE_LEADER;
+  emit_state_if_changed(r, before);
+  /* pendingConf scan of (committed, last] entries: host side (entry types) */
+  orc_raft_append_entry(r, 1, 1);                         /* appendEntry(pb.Entry{Data: nil}) */
+}
+
+int orc_raft_poll(orc_raft* r, uint64_t id, int v) {      /* poll raft/raft.go:445-460 */
+  int found = 0;
+  for (int i = 0; i < r->nvotes; i++)
+    if (r->vote_ids[i] == id) found = 1;
+  if (!found && r->nvotes < ORC_MAX_PEERS + 1) {
+    r->vote_ids[r->nvotes] = id;
+    r->vote_vals[r->nvotes] = v;
+    r->nvotes++;
+  }
+  int granted = 0;
+  for (int i = 0; i < r->nvotes; i++) granted += r->vote_vals[i] ? 1 : 0;
+  return granted;
+}
+
+void orc_raft_campaign(orc_raft* r) {                     /* campaign raft/raft.go:429-443 */
+  orc_raft_become_candidate(r);
+  if (r->fault) return;
+  if (orc_raft_q(r) == orc_raft_poll(r, r->id, 1)) {
+    r->n_won++;
+    orc_raft_become_leader(r);
+    return;
+  }
+  for (int i = 0; i < r->n; i++) {
+    if (r->ids[i] == r->id) continue;
+    orc_msg m;
+    memset(&m, 0, sizeof(m));
+    m.to = r->ids[i];
+    m.type = HB_MSG_VOTE;
+    m.index = r->log.last_index;
+    m.log_term = orc_log_last_term(&r->log);
+    send(r, m);
+  }
+}
+
+static void step_leader(orc_raft* r, const orc_msg* m) {  /* stepLeader raft/raft.go:494-583 */
+  orc_progress* pr = orc_raft_pr(r, m->from);
+  switch (m->type) {
+    case HB_MSG_BEAT:
+      orc_raft_bcast_heartbeat(r);
+      break;
+    case HB_MSG_PROP:
+      if (m->nents == 0) { fault(r, HB_FAULT_EMPTY_PROP); return; }
+      /* EntryConfChange / pendingConf rewriting (:504-511) acts on entry
+       * payloads, which stay on the host. */
+      orc_raft_append_entry(r, m->nents, 0);
+      if (r->fault) return;
+      orc_raft_bcast_append(r);
+      break;
+    case HB_MSG_APP_RESP:
+      if (!pr) { fault(r, HB_FAULT_NIL_PROGRESS); return; }
+      if (m->reject) {
+        if (orc_pr_maybe_decr_to(pr, m->index, m->reject_hint)) {
+          if (pr->state == HB_PR_REPLICATE) orc_pr_become_probe(pr);
+          orc_raft_send_append(r, m->from);
+        }
+      } else {
+        int old_paused = orc_pr_is_paused(pr);
+        if (orc_pr_maybe_update(pr, m->index)) {
+          if (pr->state == HB_PR_PROBE) {
+            orc_pr_become_replicate(pr);
+          } else if (pr->state == HB_PR_SNAPSHOT && orc_pr_maybe_snapshot_abort(pr)) {
+            orc_pr_become_probe(pr);
+          } else if (pr->state == HB_PR_REPLICATE) {
+            orc_ins_free_to(&pr->ins, m->index);
+          }
+          if (orc_raft_maybe_commit(r)) {
+            orc_raft_bcast_append(r);
+          } else if (old_paused && !r->fault) {
+            orc_raft_send_append(r, m->from);
+          }
+        }
+      }
+      break;
+    case HB_MSG_HEARTBEAT_RESP:
+      if (!pr) { fault(r, HB_FAULT_NIL_PROGRESS); return; }
+      if (pr->state == HB_PR_REPLICATE && orc_ins_full(&pr->ins)) orc_ins_free_first_one(&pr->ins);
+      if (pr->match < r->log.last_index) orc_raft_send_append(r, m->from);
+      break;
+    case HB_MSG_VOTE: {
+      orc_msg resp;
+      memset(&resp, 0, sizeof(resp));
+      resp.to = m->from;
+      resp.type = HB_MSG_VOTE_RESP;
+      resp.reject = 1;
+      send(r, resp);
+      break;
+    }
+    case HB_MSG_SNAP_STATUS:
+      if (!pr) { fault(r, HB_FAULT_NIL_PROGRESS); return; }
+      if (pr->state != HB_PR_SNAPSHOT) return;
+      if (!m->reject) {
+        orc_pr_become_probe(pr);
+      } else {
+        orc_pr_snapshot_failure(pr);
+        orc_pr_become_probe(pr);
+      }
+      orc_pr_pause(pr);
+      break;
+    case HB_MSG_UNREACHABLE:
+      if (!pr) { fault(r, HB_FAULT_NIL_PROGRESS); return; }
+      if (pr->state == HB_PR_REPLICATE) orc_pr_become_probe(pr);
+      break;
+    default:
+      break;
+  }
+}
+
+static void step_candidate(orc_raft* r, const orc_msg* m) {  /* stepCandidate raft/raft.go:585-614 */
+  switch (m->type) {
+    case HB_MSG_PROP:
+      emit(r, HB_EV_PROP_DROP, 0, r->arrival, 0);          /* "no leader ... dropping proposal" */
+      return;
+    case HB_MSG_VOTE: {
+      orc_msg resp;
+      memset(&resp, 0, sizeof(resp));
+      resp.to = m->from;
+      resp.type = HB_MSG_VOTE_RESP;
+      resp.reject = 1;
+      send(r, resp);
+      break;
+    }
+    case HB_MSG_VOTE_RESP: {
+      int gr = orc_raft_poll(r, m->from, !m->reject);
+      int q = orc_raft_q(r);
+      if (q == gr) {
+        r->n_won++;
+        orc_raft_become_leader(r);
+        if (!r->fault) orc_raft_bcast_append(r);
+      } else if (q == r->nvotes - gr) {
+        r->n_lost++;
+        orc_raft_become_follower(r, r->term, ORC_NONE);
+      }
+      break;
+    }
+    default:
+      break;  /* MsgApp/MsgHeartbeat/MsgSnap: follower side, off the engine's path */
+  }
+}
+
+static void step_follower(orc_raft* r, const orc_msg* m) {   /* stepFollower raft/raft.go:616-649 */
+  switch (m->type) {
+    case HB_MSG_PROP:
+      if (r->lead == ORC_NONE) {
+        emit(r, HB_EV_PROP_DROP, 0, r->arrival, 0);
+        return;
+      } else {
+        orc_msg fwd = *m;
+        fwd.to = r->lead;
+        send(r, fwd);
+      }
+      break;
+    default:
+      break;  /* MsgApp/MsgHeartbeat/MsgSnap/MsgVote: follower side, off the engine's path */
+  }
+}
+
+void orc_raft_step(orc_raft* r, const orc_msg* m) {       /* Step raft/raft.go:462-490 */
+  if (r->fault) return;
+  if (m->type == HB_MSG_HUP) {
+    orc_raft_campaign(r);
+    r->commit = r->log.committed;
+    return;
+  }
+  if (m->term == 0) {
+    /* local message */
+  } else if (m->term > r->term) {
+    uint64_t lead = m->from;
+    if (m->type == HB_MSG_VOTE) lead = ORC_NONE;
+    orc_raft_become_follower(r, m->term, lead);
+  } else if (m->term < r->term) {
+    return;                                               /* ignore */
+  }
+  if (r->fault) return;
+  switch (r->state) {
+    case HB_STATE_LEADER: step_leader(r, m); break;
+    case HB_STATE_CANDIDATE: step_candidate(r, m); break;
+    default: step_follower(r, m); break;
+  }
+  r->commit = r->log.committed;
+}
+
+/* ========================================================================
+ * engine-format conversion + batch driver
+ * ======================================================================== */
+static uint64_t slot_id(const hb_group* g, uint32_t ref) {
+  if (ref == HB_REF_NONE) return ORC_NONE;
+  if (ref == HB_REF_SELF) return 100;
+  if (ref == HB_REF_OTHER) return 99;
+  (void)g;
+  return (uint64_t)ref + 1;
+}
+
+int orc_raft_from_group(orc_raft* r, const hb_group* g, const orc_run* runs, int nruns,
+                        int max_inflight, uint64_t max_msg_size) {
+  if (g->n < 1 || g->n > HB_MAX_REPLICAS || nruns < 1) return -1;
+  memset(r, 0, sizeof(*r));
+  orc_log_init(&r->log, g->first_index, runs[0].term);
+  for (int k = 1; k < nruns; k++) {
+    orc_log_push(&r->log, runs[k - 1].term, runs[k].index - (r->log.last_index + 1));
+  }
+  /* last run extends to last_index */
+  if (g->last_index >= r->log.last_index + 1)
+    orc_log_push(&r->log, runs[nruns - 1].term, g->last_index - r->log.last_index);
+  if (r->log.last_index != g->last_index) return -2;
+  r->log.committed = g->committed;
+  r->log.applied = g->committed;
+  r->log.snap_index = g->snap_index;
+  r->id = g->self_slot == HB_SLOT_NONE ? 100 : (uint64_t)g->self_slot + 1;
+  r->max_inflight = max_inflight;
+  r->max_msg_size = max_msg_size;
+  r->term = g->term;
+  r->commit = g->committed;
+  r->vote = slot_id(g, g->vote);
+  r->lead = slot_id(g, g->lead);
+  r->state = (int)g->state;
+  r->n = (int)g->n;
+  for (int i = 0; i < r->n; i++) {
+    r->ids[i] = (uint64_t)i + 1;
+    orc_progress* pr = &r->prs[i];
+    pr->match = g->pr[i].match;
+    pr->next = g->pr[i].next;
+    pr->state = (int)g->pr[i].state;
+    pr->paused = (int)g->pr[i].paused;
+    pr->pending_snapshot = g->pr[i].pending_snapshot;
+    orc_ins_init(&pr->ins, max_inflight);
+    pr->ins.start = (int)g->pr[i].ins_start;
+    pr->ins.count = (int)g->pr[i].ins_count;
+  }
+  r->nvotes = 0;
+  for (int i = 0; i < 8; i++) {
+    if (!(g->votes_resp & (1u << i))) continue;
+    r->vote_ids[r->nvotes] = i == 7 ? r->id : (uint64_t)i + 1;
+    r->vote_vals[r->nvotes] = (g->votes_grant >> i) & 1u;
+    r->nvotes++;
+  }
+  r->fault = (int)g->fault;
+  return 0;
+}
+
+void orc_raft_to_group(const orc_raft* r, hb_group* g) {
+  memset(g, 0, sizeof(*g));
+  g->term = r->term;
+  g->committed = r->log.committed;
+  g->first_index = r->log.first_index;
+  g->last_index = r->log.last_index;
+  g->snap_index = r->log.snap_index;
+  /* maximal run of indices in [first-1, last] whose term == r->term */
+  g->term_first = HB_NO_INDEX;
+  g->term_last = 0;
+  for (int k = 0; k < r->log.nruns; k++) {
+    if (r->log.runs[k].term != r->term) continue;
+    uint64_t lo = r->log.runs[k].index;
+    uint64_t hi = (k + 1 < r->log.nruns) ? r->log.runs[k + 1].index - 1 : r->log.last_index;
+    if (lo > hi) continue;
+    if (g->term_first == HB_NO_INDEX) g->term_first = lo;
+    g->term_last = hi;
+  }
+  g->state = (uint32_t)r->state;
+  g->n = (uint32_t)r->n;
+  int self = orc_raft_slot(r, r->id);
+  g->self_slot = self < 0 ? HB_SLOT_NONE : (uint32_t)self;
+  g->lead = orc_raft_ref(r, r->lead);
+  g->vote = orc_raft_ref(r, r->vote);
+  for (int i = 0; i < r->nvotes; i++) {
+    int s = orc_raft_slot(r, r->vote_ids[i]);
+    uint32_t bit = s < 0 ? 7u : (uint32_t)s;
+    g->votes_resp |= 1u << bit;
+    if (r->vote_vals[i]) g->votes_grant |= 1u << bit;
+  }
+  g->fault = (uint32_t)r->fault;
+  for (int i = 0; i < r->n && i < HB_MAX_REPLICAS; i++) {
+    const orc_progress* pr = &r->prs[i];
+    g->pr[i].match = pr->match;
+    g->pr[i].next = pr->next;
+    g->pr[i].state = (uint32_t)pr->state;
+    g->pr[i].paused = (uint32_t)pr->paused;
+    g->pr[i].pending_snapshot = pr->state == HB_PR_SNAPSHOT ? pr->pending_snapshot : 0;
+    g->pr[i].ins_start = (uint32_t)pr->ins.start;
+    g->pr[i].ins_count = (uint32_t)pr->ins.count;
+  }
+}
+
+int orc_raft_set_inflights(orc_raft* r, int slot, int start, int count, const uint64_t* vals) {
+  if (slot < 0 || slot >= r->n) return -1;
+  orc_inflights* in = &r->prs[slot].ins;
+  if (start < 0 || start >= in->size || count < 0 || count > in->size) return -1;
+  in->start = start;
+  in->count = count;
+  for (int i = 0; i < count; i++) in->buffer[(start + i) % in->size] = vals[i];
+  return 0;
+}
+
+int orc_raft_get_inflights(const orc_raft* r, int slot, uint64_t* vals) {
+  if (slot < 0 || slot >= r->n) return -1;
+  const orc_inflights* in = &r->prs[slot].ins;
+  for (int i = 0; i < in->count; i++) vals[i] = in->buffer[(in->start + i) % in->size];
+  return in->count;
+}
+
+static int is_response(int type) {                        /* IsResponseMsg raft/util.go:53-55 */
+  return type == HB_MSG_APP_RESP || type == HB_MSG_VOTE_RESP ||
+         type == HB_MSG_HEARTBEAT_RESP || type == HB_MSG_UNREACHABLE;
+}
+
+static void account(orc_raft* r, int type, uint64_t stats[HB_STAT_COUNT]) {
+  stats[HB_STAT_MSGS]++;
+  if (type == HB_MSG_APP_RESP) stats[HB_STAT_APPRESP]++;
+  if (type == HB_MSG_VOTE_RESP) stats[HB_STAT_VOTERESP]++;
+  (void)r;
+}
+
+int orc_step_batch(orc_raft* groups, uint32_t ngroups, const hb_batch* b,
+                   hb_event* ev, uint64_t ev_cap, uint64_t* nev,
+                   uint64_t stats[HB_STAT_COUNT]) {
+  memset(stats, 0, sizeof(uint64_t) * HB_STAT_COUNT);
+  uint64_t* commit0 = (uint64_t*)malloc(sizeof(uint64_t) * (ngroups ? ngroups : 1));
+  uint64_t* last0 = (uint64_t*)malloc(sizeof(uint64_t) * (ngroups ? ngroups : 1));
+  int* fault0 = (int*)malloc(sizeof(int) * (ngroups ? ngroups : 1));
+  uint64_t total = 0;
+  uint64_t won0 = 0, lost0 = 0;
+  for (uint32_t g = 0; g < ngroups; g++) {
+    won0 += groups[g].n_won;
+    lost0 += groups[g].n_lost;
+    commit0[g] = groups[g].log.committed;
+    last0[g] = groups[g].log.last_index;
+    fault0[g] = groups[g].fault;
+    groups[g].group = g;
+  }
+  /* one sink shared by all groups, appended in processing order */
+  #define BIND(r) do { (r)->ev = ev; (r)->ev_cap = ev_cap; (r)->nev = total; } while (0)
+  #define UNBIND(r) do { total = (r)->nev; (r)->ev = NULL; } while (0)
+
+  /* dense proposals: one MsgProp{Entries: props[g]} per group, stepped first */
+  if (b->props) {
+    for (uint32_t g = 0; g < ngroups; g++) {
+      if (b->props[g] == 0) continue;
+      orc_raft* r = &groups[g];
+      if (r->fault || r->n == 0) continue;
+      BIND(r);
+      r->arrival = HB_NO_INDEX;
+      orc_msg m;
+      memset(&m, 0, sizeof(m));
+      m.type = HB_MSG_PROP;
+      m.from = r->id;                                     /* raft/multinode.go:229 */
+      m.nents = b->props[g];
+      orc_raft_step(r, &m);
+      UNBIND(r);
+    }
+  }
+  for (uint64_t i = 0; i < b->n; i++) {
+    uint32_t g = b->group[i];
+    if (g >= ngroups) continue;
+    orc_raft* r = &groups[g];
+    if (r->n == 0) continue;                              /* removed group */
+    uint32_t info = b->info[i];
+    int type = (int)(info & 0xF);
+    uint32_t from_slot = (info >> 4) & 0xF;
+    int reject = (int)((info >> 8) & 1);
+    if (r->fault) continue;
+    uint64_t from = from_slot < (uint32_t)r->n ? r->ids[from_slot] : 0xFFFFFFFFull;
+    /* MultiNode recvc filter raft/multinode.go:235 */
+    if (from_slot >= (uint32_t)r->n && is_response(type)) {
+      stats[HB_STAT_DROPPED]++;
+      continue;
+    }
+    if (from_slot >= (uint32_t)r->n && (type == HB_MSG_HUP || type == HB_MSG_BEAT || type == HB_MSG_PROP))
+      from = r->id;
+    BIND(r);
+    r->arrival = i;
+    orc_msg m;
+    memset(&m, 0, sizeof(m));
+    m.type = type;
+    m.from = from;
+    m.to = r->id;
+    m.term = b->term[i];
+    m.index = b->index[i];
+    m.reject = reject;
+    m.reject_hint = (reject && b->hint) ? b->hint[i] : 0;
+    if (type == HB_MSG_PROP) { m.nents = b->index[i]; m.index = 0; }
+    orc_raft_step(r, &m);
+    account(r, type, stats);
+    UNBIND(r);
+  }
+  for (uint32_t g = 0; g < ngroups; g++) {
+    orc_raft* r = &groups[g];
+    if (r->log.committed > commit0[g]) stats[HB_STAT_COMMITS]++;
+    if (r->fault && !fault0[g]) stats[HB_STAT_FAULTS]++;
+    stats[HB_STAT_ENTRIES] += r->log.last_index - last0[g];
+    r->nmsgs = 0;                                          /* msgs handed to the app via Ready */
+  }
+  uint64_t won1 = 0, lost1 = 0;
+  for (uint32_t g = 0; g < ngroups; g++) {
+    won1 += groups[g].n_won;
+    lost1 += groups[g].n_lost;
+  }
+  stats[HB_STAT_WON] = won1 - won0;
+  stats[HB_STAT_LOST] = lost1 - lost0;
+  free(commit0);
+  free(last0);
+  free(fault0);
+  stats[HB_STAT_EVENTS] = total;
+  *nev = total;
+  #undef BIND
+  #undef UNBIND
+  return total <= ev_cap ? 0 : -1;
+}
+
+orc_raft* orc_groups_new(uint32_t ngroups) {
+  return (orc_raft*)calloc(ngroups ? ngroups : 1, sizeof(orc_raft));
+}
+
+void orc_groups_free(orc_raft* g, uint32_t ngroups) {
+  for (uint32_t i = 0; i < ngroups; i++) orc_raft_free(&g[i]);
+  free(g);
+}
+
+orc_raft* orc_groups_at(orc_raft* g, uint32_t i) { return &g[i]; }
+
+size_t orc_sizeof_raft(void) { return sizeof(orc_raft); }

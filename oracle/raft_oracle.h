@@ -1,0 +1,204 @@
+/*
+ * raft_oracle.h — CPU restatement of the reference's raft leader bookkeeping.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity oracle for the MI355X engine
+ * (etcd_amd/csrc).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it, and only as the checker / CPU baseline; the
+ * product path never calls it.
+ *
+ * It restates, sequentially and per group, the Go functions of the reference
+ * (holandes22/etcd @ 2.1.0-alpha, package raft) that the engine replaces:
+ *   raft/progress.go:69-237    Progress state machine + inflights ring
+ *   raft/raft.go:215-490       q, send, sendAppend, bcast*, maybeCommit, reset,
+ *                              appendEntry, become*, campaign, poll, Step
+ *   raft/raft.go:494-649       stepLeader / stepCandidate / stepFollower (the
+ *                              branches on the leader-bookkeeping path)
+ *   raft/log.go:172-247        commitTo, term, maybeCommit
+ *   raft/multinode.go:233-237  recvc membership filter
+ * Each function below cites the lines it follows.  Go's map iteration order in
+ * bcastAppend / bcastHeartbeat / campaign is unspecified; the oracle iterates
+ * prs in slot order and parity on emitted messages is per-(group, peer).
+ *
+ * Parity status: pinned by transcriptions of the reference's own known-answer
+ * tests (tests/test_oracle_kat.py).  The Go reference cannot be
+ * built in this image (no Go toolchain), so there is no oracle/_ref build.
+ */
+#ifndef RAFT_ORACLE_H_
+#define RAFT_ORACLE_H_
+
+#include <stdint.h>
+#include "../include/hipbatch.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORC_MAX_PEERS 8
+#define ORC_NONE 0ull   /* raft.None, raft/raft.go:29 */
+
+/* inflights, raft/progress.go:172-181 */
+typedef struct orc_inflights {
+  int start;
+  int count;
+  int size;
+  uint64_t* buffer;
+} orc_inflights;
+
+/* Progress, raft/progress.go:37-67 */
+typedef struct orc_progress {
+  uint64_t match, next;
+  int state;
+  int paused;
+  uint64_t pending_snapshot;
+  orc_inflights ins;
+} orc_progress;
+
+/* Log term metadata.  raftLog.term(i) (raft/log.go:198-217) is 0 outside
+ * [first_index-1, last_index] and otherwise the term of entry i (the dummy
+ * entry first_index-1 carries the snapshot term).  Entry terms are stored
+ * run-length encoded: run k covers [runs[k].index, runs[k+1].index). */
+typedef struct orc_run {
+  uint64_t index;
+  uint64_t term;
+} orc_run;
+
+typedef struct orc_log {
+  uint64_t first_index;
+  uint64_t last_index;
+  uint64_t committed;
+  uint64_t applied;
+  uint64_t snap_index;  /* raftLog.snapshot().Metadata.Index */
+  int nruns, cap;
+  orc_run* runs;
+} orc_log;
+
+/* pb.Message fields on this path (raft/raftpb/raft.pb.go:200-213).
+ * Entries are represented by their index range [ent_lo, ent_hi]. */
+typedef struct orc_msg {
+  int type;
+  uint64_t to, from, term, log_term, index, commit;
+  int reject;
+  uint64_t reject_hint;
+  uint64_t nents;       /* len(m.Entries) */
+  uint64_t ent_lo;      /* index of first entry (MsgApp) */
+  uint64_t snap_index;  /* MsgSnap snapshot metadata index */
+} orc_msg;
+
+typedef struct orc_raft {
+  /* pb.HardState + id, raft/raft.go:125-155 */
+  uint64_t id;
+  uint64_t term, vote, commit;
+  orc_log log;
+  int max_inflight;
+  uint64_t max_msg_size;
+  int n;                          /* len(prs) */
+  uint64_t ids[ORC_MAX_PEERS];    /* prs keys, slot order */
+  orc_progress prs[ORC_MAX_PEERS];
+  int state;
+  uint64_t lead;
+  int pending_conf;
+  int elapsed;
+  int nvotes;                     /* r.votes map */
+  uint64_t vote_ids[ORC_MAX_PEERS + 1];
+  int vote_vals[ORC_MAX_PEERS + 1];
+  /* r.msgs */
+  orc_msg* msgs;
+  int nmsgs, msgs_cap;
+  /* event sink (the engine's delta format, include/hipbatch.h) */
+  hb_event* ev;
+  uint64_t nev, ev_cap;
+  uint32_t group;
+  uint64_t arrival;               /* arrival index of the message being stepped */
+  int fault;                      /* HB_FAULT_* once a reference panic happened */
+  uint64_t n_won, n_lost;         /* elections won (-> leader) / lost by poll (-> follower) */
+} orc_raft;
+
+/* ---- inflights (raft/progress.go:183-237) ---- */
+void orc_ins_init(orc_inflights* in, int size);
+void orc_ins_free(orc_inflights* in);
+int  orc_ins_add(orc_inflights* in, uint64_t inflight);  /* -1 = panic (full) */
+void orc_ins_free_to(orc_inflights* in, uint64_t to);
+void orc_ins_free_first_one(orc_inflights* in);
+int  orc_ins_full(const orc_inflights* in);
+void orc_ins_reset(orc_inflights* in);
+
+/* ---- Progress (raft/progress.go:69-166) ---- */
+void orc_pr_reset_state(orc_progress* pr, int state);
+void orc_pr_become_probe(orc_progress* pr);
+void orc_pr_become_replicate(orc_progress* pr);
+void orc_pr_become_snapshot(orc_progress* pr, uint64_t snapshoti);
+int  orc_pr_maybe_update(orc_progress* pr, uint64_t n);
+void orc_pr_optimistic_update(orc_progress* pr, uint64_t n);
+int  orc_pr_maybe_decr_to(orc_progress* pr, uint64_t rejected, uint64_t last);
+void orc_pr_pause(orc_progress* pr);
+void orc_pr_resume(orc_progress* pr);
+int  orc_pr_is_paused(const orc_progress* pr);
+void orc_pr_snapshot_failure(orc_progress* pr);
+int  orc_pr_maybe_snapshot_abort(const orc_progress* pr);
+
+/* ---- log (raft/log.go) ---- */
+void     orc_log_init(orc_log* l, uint64_t first_index, uint64_t dummy_term);
+void     orc_log_free(orc_log* l);
+void     orc_log_push(orc_log* l, uint64_t term, uint64_t k);    /* append k entries of term */
+uint64_t orc_log_term(const orc_log* l, uint64_t i);
+uint64_t orc_log_last_term(const orc_log* l);
+
+/* ---- raft ---- */
+/* newRaft (raft/raft.go:157-209) with Config peers; the log must be set up
+ * with orc_raft_log() first (or left empty = NewMemoryStorage()). */
+void orc_raft_init(orc_raft* r, uint64_t id, const uint64_t* peers, int npeers,
+                   int max_inflight, uint64_t max_msg_size);
+void orc_raft_free(orc_raft* r);
+orc_log* orc_raft_log(orc_raft* r);
+int  orc_raft_slot(const orc_raft* r, uint64_t id);  /* -1 if id not in prs */
+orc_progress* orc_raft_pr(orc_raft* r, uint64_t id);
+void orc_raft_set_progress(orc_raft* r, uint64_t id, uint64_t match, uint64_t next);
+void orc_raft_load_state(orc_raft* r, uint64_t term, uint64_t vote, uint64_t commit);
+int  orc_raft_q(const orc_raft* r);
+void orc_raft_reset(orc_raft* r, uint64_t term);
+void orc_raft_send_append(orc_raft* r, uint64_t to);
+void orc_raft_bcast_append(orc_raft* r);
+void orc_raft_bcast_heartbeat(orc_raft* r);
+int  orc_raft_maybe_commit(orc_raft* r);
+void orc_raft_append_entry(orc_raft* r, uint64_t k, int noop);
+void orc_raft_become_follower(orc_raft* r, uint64_t term, uint64_t lead);
+void orc_raft_become_candidate(orc_raft* r);
+void orc_raft_become_leader(orc_raft* r);
+void orc_raft_campaign(orc_raft* r);
+int  orc_raft_poll(orc_raft* r, uint64_t id, int v);
+void orc_raft_step(orc_raft* r, const orc_msg* m);
+void orc_raft_commit_to(orc_raft* r, uint64_t tocommit);
+/* readMessages (raft/raft_test.go:44-49): copies up to cap, clears, returns count */
+int  orc_raft_read_messages(orc_raft* r, orc_msg* out, int cap);
+
+/* ---- engine-format conversion + batch driver (parity harness) ---- */
+uint32_t orc_raft_ref(const orc_raft* r, uint64_t id);   /* node id -> HB_REF_* */
+/* Build a group from the engine record plus its log term runs (runs[0].index
+ * must be first_index-1; terms non-decreasing).  Node ids are slot+1 and the
+ * local id is self_slot+1 (or 100 when HB_SLOT_NONE); lead/vote refs of
+ * HB_REF_OTHER become id 99. */
+int  orc_raft_from_group(orc_raft* r, const hb_group* g, const orc_run* runs, int nruns,
+                         int max_inflight, uint64_t max_msg_size);
+/* Export to the engine record (term_first/term_last derived from the runs). */
+void orc_raft_to_group(const orc_raft* r, hb_group* g);
+/* Inflight window of prs[slot]: buffer[(start+i) % size] = vals[i]. */
+int  orc_raft_set_inflights(orc_raft* r, int slot, int start, int count, const uint64_t* vals);
+int  orc_raft_get_inflights(const orc_raft* r, int slot, uint64_t* vals /* [count] */);
+
+/* Step one engine batch over `ngroups` groups exactly as MultiNode.run would
+ * (props first per group, then messages in arrival order).  Events go to
+ * ev[0..*nev).  Returns 0, or -1 if ev_cap was too small. */
+int orc_step_batch(orc_raft* groups, uint32_t ngroups, const hb_batch* b,
+                   hb_event* ev, uint64_t ev_cap, uint64_t* nev,
+                   uint64_t stats[HB_STAT_COUNT]);
+
+/* Flat-array helpers so the Python harness can drive many groups via ctypes. */
+orc_raft* orc_groups_new(uint32_t ngroups);
+void      orc_groups_free(orc_raft* g, uint32_t ngroups);
+orc_raft* orc_groups_at(orc_raft* g, uint32_t i);
+size_t    orc_sizeof_raft(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,608 @@
+"""Known-answer tests that pin the C parity oracle to the reference.
+
+Each test transcribes one of the reference's own Go tests (file:line cited) onto
+the oracle (oracle/raft_oracle.c).  The Go toolchain is absent from this image,
+so these tables ARE the oracle's pin (DESIGN.md "Parity").  Substitutions are
+named where a test drives a follower-side path the engine does not cover.
+"""
+import pytest
+
+from etcd_amd import abi
+from oracle.pyoracle import Inflights, Msg, Progress, Raft
+
+P, R, S = abi.HB_PR_PROBE, abi.HB_PR_REPLICATE, abi.HB_PR_SNAPSHOT
+F, Cd, L = abi.HB_STATE_FOLLOWER, abi.HB_STATE_CANDIDATE, abi.HB_STATE_LEADER
+None_ = 0
+
+
+# ---------------------------------------------------------------- inflights
+def test_inflights_add():  # raft/progress_test.go:22-94
+    inf = Inflights(10)
+    for i in range(5):
+        inf.add(i)
+    assert inf.as_tuple() == (0, 5, 10, [0, 1, 2, 3, 4, 0, 0, 0, 0, 0])
+    for i in range(5, 10):
+        inf.add(i)
+    assert inf.as_tuple() == (0, 10, 10, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+    in2 = Inflights(10, start=5)
+    for i in range(5):
+        in2.add(i)
+    assert in2.as_tuple() == (5, 5, 10, [0, 0, 0, 0, 0, 0, 1, 2, 3, 4])
+    for i in range(5, 10):
+        in2.add(i)
+    assert in2.as_tuple() == (5, 10, 10, [5, 6, 7, 8, 9, 0, 1, 2, 3, 4])
+    with pytest.raises(RuntimeError):  # add panics when full (raft/progress.go:192-194)
+        in2.add(10)
+
+
+def test_inflight_free_to():  # raft/progress_test.go:96-167
+    inf = Inflights(10)
+    for i in range(10):
+        inf.add(i)
+    inf.freeTo(4)
+    assert inf.as_tuple() == (5, 5, 10, list(range(10)))
+    inf.freeTo(8)
+    assert inf.as_tuple() == (9, 1, 10, list(range(10)))
+    for i in range(10, 15):
+        inf.add(i)
+    inf.freeTo(12)
+    assert inf.as_tuple() == (3, 2, 10, [10, 11, 12, 13, 14, 5, 6, 7, 8, 9])
+    inf.freeTo(14)
+    assert inf.as_tuple() == (5, 0, 10, [10, 11, 12, 13, 14, 5, 6, 7, 8, 9])
+
+
+def test_inflight_free_first_one():  # raft/progress_test.go:169-189
+    inf = Inflights(10)
+    for i in range(10):
+        inf.add(i)
+    inf.freeFirstOne()
+    assert inf.as_tuple() == (1, 9, 10, list(range(10)))
+
+
+# ---------------------------------------------------------------- Progress
+@pytest.mark.parametrize("p,wnext", [  # raft/raft_test.go:51-83
+    (dict(State=R, Match=1, Next=5), 2),
+    (dict(State=S, Match=1, Next=5, PendingSnapshot=10), 11),
+    (dict(State=S, Match=1, Next=5, PendingSnapshot=0), 2),
+])
+def test_progress_become_probe(p, wnext):
+    pr = Progress(**p)
+    pr.becomeProbe()
+    assert (pr.State, pr.Match, pr.Next) == (P, 1, wnext)
+
+
+def test_progress_become_replicate():  # raft/raft_test.go:85-99
+    pr = Progress(State=P, Match=1, Next=5)
+    pr.becomeReplicate()
+    assert (pr.State, pr.Match, pr.Next) == (R, 1, 2)
+
+
+def test_progress_become_snapshot():  # raft/raft_test.go:101-115
+    pr = Progress(State=P, Match=1, Next=5)
+    pr.becomeSnapshot(10)
+    assert (pr.State, pr.Match, pr.PendingSnapshot) == (S, 1, 10)
+
+
+@pytest.mark.parametrize("update,wm,wn,wok", [  # raft/raft_test.go:117-148
+    (2, 3, 5, False), (3, 3, 5, False), (4, 4, 5, True), (5, 5, 6, True)])
+def test_progress_update(update, wm, wn, wok):
+    pr = Progress(Match=3, Next=5)
+    assert pr.maybeUpdate(update) == wok
+    assert (pr.Match, pr.Next) == (wm, wn)
+
+
+@pytest.mark.parametrize("state,m,n,rejected,last,w,wn", [  # raft/raft_test.go:150-212
+    (R, 5, 10, 5, 5, False, 10), (R, 5, 10, 4, 4, False, 10), (R, 5, 10, 9, 9, True, 6),
+    (P, 0, 0, 0, 0, False, 0), (P, 0, 10, 5, 5, False, 10), (P, 0, 10, 9, 9, True, 9),
+    (P, 0, 2, 1, 1, True, 1), (P, 0, 1, 0, 0, True, 1), (P, 0, 10, 9, 2, True, 3),
+    (P, 0, 10, 9, 0, True, 1)])
+def test_progress_maybe_decr(state, m, n, rejected, last, w, wn):
+    pr = Progress(State=state, Match=m, Next=n)
+    assert pr.maybeDecrTo(rejected, last) == w
+    assert (pr.Match, pr.Next) == (m, wn)
+
+
+@pytest.mark.parametrize("state,paused,w", [  # raft/raft_test.go:214-238
+    (P, False, False), (P, True, True), (R, False, False), (R, True, False),
+    (S, False, True), (S, True, True)])
+def test_progress_is_paused(state, paused, w):
+    assert Progress(State=state, Paused=paused).isPaused() == w
+
+
+def test_progress_resume():  # raft/raft_test.go:240-261
+    pr = Progress(Next=2, Paused=True)
+    pr.maybeDecrTo(1, 1)
+    assert not pr.Paused
+    pr.p.Paused = 1
+    pr.maybeUpdate(2)
+    assert not pr.Paused
+
+
+def test_progress_resume_by_heartbeat():  # raft/raft_test.go:264-275
+    r = Raft(1, [1, 2])
+    r.becomeCandidate()
+    r.becomeLeader()
+    r.pr(2).Paused = 1
+    r.Step(Msg(abi.HB_MSG_BEAT, From=1, To=1))
+    assert r.pr(2).Paused == 0
+
+
+def test_progress_paused():  # raft/raft_test.go:277-288
+    r = Raft(1, [1, 2])
+    r.becomeCandidate()
+    r.becomeLeader()
+    for _ in range(3):
+        r.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+    assert len(r.readMessages()) == 1
+
+
+# ---------------------------------------------------------------- commit
+COMMIT_TABLE = [  # raft/raft_test.go:706-748 (matches, log terms, smTerm, w)
+    ([1], [1], 1, 1), ([1], [1], 2, 0), ([2], [1, 2], 2, 2), ([1], [2], 2, 1),
+    ([2, 1, 1], [1, 2], 1, 1), ([2, 1, 1], [1, 1], 2, 0), ([2, 1, 2], [1, 2], 2, 2),
+    ([2, 1, 2], [1, 1], 2, 0),
+    ([2, 1, 1, 1], [1, 2], 1, 1), ([2, 1, 1, 1], [1, 1], 2, 0), ([2, 1, 1, 2], [1, 2], 1, 1),
+    ([2, 1, 1, 2], [1, 1], 2, 0), ([2, 1, 2, 2], [1, 2], 2, 2), ([2, 1, 2, 2], [1, 1], 2, 0),
+]
+
+
+@pytest.mark.parametrize("matches,terms,smterm,w", COMMIT_TABLE)
+def test_commit(matches, terms, smterm, w):
+    sm = Raft(1, [1], ents=[(i + 1, t) for i, t in enumerate(terms)], hard=(smterm, 0, 0))
+    for j, m in enumerate(matches):
+        sm.setProgress(j + 1, m, m + 1)
+    sm.maybeCommit()
+    assert sm.committed == w
+
+
+def test_commit_to():  # raft/log_test.go:399-429
+    for commit, wcommit, wpanic in [(3, 3, False), (1, 2, False), (4, 0, True)]:
+        r = Raft(1, [1], ents=[(1, 1), (2, 2), (3, 3)])
+        r.r.log.committed = 2
+        r.commitTo(commit)
+        if wpanic:
+            assert r.fault == abi.HB_FAULT_COMMIT_RANGE
+        else:
+            assert r.committed == wcommit and r.fault == 0
+
+
+def test_term():  # raft/log_test.go:629-658
+    offset, num = 100, 100
+    r = Raft(1, [1], snapshot=(offset, 1), ents=[(offset + i, i) for i in range(1, num)])
+    for index, w in [(offset - 1, 0), (offset, 1), (offset + num // 2, num // 2),
+                     (offset + num - 1, num - 1), (offset + num, 0)]:
+        assert r.term(index) == w
+
+
+def test_term_with_unstable_snapshot():  # raft/log_test.go:660-688
+    storagesnapi, unstablesnapi = 100, 105
+    r = Raft(1, [1], snapshot=(unstablesnapi, 1))  # restore() -> firstIndex = 106
+    for index, w in [(storagesnapi, 0), (storagesnapi + 1, 0), (unstablesnapi - 1, 0),
+                     (unstablesnapi, 1)]:
+        assert r.term(index) == w
+
+
+# ---------------------------------------------------------------- leader responses
+@pytest.mark.parametrize("index,reject,wmatch,wnext,wmsgnum,windex,wcommitted", [
+    (3, True, 0, 3, 0, 0, 0), (2, True, 0, 2, 1, 1, 0), (2, False, 2, 4, 2, 2, 2),
+    (0, False, 0, 3, 0, 0, 0)])
+def test_leader_app_resp(index, reject, wmatch, wnext, wmsgnum, windex, wcommitted):
+    # raft/raft_test.go:1175-1229 — log {1: term 0, 2: term 1}; becomes leader at term 1
+    sm = Raft(1, [1, 2, 3], ents=[(1, 0), (2, 1)])
+    sm.becomeCandidate()
+    sm.becomeLeader()
+    sm.readMessages()
+    sm.Step(Msg(abi.HB_MSG_APP_RESP, From=2, Index=index, Term=sm.Term, Reject=reject, RejectHint=index))
+    p = sm.pr(2)
+    assert (p.Match, p.Next) == (wmatch, wnext)
+    msgs = sm.readMessages()
+    assert len(msgs) == wmsgnum
+    for m in msgs:
+        assert (m.Index, m.Commit) == (windex, wcommitted)
+
+
+def test_msg_app_resp_wait_reset():  # raft/raft_test.go:944-1002
+    sm = Raft(1, [1, 2, 3])
+    sm.becomeCandidate()
+    sm.becomeLeader()
+    sm.bcastAppend()
+    sm.readMessages()
+    sm.Step(Msg(abi.HB_MSG_APP_RESP, From=2, Index=1))
+    assert sm.Commit == 1
+    sm.readMessages()
+    sm.Step(Msg(abi.HB_MSG_PROP, From=1, Entries=1))
+    msgs = sm.readMessages()
+    assert len(msgs) == 1
+    assert (msgs[0].Type, msgs[0].To, msgs[0].nents, msgs[0].ent_lo) == (abi.HB_MSG_APP, 2, 1, 2)
+    sm.Step(Msg(abi.HB_MSG_APP_RESP, From=3, Index=1))
+    msgs = sm.readMessages()
+    assert len(msgs) == 1
+    assert (msgs[0].Type, msgs[0].To, msgs[0].nents, msgs[0].ent_lo) == (abi.HB_MSG_APP, 3, 1, 2)
+
+
+def test_handle_heartbeat_resp():  # raft/raft_test.go:883-940
+    sm = Raft(1, [1, 2], ents=[(1, 1), (2, 2), (3, 3)])
+    sm.becomeCandidate()
+    sm.becomeLeader()
+    sm.commitTo(sm.lastIndex)
+    sm.Step(Msg(abi.HB_MSG_HEARTBEAT_RESP, From=2))
+    msgs = sm.readMessages()
+    assert [m.Type for m in msgs] == [abi.HB_MSG_APP]
+    sm.Step(Msg(abi.HB_MSG_HEARTBEAT_RESP, From=2))
+    assert sm.readMessages() == []
+    sm.bcastHeartbeat()
+    sm.Step(Msg(abi.HB_MSG_HEARTBEAT_RESP, From=2))
+    msgs = sm.readMessages()
+    assert [m.Type for m in msgs] == [abi.HB_MSG_HEARTBEAT, abi.HB_MSG_APP]
+    sm.Step(Msg(abi.HB_MSG_APP_RESP, From=2, Index=msgs[1].Index + msgs[1].nents))
+    sm.readMessages()
+    sm.bcastHeartbeat()
+    sm.Step(Msg(abi.HB_MSG_HEARTBEAT_RESP, From=2))
+    msgs = sm.readMessages()
+    assert [m.Type for m in msgs] == [abi.HB_MSG_HEARTBEAT]
+
+
+def test_recv_msg_unreachable():  # raft/raft_test.go:1442-1463
+    r = Raft(1, [1, 2], ents=[(1, 1), (2, 1), (3, 1)])
+    r.becomeCandidate()
+    r.becomeLeader()
+    r.readMessages()
+    p = r.pr(2)
+    p.Match = 3
+    # becomeReplicate + optimisticUpdate(5)
+    p.State, p.Next = R, 4
+    p.Next = 6
+    r.Step(Msg(abi.HB_MSG_UNREACHABLE, From=2, To=1))
+    assert (r.pr(2).State, r.pr(2).Next) == (P, r.pr(2).Match + 1)
+
+
+@pytest.mark.parametrize("state,nxt,wnext", [(R, 2, 3 + 1 + 1 + 1), (P, 2, 2)])
+def test_leader_increase_next(state, nxt, wnext):  # raft/raft_test.go:1330-1360
+    sm = Raft(1, [1, 2], ents=[(1, 1), (2, 1), (3, 1)])
+    sm.becomeCandidate()
+    sm.becomeLeader()
+    sm.pr(2).State = state
+    sm.pr(2).Next = nxt
+    sm.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+    assert sm.pr(2).Next == wnext
+
+
+def test_send_append_for_progress_probe():  # raft/raft_test.go:1362-1403
+    r = Raft(1, [1, 2])
+    r.becomeCandidate()
+    r.becomeLeader()
+    r.readMessages()
+    p = r.pr(2)
+    p.State, p.Next = P, p.Match + 1  # becomeProbe
+    for _ in range(3):
+        r.appendEntry()
+        r.sendAppend(2)
+        msg = r.readMessages()
+        assert len(msg) == 1 and msg[0].Index == 0
+        assert r.pr(2).Paused == 1
+        for _ in range(10):
+            r.appendEntry()
+            r.sendAppend(2)
+            assert len(r.readMessages()) == 0
+        r.Step(Msg(abi.HB_MSG_BEAT, From=1, To=1))  # heartbeatTimeout = 1
+        msg = r.readMessages()
+        assert len(msg) == 1 and msg[0].Type == abi.HB_MSG_HEARTBEAT
+
+
+def test_send_append_for_progress_replicate():  # raft/raft_test.go:1405-1420
+    r = Raft(1, [1, 2])
+    r.becomeCandidate()
+    r.becomeLeader()
+    r.readMessages()
+    p = r.pr(2)
+    p.State, p.Next = R, p.Match + 1
+    for _ in range(10):
+        r.appendEntry()
+        r.sendAppend(2)
+        assert len(r.readMessages()) == 1
+
+
+def test_send_append_for_progress_snapshot():  # raft/raft_test.go:1422-1440
+    r = Raft(1, [1, 2])
+    r.becomeCandidate()
+    r.becomeLeader()
+    r.readMessages()
+    p = r.pr(2)
+    p.State, p.PendingSnapshot = S, 10
+    for _ in range(10):
+        r.appendEntry()
+        r.sendAppend(2)
+        assert len(r.readMessages()) == 0
+
+
+def test_bcast_beat():  # raft/raft_test.go:1231-1284
+    offset = 1000
+    sm = Raft(1, [1, 2, 3], snapshot=(offset, 1))
+    sm.Term = 1
+    sm.becomeCandidate()
+    sm.becomeLeader()
+    for _ in range(10):
+        sm.appendEntry()
+    sm.pr(2).Match, sm.pr(2).Next = 5, 6
+    sm.pr(3).Match, sm.pr(3).Next = sm.lastIndex, sm.lastIndex + 1
+    sm.Step(Msg(abi.HB_MSG_BEAT))
+    msgs = sm.readMessages()
+    assert len(msgs) == 2
+    want = {2: min(sm.committed, 5), 3: min(sm.committed, sm.lastIndex)}
+    for m in msgs:
+        assert m.Type == abi.HB_MSG_HEARTBEAT and m.Index == 0 and m.LogTerm == 0 and m.nents == 0
+        assert m.Commit == want.pop(m.To)
+
+
+@pytest.mark.parametrize("state,wmsg", [(L, 2), (Cd, 0), (F, 0)])
+def test_recv_msg_beat(state, wmsg):  # raft/raft_test.go:1286-1328
+    sm = Raft(1, [1, 2, 3], ents=[(1, 0), (2, 1)])
+    sm.Term = 1
+    sm.r.state = state
+    sm.Step(Msg(abi.HB_MSG_BEAT, From=1, To=1))
+    msgs = sm.readMessages()
+    assert len(msgs) == wmsg
+    assert all(m.Type == abi.HB_MSG_HEARTBEAT for m in msgs)
+
+
+# ---------------------------------------------------------------- flow control
+def _leader_with_replicating_2(max_inflight=256):
+    r = Raft(1, [1, 2], max_inflight=max_inflight)
+    r.becomeCandidate()
+    r.becomeLeader()
+    p = r.pr(2)
+    p.State, p.Next = R, p.Match + 1  # pr2.becomeReplicate()
+    return r
+
+
+def test_msg_app_flow_control_full():  # raft/raft_flow_control_test.go:26-56
+    r = _leader_with_replicating_2()
+    for i in range(256):
+        r.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+        assert len(r.readMessages()) == 1
+    assert r.pr(2).ins.count == 256
+    for i in range(10):
+        r.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+        assert len(r.readMessages()) == 0
+
+
+def test_msg_app_flow_control_move_forward():  # raft/raft_flow_control_test.go:62-101
+    r = _leader_with_replicating_2()
+    for i in range(256):
+        r.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+        r.readMessages()
+    for tt in range(2, 256):
+        r.Step(Msg(abi.HB_MSG_APP_RESP, From=2, To=1, Index=tt))
+        r.readMessages()
+        r.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+        assert len(r.readMessages()) == 1
+        assert r.pr(2).ins.count == r.pr(2).ins.size
+        for i in range(tt):
+            r.Step(Msg(abi.HB_MSG_APP_RESP, From=2, To=1, Index=i))
+            assert r.pr(2).ins.count == r.pr(2).ins.size
+
+
+def test_msg_app_flow_control_recv_heartbeat():  # raft/raft_flow_control_test.go:105-155
+    r = _leader_with_replicating_2()
+    for i in range(256):
+        r.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+        r.readMessages()
+    for tt in range(1, 5):
+        assert r.pr(2).ins.count == 256
+        for i in range(tt):
+            r.Step(Msg(abi.HB_MSG_HEARTBEAT_RESP, From=2, To=1))
+            r.readMessages()
+            assert r.pr(2).ins.count < 256
+        r.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+        assert len(r.readMessages()) == 1
+        for i in range(10):
+            r.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+            assert len(r.readMessages()) == 0
+        r.Step(Msg(abi.HB_MSG_HEARTBEAT_RESP, From=2, To=1))
+        r.readMessages()
+
+
+# ---------------------------------------------------------------- snapshots
+def _snap_leader(peers):
+    # newTestRaft(1, peers) + restore(testingSnap{Index 11, Term 11, Nodes [1 2]})
+    sm = Raft(1, [1, 2], snapshot=(11, 11))
+    sm.becomeCandidate()
+    sm.becomeLeader()
+    return sm
+
+
+def test_sending_snapshot_set_pending_snapshot():  # raft/raft_snap_test.go:33-49
+    sm = _snap_leader([1])
+    sm.pr(2).Next = sm.firstIndex
+    sm.Step(Msg(abi.HB_MSG_APP_RESP, From=2, To=1, Index=sm.pr(2).Next - 1, Reject=True))
+    assert sm.pr(2).PendingSnapshot == 11
+
+
+def test_pending_snapshot_pause_replication():  # raft/raft_snap_test.go:51-66
+    sm = _snap_leader([1, 2])
+    p = sm.pr(2)
+    p.State, p.PendingSnapshot = S, 11
+    sm.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+    assert len(sm.readMessages()) == 0
+
+
+def test_snapshot_failure():  # raft/raft_snap_test.go:68-89
+    sm = _snap_leader([1, 2])
+    p = sm.pr(2)
+    p.Next = 1
+    p.State, p.PendingSnapshot = S, 11
+    sm.Step(Msg(abi.HB_MSG_SNAP_STATUS, From=2, To=1, Reject=True))
+    p = sm.pr(2)
+    assert (p.PendingSnapshot, p.Next, p.Paused) == (0, 1, 1)
+
+
+def test_snapshot_succeed():  # raft/raft_snap_test.go:91-112
+    sm = _snap_leader([1, 2])
+    p = sm.pr(2)
+    p.Next = 1
+    p.State, p.PendingSnapshot = S, 11
+    sm.Step(Msg(abi.HB_MSG_SNAP_STATUS, From=2, To=1, Reject=False))
+    p = sm.pr(2)
+    assert (p.PendingSnapshot, p.Next, p.Paused) == (0, 12, 1)
+
+
+def test_snapshot_abort():  # raft/raft_snap_test.go:114-134
+    sm = _snap_leader([1, 2])
+    p = sm.pr(2)
+    p.Next = 1
+    p.State, p.PendingSnapshot = S, 11
+    sm.Step(Msg(abi.HB_MSG_APP_RESP, From=2, To=1, Index=11))
+    p = sm.pr(2)
+    assert (p.PendingSnapshot, p.Next) == (0, 12)
+
+
+# ---------------------------------------------------------------- elections / terms
+ELECTION_TABLE = [  # raft/raft_paper_test.go:192-232
+    (1, {}, L), (3, {2: True, 3: True}, L), (3, {2: True}, L),
+    (5, {2: True, 3: True, 4: True, 5: True}, L), (5, {2: True, 3: True, 4: True}, L),
+    (5, {2: True, 3: True}, L),
+    (3, {2: False, 3: False}, F), (5, {2: False, 3: False, 4: False, 5: False}, F),
+    (5, {2: True, 3: False, 4: False, 5: False}, F),
+    (3, {}, Cd), (5, {2: True}, Cd), (5, {2: False, 3: False}, Cd), (5, {}, Cd),
+]
+
+
+@pytest.mark.parametrize("size,votes,state", ELECTION_TABLE)
+def test_leader_election_in_one_round_rpc(size, votes, state):
+    r = Raft(1, list(range(1, size + 1)))
+    r.Step(Msg(abi.HB_MSG_HUP, From=1, To=1))
+    for id_, vote in votes.items():
+        r.Step(Msg(abi.HB_MSG_VOTE_RESP, From=id_, To=1, Reject=not vote))
+    assert r.state == state
+    assert r.Term == 1
+
+
+def _commit_noop_entry(r):  # raft/raft_paper_test.go:907-925
+    r.bcastAppend()
+    for m in r.readMessages():
+        assert m.Type == abi.HB_MSG_APP and m.nents == 1
+        r.Step(Msg(abi.HB_MSG_APP_RESP, From=m.To, To=m.From, Term=m.Term, Index=m.Index + m.nents))
+    r.readMessages()
+
+
+def test_leader_commit_entry():  # raft/raft_paper_test.go:436-469
+    r = Raft(1, [1, 2, 3])
+    r.becomeCandidate()
+    r.becomeLeader()
+    _commit_noop_entry(r)
+    li = r.lastIndex
+    r.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+    for m in r.readMessages():
+        r.Step(Msg(abi.HB_MSG_APP_RESP, From=m.To, To=m.From, Term=m.Term, Index=m.Index + m.nents))
+    assert r.committed == li + 1
+    msgs = sorted(r.readMessages(), key=lambda m: m.To)
+    for i, m in enumerate(msgs):
+        assert (m.To, m.Type, m.Commit) == (i + 2, abi.HB_MSG_APP, li + 1)
+
+
+@pytest.mark.parametrize("size,acceptors,wack", [  # raft/raft_paper_test.go:474-509
+    (1, {}, True), (3, {}, False), (3, {2}, True), (3, {2, 3}, True), (5, {}, False),
+    (5, {2}, False), (5, {2, 3}, True), (5, {2, 3, 4}, True), (5, {2, 3, 4, 5}, True)])
+def test_leader_acknowledge_commit(size, acceptors, wack):
+    r = Raft(1, list(range(1, size + 1)))
+    r.becomeCandidate()
+    r.becomeLeader()
+    _commit_noop_entry(r)
+    li = r.lastIndex
+    r.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+    for m in r.readMessages():
+        if m.To in acceptors:
+            r.Step(Msg(abi.HB_MSG_APP_RESP, From=m.To, To=m.From, Term=m.Term, Index=m.Index + m.nents))
+    assert (r.committed > li) == wack
+
+
+@pytest.mark.parametrize("index,wcommit", [(1, 0), (2, 0), (3, 3)])
+def test_leader_only_commits_log_from_current_term(index, wcommit):  # raft/raft_paper_test.go:866-895
+    r = Raft(1, [1, 2], ents=[(1, 1), (2, 2)], hard=(2, 0, 0))
+    r.becomeCandidate()
+    r.becomeLeader()
+    r.readMessages()
+    r.Step(Msg(abi.HB_MSG_PROP, From=1, To=1, Entries=1))
+    r.Step(Msg(abi.HB_MSG_APP_RESP, From=2, To=1, Term=r.Term, Index=index))
+    assert r.committed == wcommit
+
+
+@pytest.mark.parametrize("state", [F, Cd, L])
+def test_update_term_from_message(state):  # raft/raft_paper_test.go:54-74
+    # The Go test steps a MsgApp (follower-side handling, off the engine path);
+    # the term gate (raft/raft.go:473-480) is type independent except for MsgVote,
+    # so a MsgHeartbeatResp exercises the same transition.
+    r = Raft(1, [1, 2, 3])
+    if state == F:
+        r.becomeFollower(1, 2)
+    elif state == Cd:
+        r.becomeCandidate()
+    else:
+        r.becomeCandidate()
+        r.becomeLeader()
+    r.Step(Msg(abi.HB_MSG_HEARTBEAT_RESP, From=2, Term=2))
+    assert (r.Term, r.state, r.lead) == (2, F, 2)
+
+
+def test_reject_stale_term_message():  # raft/raft_paper_test.go:80-94
+    r = Raft(1, [1, 2, 3], hard=(2, 0, 0))
+    r.becomeCandidate()
+    r.becomeLeader()
+    r.readMessages()
+    before = bytes(r.to_group())
+    r.Step(Msg(abi.HB_MSG_APP_RESP, From=2, Term=r.Term - 1, Index=1))
+    assert bytes(r.to_group()) == before
+    assert r.readMessages() == []
+
+
+STATE_TRANSITION = [  # raft/raft_test.go:1068-1119 (from, to, wallow, wterm, wlead)
+    (F, F, True, 1, None_), (F, Cd, True, 1, None_), (F, L, False, 0, None_),
+    (Cd, F, True, 0, None_), (Cd, Cd, True, 1, None_), (Cd, L, True, 0, 1),
+    (L, F, True, 1, None_), (L, Cd, False, 1, None_), (L, L, True, 0, 1),
+]
+
+
+@pytest.mark.parametrize("frm,to,wallow,wterm,wlead", STATE_TRANSITION)
+def test_state_transition(frm, to, wallow, wterm, wlead):
+    sm = Raft(1, [1])
+    sm.r.state = frm
+    if to == F:
+        sm.becomeFollower(wterm, wlead)
+    elif to == Cd:
+        sm.becomeCandidate()
+    else:
+        sm.becomeLeader()
+    if not wallow:
+        assert sm.fault != 0
+        return
+    assert sm.fault == 0
+    assert (sm.Term, sm.lead) == (wterm, wlead)
+
+
+@pytest.mark.parametrize("state,wstate,wterm,windex", [(F, F, 3, 0), (Cd, F, 3, 0), (L, F, 3, 1)])
+def test_all_server_stepdown(state, wstate, wterm, windex):  # raft/raft_test.go:1121-1173
+    # MsgApp is replaced by MsgAppResp (same term-gate behaviour, lead = From);
+    # MsgVote keeps lead = None.
+    for mtype, wlead in [(abi.HB_MSG_VOTE, None_), (abi.HB_MSG_APP_RESP, 2)]:
+        sm = Raft(1, [1, 2, 3])
+        if state == F:
+            sm.becomeFollower(1, None_)
+        elif state == Cd:
+            sm.becomeCandidate()
+        else:
+            sm.becomeCandidate()
+            sm.becomeLeader()
+        sm.Step(Msg(mtype, From=2, Term=3, LogTerm=3))
+        assert (sm.state, sm.Term, sm.lastIndex, sm.lead) == (wstate, wterm, windex, wlead)
+
+
+def test_multinode_start_campaign_single():  # raft/multinode_test.go:246-300 (raft-level part)
+    # CreateGroup on an empty log with peers [1]: becomeFollower(1, None), conf entry
+    # at index 1 term 1 committed; Campaign -> leader at term 2, noop at 2, commit 2.
+    r = Raft(1, [1], ents=[(1, 1)])
+    r.becomeFollower(1, None_)
+    r.r.log.committed = 1
+    r.Step(Msg(abi.HB_MSG_HUP))
+    assert (r.state, r.lead, r.Term, r.Vote, r.committed, r.lastIndex) == (L, 1, 2, 1, 2, 2)
+    r.Step(Msg(abi.HB_MSG_PROP, From=1, Entries=1))
+    assert (r.committed, r.lastIndex) == (3, 3)
