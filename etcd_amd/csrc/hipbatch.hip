@@ -1,0 +1,970 @@
+// hipbatch.hip — MI355X (gfx950) batched Raft leader-bookkeeping engine.
+//
+// One hb_step() = three phases on the handle's stream:
+//   1. partition  (k_hist, k_scan_*, k_scatter): a stable multi-split of the
+//      arrival-ordered batch by partition = group >> PART_LOG.  Each wave owns
+//      a contiguous span of messages; within a wave the rank of a message among
+//      same-partition messages comes from ballot matching, so the permuted
+//      segment of every partition keeps arrival order.
+//   2. apply      (k_apply<NMAX>): one 1024-lane workgroup per partition, one
+//      lane per raft group.  The lane loads its group's SoA state into
+//      registers once, steps the group's messages in arrival order (LDS
+//      counting sort of the staged segment), emits events through a
+//      wave-cooperative chunk allocator, and writes back only dirty fields.
+//   3. finish     (k_finish): per-workgroup statistics are reduced to one
+//      HB_STAT_COUNT vector (RCCL-reducible) and the event count is closed.
+//
+// The work is integer and HBM-bound; there is no MFMA.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "hipbatch_kernels.h"
+
+using namespace hb;
+
+#define HB_CHECK(expr)                                                       \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess) {                                                  \
+      if (getenv("HB_DEBUG"))                                                \
+        fprintf(stderr, "hipbatch: %s failed: %s (%s:%d)\n", #expr,          \
+                hipGetErrorString(_e), __FILE__, __LINE__);                  \
+      return HB_EDEVICE;                                                     \
+    }                                                                        \
+  } while (0)
+
+// ============================================================================
+// Phase 1: stable partition of the batch
+// ============================================================================
+struct BatchDev {
+  const uint32_t* group;
+  const uint32_t* info;
+  const uint64_t* term;
+  const uint64_t* index;
+  const uint64_t* hint;
+  const uint32_t* props;
+  uint64_t n;
+};
+
+struct PartArgs {
+  BatchDev b;
+  uint32_t G;        // group capacity
+  uint32_t NB;       // partitions
+  uint32_t NW;       // waves (message spans)
+  uint32_t span;     // messages per wave
+  uint32_t wpb;      // waves per block
+  uint32_t key_bits; // ceil(log2(NB))
+  uint32_t* hist;    // [NB][NW] counts, then exclusive offsets (in place)
+  // permuted batch (SoA)
+  uint32_t* p_info;  // info | (group & (PART-1)) << 16
+  uint32_t* p_orig;  // arrival index
+  uint64_t* p_term;
+  uint64_t* p_index;
+};
+
+// Per-wave histogram of partition ids over the wave's span.
+__global__ void __launch_bounds__(256) k_hist(PartArgs a) {
+  extern __shared__ uint32_t sh[];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t w = blockIdx.x * a.wpb + wave;
+  uint32_t* cnt = sh + (size_t)wave * a.NB;
+  if (wave < a.wpb)
+    for (uint32_t b = lane; b < a.NB; b += 64) cnt[b] = 0;
+  __syncthreads();
+  if (wave < a.wpb && w < a.NW) {
+    const uint64_t lo = (uint64_t)w * a.span;
+    const uint64_t hi = lo + a.span < a.b.n ? lo + a.span : a.b.n;
+    for (uint64_t i = lo + lane; i < hi; i += 64) {
+      const uint32_t gg = a.b.group[i];
+      if (gg < a.G) atomicAdd(&cnt[gg >> PART_LOG], 1u);
+    }
+  }
+  __syncthreads();
+  if (wave < a.wpb && w < a.NW)
+    for (uint32_t b = lane; b < a.NB; b += 64) a.hist[(size_t)b * a.NW + w] = cnt[b];
+}
+
+// Exclusive scan of u32 (three kernels: per-tile sums, scan of sums, rescan).
+constexpr uint32_t SCAN_TILE = 4096;  // 1024 threads x 4
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(v, d);
+    if (lane >= (uint32_t)d) v += t;
+  }
+  return v;
+}
+
+// Block-wide exclusive scan (blockDim.x = 1024); returns exclusive prefix, *total = block sum.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh16, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t incl = wave_incl_scan(v);
+  if (lane == 63) sh16[wave] = incl;
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t nw = blockDim.x >> 6;
+    uint32_t x = lane < nw ? sh16[lane] : 0;
+    x = wave_incl_scan(x);
+    if (lane < nw) sh16[lane] = x;
+  }
+  __syncthreads();
+  const uint32_t before = wave == 0 ? 0 : sh16[wave - 1];
+  *total = sh16[(blockDim.x >> 6) - 1];
+  __syncthreads();
+  return before + incl - v;
+}
+
+__global__ void __launch_bounds__(1024) k_scan_sums(const uint32_t* in, uint64_t len, uint32_t* sums) {
+  __shared__ uint32_t sh16[16];
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (base + k < len) v += in[base + k];
+  uint32_t total;
+  block_excl_scan(v, sh16, &total);
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(1024) k_scan_top(uint32_t* sums, uint32_t nsums) {
+  __shared__ uint32_t sh16[16];
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < nsums; base += 1024) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t v = i < nsums ? sums[i] : 0;
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(v, sh16, &total);
+    if (i < nsums) sums[i] = carry + ex;
+    carry += total;
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_scan_apply(uint32_t* data, uint64_t len, const uint32_t* sums,
+                                                     uint32_t NW, uint32_t NB, uint32_t* part_off,
+                                                     uint32_t total_slot) {
+  __shared__ uint32_t sh16[16];
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * 4;
+  uint32_t v[4];
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = base + k < len ? data[base + k] : 0;
+    s += v[k];
+  }
+  uint32_t total;
+  uint32_t ex = block_excl_scan(s, sh16, &total) + sums[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t i = base + k;
+    if (i < len) {
+      data[i] = ex;
+      if (i % NW == 0) part_off[i / NW] = ex;  // partition start
+    }
+    ex += v[k];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == blockDim.x - 1) part_off[NB] = ex;
+  (void)total_slot;
+}
+
+// Stable scatter: within a wave, messages of the same partition get
+// consecutive slots in arrival order (ballot match on the key bits).
+__global__ void __launch_bounds__(256) k_scatter(PartArgs a) {
+  extern __shared__ uint32_t sh[];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t w = blockIdx.x * a.wpb + wave;
+  uint32_t* cnt = sh + (size_t)wave * a.NB;
+  const bool live = wave < a.wpb && w < a.NW;
+  if (live)
+    for (uint32_t b = lane; b < a.NB; b += 64) cnt[b] = a.hist[(size_t)b * a.NW + w];
+  __syncthreads();
+  if (!live) return;
+  const uint64_t lo = (uint64_t)w * a.span;
+  const uint64_t hi = lo + a.span < a.b.n ? lo + a.span : a.b.n;
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (uint64_t base = lo; base < hi; base += 64) {
+    const uint64_t i = base + lane;
+    bool valid = i < hi;
+    const uint32_t gg = valid ? a.b.group[i] : 0u;
+    valid = valid && gg < a.G;
+    const uint32_t key = gg >> PART_LOG;
+    uint64_t peers = __ballot(valid);
+    for (uint32_t k = 0; k < a.key_bits; ++k) {
+      const bool bit = (key >> k) & 1u;
+      const uint64_t bk = __ballot(bit);
+      peers &= bit ? bk : ~bk;
+    }
+    if (valid) {
+      const uint32_t rank = (uint32_t)__popcll(peers & lt);
+      const uint32_t basepos = cnt[key];
+      const uint32_t pos = basepos + rank;
+      a.p_info[pos] = (a.b.info[i] & 0xFFFFu) | ((gg & (PART - 1)) << 16);
+      a.p_orig[pos] = (uint32_t)i;
+      a.p_term[pos] = a.b.term[i];
+      a.p_index[pos] = a.b.index[i];
+      if (rank == 0) cnt[key] = basepos + (uint32_t)__popcll(peers);
+    }
+  }
+}
+
+// ============================================================================
+// Phase 2: apply
+// ============================================================================
+struct ApplyArgs {
+  DevState S;
+  const uint32_t* p_info;
+  const uint32_t* p_orig;
+  const uint64_t* p_term;
+  const uint64_t* p_index;
+  const uint64_t* hint;     // original-order RejectHint
+  const uint32_t* props;    // dense proposals or null
+  const uint32_t* part_off; // [NB+1]
+  hb_event* ev;             // event region base
+  uint32_t ev_per_msg;      // bound on events per stepped message (EV_MAX)
+  uint32_t props_on;        // 1 if props[] is present (one proposal slot per group)
+  uint32_t* ev_counts;      // [NB] records in each chunk
+  uint64_t* ev_off;         // [NB] chunk offsets (records)
+  uint64_t* stats_part;     // [NB][HB_STAT_COUNT]
+};
+
+// stats slots reduced per workgroup
+enum { ST_MSGS, ST_APPRESP, ST_VOTERESP, ST_DROPPED, ST_COMMITS, ST_WON, ST_LOST, ST_FAULTS, ST_ENTRIES, ST_N };
+
+template <int NMAX>
+__global__ void __launch_bounds__(1024) k_apply(ApplyArgs a) {
+  __shared__ uint32_t l_info[CHUNK];
+  __shared__ uint32_t l_orig[CHUNK];
+  __shared__ uint64_t l_term[CHUNK];
+  __shared__ uint64_t l_index[CHUNK];
+  __shared__ uint16_t l_perm[CHUNK];
+  __shared__ uint32_t l_cnt[PART];
+  __shared__ uint32_t sh16[16];
+  __shared__ EvSink l_sink;
+  __shared__ uint64_t l_stats[ST_N];
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t part = blockIdx.x;
+  const uint32_t g = part * PART + tid;
+  const bool gvalid = g < a.S.G;
+
+  if (tid == 0) {
+    // Exact chunk: every event is emitted while stepping a message (or the
+    // group's proposal), at most ev_per_msg per message, so the partition's
+    // chunk is ev_per_msg x (its messages + its proposal slots).
+    const uint64_t off = (uint64_t)a.ev_per_msg * ((uint64_t)a.part_off[part] + (uint64_t)part * PART * a.props_on);
+    l_sink.chunk = a.ev + off;
+    l_sink.fill = 0;
+    a.ev_off[part] = off;
+  }
+  if (tid < ST_N) l_stats[tid] = 0;
+
+  Lane<NMAX> L;
+  L.S = a.S;
+  L.E = &l_sink;
+  L.g = g;
+  L.won = 0;
+  L.lost = 0;
+  L.dirty = 0;
+
+  // A group takes part when its slot is live (n > 0) and not faulted.
+  L.meta = gvalid ? a.S.meta[g] : 0;
+  const bool live = gvalid && m_n(L.meta) != 0 && m_fault(L.meta) == 0;
+  bool loaded = false;
+  uint64_t commit0 = 0, last0 = 0;
+  uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
+
+  __syncthreads();
+
+  const uint32_t prop_k = (a.props && live) ? a.props[g] : 0u;
+  if (prop_k) {
+    L.load();
+    loaded = true;
+    commit0 = L.committed;
+    last0 = L.last;
+    L.arrival = HB_NO_INDEX;
+    L.step(HB_MSG_PROP, L.self(), 0, prop_k, false, 0);
+  }
+
+  const uint32_t seg_lo = a.part_off[part], seg_hi = a.part_off[part + 1];
+  for (uint32_t c0 = seg_lo; c0 < seg_hi; c0 += CHUNK) {
+    const uint32_t len = (seg_hi - c0) < CHUNK ? (seg_hi - c0) : CHUNK;
+    l_cnt[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < len; i += PART) {
+      const uint32_t inf = a.p_info[c0 + i];
+      l_info[i] = inf;
+      l_orig[i] = a.p_orig[c0 + i];
+      l_term[i] = a.p_term[c0 + i];
+      l_index[i] = a.p_index[c0 + i];
+      atomicAdd(&l_cnt[inf >> 16], 1u);
+    }
+    __syncthreads();
+    const uint32_t my_cnt = l_cnt[tid];
+    uint32_t total;
+    const uint32_t my_start = block_excl_scan(my_cnt, sh16, &total);
+    l_cnt[tid] = my_start;  // becomes the fill cursor
+    __syncthreads();
+    for (uint32_t i = tid; i < len; i += PART) {
+      const uint32_t pos = atomicAdd(&l_cnt[l_info[i] >> 16], 1u);
+      l_perm[pos] = (uint16_t)i;
+    }
+    __syncthreads();
+    if (my_cnt && live) {
+      // restore arrival order inside this lane's run (tiny insertion sort)
+      for (uint32_t x = 1; x < my_cnt; ++x) {
+        const uint16_t v = l_perm[my_start + x];
+        uint32_t y = x;
+        while (y > 0 && l_perm[my_start + y - 1] > v) {
+          l_perm[my_start + y] = l_perm[my_start + y - 1];
+          --y;
+        }
+        l_perm[my_start + y] = v;
+      }
+      if (!loaded) {
+        L.load();
+        loaded = true;
+        commit0 = L.committed;
+        last0 = L.last;
+      }
+      for (uint32_t j = 0; j < my_cnt; ++j) {
+        const uint32_t i = l_perm[my_start + j];
+        const uint32_t inf = l_info[i];
+        const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
+        const bool reject = (inf >> 8) & 1u;
+        if (L.faulted()) break;
+        const bool response = type == HB_MSG_APP_RESP || type == HB_MSG_VOTE_RESP ||
+                              type == HB_MSG_HEARTBEAT_RESP || type == HB_MSG_UNREACHABLE;
+        if (from >= L.n() && response) {  // raft/multinode.go:235
+          st_drop++;
+          continue;
+        }
+        L.arrival = l_orig[i];
+        L.step(type, from, l_term[i], l_index[i], reject, (reject && a.hint) ? a.hint[l_orig[i]] : 0ull);
+        st_msgs++;
+        st_app += type == HB_MSG_APP_RESP;
+        st_vote += type == HB_MSG_VOTE_RESP;
+      }
+    }
+    __syncthreads();
+  }
+
+  uint32_t st_commit = 0, st_fault = 0;
+  uint64_t st_entries = 0;
+  if (loaded) {
+    L.store();
+    st_commit = L.committed > commit0;
+    st_fault = L.faulted() != 0;
+    st_entries = L.last - last0;
+  }
+
+  // workgroup reduction of the statistics
+  uint64_t vals[ST_N] = {st_msgs, st_app, st_vote, st_drop, st_commit, L.won, L.lost, st_fault, st_entries};
+#pragma unroll
+  for (int k = 0; k < ST_N; ++k) {
+    uint64_t v = vals[k];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    if ((tid & 63) == 0 && v) atomicAdd((unsigned long long*)&l_stats[k], (unsigned long long)v);
+  }
+  __syncthreads();
+  if (tid < ST_N) a.stats_part[(size_t)part * ST_N + tid] = l_stats[tid];
+  if (tid == 0) a.ev_counts[part] = l_sink.fill;
+  if (tid == 1) a.stats_part[(size_t)gridDim.x * ST_N + part] = l_sink.fill;  // events reserved
+}
+
+// ============================================================================
+// Phase 3: finish
+// ============================================================================
+__global__ void __launch_bounds__(1024) k_finish(const uint64_t* stats_part, uint32_t NB, uint64_t* stats) {
+  __shared__ uint64_t acc[HB_STAT_COUNT];
+  if (threadIdx.x < HB_STAT_COUNT) acc[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t v[ST_N + 1] = {};
+  for (uint32_t p = threadIdx.x; p < NB; p += blockDim.x) {
+#pragma unroll
+    for (int k = 0; k < ST_N; ++k) v[k] += stats_part[(size_t)p * ST_N + k];
+    v[ST_N] += stats_part[(size_t)NB * ST_N + p];
+  }
+  const int map[ST_N + 1] = {HB_STAT_MSGS,  HB_STAT_APPRESP, HB_STAT_VOTERESP, HB_STAT_DROPPED, HB_STAT_COMMITS,
+                             HB_STAT_WON,   HB_STAT_LOST,    HB_STAT_FAULTS,   HB_STAT_ENTRIES, HB_STAT_EVENTS};
+#pragma unroll
+  for (int k = 0; k <= ST_N; ++k) {
+    uint64_t x = v[k];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+    if ((threadIdx.x & 63) == 0 && x) atomicAdd((unsigned long long*)&acc[map[k]], (unsigned long long)x);
+  }
+  __syncthreads();
+  if (threadIdx.x < HB_STAT_COUNT) stats[threadIdx.x] = acc[threadIdx.x];
+}
+
+// ============================================================================
+// group load / gather / inflights
+// ============================================================================
+__global__ void k_load(DevState S, uint32_t first, uint32_t count, const hb_group* src) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint32_t g = first + i;
+  const hb_group& r = src[i];
+  S.term[g] = r.term;
+  S.commit[g] = r.committed;
+  S.first[g] = r.first_index;
+  S.last[g] = r.last_index;
+  S.tfirst[g] = r.term_first;
+  S.tlast[g] = r.term_last;
+  S.snap[g] = r.snap_index;
+  S.meta[g] = meta_make(r.state, r.n, r.self_slot, r.lead, r.vote, r.fault, r.votes_resp, r.votes_grant);
+  for (uint32_t s = 0; s < S.nmax; ++s) {
+    const bool on = s < r.n;
+    const size_t o = (size_t)s * S.G + g;
+    S.match[o] = on ? r.pr[s].match : 0;
+    S.next[o] = on ? r.pr[s].next : 0;
+    S.pending[o] = on ? r.pr[s].pending_snapshot : 0;
+    S.pm[o] = on ? pm_make(r.pr[s].state, r.pr[s].paused, r.pr[s].ins_start, r.pr[s].ins_count) : 0;
+  }
+}
+
+__global__ void k_gather(DevState S, uint32_t first, uint32_t count, hb_group* dst) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint32_t g = first + i;
+  hb_group r;
+  memset(&r, 0, sizeof(r));
+  const uint64_t m = S.meta[g];
+  r.term = S.term[g];
+  r.committed = S.commit[g];
+  r.first_index = S.first[g];
+  r.last_index = S.last[g];
+  r.term_first = S.tfirst[g];
+  r.term_last = S.tlast[g];
+  r.snap_index = S.snap[g];
+  r.state = m_state(m);
+  r.n = m_n(m);
+  r.self_slot = m_self(m);
+  r.lead = m_lead(m);
+  r.vote = m_vote(m);
+  r.fault = m_fault(m);
+  r.votes_resp = m_resp(m);
+  r.votes_grant = m_grant(m);
+  for (uint32_t s = 0; s < S.nmax && s < r.n; ++s) {
+    const size_t o = (size_t)s * S.G + g;
+    const uint32_t p = S.pm[o];
+    r.pr[s].match = S.match[o];
+    r.pr[s].next = S.next[o];
+    r.pr[s].state = pm_state(p);
+    r.pr[s].paused = pm_paused(p);
+    r.pr[s].ins_start = pm_start(p);
+    r.pr[s].ins_count = pm_count(p);
+    r.pr[s].pending_snapshot = pm_state(p) == HB_PR_SNAPSHOT ? S.pending[o] : 0;
+  }
+  dst[i] = r;
+}
+
+__global__ void k_remove(DevState S, uint32_t first, uint32_t count) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) S.meta[first + i] = 0;
+}
+
+__global__ void k_set_ins(DevState S, uint32_t g, uint32_t s, uint32_t start, uint32_t count, const uint64_t* vals) {
+  for (uint32_t i = threadIdx.x; i < count; i += blockDim.x) {
+    uint32_t idx = start + i;
+    if (idx >= S.W) idx -= S.W;
+    S.ring[((size_t)s * S.W + idx) * S.G + g] = vals[i];
+  }
+  if (threadIdx.x == 0) {
+    const size_t o = (size_t)s * S.G + g;
+    const uint32_t p = S.pm[o];
+    S.pm[o] = pm_make(pm_state(p), pm_paused(p), start, count);
+  }
+}
+
+__global__ void k_get_ins(DevState S, uint32_t g, uint32_t s, uint64_t* vals, uint32_t* sc) {
+  const size_t o = (size_t)s * S.G + g;
+  const uint32_t p = S.pm[o];
+  const uint32_t start = pm_start(p), count = pm_count(p);
+  for (uint32_t i = threadIdx.x; i < count; i += blockDim.x) {
+    uint32_t idx = start + i;
+    if (idx >= S.W) idx -= S.W;
+    vals[i] = S.ring[((size_t)s * S.W + idx) * S.G + g];
+  }
+  if (threadIdx.x == 0) {
+    sc[0] = start;
+    sc[1] = count;
+  }
+}
+
+// Dense gather of the chunked events (chunk c at base + c*cap, counts[c]).
+__global__ void __launch_bounds__(256) k_gather_events(const hb_event* base, const uint32_t* counts,
+                                                       const uint64_t* offs, hb_event* out) {
+  __shared__ uint64_t s_off;
+  const uint32_t c = blockIdx.x;
+  if (threadIdx.x == 0) {
+    uint64_t off = 0;
+    for (uint32_t k = 0; k < c; ++k) off += counts[k];
+    s_off = off;
+  }
+  __syncthreads();
+  const uint32_t cnt = counts[c];
+  const hb_event* src = base + offs[c];
+  for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) out[s_off + i] = src[i];
+}
+
+// ============================================================================
+// host side
+// ============================================================================
+struct hb_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint32_t G = 0, nmax = 0, W = 0, NB = 0;
+  uint64_t max_msg_size = 0, max_batch = 0;
+  DevState st{};
+  std::vector<void*> allocs;
+  // partition scratch
+  uint32_t* hist = nullptr;
+  uint64_t hist_cap = 0;
+  uint32_t* scan_sums = nullptr;
+  uint32_t* part_off = nullptr;
+  uint32_t* p_info = nullptr;
+  uint32_t* p_orig = nullptr;
+  uint64_t* p_term = nullptr;
+  uint64_t* p_index = nullptr;
+  // host-pointer staging
+  uint32_t* s_group = nullptr;
+  uint32_t* s_info = nullptr;
+  uint32_t* s_props = nullptr;
+  uint64_t* s_term = nullptr;
+  uint64_t* s_index = nullptr;
+  uint64_t* s_hint = nullptr;
+  // events
+  hb_event* ev = nullptr;
+  uint64_t ev_region = 0;  // records
+  uint32_t ev_per_msg = 0;
+  uint32_t* ev_counts = nullptr;  // [NB]
+  uint64_t* ev_off = nullptr;     // [NB]
+  uint64_t* stats_part = nullptr;
+  uint64_t* stats = nullptr;
+  hipEvent_t ph[HB_PHASE_COUNT + 1] = {};
+  bool profiled = false;
+  bool stepped = false;
+};
+
+namespace {
+
+int dalloc(hb_handle* h, void** p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (hipMalloc(p, bytes) != hipSuccess) return HB_ENOMEM;
+  h->allocs.push_back(*p);
+  return HB_OK;
+}
+
+template <class T>
+int dalloc_t(hb_handle* h, T** p, size_t count) {
+  return dalloc(h, reinterpret_cast<void**>(p), count * sizeof(T));
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+uint32_t ceil_log2(uint32_t x) {
+  uint32_t b = 0;
+  while ((1u << b) < x) ++b;
+  return b;
+}
+
+template <int NMAX>
+void launch_apply(hb_handle* h, const ApplyArgs& a) {
+  hipLaunchKernelGGL(k_apply<NMAX>, dim3(h->NB), dim3(PART), 0, h->stream, a);
+}
+
+}  // namespace
+
+extern "C" {
+
+int hb_abi_version(void) { return HB_ABI_VERSION; }
+
+const char* hb_strerror(int code) {
+  switch (code) {
+    case HB_OK: return "ok";
+    case HB_EINVAL: return "invalid argument";
+    case HB_ENOMEM: return "out of memory";
+    case HB_EDEVICE: return "device error";
+    case HB_EINVARIANT: return "device invariant violated";
+    default: return "unknown error";
+  }
+}
+
+int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max_inflight,
+              uint64_t max_msg_size, uint64_t max_batch, hb_handle** out) {
+  if (!out || capacity == 0 || max_replicas < 1 || max_replicas > HB_MAX_REPLICAS || max_inflight < 1 ||
+      max_inflight > HB_MAX_INFLIGHT || (max_msg_size != 0 && max_msg_size != HB_NO_LIMIT) ||
+      max_batch >= (1ull << 31) || capacity > (1u << 24))
+    return HB_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return HB_EDEVICE;
+  DeviceGuard guard(device);
+  hb_handle* h = new hb_handle();
+  h->device = device;
+  h->G = capacity;
+  h->nmax = max_replicas <= 3 ? 3 : (max_replicas <= 5 ? 5 : 7);
+  h->W = max_inflight;
+  h->max_msg_size = max_msg_size;
+  h->max_batch = max_batch;
+  h->NB = (capacity + PART - 1) / PART;
+  const size_t G = capacity, R = h->nmax;
+  DevState& s = h->st;
+  s.G = capacity;
+  s.W = max_inflight;
+  s.nmax = h->nmax;
+  s.max_msg_size = max_msg_size;
+  int rc = HB_OK;
+#define ALLOC(ptr, count) \
+  if (rc == HB_OK) rc = dalloc_t(h, &(ptr), (count))
+  ALLOC(s.term, G);
+  ALLOC(s.commit, G);
+  ALLOC(s.first, G);
+  ALLOC(s.last, G);
+  ALLOC(s.tfirst, G);
+  ALLOC(s.tlast, G);
+  ALLOC(s.snap, G);
+  ALLOC(s.meta, G);
+  ALLOC(s.match, R * G);
+  ALLOC(s.next, R * G);
+  ALLOC(s.pending, R * G);
+  ALLOC(s.pm, R * G);
+  ALLOC(s.ring, R * (size_t)max_inflight * G);
+  // partition scratch: hist budget ~ max(batch, 1M) entries
+  h->hist_cap = std::max<uint64_t>(max_batch, 1u << 20) + (uint64_t)h->NB * 64;
+  ALLOC(h->hist, h->hist_cap);
+  ALLOC(h->scan_sums, h->hist_cap / SCAN_TILE + 2);
+  ALLOC(h->part_off, h->NB + 1);
+  const size_t mb = max_batch ? max_batch : 1;
+  ALLOC(h->p_info, mb);
+  ALLOC(h->p_orig, mb);
+  ALLOC(h->p_term, mb);
+  ALLOC(h->p_index, mb);
+  ALLOC(h->s_group, mb);
+  ALLOC(h->s_info, mb);
+  ALLOC(h->s_term, mb);
+  ALLOC(h->s_index, mb);
+  ALLOC(h->s_hint, mb);
+  ALLOC(h->s_props, G);
+  // events: (batch + one proposal slot per group) x EV_MAX (exact bound)
+  h->ev_per_msg = h->nmax + 4;
+  h->ev_region = (mb + (uint64_t)h->NB * PART) * h->ev_per_msg;
+  ALLOC(h->ev, h->ev_region);
+  ALLOC(h->ev_counts, h->NB);
+  ALLOC(h->ev_off, h->NB);
+  ALLOC(h->stats_part, (size_t)h->NB * (ST_N + 1) + 16);
+  ALLOC(h->stats, HB_STAT_COUNT);
+#undef ALLOC
+  if (rc != HB_OK) {
+    hb_destroy(h);
+    return rc;
+  }
+  for (auto& e : h->ph)
+    if (hipEventCreate(&e) != hipSuccess) {
+      hb_destroy(h);
+      return HB_EDEVICE;
+    }
+  // empty slots (n = 0), zeroed progress
+  if (hipMemset(s.meta, 0, G * 8) != hipSuccess || hipMemset(s.pm, 0, R * G * 4) != hipSuccess ||
+      hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess ||
+      hipMemset(h->ev_counts, 0, h->NB * 4ull) != hipSuccess || hipMemset(h->ev_off, 0, h->NB * 8ull) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    hb_destroy(h);
+    return HB_EDEVICE;
+  }
+  *out = h;
+  return HB_OK;
+}
+
+int hb_destroy(hb_handle* h) {
+  if (!h) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  (void)hipDeviceSynchronize();
+  for (void* p : h->allocs) (void)hipFree(p);
+  for (auto& e : h->ph)
+    if (e) (void)hipEventDestroy(e);
+  delete h;
+  return HB_OK;
+}
+
+int hb_set_stream(hb_handle* h, void* stream) {
+  if (!h) return HB_EINVAL;
+  h->stream = reinterpret_cast<hipStream_t>(stream);
+  return HB_OK;
+}
+
+int hb_sync(hb_handle* h) {
+  if (!h) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  HB_CHECK(hipStreamSynchronize(h->stream));
+  return HB_OK;
+}
+
+static bool valid_ref(uint32_t r, uint32_t n) {
+  return r < n || r == HB_REF_OTHER || r == HB_REF_SELF || r == HB_REF_NONE;
+}
+
+int hb_load_groups(hb_handle* h, uint32_t first, uint32_t count, const hb_group* groups) {
+  if (!h || !groups || (uint64_t)first + count > h->G) return HB_EINVAL;
+  if (count == 0) return HB_OK;
+  for (uint32_t i = 0; i < count; ++i) {
+    const hb_group& r = groups[i];
+    if (r.n < 1 || r.n > h->nmax || r.state > 2 || r.fault > 15) return HB_EINVAL;
+    if (!(r.self_slot < r.n || r.self_slot == HB_SLOT_NONE)) return HB_EINVAL;
+    if (!valid_ref(r.lead, r.n) || !valid_ref(r.vote, r.n)) return HB_EINVAL;
+    if (r.first_index == 0 || r.last_index + 1 < r.first_index) return HB_EINVAL;
+    if (r.term_first != HB_NO_INDEX &&
+        (r.term_first > r.term_last || r.term_first + 1 < r.first_index || r.term_last > r.last_index))
+      return HB_EINVAL;
+    if ((r.votes_resp | r.votes_grant) > 0xFF || (r.votes_grant & ~r.votes_resp)) return HB_EINVAL;
+    for (uint32_t s = 0; s < r.n; ++s) {
+      const hb_progress& p = r.pr[s];
+      if (p.state > 2 || p.paused > 1 || p.ins_start >= h->W || p.ins_count > h->W) return HB_EINVAL;
+    }
+  }
+  DeviceGuard guard(h->device);
+  hb_group* d = nullptr;
+  HB_CHECK(hipMalloc(&d, sizeof(hb_group) * count));
+  hipError_t e = hipMemcpyAsync(d, groups, sizeof(hb_group) * count, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_load, dim3((count + 255) / 256), dim3(256), 0, h->stream, h->st, first, count, d);
+    e = hipStreamSynchronize(h->stream);
+  }
+  (void)hipFree(d);
+  return e == hipSuccess ? HB_OK : HB_EDEVICE;
+}
+
+int hb_get_groups(hb_handle* h, uint32_t first, uint32_t count, hb_group* out) {
+  if (!h || !out || (uint64_t)first + count > h->G) return HB_EINVAL;
+  if (count == 0) return HB_OK;
+  DeviceGuard guard(h->device);
+  hb_group* d = nullptr;
+  HB_CHECK(hipMalloc(&d, sizeof(hb_group) * count));
+  hipLaunchKernelGGL(k_gather, dim3((count + 255) / 256), dim3(256), 0, h->stream, h->st, first, count, d);
+  hipError_t e = hipMemcpyAsync(out, d, sizeof(hb_group) * count, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  return e == hipSuccess ? HB_OK : HB_EDEVICE;
+}
+
+int hb_remove_groups(hb_handle* h, uint32_t first, uint32_t count) {
+  if (!h || (uint64_t)first + count > h->G) return HB_EINVAL;
+  if (count == 0) return HB_OK;
+  DeviceGuard guard(h->device);
+  hipLaunchKernelGGL(k_remove, dim3((count + 255) / 256), dim3(256), 0, h->stream, h->st, first, count);
+  HB_CHECK(hipStreamSynchronize(h->stream));
+  return HB_OK;
+}
+
+int hb_set_inflights(hb_handle* h, uint32_t group, uint32_t slot, uint32_t start, uint32_t count,
+                     const uint64_t* vals) {
+  if (!h || group >= h->G || slot >= h->nmax || start >= h->W || count > h->W || (count && !vals))
+    return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  uint64_t* d = nullptr;
+  HB_CHECK(hipMalloc(&d, 8ull * (count ? count : 1)));
+  hipError_t e = hipSuccess;
+  if (count) e = hipMemcpyAsync(d, vals, 8ull * count, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_set_ins, dim3(1), dim3(256), 0, h->stream, h->st, group, slot, start, count, d);
+    e = hipStreamSynchronize(h->stream);
+  }
+  (void)hipFree(d);
+  return e == hipSuccess ? HB_OK : HB_EDEVICE;
+}
+
+int hb_get_inflights(hb_handle* h, uint32_t group, uint32_t slot, uint32_t* start, uint32_t* count,
+                     uint64_t* vals) {
+  if (!h || group >= h->G || slot >= h->nmax || !start || !count || !vals) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  uint64_t* d = nullptr;
+  uint32_t* sc = nullptr;
+  HB_CHECK(hipMalloc(&d, 8ull * h->W));
+  if (hipMalloc(&sc, 8) != hipSuccess) {
+    (void)hipFree(d);
+    return HB_EDEVICE;
+  }
+  hipLaunchKernelGGL(k_get_ins, dim3(1), dim3(256), 0, h->stream, h->st, group, slot, d, sc);
+  uint32_t hsc[2] = {0, 0};
+  hipError_t e = hipMemcpyAsync(hsc, sc, 8, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e == hipSuccess && hsc[1]) e = hipMemcpy(vals, d, 8ull * hsc[1], hipMemcpyDeviceToHost);
+  *start = hsc[0];
+  *count = hsc[1];
+  (void)hipFree(d);
+  (void)hipFree(sc);
+  return e == hipSuccess ? HB_OK : HB_EDEVICE;
+}
+
+int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
+  if (!h || !b || b->n > h->max_batch) return HB_EINVAL;
+  if (b->n && (!b->group || !b->info || !b->term || !b->index)) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  hipStream_t st = h->stream;
+  const bool prof = (flags & HB_STEP_PROFILE) != 0;
+  BatchDev bd{b->group, b->info, b->term, b->index, b->hint, b->props, b->n};
+  if (flags & HB_STEP_HOST_PTRS) {
+    const size_t n = b->n;
+    if (n) {
+      HB_CHECK(hipMemcpyAsync(h->s_group, b->group, n * 4, hipMemcpyHostToDevice, st));
+      HB_CHECK(hipMemcpyAsync(h->s_info, b->info, n * 4, hipMemcpyHostToDevice, st));
+      HB_CHECK(hipMemcpyAsync(h->s_term, b->term, n * 8, hipMemcpyHostToDevice, st));
+      HB_CHECK(hipMemcpyAsync(h->s_index, b->index, n * 8, hipMemcpyHostToDevice, st));
+      if (b->hint) HB_CHECK(hipMemcpyAsync(h->s_hint, b->hint, n * 8, hipMemcpyHostToDevice, st));
+    }
+    if (b->props) HB_CHECK(hipMemcpyAsync(h->s_props, b->props, (size_t)h->G * 4, hipMemcpyHostToDevice, st));
+    bd.group = h->s_group;
+    bd.info = h->s_info;
+    bd.term = h->s_term;
+    bd.index = h->s_index;
+    bd.hint = b->hint ? h->s_hint : nullptr;
+    bd.props = b->props ? h->s_props : nullptr;
+  }
+  if (prof) HB_CHECK(hipEventRecord(h->ph[0], st));
+
+  // ---- phase 1: partition ----------------------------------------------------
+  const uint32_t NB = h->NB;
+  if (b->n == 0) {
+    HB_CHECK(hipMemsetAsync(h->part_off, 0, (NB + 1) * 4ull, st));
+  } else {
+    const uint32_t wpb_max = NB * 4u <= 16384u ? 4u : (NB * 4u <= 32768u ? 2u : 1u);
+    if ((uint64_t)NB * 4u > 65536u) return HB_EINVAL;  // > 16384 partitions: not supported
+    // waves so that NB * NW fits the histogram budget and spans are >= 256 messages
+    uint64_t nw_budget = (h->hist_cap - 64) / NB;
+    uint64_t nw_target = std::min<uint64_t>(std::max<uint64_t>(nw_budget, 1), 4096);
+    uint64_t span = (b->n + nw_target - 1) / nw_target;
+    span = std::max<uint64_t>(256, (span + 63) / 64 * 64);
+    const uint32_t NW = (uint32_t)((b->n + span - 1) / span);
+    if ((uint64_t)NB * NW > h->hist_cap) return HB_EINVAL;
+    PartArgs pa;
+    pa.b = bd;
+    pa.G = h->G;
+    pa.NB = NB;
+    pa.NW = NW;
+    pa.span = (uint32_t)span;
+    pa.wpb = wpb_max;
+    pa.key_bits = ceil_log2(NB);
+    pa.hist = h->hist;
+    pa.p_info = h->p_info;
+    pa.p_orig = h->p_orig;
+    pa.p_term = h->p_term;
+    pa.p_index = h->p_index;
+    const uint32_t blocks = (NW + pa.wpb - 1) / pa.wpb;
+    const size_t shm = (size_t)pa.wpb * NB * 4;
+    hipLaunchKernelGGL(k_hist, dim3(blocks), dim3(256), shm, st, pa);
+    const uint64_t len = (uint64_t)NB * NW;
+    const uint32_t tiles = (uint32_t)((len + SCAN_TILE - 1) / SCAN_TILE);
+    hipLaunchKernelGGL(k_scan_sums, dim3(tiles), dim3(1024), 0, st, h->hist, len, h->scan_sums);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, st, h->scan_sums, tiles);
+    hipLaunchKernelGGL(k_scan_apply, dim3(tiles), dim3(1024), 0, st, h->hist, len, h->scan_sums, NW, NB,
+                       h->part_off, 0u);
+    hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(256), shm, st, pa);
+  }
+  if (prof) HB_CHECK(hipEventRecord(h->ph[1], st));
+
+  // ---- phase 2: apply ----------------------------------------------------------
+  ApplyArgs aa;
+  aa.S = h->st;
+  aa.p_info = h->p_info;
+  aa.p_orig = h->p_orig;
+  aa.p_term = h->p_term;
+  aa.p_index = h->p_index;
+  aa.hint = bd.hint;
+  aa.props = bd.props;
+  aa.part_off = h->part_off;
+  aa.ev = h->ev;
+  aa.ev_per_msg = h->ev_per_msg;
+  aa.props_on = bd.props ? 1u : 0u;
+  aa.ev_counts = h->ev_counts;
+  aa.ev_off = h->ev_off;
+  aa.stats_part = h->stats_part;
+  switch (h->nmax) {
+    case 3: launch_apply<3>(h, aa); break;
+    case 5: launch_apply<5>(h, aa); break;
+    default: launch_apply<7>(h, aa); break;
+  }
+  if (prof) HB_CHECK(hipEventRecord(h->ph[2], st));
+  // ---- phase 3: finish -----------------------------------------------------------
+  hipLaunchKernelGGL(k_finish, dim3(1), dim3(1024), 0, st, h->stats_part, NB, h->stats);
+  if (prof) HB_CHECK(hipEventRecord(h->ph[3], st));
+  HB_CHECK(hipGetLastError());
+  h->profiled = prof;
+  h->stepped = true;
+  return HB_OK;
+}
+
+int hb_events_device(hb_handle* h, const hb_event** base, const uint64_t** chunk_off, const uint32_t** counts,
+                     uint32_t* n_chunks) {
+  if (!h || !base || !chunk_off || !counts || !n_chunks) return HB_EINVAL;
+  *base = h->ev;
+  *chunk_off = h->ev_off;
+  *counts = h->ev_counts;
+  *n_chunks = h->NB;
+  return HB_OK;
+}
+
+int hb_copy_events(hb_handle* h, hb_event* out, uint64_t cap, uint64_t* n) {
+  if (!h || !n) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  uint64_t stats[HB_STAT_COUNT];
+  HB_CHECK(hipMemcpyAsync(stats, h->stats, sizeof(stats), hipMemcpyDeviceToHost, h->stream));
+  HB_CHECK(hipStreamSynchronize(h->stream));
+  const uint64_t total = h->stepped ? stats[HB_STAT_EVENTS] : 0;
+  *n = total;
+  if (total == 0) return HB_OK;
+  if (!out || cap < total) return HB_EINVAL;
+  hb_event* d = nullptr;
+  HB_CHECK(hipMalloc(&d, total * sizeof(hb_event)));
+  hipLaunchKernelGGL(k_gather_events, dim3(h->NB), dim3(256), 0, h->stream, h->ev, h->ev_counts, h->ev_off, d);
+  hipError_t e = hipMemcpyAsync(out, d, total * sizeof(hb_event), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d);
+  return e == hipSuccess ? HB_OK : HB_EDEVICE;
+}
+
+int hb_stats_device(hb_handle* h, uint64_t** dev_stats) {
+  if (!h || !dev_stats) return HB_EINVAL;
+  *dev_stats = h->stats;
+  return HB_OK;
+}
+
+int hb_stats(hb_handle* h, uint64_t* out) {
+  if (!h || !out) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  HB_CHECK(hipMemcpyAsync(out, h->stats, HB_STAT_COUNT * 8, hipMemcpyDeviceToHost, h->stream));
+  HB_CHECK(hipStreamSynchronize(h->stream));
+  return HB_OK;
+}
+
+int hb_phase_ms(hb_handle* h, float* out) {
+  if (!h || !out || !h->profiled) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  HB_CHECK(hipEventSynchronize(h->ph[HB_PHASE_COUNT]));
+  for (int i = 0; i < HB_PHASE_COUNT; ++i) HB_CHECK(hipEventElapsedTime(&out[i], h->ph[i], h->ph[i + 1]));
+  return HB_OK;
+}
+
+int hb_alloc_pinned(size_t bytes, void** out) {
+  if (!out) return HB_EINVAL;
+  return hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? HB_OK : HB_ENOMEM;
+}
+
+int hb_free_pinned(void* p) { return hipHostFree(p) == hipSuccess ? HB_OK : HB_EDEVICE; }
+
+}  // extern "C"

@@ -1,0 +1,646 @@
+// hipbatch_kernels.h — device-side layout and per-group logic of the engine.
+//
+// Group state lives in HBM as structure-of-arrays (one array per field, group
+// index fastest) so that a wave of 64 lanes, one lane per group, reads every
+// field with one coalesced 256/512-byte access.  Per-peer progress is
+// replica-major ([slot][group]) for the same reason; the inflight rings are
+// [slot][ring index][group] so that lanes whose rings advance in lockstep
+// (steady-state replication) touch adjacent words.
+//
+// The per-group logic below is the device restatement of the reference's
+// leader bookkeeping; each function cites the Go it mirrors and the oracle
+// (oracle/raft_oracle.c) restates the same lines sequentially.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hipbatch.h"
+
+namespace hb {
+
+constexpr int PART_LOG = 10;                 // groups per partition = apply workgroup
+constexpr uint32_t PART = 1u << PART_LOG;    // 1024 lanes, one group each
+constexpr uint32_t CHUNK = 2048;             // messages staged in LDS per round
+
+// ---- packed group meta (u64) ------------------------------------------------
+//  [0:2) state  [2:5) n  [5:9) self slot  [9:13) lead ref  [13:17) vote ref
+//  [17:21) fault  [24:32) votes responded  [32:40) votes granted
+__host__ __device__ inline uint64_t meta_make(uint32_t state, uint32_t n, uint32_t self, uint32_t lead,
+                                              uint32_t vote, uint32_t fault, uint32_t resp, uint32_t grant) {
+  return (uint64_t)(state & 3) | ((uint64_t)(n & 7) << 2) | ((uint64_t)(self & 0xF) << 5) |
+         ((uint64_t)(lead & 0xF) << 9) | ((uint64_t)(vote & 0xF) << 13) | ((uint64_t)(fault & 0xF) << 17) |
+         ((uint64_t)(resp & 0xFF) << 24) | ((uint64_t)(grant & 0xFF) << 32);
+}
+__host__ __device__ inline uint32_t m_state(uint64_t m) { return (uint32_t)(m & 3); }
+__host__ __device__ inline uint32_t m_n(uint64_t m) { return (uint32_t)((m >> 2) & 7); }
+__host__ __device__ inline uint32_t m_self(uint64_t m) { return (uint32_t)((m >> 5) & 0xF); }
+__host__ __device__ inline uint32_t m_lead(uint64_t m) { return (uint32_t)((m >> 9) & 0xF); }
+__host__ __device__ inline uint32_t m_vote(uint64_t m) { return (uint32_t)((m >> 13) & 0xF); }
+__host__ __device__ inline uint32_t m_fault(uint64_t m) { return (uint32_t)((m >> 17) & 0xF); }
+__host__ __device__ inline uint32_t m_resp(uint64_t m) { return (uint32_t)((m >> 24) & 0xFF); }
+__host__ __device__ inline uint32_t m_grant(uint64_t m) { return (uint32_t)((m >> 32) & 0xFF); }
+
+// ---- packed progress meta (u32) ----------------------------------------------
+//  [0:2) ProgressState  [2] Paused  [3:13) inflights.start  [13:24) inflights.count
+__host__ __device__ inline uint32_t pm_make(uint32_t st, uint32_t paused, uint32_t start, uint32_t count) {
+  return (st & 3) | ((paused & 1) << 2) | ((start & 0x3FF) << 3) | ((count & 0x7FF) << 13);
+}
+__host__ __device__ inline uint32_t pm_state(uint32_t p) { return p & 3; }
+__host__ __device__ inline uint32_t pm_paused(uint32_t p) { return (p >> 2) & 1; }
+__host__ __device__ inline uint32_t pm_start(uint32_t p) { return (p >> 3) & 0x3FF; }
+__host__ __device__ inline uint32_t pm_count(uint32_t p) { return (p >> 13) & 0x7FF; }
+constexpr uint32_t PM_PAUSED = 1u << 2;
+
+// ---- device state (SoA in HBM) -------------------------------------------------
+struct DevState {
+  uint32_t G;                 // group capacity
+  uint32_t W;                 // MaxInflightMsgs
+  uint32_t nmax;              // max replicas of this handle
+  uint32_t pad;
+  uint64_t max_msg_size;      // HB_NO_LIMIT or 0
+  uint64_t* term;             // [G] HardState.Term
+  uint64_t* commit;           // [G] raftLog.committed
+  uint64_t* first;            // [G] raftLog.firstIndex()
+  uint64_t* last;             // [G] raftLog.lastIndex()
+  uint64_t* tfirst;           // [G] first index of the current-term run
+  uint64_t* tlast;            // [G] last index of the current-term run
+  uint64_t* snap;             // [G] snapshot index (read only for MsgSnap)
+  uint64_t* meta;             // [G] packed meta
+  uint64_t* match;            // [nmax][G]
+  uint64_t* next;             // [nmax][G]
+  uint64_t* pending;          // [nmax][G] PendingSnapshot (valid in Snapshot state)
+  uint32_t* pm;               // [nmax][G] packed progress meta
+  uint64_t* ring;             // [nmax][W][G] inflight ring
+};
+
+// ---- event sink ---------------------------------------------------------------
+// The sink of the apply workgroup lives in LDS so that emit() needs no
+// per-lane state: the kernel fills g_sink once, emit() reads it.
+struct EvSink {
+  hb_event* chunk;            // this workgroup's chunk
+  uint32_t fill;              // records written by the workgroup
+  uint32_t pad;
+};
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a > b ? b : a; }
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ void store_event(hb_event* dst, uint32_t group, uint32_t tta, uint64_t x) {
+  uint4 v;
+  v.x = (uint32_t)x;
+  v.y = (uint32_t)(x >> 32);
+  v.z = group;
+  v.w = tta;
+  *reinterpret_cast<uint4*>(dst) = v;
+}
+
+__host__ __device__ constexpr uint32_t tta(uint32_t type, uint32_t to, uint32_t aux) {
+  return (type & 0xFF) | ((to & 0xFF) << 8) | ((aux & 0xFFFF) << 16);
+}
+
+// Append one 16-byte record to the workgroup's chunk.  The chunk is sized
+// from the partition's exact message count (events per message are bounded),
+// so it never overflows.  One LDS atomic per active lane; the compiler's
+// atomic optimizer turns it into one ds_add per wave plus mbcnt, and the
+// lanes of a wave write side by side.  A lane's records keep their order.
+__device__ __forceinline__ void emit_ev(EvSink* sink, uint32_t group, uint32_t ttav, uint64_t x) {
+  const uint32_t pos = atomicAdd(&sink->fill, 1u);
+  store_event(sink->chunk + pos, group, ttav, x);
+}
+
+template <int N>
+__device__ __forceinline__ uint64_t sel64(const uint64_t (&a)[N], uint32_t s) {
+  uint64_t v = a[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) v = (s == (uint32_t)i) ? a[i] : v;
+  return v;
+}
+template <int N>
+__device__ __forceinline__ uint32_t sel32(const uint32_t (&a)[N], uint32_t s) {
+  uint32_t v = a[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) v = (s == (uint32_t)i) ? a[i] : v;
+  return v;
+}
+
+// dirty bits
+constexpr uint32_t D_META = 1u << 0;
+constexpr uint32_t D_TERM = 1u << 1;
+constexpr uint32_t D_COMMIT = 1u << 2;
+constexpr uint32_t D_LAST = 1u << 3;
+constexpr uint32_t D_TRUN = 1u << 4;
+constexpr uint32_t D_SLOT0 = 8;  // bit D_SLOT0 + s: slot s (match, next, pm)
+
+struct Pr {
+  uint64_t match, next;
+  uint32_t pm;
+};
+
+// Per-slot state is held in vector registers: a runtime slot index becomes a
+// register-indexed extract/insert instead of a private-memory array access
+// (which would push the whole lane state to scratch).
+template <int NMAX> struct SlotVec;
+template <> struct SlotVec<3> {
+  typedef uint64_t u64 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32 __attribute__((ext_vector_type(4)));
+};
+template <> struct SlotVec<5> {
+  typedef uint64_t u64 __attribute__((ext_vector_type(8)));
+  typedef uint32_t u32 __attribute__((ext_vector_type(8)));
+};
+template <> struct SlotVec<7> {
+  typedef uint64_t u64 __attribute__((ext_vector_type(8)));
+  typedef uint32_t u32 __attribute__((ext_vector_type(8)));
+};
+
+// One lane = one raft group.  All state of the group is held in registers
+// between load() and store().
+template <int NMAX>
+struct Lane {
+  DevState S;
+  EvSink* E;  // LDS
+  uint32_t g;
+  uint64_t arrival;
+  uint64_t term, committed, first, last, tfirst, tlast, meta;
+  typename SlotVec<NMAX>::u64 match, next;
+  typename SlotVec<NMAX>::u32 pm;
+  uint32_t dirty;
+  uint32_t won, lost;
+
+  // ---------------------------------------------------------------- meta
+  __device__ __forceinline__ uint32_t n() const { return m_n(meta); }
+  __device__ __forceinline__ uint32_t state() const { return m_state(meta); }
+  __device__ __forceinline__ uint32_t self() const { return m_self(meta); }
+  __device__ __forceinline__ uint32_t lead() const { return m_lead(meta); }
+  __device__ __forceinline__ uint32_t vote() const { return m_vote(meta); }
+  __device__ __forceinline__ uint32_t faulted() const { return m_fault(meta); }
+  __device__ __forceinline__ uint32_t self_ref() const { return self() == HB_SLOT_NONE ? HB_REF_SELF : self(); }
+  __device__ __forceinline__ uint64_t soft() const {
+    return (uint64_t)state() | ((uint64_t)lead() << 8) | ((uint64_t)vote() << 16);
+  }
+  __device__ __forceinline__ void set_field(int shift, uint64_t mask, uint64_t v) {
+    meta = (meta & ~(mask << shift)) | ((v & mask) << shift);
+    dirty |= D_META;
+  }
+  __device__ __forceinline__ void set_state(uint32_t v) { set_field(0, 3, v); }
+  __device__ __forceinline__ void set_lead(uint32_t v) { set_field(9, 0xF, v); }
+  __device__ __forceinline__ void set_vote(uint32_t v) { set_field(13, 0xF, v); }
+  __device__ __forceinline__ void set_votes(uint32_t resp, uint32_t grant) {
+    set_field(24, 0xFF, resp);
+    set_field(32, 0xFF, grant);
+  }
+
+  __device__ __forceinline__ void ev(uint32_t type, uint32_t to, uint32_t aux, uint64_t x) {
+    emit_ev(E, g, tta(type, to, aux), x);
+  }
+  // A reference panic: the group stops; the FAULT event is emitted once, at
+  // the end of the message (nothing else is emitted after a fault).
+  __device__ __forceinline__ void fault(uint32_t code) {
+    if (faulted()) return;
+    set_field(17, 0xF, code);
+  }
+
+  // ---------------------------------------------------------------- memory
+  __device__ __forceinline__ uint64_t* ring_at(uint32_t s, uint32_t idx) const {
+    return S.ring + ((size_t)s * S.W + idx) * S.G + g;
+  }
+  __device__ __forceinline__ Pr get(uint32_t s) const {
+    Pr p;
+    p.match = match[s];
+    p.next = next[s];
+    p.pm = pm[s];
+    return p;
+  }
+  __device__ __forceinline__ void put(uint32_t s, const Pr& p) {
+    match[s] = p.match;
+    next[s] = p.next;
+    pm[s] = p.pm;
+    dirty |= 1u << (D_SLOT0 + s);
+  }
+
+  __device__ __forceinline__ void load() {
+    term = S.term[g];
+    committed = S.commit[g];
+    first = S.first[g];
+    last = S.last[g];
+    tfirst = S.tfirst[g];
+    tlast = S.tlast[g];
+    const uint32_t nn = n();
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) {
+      if ((uint32_t)s < nn) {
+        match[s] = S.match[(size_t)s * S.G + g];
+        next[s] = S.next[(size_t)s * S.G + g];
+        pm[s] = S.pm[(size_t)s * S.G + g];
+      } else {
+        match[s] = 0;
+        next[s] = 0;
+        pm[s] = 0;
+      }
+    }
+    dirty = 0;
+  }
+
+  __device__ __forceinline__ void store() {
+    if (dirty & D_META) S.meta[g] = meta;
+    if (dirty & D_TERM) S.term[g] = term;
+    if (dirty & D_COMMIT) S.commit[g] = committed;
+    if (dirty & D_LAST) S.last[g] = last;
+    if (dirty & D_TRUN) {
+      S.tfirst[g] = tfirst;
+      S.tlast[g] = tlast;
+    }
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) {
+      if (dirty & (1u << (D_SLOT0 + s))) {
+        S.match[(size_t)s * S.G + g] = match[s];
+        S.next[(size_t)s * S.G + g] = next[s];
+        S.pm[(size_t)s * S.G + g] = pm[s];
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- Progress
+  // raft/progress.go:147-158
+  __device__ __forceinline__ bool is_paused(uint32_t p) const {
+    const uint32_t st = pm_state(p);
+    if (st == HB_PR_PROBE) return pm_paused(p) != 0;
+    if (st == HB_PR_REPLICATE) return pm_count(p) == S.W;
+    return true;
+  }
+  // becomeProbe raft/progress.go:76-88
+  __device__ __forceinline__ void become_probe(uint32_t s, Pr& p) const {
+    if (pm_state(p.pm) == HB_PR_SNAPSHOT) {
+      const uint64_t pending = S.pending[(size_t)s * S.G + g];
+      p.pm = pm_make(HB_PR_PROBE, 0, 0, 0);
+      p.next = umax64(p.match + 1, pending + 1);
+    } else {
+      p.pm = pm_make(HB_PR_PROBE, 0, 0, 0);
+      p.next = p.match + 1;
+    }
+  }
+  // becomeReplicate raft/progress.go:90-93
+  __device__ __forceinline__ void become_replicate(Pr& p) const {
+    p.pm = pm_make(HB_PR_REPLICATE, 0, 0, 0);
+    p.next = p.match + 1;
+  }
+  // maybeUpdate raft/progress.go:102-113
+  __device__ __forceinline__ bool maybe_update(Pr& p, uint64_t nidx) const {
+    bool updated = false;
+    if (p.match < nidx) {
+      p.match = nidx;
+      updated = true;
+      p.pm &= ~PM_PAUSED;
+    }
+    if (p.next < nidx + 1) p.next = nidx + 1;
+    return updated;
+  }
+  // maybeDecrTo raft/progress.go:119-141
+  __device__ __forceinline__ bool maybe_decr_to(Pr& p, uint64_t rejected, uint64_t lasthint) const {
+    if (pm_state(p.pm) == HB_PR_REPLICATE) {
+      if (rejected <= p.match) return false;
+      p.next = p.match + 1;
+      return true;
+    }
+    if (p.next - 1 != rejected) return false;
+    p.next = umin64(rejected, lasthint + 1);
+    if (p.next < 1) p.next = 1;
+    p.pm &= ~PM_PAUSED;
+    return true;
+  }
+  // inflights.freeTo raft/progress.go:204-224
+  __device__ __forceinline__ void free_to(uint32_t s, Pr& p, uint64_t to) const {
+    uint32_t cnt = pm_count(p.pm);
+    if (cnt == 0) return;
+    uint32_t idx = pm_start(p.pm);
+    const uint32_t W = S.W;
+    uint32_t i = 0;
+    for (; i < cnt; ++i) {
+      if (to < *ring_at(s, idx)) break;
+      if (++idx >= W) idx -= W;
+    }
+    p.pm = pm_make(pm_state(p.pm), pm_paused(p.pm), idx, cnt - i);
+  }
+
+  // ---------------------------------------------------------------- log
+  // raftLog.term(i) == Term, restated over the current-term run (raft/log.go:198-217)
+  __device__ __forceinline__ bool term_eq(uint64_t i) const {
+    if (i + 1 < first || i > last) return term == 0;
+    return tfirst <= i && i <= tlast;
+  }
+  // commitTo raft/log.go:172-180
+  __device__ __forceinline__ void commit_to(uint64_t to) {
+    if (committed < to) {
+      if (last < to) {
+        fault(HB_FAULT_COMMIT_RANGE);
+        return;
+      }
+      committed = to;
+      dirty |= D_COMMIT;
+      ev(HB_EV_COMMIT, 0, 0, to);
+    }
+  }
+  // maybeCommit raft/raft.go:323-332 + raftLog.maybeCommit raft/log.go:241-247:
+  // the q-th largest Match by a register sorting network.
+  __device__ __forceinline__ bool maybe_commit() {
+    typename SlotVec<NMAX>::u64 v;
+    const uint32_t nn = n();
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) v[s] = ((uint32_t)s < nn) ? match[s] : 0;
+#pragma unroll
+    for (int r = 0; r < NMAX; ++r) {
+#pragma unroll
+      for (int j = (r & 1); j + 1 < NMAX; j += 2) {
+        const uint64_t a = v[j], b = v[j + 1];
+        v[j] = a > b ? a : b;
+        v[j + 1] = a > b ? b : a;
+      }
+    }
+    const uint64_t mci = v[nn / 2];  // q-1 with q = n/2+1
+    if (mci > committed && term_eq(mci)) {
+      commit_to(mci);
+      return faulted() == 0;
+    }
+    return false;
+  }
+
+  // ---------------------------------------------------------------- sends
+  // sendAppend raft/raft.go:239-282 for the progress p of slot s
+  __device__ __forceinline__ void send_append(uint32_t s, Pr& p) {
+    if (is_paused(p.pm)) return;
+    if (p.next < first) {  // needSnapshot raft/raft.go:715-717
+      const uint64_t snapi = S.snap[g];
+      if (snapi == 0) {
+        fault(HB_FAULT_EMPTY_SNAPSHOT);
+        return;
+      }
+      p.pm = pm_make(HB_PR_SNAPSHOT, 0, 0, 0);  // becomeSnapshot
+      S.pending[(size_t)s * S.G + g] = snapi;
+      ev(HB_EV_SNAP, s, 0, snapi);
+      return;
+    }
+    const uint64_t x = p.next - 1;
+    if (p.next <= last) {
+      const uint64_t lastsent = S.max_msg_size == 0 ? p.next : last;
+      const uint32_t st = pm_state(p.pm);
+      if (st == HB_PR_REPLICATE) {
+        const uint32_t cnt = pm_count(p.pm), start = pm_start(p.pm);
+        if (cnt == S.W) {
+          fault(HB_FAULT_INFLIGHTS_FULL);
+          return;
+        }
+        uint32_t idx = start + cnt;
+        if (idx >= S.W) idx -= S.W;
+        *ring_at(s, idx) = lastsent;                    // inflights.add
+        p.next = lastsent + 1;                          // optimisticUpdate
+        p.pm = pm_make(HB_PR_REPLICATE, pm_paused(p.pm), start, cnt + 1);
+      } else if (st == HB_PR_PROBE) {
+        p.pm |= PM_PAUSED;                              // pause
+      }
+    }
+    ev(HB_EV_APP, s, 0, x);
+  }
+
+  // ---------------------------------------------------------------- transitions
+  // reset raft/raft.go:334-349
+  __device__ __forceinline__ void reset(uint64_t t) {
+    if (term != t) {
+      term = t;
+      set_vote(HB_REF_NONE);
+      tfirst = HB_NO_INDEX;  // no entry carries a term newer than the old Term
+      tlast = 0;
+      dirty |= D_TERM | D_TRUN;
+      ev(HB_EV_TERM, 0, 0, t);
+    }
+    set_lead(HB_REF_NONE);
+    set_votes(0, 0);
+    const uint32_t nn = n(), sf = self();
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) {
+      if ((uint32_t)s < nn) {
+        match[s] = ((uint32_t)s == sf) ? last : 0;
+        next[s] = last + 1;
+        pm[s] = pm_make(HB_PR_PROBE, 0, 0, 0);
+        dirty |= 1u << (D_SLOT0 + s);
+      }
+    }
+  }
+  // becomeFollower :384-391 / becomeCandidate :393-404 / becomeLeader :406-427.
+  // Returns true when the transition happened (false on a reference panic).
+  __device__ __forceinline__ bool transition(uint32_t kind, uint64_t t, uint32_t ld) {
+    if (kind == HB_STATE_CANDIDATE && state() == HB_STATE_LEADER) {
+      fault(HB_FAULT_LEADER_CAMPAIGN);
+      return false;
+    }
+    if (kind == HB_STATE_LEADER && state() == HB_STATE_FOLLOWER) {
+      fault(HB_FAULT_FOLLOWER_LEADER);
+      return false;
+    }
+    const uint64_t before = soft();
+    reset(kind == HB_STATE_CANDIDATE ? term + 1 : (kind == HB_STATE_FOLLOWER ? t : term));
+    set_lead(kind == HB_STATE_LEADER ? self_ref() : (kind == HB_STATE_FOLLOWER ? ld : (uint32_t)HB_REF_NONE));
+    if (kind == HB_STATE_CANDIDATE) set_vote(self_ref());
+    set_state(kind);
+    if (soft() != before) ev(HB_EV_STATE, 0, 0, soft());
+    return true;
+  }
+  // poll raft/raft.go:445-460 (votes map as responded/granted bitmasks)
+  __device__ __forceinline__ uint32_t poll(uint32_t bit, bool v) {
+    uint32_t resp = m_resp(meta), grant = m_grant(meta);
+    if (!((resp >> bit) & 1u)) {
+      resp |= 1u << bit;
+      if (v) grant |= 1u << bit;
+      set_votes(resp, grant);
+    }
+    return (uint32_t)__popc(grant);
+  }
+
+  // ---------------------------------------------------------------- step
+  // Step (raft/raft.go:462-490) + stepLeader/stepCandidate/stepFollower
+  // (:494-649) for the engine's message types, as one straight-line pipeline
+  // so that each primitive (and each event site) exists once in the code:
+  //   gate -> transition 1 -> progress / poll -> transition 2 -> append ->
+  //   maybeCommit -> sends.
+  // The order of effects (and events) equals the reference's call order.
+  enum : uint32_t { SEND_NONE = 0, SEND_ONE, SEND_BCAST, SEND_VOTES, SEND_BEATS };
+
+  __device__ __forceinline__ void step(uint32_t type, uint32_t from, uint64_t mterm, uint64_t index, bool reject,
+                                       uint64_t lasthint) {
+    uint32_t t1 = 0xFF, t2 = 0xFF, ld1 = HB_REF_NONE;
+    uint64_t tt1 = 0;
+    // ---- gate (raft/raft.go:462-486)
+    if (type == HB_MSG_HUP) {
+      t1 = HB_STATE_CANDIDATE;                                   // campaign -> becomeCandidate
+    } else if (mterm != 0) {
+      if (mterm < term) return;                                  // ignore lower term
+      if (mterm > term) {
+        t1 = HB_STATE_FOLLOWER;
+        tt1 = mterm;
+        if (from < n()) ld1 = from;
+        else if (type == HB_MSG_BEAT || type == HB_MSG_PROP) ld1 = self_ref();
+        else ld1 = HB_REF_OTHER;
+      }
+    }
+    if (t1 != 0xFF) transition(t1, tt1, ld1);
+
+    uint32_t send = SEND_NONE, send_to = 0;
+    uint64_t append_k = 0;
+    uint32_t noop = 0;
+    bool resolve_accept = false, old_paused = false;
+    if (!faulted()) {
+      const uint32_t st = state();
+      const uint32_t nn = n();
+      const uint32_t q = nn / 2 + 1;
+      if (type == HB_MSG_HUP) {
+        // campaign raft/raft.go:429-443 (after becomeCandidate)
+        const uint32_t sf = self();
+        if (q == poll(sf == HB_SLOT_NONE ? 7u : sf, true)) {
+          won++;
+          t2 = HB_STATE_LEADER;
+        } else {
+          send = SEND_VOTES;
+        }
+      } else if (st == HB_STATE_LEADER) {
+        if (type == HB_MSG_BEAT) {
+          send = SEND_BEATS;                                     // bcastHeartbeat
+        } else if (type == HB_MSG_PROP) {
+          if (index == 0) fault(HB_FAULT_EMPTY_PROP);
+          else {
+            append_k = index;                                    // appendEntry + bcastAppend
+            send = SEND_BCAST;
+          }
+        } else if (type == HB_MSG_APP_RESP || type == HB_MSG_HEARTBEAT_RESP || type == HB_MSG_SNAP_STATUS ||
+                   type == HB_MSG_UNREACHABLE) {
+          if (from >= nn) {
+            fault(HB_FAULT_NIL_PROGRESS);                        // r.prs[m.From] == nil
+          } else {
+            Pr p = get(from);
+            const uint32_t ps = pm_state(p.pm);
+            if (type == HB_MSG_APP_RESP) {                       // :514-546
+              if (reject) {
+                if (maybe_decr_to(p, index, lasthint)) {
+                  if (ps == HB_PR_REPLICATE) become_probe(from, p);
+                  send = SEND_ONE;
+                  send_to = from;
+                }
+              } else {
+                old_paused = is_paused(p.pm);
+                if (maybe_update(p, index)) {
+                  if (ps == HB_PR_PROBE) {
+                    become_replicate(p);
+                  } else if (ps == HB_PR_SNAPSHOT) {
+                    if (p.match >= S.pending[(size_t)from * S.G + g]) become_probe(from, p);  // maybeSnapshotAbort
+                  } else {
+                    free_to(from, p, index);
+                  }
+                  resolve_accept = true;
+                }
+              }
+            } else if (type == HB_MSG_HEARTBEAT_RESP) {          // :547-554
+              if (ps == HB_PR_REPLICATE && pm_count(p.pm) == S.W)
+                free_to(from, p, *ring_at(from, pm_start(p.pm)));  // freeFirstOne
+              if (p.match < last) {
+                send = SEND_ONE;
+                send_to = from;
+              }
+            } else if (type == HB_MSG_SNAP_STATUS) {             // :559-574
+              if (ps == HB_PR_SNAPSHOT) {
+                if (!reject) become_probe(from, p);
+                else {                                           // snapshotFailure, becomeProbe
+                  p.pm = pm_make(HB_PR_PROBE, 0, 0, 0);
+                  p.next = p.match + 1;
+                }
+                p.pm |= PM_PAUSED;
+              }
+            } else {                                             // MsgUnreachable :575-581
+              if (ps == HB_PR_REPLICATE) become_probe(from, p);
+            }
+            put(from, p);
+          }
+        }
+      } else if (st == HB_STATE_CANDIDATE) {
+        if (type == HB_MSG_PROP) {
+          ev(HB_EV_PROP_DROP, 0, 0, arrival);                    // :587-589
+        } else if (type == HB_MSG_VOTE_RESP) {                   // :603-612
+          const uint32_t gr = poll(from < nn ? from : 7u, !reject);
+          if (q == gr) {
+            won++;
+            t2 = HB_STATE_LEADER;
+            send = SEND_BCAST;
+          } else if (q == (uint32_t)__popc(m_resp(meta)) - gr) {
+            lost++;
+            t2 = HB_STATE_FOLLOWER;
+          }
+        }
+      } else if (type == HB_MSG_PROP) {                          // stepFollower :618-624
+        if (lead() == HB_REF_NONE) ev(HB_EV_PROP_DROP, 0, 0, arrival);
+        else ev(HB_EV_PROP_FWD, lead(), 0, arrival);
+      }
+    }
+    // ---- transition 2: becomeLeader (+ noop entry) or becomeFollower(Term, None)
+    if (t2 != 0xFF && !faulted()) {
+      if (transition(t2, term, HB_REF_NONE) && t2 == HB_STATE_LEADER) {
+        append_k = 1;
+        noop = 1;
+      }
+    }
+    // ---- appendEntry raft/raft.go:351-360
+    bool check_commit = resolve_accept;
+    if (append_k && !faulted()) {
+      const uint64_t old = last;
+      last += append_k;
+      if (tfirst == HB_NO_INDEX) tfirst = old + 1;
+      tlast = last;
+      dirty |= D_LAST | D_TRUN;
+      ev(HB_EV_LAST, 0, noop, last);
+      const uint32_t sf = self();
+      if (sf == HB_SLOT_NONE) {
+        fault(HB_FAULT_NO_SELF);
+      } else {
+        Pr p = get(sf);
+        maybe_update(p, last);
+        put(sf, p);
+        check_commit = true;
+      }
+    }
+    // ---- maybeCommit
+    if (check_commit && !faulted()) {
+      const bool c = maybe_commit();
+      if (resolve_accept) {
+        if (c) send = SEND_BCAST;
+        else if (old_paused) {
+          send = SEND_ONE;
+          send_to = from;
+        }
+      }
+    }
+    // ---- sends: bcastAppend / sendAppend / MsgVote / bcastHeartbeat (slot order)
+    if (send != SEND_NONE) {
+      const uint32_t nn = n(), sf = self();
+#pragma nounroll
+      for (uint32_t s = 0; s < nn; ++s) {
+        if (faulted()) break;
+        if (send == SEND_ONE ? s != send_to : s == sf) continue;
+        Pr p = get(s);
+        if (send == SEND_VOTES) {
+          ev(HB_EV_VOTE, s, 0, last);
+          continue;
+        }
+        if (send == SEND_BEATS) {
+          ev(HB_EV_HEARTBEAT, s, 0, umin64(p.match, committed));
+          p.pm &= ~PM_PAUSED;
+        } else {
+          send_append(s, p);
+        }
+        put(s, p);
+      }
+    }
+    if (faulted()) ev(HB_EV_FAULT, 0, faulted(), arrival);  // faulted groups are never stepped
+  }
+};
+
+}  // namespace hb

@@ -1,0 +1,191 @@
+"""Python binding of the engine's C ABI (include/hipbatch.h -> libhipbatch.so).
+
+This is the product path: every call goes to the HIP library.  There is no CPU
+fallback — if the library is missing or the device is unusable, construction
+fails loudly.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhipbatch.so")
+_lib = None
+
+
+class HipBatchError(RuntimeError):
+    def __init__(self, fn, code):
+        self.code = code
+        super().__init__(f"{fn} failed: {code} ({_strerror(code)})")
+
+
+def _strerror(code):
+    try:
+        return lib().hb_strerror(code).decode()
+    except Exception:
+        return "?"
+
+
+def lib():
+    """Load libhipbatch.so (built by `make -C etcd_amd/csrc`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C etcd_amd/csrc` "
+                          "(there is no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    H = C.c_void_p
+    sig = {
+        "hb_abi_version": (C.c_int, []),
+        "hb_strerror": (C.c_char_p, [C.c_int]),
+        "hb_create": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, P(H)]),
+        "hb_destroy": (C.c_int, [H]),
+        "hb_set_stream": (C.c_int, [H, C.c_void_p]),
+        "hb_sync": (C.c_int, [H]),
+        "hb_load_groups": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
+        "hb_get_groups": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
+        "hb_remove_groups": (C.c_int, [H, C.c_uint32, C.c_uint32]),
+        "hb_set_inflights": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
+        "hb_get_inflights": (C.c_int, [H, C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32), C.c_void_p]),
+        "hb_step": (C.c_int, [H, P(abi.hb_batch), C.c_uint32]),
+        "hb_events_device": (C.c_int, [H, P(C.c_void_p), P(C.c_void_p), P(C.c_void_p), P(C.c_uint32)]),
+        "hb_copy_events": (C.c_int, [H, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
+        "hb_stats_device": (C.c_int, [H, P(C.c_void_p)]),
+        "hb_stats": (C.c_int, [H, C.c_void_p]),
+        "hb_phase_ms": (C.c_int, [H, C.c_void_p]),
+        "hb_alloc_pinned": (C.c_int, [C.c_size_t, P(C.c_void_p)]),
+        "hb_free_pinned": (C.c_int, [C.c_void_p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    if L.hb_abi_version() != abi.HB_ABI_VERSION:
+        raise ImportError("libhipbatch ABI version mismatch")
+    _lib = L
+    return L
+
+
+def _check(fn, rc):
+    if rc != abi.HB_OK:
+        raise HipBatchError(fn, rc)
+
+
+def _ptr(a):
+    """Address of a numpy array or a torch tensor (host or device)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+class Engine:
+    """One device-resident shard of raft groups (one hb_handle)."""
+
+    def __init__(self, capacity, max_replicas=3, max_inflight=256, max_msg_size=abi.HB_NO_LIMIT,
+                 max_batch=1 << 20, device=0, stream=None):
+        L = lib()
+        h = C.c_void_p()
+        _check("hb_create", L.hb_create(device, capacity, max_replicas, max_inflight, max_msg_size,
+                                        max_batch, C.byref(h)))
+        self.h = h
+        self.capacity = capacity
+        self.max_inflight = max_inflight
+        self.max_batch = max_batch
+        self.device = device
+        if stream is not None:
+            self.set_stream(stream)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().hb_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream):
+        """stream: a torch.cuda.Stream, a raw hipStream_t int, or None."""
+        raw = getattr(stream, "cuda_stream", stream)
+        _check("hb_set_stream", lib().hb_set_stream(self.h, C.c_void_p(raw or 0)))
+
+    def sync(self):
+        _check("hb_sync", lib().hb_sync(self.h))
+
+    # ---- group state ---------------------------------------------------------
+    def load_groups(self, groups, first=0):
+        g = np.ascontiguousarray(groups, dtype=abi.GROUP_DTYPE)
+        _check("hb_load_groups", lib().hb_load_groups(self.h, first, len(g), g.ctypes.data))
+
+    def get_groups(self, first=0, count=None):
+        count = self.capacity - first if count is None else count
+        out = np.zeros(count, dtype=abi.GROUP_DTYPE)
+        _check("hb_get_groups", lib().hb_get_groups(self.h, first, count, out.ctypes.data))
+        return out
+
+    def remove_groups(self, first, count):
+        _check("hb_remove_groups", lib().hb_remove_groups(self.h, first, count))
+
+    def set_inflights(self, group, slot, start, vals):
+        v = np.ascontiguousarray(vals, dtype=np.uint64)
+        _check("hb_set_inflights", lib().hb_set_inflights(self.h, group, slot, start, len(v),
+                                                          v.ctypes.data if len(v) else None))
+
+    def get_inflights(self, group, slot):
+        out = np.zeros(self.max_inflight, dtype=np.uint64)
+        s, c = C.c_uint32(), C.c_uint32()
+        _check("hb_get_inflights", lib().hb_get_inflights(self.h, group, slot, C.byref(s), C.byref(c),
+                                                          out.ctypes.data))
+        return s.value, out[: c.value].copy()
+
+    # ---- hot path --------------------------------------------------------------
+    def step(self, group, info, term, index, hint=None, props=None, host=None, profile=False):
+        """Step one batch.  Arrays are numpy (host) or torch tensors (host or cuda)."""
+        b = abi.hb_batch()
+        b.n = len(group)
+        b.group, b.info, b.term, b.index = _ptr(group), _ptr(info), _ptr(term), _ptr(index)
+        b.hint, b.props = _ptr(hint), _ptr(props)
+        if host is None:
+            host = not (hasattr(group, "is_cuda") and group.is_cuda)
+        flags = (abi.HB_STEP_HOST_PTRS if host else 0) | (abi.HB_STEP_PROFILE if profile else 0)
+        self._keep = (group, info, term, index, hint, props)
+        _check("hb_step", lib().hb_step(self.h, C.byref(b), flags))
+
+    def step_batch(self, batch, **kw):
+        return self.step(batch["group"], batch["info"], batch["term"], batch["index"],
+                         batch.get("hint"), batch.get("props"), **kw)
+
+    def events(self):
+        """Dense events of the last step (host copy, synchronizes)."""
+        n = C.c_uint64()
+        L = lib()
+        rc = L.hb_copy_events(self.h, None, 0, C.byref(n))
+        if rc not in (abi.HB_OK, abi.HB_EINVAL):
+            _check("hb_copy_events", rc)
+        out = np.zeros(max(n.value, 1), dtype=abi.EVENT_DTYPE)
+        _check("hb_copy_events", L.hb_copy_events(self.h, out.ctypes.data, len(out), C.byref(n)))
+        return out[: n.value]
+
+    def stats(self):
+        out = np.zeros(abi.HB_STAT_COUNT, dtype=np.uint64)
+        _check("hb_stats", lib().hb_stats(self.h, out.ctypes.data))
+        return out
+
+    def stats_device_ptr(self):
+        p = C.c_void_p()
+        _check("hb_stats_device", lib().hb_stats_device(self.h, C.byref(p)))
+        return p.value
+
+    def phase_ms(self):
+        out = np.zeros(abi.HB_PHASE_COUNT, dtype=np.float32)
+        _check("hb_phase_ms", lib().hb_phase_ms(self.h, out.ctypes.data))
+        return out

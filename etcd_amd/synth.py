@@ -1,0 +1,318 @@
+"""Synthetic raft-group states and message streams (BASELINE.json configs).
+
+Everything here is seeded and deterministic.  The generators build the
+engine's record format (etcd_amd.abi) plus, for the parity oracle, the log term
+runs of every group, so the oracle sees real per-entry terms while the device
+sees only the current-term run.
+
+  steady_groups / cfg2_batch    cfg2: 1M x 3 steady-state replication
+  random_groups / random_batch  fuzz: every device message type and state
+  election_groups / cfg4_batch  cfg4: election storm (MsgHup + MsgVoteResp)
+  FollowerSim                   cfg3: closed-loop lagging followers driven by
+                                the leader's MsgApp events
+"""
+import numpy as np
+
+from . import abi
+
+A = abi
+
+
+def splitmix64(x):
+    """splitmix64 finalizer (vectorized, uint64) — used to shard group ids."""
+    x = np.asarray(x, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def _runs_for(first, tf, last, term):
+    """Log term runs for a group whose current-term run is [tf, last]: the dummy
+    entry (first-1) and the entries before tf carry term-1."""
+    if tf <= first - 1:
+        return [(first - 1, int(term))]
+    return [(first - 1, max(int(term) - 1, 0)), (int(tf), int(term))]
+
+
+# ---------------------------------------------------------------------------- cfg2
+def steady_groups(G, n=3, seed=0x5EED0002, last_hi=1 << 20, term_hi=1000, with_runs=True):
+    """All groups leader (self = slot 0), followers Replicate with empty inflights,
+    every Match = committed = lastIndex; term ~ U[1, term_hi]; termFirst ~ U[1, last]."""
+    rng = np.random.default_rng(seed)
+    g = np.zeros(G, dtype=A.GROUP_DTYPE)
+    term = rng.integers(1, term_hi + 1, G, dtype=np.uint64)
+    last = rng.integers(1, last_hi + 1, G, dtype=np.uint64)
+    tf = (rng.random(G) * last).astype(np.uint64) + np.uint64(1)
+    tf = np.minimum(tf, last)
+    g["term"], g["committed"], g["first_index"], g["last_index"] = term, last, 1, last
+    g["term_first"], g["term_last"], g["snap_index"] = tf, last, 0
+    g["state"], g["n"], g["self_slot"] = A.HB_STATE_LEADER, n, 0
+    g["lead"], g["vote"] = 0, 0
+    pr = g["pr"]
+    for s in range(n):
+        pr[:, s]["match"] = last
+        pr[:, s]["next"] = last + np.uint64(1)
+        pr[:, s]["state"] = A.HB_PR_PROBE if s == 0 else A.HB_PR_REPLICATE
+    runs = None
+    if with_runs:
+        runs = [_runs_for(1, int(tf[i]), int(last[i]), int(term[i])) for i in range(G)]
+    return g, runs
+
+
+def cfg2_batch(groups, step, seed=0x5EED0002, xp=np):
+    """One cfg2 step: one proposal per group (dense props) then every follower acks
+    the new last index (MsgAppResp, Term = group term), in a random permutation."""
+    G = len(groups)
+    n = int(groups["n"][0])
+    rng = np.random.default_rng(seed + 7919 * step)
+    nf = n - 1
+    grp = np.repeat(np.arange(G, dtype=np.uint32), nf)
+    slot = np.tile(np.arange(1, n, dtype=np.uint32), G)
+    perm = rng.permutation(G * nf)
+    grp, slot = grp[perm], slot[perm]
+    info = (np.uint32(A.HB_MSG_APP_RESP) | (slot << np.uint32(4))).astype(np.uint32)
+    term = groups["term"][grp].astype(np.uint64)
+    index = (groups["last_index"][grp] + np.uint64(step + 1)).astype(np.uint64)
+    props = np.ones(G, dtype=np.uint32)
+    return dict(group=grp, info=info, term=term, index=index, hint=None, props=props)
+
+
+# ---------------------------------------------------------------------------- fuzz
+def random_groups(G, nmax=3, seed=1, W=8, state_mix=(0.6, 0.2, 0.2)):
+    """Diverse, internally consistent group states for fuzz parity.
+
+    Returns (groups, runs, inflights{(g, slot): values})."""
+    rng = np.random.default_rng(seed)
+    g = np.zeros(G, dtype=A.GROUP_DTYPE)
+    runs, ins = [], {}
+    for i in range(G):
+        r = g[i]
+        n = int(rng.integers(1, nmax + 1))
+        term = int(rng.integers(1, 40))
+        first = int(rng.integers(1, 20))
+        last = first - 1 + int(rng.integers(0, 30))
+        # non-decreasing terms <= term over [first-1, last]
+        k = int(rng.integers(1, 4))
+        cuts = sorted(set([first - 1] + [int(x) for x in rng.integers(first - 1, last + 1, k)]))
+        ts = sorted(int(x) for x in rng.integers(0, term + 1, len(cuts)))
+        if rng.random() < 0.5:
+            ts[-1] = term
+        rr = []
+        for c, t in zip(cuts, ts):
+            if rr and rr[-1][1] == t:
+                continue
+            rr.append((c, t))
+        runs.append(rr)
+        st = int(rng.choice(3, p=[state_mix[1] if j == 1 else state_mix[0] if j == 2 else state_mix[2]
+                                   for j in range(3)]))
+        self_slot = int(rng.integers(0, n)) if rng.random() > 0.05 else A.HB_SLOT_NONE
+        committed = int(rng.integers(first - 1, last + 1))
+        r["term"], r["committed"], r["first_index"], r["last_index"] = term, committed, first, last
+        r["snap_index"] = first - 1 if (first > 1 or rng.random() < 0.5) else 0
+        r["state"], r["n"], r["self_slot"] = st, n, self_slot
+        refs = list(range(n)) + [A.HB_REF_NONE, A.HB_REF_NONE, A.HB_REF_OTHER]
+        self_ref = self_slot if self_slot != A.HB_SLOT_NONE else A.HB_REF_SELF
+        if st == A.HB_STATE_LEADER:
+            r["lead"], r["vote"] = self_ref, self_ref
+        elif st == A.HB_STATE_CANDIDATE:
+            r["lead"], r["vote"] = A.HB_REF_NONE, self_ref
+            bits = [s for s in range(n)] + ([7] if self_slot == A.HB_SLOT_NONE else [])
+            resp = 0
+            grant = 0
+            for b in bits:
+                if rng.random() < 0.4:
+                    resp |= 1 << b
+                    if rng.random() < 0.5:
+                        grant |= 1 << b
+            sb = 7 if self_slot == A.HB_SLOT_NONE else self_slot
+            resp |= 1 << sb
+            grant |= 1 << sb
+            r["votes_resp"], r["votes_grant"] = resp, grant
+        else:
+            r["lead"] = int(rng.choice(refs))
+            r["vote"] = int(rng.choice(refs))
+        for s in range(n):
+            p = r["pr"][s]
+            if st != A.HB_STATE_LEADER or rng.random() < 0.2:
+                p["match"] = last if s == self_slot else 0
+                p["next"] = last + 1
+                continue
+            m = int(rng.integers(0, last + 1))
+            nx = int(rng.integers(m + 1, last + 2))
+            ps = int(rng.choice(3, p=[0.4, 0.45, 0.15]))
+            p["match"], p["next"], p["state"] = m, nx, ps
+            if ps == A.HB_PR_PROBE:
+                p["paused"] = int(rng.random() < 0.4)
+            elif ps == A.HB_PR_SNAPSHOT:
+                p["pending_snapshot"] = int(rng.integers(0, last + 2))
+            else:
+                p["ins_start"] = int(rng.integers(0, W))
+                room = nx - 1 - m
+                cnt = int(rng.integers(0, min(W, room) + 1)) if room > 0 else 0
+                if rng.random() < 0.15 and room >= W:
+                    cnt = W
+                if cnt:
+                    vals = np.sort(rng.choice(np.arange(m + 1, nx), size=cnt, replace=False)).astype(np.uint64)
+                    ins[(i, s)] = vals
+                p["ins_count"] = cnt
+    return g, runs, ins
+
+
+_TYPES = np.array([A.HB_MSG_APP_RESP, A.HB_MSG_HEARTBEAT_RESP, A.HB_MSG_VOTE_RESP, A.HB_MSG_UNREACHABLE,
+                   A.HB_MSG_SNAP_STATUS, A.HB_MSG_PROP, A.HB_MSG_BEAT, A.HB_MSG_HUP])
+_TYPE_P = np.array([0.42, 0.10, 0.16, 0.04, 0.05, 0.12, 0.05, 0.06])
+
+
+def random_batch(groups, nmsg, seed=2, nonmember=0.04, props=True):
+    """Random messages of every device type against `groups` (ids < len(groups))."""
+    rng = np.random.default_rng(seed)
+    G = len(groups)
+    grp = rng.integers(0, G, nmsg).astype(np.uint32)
+    t = rng.choice(_TYPES, size=nmsg, p=_TYPE_P / _TYPE_P.sum()).astype(np.uint32)
+    n = groups["n"][grp].astype(np.int64)
+    slot = (rng.random(nmsg) * n).astype(np.uint32)
+    slot[rng.random(nmsg) < nonmember] = A.HB_SLOT_NONE
+    reject = (rng.random(nmsg) < 0.25).astype(np.uint32)
+    gterm = groups["term"][grp].astype(np.int64)
+    u = rng.random(nmsg)
+    term = np.where(u < 0.62, gterm, np.where(u < 0.74, 0, np.where(u < 0.87, gterm - 1, gterm + 1)))
+    term = np.maximum(term, 0).astype(np.uint64)
+    local = (t == A.HB_MSG_HUP) | (t == A.HB_MSG_BEAT) | (t == A.HB_MSG_PROP) | (t == A.HB_MSG_SNAP_STATUS) | \
+            (t == A.HB_MSG_UNREACHABLE)
+    term[local & (rng.random(nmsg) < 0.85)] = 0
+    last = groups["last_index"][grp].astype(np.int64)
+    index = np.maximum(last + rng.integers(-4, 4, nmsg), 0).astype(np.uint64)
+    pm = t == A.HB_MSG_PROP
+    index[pm] = rng.integers(1, 4, int(pm.sum()))
+    index[pm & (rng.random(nmsg) < 0.02)] = 0
+    hint = np.maximum(last + rng.integers(-6, 2, nmsg), 0).astype(np.uint64)
+    info = (t | (slot << np.uint32(4)) | (reject << np.uint32(8))).astype(np.uint32)
+    pr = None
+    if props:
+        pr = np.where(rng.random(G) < 0.3, rng.integers(1, 3, G), 0).astype(np.uint32)
+    return dict(group=grp, info=info, term=term, index=index, hint=hint, props=pr)
+
+
+# ---------------------------------------------------------------------------- cfg4
+def election_groups(G, n=7, seed=0x5EED0004, term_hi=1000):
+    """All groups follower at term T ~ U[1, term_hi], no leader, fresh progress."""
+    rng = np.random.default_rng(seed)
+    g = np.zeros(G, dtype=A.GROUP_DTYPE)
+    term = rng.integers(1, term_hi + 1, G, dtype=np.uint64)
+    last = rng.integers(1, 1 << 16, G, dtype=np.uint64)
+    g["term"], g["committed"], g["first_index"], g["last_index"] = term, last, 1, last
+    g["term_first"], g["term_last"] = A.HB_NO_INDEX, 0
+    g["state"], g["n"], g["self_slot"] = A.HB_STATE_FOLLOWER, n, 0
+    g["lead"], g["vote"] = A.HB_REF_NONE, A.HB_REF_NONE
+    for s in range(n):
+        g["pr"][:, s]["match"] = last if s == 0 else 0
+        g["pr"][:, s]["next"] = last + np.uint64(1)
+    runs = [[(0, 0), (1, max(int(term[i]) - 1, 0))] if term[i] > 1 else [(0, 0)] for i in range(G)]
+    return g, runs
+
+
+def cfg4_batch(groups, seed=0x5EED0004, grant_p=0.5, higher_p=0.05):
+    """MsgHup for every group, then n-1 MsgVoteResp per group (random order):
+    granted with p = grant_p; a fraction carries Term+2 (step down, lead = From)."""
+    rng = np.random.default_rng(seed)
+    G = len(groups)
+    n = int(groups["n"][0])
+    hup_g = rng.permutation(G).astype(np.uint32)
+    nv = n - 1
+    vg = np.repeat(np.arange(G, dtype=np.uint32), nv)
+    vs = np.tile(np.arange(1, n, dtype=np.uint32), G)
+    perm = rng.permutation(G * nv)
+    vg, vs = vg[perm], vs[perm]
+    rej = (rng.random(G * nv) >= grant_p).astype(np.uint32)
+    vterm = groups["term"][vg].astype(np.uint64) + np.uint64(1)
+    hi = rng.random(G * nv) < higher_p
+    vterm[hi] += np.uint64(1)
+    grp = np.concatenate([hup_g, vg])
+    info = np.concatenate([np.full(G, A.HB_MSG_HUP, np.uint32),
+                           (np.uint32(A.HB_MSG_VOTE_RESP) | (vs << np.uint32(4)) | (rej << np.uint32(8)))])
+    term = np.concatenate([np.zeros(G, np.uint64), vterm])
+    index = np.zeros(len(grp), np.uint64)
+    return dict(group=grp, info=info.astype(np.uint32), term=term, index=index, hint=None, props=None)
+
+
+# ---------------------------------------------------------------------------- cfg3
+class FollowerSim:
+    """Closed-loop followers for the lagging-follower workload (cfg3).
+
+    Each (group, slot) follower holds a log prefix length `flast`.  The leader's
+    MsgApp events (HB_EV_APP: index = prev) are delivered with loss/lag; a
+    follower accepts when it has `prev` (acks prev + entries) and rejects with
+    RejectHint = flast otherwise.  Heartbeat responses and MsgUnreachable are
+    sprinkled in.  All message terms are the leader's current term."""
+
+    def __init__(self, groups, seed=0x5EED0003, lag_p=0.2, drop_p=0.1, hb_p=0.1, unreach_p=0.001):
+        self.rng = np.random.default_rng(seed)
+        G = len(groups)
+        self.n = groups["n"].astype(np.int64)
+        nmax = int(self.n.max())
+        self.flast = np.zeros((G, nmax), dtype=np.int64)
+        for s in range(nmax):
+            self.flast[:, s] = groups["pr"][:, s]["match"].astype(np.int64)
+        self.pending = []
+        self.lag_p, self.drop_p, self.hb_p, self.unreach_p = lag_p, drop_p, hb_p, unreach_p
+
+    def deliver(self, events, groups_now):
+        """Consume the leader's events of one step; return the next batch."""
+        rng = self.rng
+        msgs = list(self.pending)
+        self.pending = []
+        last = groups_now["last_index"].astype(np.int64)
+        term = groups_now["term"].astype(np.int64)
+        selfs = groups_now["self_slot"].astype(np.int64)
+        app = events[events["type"] == A.HB_EV_APP]
+        for e in app:
+            g, s, prev = int(e["group"]), int(e["to"]), int(e["x"])
+            if rng.random() < self.drop_p:
+                continue
+            L = int(last[g])
+            if self.flast[g, s] >= prev:
+                self.flast[g, s] = max(self.flast[g, s], L)
+                m = (g, A.HB_MSG_APP_RESP, s, 0, int(term[g]), L, 0)
+            else:
+                m = (g, A.HB_MSG_APP_RESP, s, 1, int(term[g]), prev, int(self.flast[g, s]))
+            if rng.random() < self.lag_p:
+                self.pending.append(m)
+            else:
+                msgs.append(m)
+        G = len(groups_now)
+        for g in np.nonzero(rng.random(G) < self.hb_p)[0]:
+            for s in range(int(self.n[g])):
+                if s != selfs[g]:
+                    msgs.append((int(g), A.HB_MSG_HEARTBEAT_RESP, s, 0, int(term[g]), 0, 0))
+        for g in np.nonzero(rng.random(G) < self.unreach_p * 10)[0]:
+            s = int(rng.integers(0, self.n[g]))
+            if s != selfs[g]:
+                msgs.append((int(g), A.HB_MSG_UNREACHABLE, s, 0, 0, 0, 0))
+        order = rng.permutation(len(msgs)) if msgs else np.zeros(0, dtype=np.int64)
+        # keep per-(group) order of delayed-before-fresh by a stable sort on a random key per group
+        arr = np.array(msgs, dtype=np.int64).reshape(-1, 7)[order] if msgs else np.zeros((0, 7), np.int64)
+        grp = arr[:, 0].astype(np.uint32)
+        info = (arr[:, 1] | (arr[:, 2] << 4) | (arr[:, 3] << 8)).astype(np.uint32)
+        props = self.rng.integers(1, 5, G).astype(np.uint32)
+        return dict(group=grp, info=info, term=arr[:, 4].astype(np.uint64), index=arr[:, 5].astype(np.uint64),
+                    hint=arr[:, 6].astype(np.uint64), props=props)
+
+
+def lagging_groups(G, n=5, seed=0x5EED0003, W=8):
+    """cfg3 start: leaders with followers spread over Probe/Replicate and lag."""
+    g, runs = steady_groups(G, n=n, seed=seed, last_hi=1 << 12, term_hi=100)
+    rng = np.random.default_rng(seed + 1)
+    for s in range(1, n):
+        lag = rng.integers(0, 64, G).astype(np.uint64)
+        m = np.maximum(g["last_index"].astype(np.int64) - lag.astype(np.int64), 0).astype(np.uint64)
+        g["pr"][:, s]["match"] = m
+        g["pr"][:, s]["next"] = m + np.uint64(1)
+        probe = rng.random(G) < 0.3
+        g["pr"][:, s]["state"] = np.where(probe, A.HB_PR_PROBE, A.HB_PR_REPLICATE)
+    # committed = q-th largest match (consistent leader state)
+    mt = np.sort(np.stack([g["pr"][:, s]["match"] for s in range(n)], 1), axis=1)[:, ::-1]
+    q = n // 2 + 1
+    g["committed"] = np.minimum(mt[:, q - 1], g["committed"])
+    return g, runs

@@ -278,11 +278,12 @@ int  hb_get_inflights(hb_handle* h, uint32_t group, uint32_t slot,
  * are read with the functions below. */
 int  hb_step(hb_handle* h, const hb_batch* b, uint32_t flags);
 
-/* Events of the last step: `n_chunks` chunks, chunk c holds counts[c] events
- * at base + c * chunk_cap; per group, events appear in order across chunks
- * taken in index order.  Device pointers; valid until the next hb_step. */
-int  hb_events_device(hb_handle* h, const hb_event** base, const uint32_t** counts,
-                      uint32_t* n_chunks, uint32_t* chunk_cap);
+/* Events of the last step, as written by the device: `n_chunks` chunks (one
+ * per 1024-group partition); chunk c holds counts[c] events at
+ * base + chunk_off[c], and all events of a group are in one chunk, in order.
+ * Device pointers; valid until the next hb_step. */
+int  hb_events_device(hb_handle* h, const hb_event** base, const uint64_t** chunk_off,
+                      const uint32_t** counts, uint32_t* n_chunks);
 /* Gather the last step's events densely into host memory (synchronizes).
  * *n = number of events; returns HB_EINVAL if cap is too small. */
 int  hb_copy_events(hb_handle* h, hb_event* out, uint64_t cap, uint64_t* n);

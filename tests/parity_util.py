@@ -1,0 +1,86 @@
+"""Shared parity harness: drive the engine (etcd_amd.hipbatch, HIP) and the C
+oracle (oracle/, CPU) with identical batches and compare bit-exactly."""
+import numpy as np
+
+from etcd_amd import abi
+from oracle.pyoracle import OracleGroups
+
+
+def sort_events(ev):
+    """Events grouped per group, keeping each group's order (the only order the
+    engine promises across groups)."""
+    order = np.argsort(ev["group"], kind="stable")
+    return ev[order]
+
+
+def assert_events_equal(dev, ora, ctx=""):
+    d, o = sort_events(dev), sort_events(ora)
+    if len(d) != len(o) or not np.array_equal(d, o):
+        gd = set(np.unique(d["group"]).tolist())
+        go = set(np.unique(o["group"]).tolist())
+        bad = sorted(g for g in gd | go
+                     if not np.array_equal(d[d["group"] == g], o[o["group"] == g]))[:3]
+        lines = [f"{ctx}: events differ (dev {len(d)}, oracle {len(o)}); first groups {bad}"]
+        for g in bad:
+            lines.append(f"  group {g}\n    dev: {d[d['group'] == g].tolist()}\n    ora: {o[o['group'] == g].tolist()}")
+        raise AssertionError("\n".join(lines))
+
+
+def assert_groups_equal(dev, ora, ctx=""):
+    assert len(dev) == len(ora)
+    # faulted groups: only the fault code is specified after the panic point
+    live = ora["fault"] == 0
+    assert np.array_equal(dev["fault"], ora["fault"]), f"{ctx}: fault codes differ"
+    d, o = dev[live], ora[live]
+    if not np.array_equal(d, o):
+        idx = np.nonzero(d != o)[0][:3]
+        gids = np.nonzero(live)[0][idx]
+        msg = [f"{ctx}: group state differs at {gids.tolist()}"]
+        for k, g in zip(idx, gids):
+            for f in abi.GROUP_DTYPE.names:
+                if not np.array_equal(d[k][f], o[k][f]):
+                    msg.append(f"  g{g}.{f}: dev {d[k][f]} ora {o[k][f]}")
+        raise AssertionError("\n".join(msg))
+
+
+def assert_inflights_equal(eng, og, groups_now, ctx=""):
+    for g in range(len(groups_now)):
+        if groups_now[g]["fault"]:
+            continue
+        for s in range(int(groups_now[g]["n"])):
+            p = groups_now[g]["pr"][s]
+            if p["state"] != abi.HB_PR_REPLICATE or p["ins_count"] == 0:
+                continue
+            start, vals = eng.get_inflights(g, s)
+            ov = og.inflights(g, s)
+            assert start == p["ins_start"], f"{ctx}: g{g}/s{s} start"
+            assert np.array_equal(vals, ov), f"{ctx}: g{g}/s{s} inflights dev {vals} ora {ov}"
+
+
+class Pair:
+    """An engine and an oracle loaded with the same groups."""
+
+    def __init__(self, groups, runs, nmax, W, ins=None, max_msg_size=abi.HB_NO_LIMIT, max_batch=1 << 16):
+        from etcd_amd.hipbatch import Engine
+        self.og = OracleGroups(groups, runs, W, max_msg_size, ins)
+        init = self.og.groups()  # canonical record (term run derived from the log)
+        self.eng = Engine(len(groups), max_replicas=nmax, max_inflight=W, max_msg_size=max_msg_size,
+                          max_batch=max_batch)
+        self.eng.load_groups(init)
+        for (g, s), vals in (ins or {}).items():
+            self.eng.set_inflights(g, s, int(init[g]["pr"][s]["ins_start"]), vals)
+        assert_groups_equal(self.eng.get_groups(), init, "load")
+
+    def step(self, batch, ctx="", check_inflights=True):
+        self.eng.step_batch(batch, host=True)
+        dev_ev = self.eng.events()
+        dev_st = self.eng.stats()
+        ora_ev, ora_st = self.og.step(batch)
+        assert_events_equal(dev_ev, ora_ev, ctx)
+        assert np.array_equal(dev_st, ora_st), \
+            f"{ctx}: stats dev {dict(zip(abi.STAT_NAMES, dev_st.tolist()))} ora {dict(zip(abi.STAT_NAMES, ora_st.tolist()))}"
+        ora_g = self.og.groups()
+        assert_groups_equal(self.eng.get_groups(), ora_g, ctx)
+        if check_inflights:
+            assert_inflights_equal(self.eng, self.og, ora_g, ctx)
+        return dev_ev, dev_st, ora_g
