@@ -1,0 +1,216 @@
+"""Benchmark: MsgAppResp applied/s (+ commits advanced/s) on the cfg2 workload.
+
+BASELINE.json metric "MsgAppResp applied/sec + commits advanced/sec, 1M raft
+groups x3, 1-8 GPUs", quoted on configs[1]: 1M groups x 3 replicas steady-state
+replication on one MI355X.  One step = one batch through the hot path: every
+group takes one proposal (dense props) and both followers' MsgAppResp for it
+arrive in a random permutation (2M MsgAppResp per GPU), i.e. the engine runs
+partition + apply (+ finish) over HBM-resident inputs and writes the sparse
+event stream to HBM.  Weak scaling: each GPU owns ~1M groups (sharded by
+splitmix64(group id) % N) and the only collective is one RCCL all-reduce of the
+step statistics.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "MsgAppResp applied/sec + commits advanced/sec, 1M raft groups×3, 1-8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def alg_bytes_per_group(n):
+    """SURVEY.md §8(d) algorithmic bytes per group per cfg2 step: each follower's
+    MsgAppResp 66 B + per-group commit/append state 80 B + per-follower
+    bcastAppend on the proposal 21 B  (= 254 B = 2 x 127 B at n = 3)."""
+    return (n - 1) * (66 + 21) + 80
+
+
+def cpu_baseline(n, groups=200_000, budget_s=10.0, max_steps=40):
+    """The C oracle (a sequential restatement of the reference loop) on a bounded
+    sample of the same workload, one host core.  Test infrastructure only."""
+    from etcd_amd import abi, synth
+    from oracle.pyoracle import OracleGroups
+    g, runs = synth.steady_groups(groups, n, seed=0x5EED0002, with_runs=True)
+    og = OracleGroups(g, runs, 256)
+    acks = commits = 0
+    spent = 0.0
+    steps = 0
+    while spent < budget_s and steps < max_steps:
+        b = synth.cfg2_batch(g, steps)
+        t0 = time.perf_counter()
+        _, st = og.step(b)
+        spent += time.perf_counter() - t0
+        acks += int(st[abi.HB_STAT_APPRESP])
+        commits += int(st[abi.HB_STAT_COMMITS])
+        steps += 1
+    return {"value": acks / spent, "unit": "MsgAppResp/s", "cores": 1, "kind": "port",
+            "commits_per_s": commits / spent,
+            "sample": f"oracle/raft_oracle.c (C restatement of the reference loop, not the Go reference), "
+                      f"{groups} groups x {n}, {steps} cfg2 steps, {acks} MsgAppResp in {spent:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--groups", type=int, default=1 << 20, help="groups per GPU (cfg2: 1M)")
+    ap.add_argument("--replicas", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-groups", type=int, default=200_000)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-profile", action="store_true", help="skip per-phase HIP events")
+    ap.add_argument("--traffic-bytes", type=float, default=None,
+                    help="HBM bytes per apply launch from a rocprofv3 PMC pass (profiles/)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from etcd_amd import abi, synth
+    from etcd_amd.hipbatch import Engine
+    from etcd_amd.shard import ShardMap
+
+    n = args.replicas
+    # ---- this rank's shard of the global groups (weak scaling: ~groups per GPU)
+    gids = np.arange(world * args.groups, dtype=np.uint64)
+    shard = ShardMap(gids, world, rank) if world > 1 else None
+    G = len(shard) if shard is not None else args.groups
+    groups, _ = synth.steady_groups(G, n, seed=0x5EED0002 + rank, with_runs=False)
+    batch = synth.cfg2_batch(groups, 0, seed=0x5EED0002 + rank)
+    nmsg = len(batch["group"])
+
+    stream = torch.cuda.current_stream()
+    eng = Engine(G, max_replicas=n, max_inflight=256, max_batch=nmsg, device=local, stream=stream)
+    eng.load_groups(groups)
+    d_group = torch.from_numpy(batch["group"].view(np.int32)).to(dev)
+    d_info = torch.from_numpy(batch["info"].view(np.int32)).to(dev)
+    d_term = torch.from_numpy(batch["term"].view(np.int64)).to(dev)
+    d_props = torch.from_numpy(batch["props"].view(np.int32)).to(dev)
+    base_index = torch.from_numpy(batch["index"].view(np.int64)).to(dev)  # last + 1
+    total = args.warmup + args.steps
+    # step k acks index last + k + 1 (prepared before timing: inputs resident in HBM)
+    d_index = [base_index + k for k in range(total)]
+    stats_step = torch.zeros(abi.HB_STAT_COUNT, dtype=torch.int64, device=dev)
+    stats_acc = torch.zeros(abi.HB_STAT_COUNT, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+
+    def one_step(k, profile):
+        eng.step(d_group, d_info, d_term, d_index[k], None, d_props, host=False, profile=profile)
+        eng.stats_to(stats_step)
+        if world > 1:
+            dist.all_reduce(stats_step)  # RCCL over xGMI: the only collective
+        stats_acc.add_(stats_step)
+
+    for k in range(args.warmup):
+        one_step(k, False)
+    torch.cuda.synchronize()
+    stats_acc.zero_()
+    eng.phase_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = torch.cuda.Event(enable_timing=True)
+    t_end = torch.cuda.Event(enable_timing=True)
+    wall0 = time.perf_counter()
+    t_start.record(stream)
+    for k in range(args.warmup, total):
+        one_step(k, not args.no_profile)
+    t_end.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - wall0
+    ms_local = t_start.elapsed_time(t_end)
+    ms_t = torch.tensor([ms_local], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(ms_t, op=dist.ReduceOp.MAX)
+    ms = float(ms_t.item())
+    st = stats_acc.cpu().numpy().astype(np.uint64)  # summed over ranks and steps
+    appresp = int(st[abi.HB_STAT_APPRESP])
+    commits = int(st[abi.HB_STAT_COMMITS])
+    # sanity: every group commits once per step, nothing faults
+    g_all = torch.tensor([G], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(g_all)
+    g_total = int(g_all.item())
+    ok = commits == g_total * args.steps and int(st[abi.HB_STAT_FAULTS]) == 0 and \
+        appresp == g_total * (n - 1) * args.steps
+
+    phase = {}
+    roof = None
+    if not args.no_profile:
+        ph, nph = eng.phase_ms()
+        phase = {"partition_ms": float(ph[abi.HB_PHASE_PARTITION]), "apply_ms": float(ph[abi.HB_PHASE_APPLY]),
+                 "finish_ms": float(ph[abi.HB_PHASE_FINISH]), "steps": nph}
+        alg = alg_bytes_per_group(n) * G  # per apply launch on this GPU
+        achieved = float(alg / (float(ph[abi.HB_PHASE_APPLY]) * 1e-3) / 1e9)
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": args.traffic_bytes,
+                "kernel": f"k_apply<{3 if n <= 3 else (5 if n <= 5 else 7)}>",
+                "alg_bytes_per_launch": alg,
+                "alg_bytes_note": f"SURVEY.md 8(d): {alg_bytes_per_group(n)} B/group = "
+                                  f"{alg_bytes_per_group(n) / (n - 1):.0f} B/MsgAppResp x {G * (n - 1)} MsgAppResp"}
+
+    out = None
+    if rank == 0:
+        sec = ms / 1e3
+        out = {
+            "metric": METRIC,
+            "value": appresp / sec,
+            "unit": "MsgAppResp/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (seeded cfg2 stream: steady-state leaders, 1 proposal + all follower acks per group per step)",
+            "config": {"workload": "cfg2: 1M raft groups x 3 replicas steady-state replication per GPU "
+                                   "(BASELINE.json configs[1])",
+                       "groups_per_gpu": G, "groups_total": g_total, "replicas": n,
+                       "msgappresp_per_step": g_total * (n - 1), "max_inflight": 256,
+                       "max_msg_size": "noLimit", "sharding": "splitmix64(group id) % N" if world > 1 else "none"},
+            "commits_per_s": commits / sec,
+            "parity_sanity": bool(ok),
+            "wall_s": wall,
+            "phases": phase,
+            "roofline": roof,
+            "cpu_baseline": None,
+        }
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(n, args.cpu_groups, args.cpu_seconds)
+            except Exception as e:  # report, never fake
+                out["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

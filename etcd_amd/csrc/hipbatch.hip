@@ -1,11 +1,10 @@
 // hipbatch.hip — MI355X (gfx950) batched Raft leader-bookkeeping engine.
 //
 // One hb_step() = three phases on the handle's stream:
-//   1. partition  (k_hist, k_scan_*, k_scatter): a stable multi-split of the
-//      arrival-ordered batch by partition = group >> PART_LOG.  Each wave owns
-//      a contiguous span of messages; within a wave the rank of a message among
-//      same-partition messages comes from ballot matching, so the permuted
-//      segment of every partition keeps arrival order.
+//   1. partition  (k_radix_hist, k_scan_rows, k_radix_scatter x passes,
+//      k_part_bounds): a stable LSD radix sort of the arrival-ordered batch by
+//      partition = group >> PART_LOG, so every partition's segment keeps
+//      arrival order.
 //   2. apply      (k_apply<NMAX>): one 1024-lane workgroup per partition, one
 //      lane per raft group.  The lane loads its group's SoA state into
 //      registers once, steps the group's messages in arrival order (LDS
@@ -38,60 +37,6 @@ using namespace hb;
     }                                                                        \
   } while (0)
 
-// ============================================================================
-// Phase 1: stable partition of the batch
-// ============================================================================
-struct BatchDev {
-  const uint32_t* group;
-  const uint32_t* info;
-  const uint64_t* term;
-  const uint64_t* index;
-  const uint64_t* hint;
-  const uint32_t* props;
-  uint64_t n;
-};
-
-struct PartArgs {
-  BatchDev b;
-  uint32_t G;        // group capacity
-  uint32_t NB;       // partitions
-  uint32_t NW;       // waves (message spans)
-  uint32_t span;     // messages per wave
-  uint32_t wpb;      // waves per block
-  uint32_t key_bits; // ceil(log2(NB))
-  uint32_t* hist;    // [NB][NW] counts, then exclusive offsets (in place)
-  // permuted batch (SoA)
-  uint32_t* p_info;  // info | (group & (PART-1)) << 16
-  uint32_t* p_orig;  // arrival index
-  uint64_t* p_term;
-  uint64_t* p_index;
-};
-
-// Per-wave histogram of partition ids over the wave's span.
-__global__ void __launch_bounds__(256) k_hist(PartArgs a) {
-  extern __shared__ uint32_t sh[];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t w = blockIdx.x * a.wpb + wave;
-  uint32_t* cnt = sh + (size_t)wave * a.NB;
-  if (wave < a.wpb)
-    for (uint32_t b = lane; b < a.NB; b += 64) cnt[b] = 0;
-  __syncthreads();
-  if (wave < a.wpb && w < a.NW) {
-    const uint64_t lo = (uint64_t)w * a.span;
-    const uint64_t hi = lo + a.span < a.b.n ? lo + a.span : a.b.n;
-    for (uint64_t i = lo + lane; i < hi; i += 64) {
-      const uint32_t gg = a.b.group[i];
-      if (gg < a.G) atomicAdd(&cnt[gg >> PART_LOG], 1u);
-    }
-  }
-  __syncthreads();
-  if (wave < a.wpb && w < a.NW)
-    for (uint32_t b = lane; b < a.NB; b += 64) a.hist[(size_t)b * a.NW + w] = cnt[b];
-}
-
-// Exclusive scan of u32 (three kernels: per-tile sums, scan of sums, rescan).
-constexpr uint32_t SCAN_TILE = 4096;  // 1024 threads x 4
-
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
@@ -121,96 +66,211 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh16, 
   return before + incl - v;
 }
 
-__global__ void __launch_bounds__(1024) k_scan_sums(const uint32_t* in, uint64_t len, uint32_t* sums) {
-  __shared__ uint32_t sh16[16];
-  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * 4;
-  uint32_t v = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (base + k < len) v += in[base + k];
-  uint32_t total;
-  block_excl_scan(v, sh16, &total);
-  if (threadIdx.x == 0) sums[blockIdx.x] = total;
-}
+// ============================================================================
+// Phase 1: stable partition of the batch
+//
+// LSD radix sort of the messages by partition id (group >> PART_LOG), 6 bits
+// (64 bins) per pass, 2 passes up to 4096 partitions (4M groups).  A 512-lane
+// workgroup owns a tile of 2048 messages: it ranks them stably per digit
+// (ballot matching inside a wave, per-wave counters across waves), stages the
+// tile in LDS in digit order, and writes each digit's run contiguously, so the
+// global stores are coalesced runs (~32 records per digit per tile) instead of
+// scattered single records.  Messages of groups >= capacity are dropped in
+// the first pass.  Arrival order is preserved within every partition.
+// ============================================================================
+struct BatchDev {
+  const uint32_t* group;
+  const uint32_t* info;
+  const uint64_t* term;
+  const uint64_t* index;
+  const uint64_t* hint;
+  const uint32_t* props;
+  uint64_t n;
+};
 
-__global__ void __launch_bounds__(1024) k_scan_top(uint32_t* sums, uint32_t nsums) {
-  __shared__ uint32_t sh16[16];
-  uint32_t carry = 0;
-  for (uint32_t base = 0; base < nsums; base += 1024) {
-    const uint32_t i = base + threadIdx.x;
-    const uint32_t v = i < nsums ? sums[i] : 0;
-    uint32_t total;
-    const uint32_t ex = block_excl_scan(v, sh16, &total);
-    if (i < nsums) sums[i] = carry + ex;
-    carry += total;
-  }
-}
+constexpr uint32_t RDX_BITS = 6;
+constexpr uint32_t RDX_BINS = 1u << RDX_BITS;
+constexpr uint32_t RDX_THREADS = 512;
+constexpr uint32_t RDX_WAVES = RDX_THREADS / 64;
+constexpr uint32_t RDX_ROUNDS = 4;
+constexpr uint32_t RDX_TILE = RDX_THREADS * RDX_ROUNDS;  // 2048
 
-__global__ void __launch_bounds__(1024) k_scan_apply(uint32_t* data, uint64_t len, const uint32_t* sums,
-                                                     uint32_t NW, uint32_t NB, uint32_t* part_off,
-                                                     uint32_t total_slot) {
-  __shared__ uint32_t sh16[16];
-  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * 4;
-  uint32_t v[4];
-  uint32_t s = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    v[k] = base + k < len ? data[base + k] : 0;
-    s += v[k];
-  }
-  uint32_t total;
-  uint32_t ex = block_excl_scan(s, sh16, &total) + sums[blockIdx.x];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint64_t i = base + k;
-    if (i < len) {
-      data[i] = ex;
-      if (i % NW == 0) part_off[i / NW] = ex;  // partition start
-    }
-    ex += v[k];
-  }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == blockDim.x - 1) part_off[NB] = ex;
-  (void)total_slot;
-}
+struct RadixSrc {
+  const uint32_t* group;
+  const uint32_t* info;
+  const uint32_t* orig;   // null: arrival index = position
+  const uint64_t* term;
+  const uint64_t* index;
+  const uint32_t* n_dev;  // null: n
+  uint32_t n;
+};
 
-// Stable scatter: within a wave, messages of the same partition get
-// consecutive slots in arrival order (ballot match on the key bits).
-__global__ void __launch_bounds__(256) k_scatter(PartArgs a) {
-  extern __shared__ uint32_t sh[];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t w = blockIdx.x * a.wpb + wave;
-  uint32_t* cnt = sh + (size_t)wave * a.NB;
-  const bool live = wave < a.wpb && w < a.NW;
-  if (live)
-    for (uint32_t b = lane; b < a.NB; b += 64) cnt[b] = a.hist[(size_t)b * a.NW + w];
+struct RadixDst {
+  uint32_t* group;
+  uint32_t* info;
+  uint32_t* orig;
+  uint64_t* term;
+  uint64_t* index;
+};
+
+__device__ __forceinline__ uint32_t src_n(const RadixSrc& s) { return s.n_dev ? *s.n_dev : s.n; }
+
+__global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t G, uint32_t shift, uint32_t ntiles,
+                                                           uint32_t* hist) {
+  __shared__ uint32_t cnt[RDX_BINS];
+  const uint32_t tid = threadIdx.x;
+  if (tid < RDX_BINS) cnt[tid] = 0;
   __syncthreads();
-  if (!live) return;
-  const uint64_t lo = (uint64_t)w * a.span;
-  const uint64_t hi = lo + a.span < a.b.n ? lo + a.span : a.b.n;
+  const uint32_t n = src_n(s);
+  const uint32_t base = blockIdx.x * RDX_TILE;
+#pragma unroll
+  for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+    const uint32_t i = base + r * RDX_THREADS + tid;
+    if (i < n) {
+      const uint32_t g = s.group[i];
+      if (g < G) atomicAdd(&cnt[((g >> PART_LOG) >> shift) & (RDX_BINS - 1)], 1u);
+    }
+  }
+  __syncthreads();
+  if (tid < RDX_BINS) hist[(size_t)tid * ntiles + blockIdx.x] = cnt[tid];
+}
+
+// Row scan: workgroup b turns row b of hist ([RDX_BINS][ntiles] tile counts)
+// into exclusive per-tile prefixes and writes the row total to totals[b].
+__global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t ntiles, uint32_t* totals) {
+  __shared__ uint32_t sh16[16];
+  uint32_t* row = hist + (size_t)blockIdx.x * ntiles;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < ntiles; base += 4096) {
+    const uint32_t i0 = base + threadIdx.x * 4;
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = i0 + k < ntiles ? row[i0 + k] : 0u;
+    uint32_t tot;
+    uint32_t run = carry + block_excl_scan(v[0] + v[1] + v[2] + v[3], sh16, &tot);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (i0 + k < ntiles) row[i0 + k] = run;
+      run += v[k];
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) totals[blockIdx.x] = carry;
+}
+
+__global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, RadixDst d, uint32_t G, uint32_t shift,
+                                                              uint32_t ntiles, const uint32_t* off,
+                                                              const uint32_t* totals, uint32_t* n_valid,
+                                                              uint32_t final_pass) {
+  __shared__ uint32_t s_off[RDX_BINS];
+  __shared__ uint32_t s_wcnt[RDX_WAVES][RDX_BINS];
+  __shared__ uint32_t s_dstart[RDX_BINS + 1];
+  __shared__ uint32_t st_group[RDX_TILE];
+  __shared__ uint32_t st_info[RDX_TILE];
+  __shared__ uint32_t st_orig[RDX_TILE];
+  __shared__ uint64_t st_term[RDX_TILE];
+  __shared__ uint64_t st_index[RDX_TILE];
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint32_t tile = blockIdx.x;
+  if (tid < RDX_BINS) {
+    // digit base = exclusive scan of the digit totals; + this tile's row prefix
+    const uint32_t t = totals[tid];
+    const uint32_t incl = wave_incl_scan(t);
+    s_off[tid] = incl - t + off[(size_t)tid * ntiles + tile];
+    if (tile == 0 && tid == RDX_BINS - 1) *n_valid = incl;
+  }
+  (&s_wcnt[0][0])[tid] = 0;  // RDX_WAVES * RDX_BINS == RDX_THREADS
+  __syncthreads();
+  const uint32_t n = src_n(s);
+  const uint32_t base = tile * RDX_TILE;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (uint64_t base = lo; base < hi; base += 64) {
-    const uint64_t i = base + lane;
-    bool valid = i < hi;
-    const uint32_t gg = valid ? a.b.group[i] : 0u;
-    valid = valid && gg < a.G;
-    const uint32_t key = gg >> PART_LOG;
-    uint64_t peers = __ballot(valid);
-    for (uint32_t k = 0; k < a.key_bits; ++k) {
-      const bool bit = (key >> k) & 1u;
+  uint32_t vg[RDX_ROUNDS], vi[RDX_ROUNDS], vo[RDX_ROUNDS], vd[RDX_ROUNDS], vr[RDX_ROUNDS];
+  uint64_t vt[RDX_ROUNDS], vx[RDX_ROUNDS];
+  bool vv[RDX_ROUNDS];
+  // load (coalesced: round r, lane l -> element wave*256 + r*64 + l)
+#pragma unroll
+  for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+    const uint32_t e = wave * (64 * RDX_ROUNDS) + r * 64 + lane;
+    const uint32_t i = base + e;
+    vv[r] = i < n;
+    vg[r] = vv[r] ? s.group[i] : 0u;
+    vv[r] = vv[r] && vg[r] < G;
+    vi[r] = vv[r] ? s.info[i] : 0u;
+    vo[r] = vv[r] ? (s.orig ? s.orig[i] : i) : 0u;
+    vt[r] = vv[r] ? s.term[i] : 0ull;
+    vx[r] = vv[r] ? s.index[i] : 0ull;
+    vd[r] = ((vg[r] >> PART_LOG) >> shift) & (RDX_BINS - 1);
+  }
+  // stable rank inside the wave: rounds in order, lanes in order
+#pragma unroll
+  for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+    uint64_t peers = __ballot(vv[r]);
+#pragma unroll
+    for (uint32_t k = 0; k < RDX_BITS; ++k) {
+      const bool bit = (vd[r] >> k) & 1u;
       const uint64_t bk = __ballot(bit);
       peers &= bit ? bk : ~bk;
     }
-    if (valid) {
-      const uint32_t rank = (uint32_t)__popcll(peers & lt);
-      const uint32_t basepos = cnt[key];
-      const uint32_t pos = basepos + rank;
-      a.p_info[pos] = (a.b.info[i] & 0xFFFFu) | ((gg & (PART - 1)) << 16);
-      a.p_orig[pos] = (uint32_t)i;
-      a.p_term[pos] = a.b.term[i];
-      a.p_index[pos] = a.b.index[i];
-      if (rank == 0) cnt[key] = basepos + (uint32_t)__popcll(peers);
+    const uint32_t rank = (uint32_t)__popcll(peers & lt);
+    const uint32_t before = vv[r] ? s_wcnt[wave][vd[r]] : 0u;
+    vr[r] = before + rank;
+    if (vv[r] && rank == 0) s_wcnt[wave][vd[r]] = before + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  // per digit: prefix over waves, then digit starts inside the tile
+  if (tid < RDX_BINS) {
+    uint32_t run = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < RDX_WAVES; ++w) {
+      const uint32_t c = s_wcnt[w][tid];
+      s_wcnt[w][tid] = run;
+      run += c;
+    }
+    const uint32_t incl = wave_incl_scan(run);
+    s_dstart[tid] = incl - run;
+    if (tid == RDX_BINS - 1) s_dstart[RDX_BINS] = incl;
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+    if (vv[r]) {
+      const uint32_t p = s_dstart[vd[r]] + s_wcnt[wave][vd[r]] + vr[r];
+      st_group[p] = vg[r];
+      st_info[p] = vi[r];
+      st_orig[p] = vo[r];
+      st_term[p] = vt[r];
+      st_index[p] = vx[r];
     }
   }
+  __syncthreads();
+  const uint32_t valid = s_dstart[RDX_BINS];
+#pragma unroll
+  for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+    const uint32_t p = r * RDX_THREADS + tid;
+    if (p < valid) {
+      const uint32_t g = st_group[p];
+      const uint32_t dg = ((g >> PART_LOG) >> shift) & (RDX_BINS - 1);
+      const uint32_t o = s_off[dg] + (p - s_dstart[dg]);
+      d.group[o] = g;
+      d.info[o] = final_pass ? ((st_info[p] & 0xFFFFu) | ((g & (PART - 1)) << 16)) : st_info[p];
+      d.orig[o] = st_orig[p];
+      d.term[o] = st_term[p];
+      d.index[o] = st_index[p];
+    }
+  }
+}
+
+// part_off[b] = first position of partition b in the sorted batch (b <= NB).
+__global__ void k_part_bounds(const uint32_t* sorted_group, const uint32_t* n_dev, uint32_t NB, uint32_t* part_off) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > NB) return;
+  uint32_t lo = 0, hi = *n_dev;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((sorted_group[mid] >> PART_LOG) < b) lo = mid + 1;
+    else hi = mid;
+  }
+  part_off[b] = lo;
 }
 
 // ============================================================================
@@ -237,7 +297,7 @@ struct ApplyArgs {
 enum { ST_MSGS, ST_APPRESP, ST_VOTERESP, ST_DROPPED, ST_COMMITS, ST_WON, ST_LOST, ST_FAULTS, ST_ENTRIES, ST_N };
 
 template <int NMAX>
-__global__ void __launch_bounds__(1024) k_apply(ApplyArgs a) {
+__global__ void __launch_bounds__(PART, (NMAX <= 3 ? 3 : 2)) k_apply(ApplyArgs a) {
   __shared__ uint32_t l_info[CHUNK];
   __shared__ uint32_t l_orig[CHUNK];
   __shared__ uint64_t l_term[CHUNK];
@@ -526,14 +586,13 @@ struct hb_handle {
   DevState st{};
   std::vector<void*> allocs;
   // partition scratch
-  uint32_t* hist = nullptr;
-  uint64_t hist_cap = 0;
-  uint32_t* scan_sums = nullptr;
-  uint32_t* part_off = nullptr;
-  uint32_t* p_info = nullptr;
-  uint32_t* p_orig = nullptr;
-  uint64_t* p_term = nullptr;
-  uint64_t* p_index = nullptr;
+  uint32_t* hist = nullptr;       // [RDX_BINS][tiles]
+  uint32_t* n_valid = nullptr;    // messages kept after pass 1 (device)
+  uint32_t* totals = nullptr;     // [RDX_BINS] digit totals of the current pass
+  uint32_t* part_off = nullptr;   // [NB + 1]
+  RadixDst tmp[2] = {};           // intermediate passes (ping-pong)
+  RadixDst fin = {};              // final pass = apply input
+  uint32_t passes = 1;
   // host-pointer staging
   uint32_t* s_group = nullptr;
   uint32_t* s_info = nullptr;
@@ -549,8 +608,9 @@ struct hb_handle {
   uint64_t* ev_off = nullptr;     // [NB]
   uint64_t* stats_part = nullptr;
   uint64_t* stats = nullptr;
-  hipEvent_t ph[HB_PHASE_COUNT + 1] = {};
-  bool profiled = false;
+  static constexpr uint32_t PROF_RING = 256;
+  hipEvent_t ph[PROF_RING][HB_PHASE_COUNT + 1] = {};
+  uint32_t prof_n = 0;  // profiled steps since hb_phase_reset
   bool stepped = false;
 };
 
@@ -646,16 +706,24 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(s.pending, R * G);
   ALLOC(s.pm, R * G);
   ALLOC(s.ring, R * (size_t)max_inflight * G);
-  // partition scratch: hist budget ~ max(batch, 1M) entries
-  h->hist_cap = std::max<uint64_t>(max_batch, 1u << 20) + (uint64_t)h->NB * 64;
-  ALLOC(h->hist, h->hist_cap);
-  ALLOC(h->scan_sums, h->hist_cap / SCAN_TILE + 2);
-  ALLOC(h->part_off, h->NB + 1);
+  // partition scratch
   const size_t mb = max_batch ? max_batch : 1;
-  ALLOC(h->p_info, mb);
-  ALLOC(h->p_orig, mb);
-  ALLOC(h->p_term, mb);
-  ALLOC(h->p_index, mb);
+  const uint32_t pbits = std::max<uint32_t>(ceil_log2(h->NB), 1);
+  h->passes = (pbits + RDX_BITS - 1) / RDX_BITS;
+  const size_t tiles_max = (mb + RDX_TILE - 1) / RDX_TILE;
+  ALLOC(h->hist, (size_t)RDX_BINS * tiles_max);
+  ALLOC(h->n_valid, 4);
+  ALLOC(h->totals, RDX_BINS);
+  ALLOC(h->part_off, h->NB + 1);
+  for (uint32_t k = 0; k < 3; ++k) {
+    RadixDst& d = k < 2 ? h->tmp[k] : h->fin;
+    if (k < 2 && h->passes < 2 + k) continue;  // ping-pong buffers only when needed
+    ALLOC(d.group, mb);
+    ALLOC(d.info, mb);
+    ALLOC(d.orig, mb);
+    ALLOC(d.term, mb);
+    ALLOC(d.index, mb);
+  }
   ALLOC(h->s_group, mb);
   ALLOC(h->s_info, mb);
   ALLOC(h->s_term, mb);
@@ -675,11 +743,12 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
     hb_destroy(h);
     return rc;
   }
-  for (auto& e : h->ph)
-    if (hipEventCreate(&e) != hipSuccess) {
-      hb_destroy(h);
-      return HB_EDEVICE;
-    }
+  for (auto& row : h->ph)
+    for (auto& e : row)
+      if (hipEventCreate(&e) != hipSuccess) {
+        hb_destroy(h);
+        return HB_EDEVICE;
+      }
   // empty slots (n = 0), zeroed progress
   if (hipMemset(s.meta, 0, G * 8) != hipSuccess || hipMemset(s.pm, 0, R * G * 4) != hipSuccess ||
       hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess ||
@@ -697,8 +766,9 @@ int hb_destroy(hb_handle* h) {
   DeviceGuard guard(h->device);
   (void)hipDeviceSynchronize();
   for (void* p : h->allocs) (void)hipFree(p);
-  for (auto& e : h->ph)
-    if (e) (void)hipEventDestroy(e);
+  for (auto& row : h->ph)
+    for (auto& e : row)
+      if (e) (void)hipEventDestroy(e);
   delete h;
   return HB_OK;
 }
@@ -836,55 +906,38 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     bd.hint = b->hint ? h->s_hint : nullptr;
     bd.props = b->props ? h->s_props : nullptr;
   }
-  if (prof) HB_CHECK(hipEventRecord(h->ph[0], st));
+  hipEvent_t* ev = h->ph[h->prof_n % hb_handle::PROF_RING];
+  if (prof) HB_CHECK(hipEventRecord(ev[0], st));
 
   // ---- phase 1: partition ----------------------------------------------------
   const uint32_t NB = h->NB;
   if (b->n == 0) {
     HB_CHECK(hipMemsetAsync(h->part_off, 0, (NB + 1) * 4ull, st));
   } else {
-    const uint32_t wpb_max = NB * 4u <= 16384u ? 4u : (NB * 4u <= 32768u ? 2u : 1u);
-    if ((uint64_t)NB * 4u > 65536u) return HB_EINVAL;  // > 16384 partitions: not supported
-    // waves so that NB * NW fits the histogram budget and spans are >= 256 messages
-    uint64_t nw_budget = (h->hist_cap - 64) / NB;
-    uint64_t nw_target = std::min<uint64_t>(std::max<uint64_t>(nw_budget, 1), 4096);
-    uint64_t span = (b->n + nw_target - 1) / nw_target;
-    span = std::max<uint64_t>(256, (span + 63) / 64 * 64);
-    const uint32_t NW = (uint32_t)((b->n + span - 1) / span);
-    if ((uint64_t)NB * NW > h->hist_cap) return HB_EINVAL;
-    PartArgs pa;
-    pa.b = bd;
-    pa.G = h->G;
-    pa.NB = NB;
-    pa.NW = NW;
-    pa.span = (uint32_t)span;
-    pa.wpb = wpb_max;
-    pa.key_bits = ceil_log2(NB);
-    pa.hist = h->hist;
-    pa.p_info = h->p_info;
-    pa.p_orig = h->p_orig;
-    pa.p_term = h->p_term;
-    pa.p_index = h->p_index;
-    const uint32_t blocks = (NW + pa.wpb - 1) / pa.wpb;
-    const size_t shm = (size_t)pa.wpb * NB * 4;
-    hipLaunchKernelGGL(k_hist, dim3(blocks), dim3(256), shm, st, pa);
-    const uint64_t len = (uint64_t)NB * NW;
-    const uint32_t tiles = (uint32_t)((len + SCAN_TILE - 1) / SCAN_TILE);
-    hipLaunchKernelGGL(k_scan_sums, dim3(tiles), dim3(1024), 0, st, h->hist, len, h->scan_sums);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, st, h->scan_sums, tiles);
-    hipLaunchKernelGGL(k_scan_apply, dim3(tiles), dim3(1024), 0, st, h->hist, len, h->scan_sums, NW, NB,
-                       h->part_off, 0u);
-    hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(256), shm, st, pa);
+    const uint32_t ntiles = (uint32_t)((b->n + RDX_TILE - 1) / RDX_TILE);
+    RadixSrc src{bd.group, bd.info, nullptr, bd.term, bd.index, nullptr, (uint32_t)b->n};
+    for (uint32_t p = 0; p < h->passes; ++p) {
+      const bool last_pass = p + 1 == h->passes;
+      const RadixDst& dst = last_pass ? h->fin : h->tmp[p & 1];
+      const uint32_t shift = p * RDX_BITS;
+      hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(RDX_THREADS), 0, st, src, h->G, shift, ntiles, h->hist);
+      hipLaunchKernelGGL(k_scan_rows, dim3(RDX_BINS), dim3(1024), 0, st, h->hist, ntiles, h->totals);
+      hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(RDX_THREADS), 0, st, src, dst, h->G, shift, ntiles,
+                         (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid, last_pass ? 1u : 0u);
+      src = RadixSrc{dst.group, dst.info, dst.orig, dst.term, dst.index, h->n_valid, (uint32_t)b->n};
+    }
+    hipLaunchKernelGGL(k_part_bounds, dim3((NB + 1 + 255) / 256), dim3(256), 0, st, (const uint32_t*)h->fin.group,
+                       (const uint32_t*)h->n_valid, NB, h->part_off);
   }
-  if (prof) HB_CHECK(hipEventRecord(h->ph[1], st));
+  if (prof) HB_CHECK(hipEventRecord(ev[1], st));
 
   // ---- phase 2: apply ----------------------------------------------------------
   ApplyArgs aa;
   aa.S = h->st;
-  aa.p_info = h->p_info;
-  aa.p_orig = h->p_orig;
-  aa.p_term = h->p_term;
-  aa.p_index = h->p_index;
+  aa.p_info = h->fin.info;
+  aa.p_orig = h->fin.orig;
+  aa.p_term = h->fin.term;
+  aa.p_index = h->fin.index;
   aa.hint = bd.hint;
   aa.props = bd.props;
   aa.part_off = h->part_off;
@@ -899,12 +952,12 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     case 5: launch_apply<5>(h, aa); break;
     default: launch_apply<7>(h, aa); break;
   }
-  if (prof) HB_CHECK(hipEventRecord(h->ph[2], st));
+  if (prof) HB_CHECK(hipEventRecord(ev[2], st));
   // ---- phase 3: finish -----------------------------------------------------------
   hipLaunchKernelGGL(k_finish, dim3(1), dim3(1024), 0, st, h->stats_part, NB, h->stats);
-  if (prof) HB_CHECK(hipEventRecord(h->ph[3], st));
+  if (prof) HB_CHECK(hipEventRecord(ev[3], st));
   HB_CHECK(hipGetLastError());
-  h->profiled = prof;
+  if (prof) h->prof_n++;
   h->stepped = true;
   return HB_OK;
 }
@@ -952,11 +1005,34 @@ int hb_stats(hb_handle* h, uint64_t* out) {
   return HB_OK;
 }
 
-int hb_phase_ms(hb_handle* h, float* out) {
-  if (!h || !out || !h->profiled) return HB_EINVAL;
+int hb_phase_ms(hb_handle* h, float* out, uint32_t* steps) {
+  if (!h || !out) return HB_EINVAL;
   DeviceGuard guard(h->device);
-  HB_CHECK(hipEventSynchronize(h->ph[HB_PHASE_COUNT]));
-  for (int i = 0; i < HB_PHASE_COUNT; ++i) HB_CHECK(hipEventElapsedTime(&out[i], h->ph[i], h->ph[i + 1]));
+  const uint32_t n = std::min<uint32_t>(h->prof_n, hb_handle::PROF_RING);
+  if (steps) *steps = n;
+  for (int i = 0; i < HB_PHASE_COUNT; ++i) out[i] = 0.f;
+  if (n == 0) return HB_EINVAL;
+  HB_CHECK(hipStreamSynchronize(h->stream));
+  for (uint32_t k = 0; k < n; ++k) {
+    for (int i = 0; i < HB_PHASE_COUNT; ++i) {
+      float ms = 0.f;
+      HB_CHECK(hipEventElapsedTime(&ms, h->ph[k][i], h->ph[k][i + 1]));
+      out[i] += ms / (float)n;
+    }
+  }
+  return HB_OK;
+}
+
+int hb_phase_reset(hb_handle* h) {
+  if (!h) return HB_EINVAL;
+  h->prof_n = 0;
+  return HB_OK;
+}
+
+int hb_stats_to(hb_handle* h, uint64_t* dev_dst) {
+  if (!h || !dev_dst) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  HB_CHECK(hipMemcpyAsync(dev_dst, h->stats, HB_STAT_COUNT * 8, hipMemcpyDeviceToDevice, h->stream));
   return HB_OK;
 }
 

@@ -19,9 +19,9 @@
 
 namespace hb {
 
-constexpr int PART_LOG = 10;                 // groups per partition = apply workgroup
-constexpr uint32_t PART = 1u << PART_LOG;    // 1024 lanes, one group each
-constexpr uint32_t CHUNK = 2048;             // messages staged in LDS per round
+constexpr int PART_LOG = 9;                  // groups per partition = apply workgroup
+constexpr uint32_t PART = 1u << PART_LOG;    // 512 lanes, one group each
+constexpr uint32_t CHUNK = 2048;             // messages staged in LDS per round (4 per lane)
 
 // ---- packed group meta (u64) ------------------------------------------------
 //  [0:2) state  [2:5) n  [5:9) self slot  [9:13) lead ref  [13:17) vote ref
@@ -137,6 +137,7 @@ constexpr uint32_t D_SLOT0 = 8;  // bit D_SLOT0 + s: slot s (match, next, pm)
 
 struct Pr {
   uint64_t match, next;
+  uint64_t head;  // inflights.buffer[start] (valid while count > 0)
   uint32_t pm;
 };
 
@@ -167,6 +168,7 @@ struct Lane {
   uint64_t arrival;
   uint64_t term, committed, first, last, tfirst, tlast, meta;
   typename SlotVec<NMAX>::u64 match, next;
+  typename SlotVec<NMAX>::u64 head;  // register copy of each ring's head entry
   typename SlotVec<NMAX>::u32 pm;
   uint32_t dirty;
   uint32_t won, lost;
@@ -213,12 +215,14 @@ struct Lane {
     p.match = match[s];
     p.next = next[s];
     p.pm = pm[s];
+    p.head = head[s];
     return p;
   }
   __device__ __forceinline__ void put(uint32_t s, const Pr& p) {
     match[s] = p.match;
     next[s] = p.next;
     pm[s] = p.pm;
+    head[s] = p.head;
     dirty |= 1u << (D_SLOT0 + s);
   }
 
@@ -236,10 +240,12 @@ struct Lane {
         match[s] = S.match[(size_t)s * S.G + g];
         next[s] = S.next[(size_t)s * S.G + g];
         pm[s] = S.pm[(size_t)s * S.G + g];
+        head[s] = pm_count(pm[s]) ? *ring_at(s, pm_start(pm[s])) : 0;
       } else {
         match[s] = 0;
         next[s] = 0;
         pm[s] = 0;
+        head[s] = 0;
       }
     }
     dirty = 0;
@@ -313,17 +319,24 @@ struct Lane {
     return true;
   }
   // inflights.freeTo raft/progress.go:204-224
+  // (the head entry comes from the register copy; only entries behind it are read)
   __device__ __forceinline__ void free_to(uint32_t s, Pr& p, uint64_t to) const {
-    uint32_t cnt = pm_count(p.pm);
+    const uint32_t cnt = pm_count(p.pm);
     if (cnt == 0) return;
+    uint64_t v = p.head;
+    if (to < v) return;
     uint32_t idx = pm_start(p.pm);
     const uint32_t W = S.W;
     uint32_t i = 0;
-    for (; i < cnt; ++i) {
-      if (to < *ring_at(s, idx)) break;
+    while (true) {
+      ++i;
       if (++idx >= W) idx -= W;
+      if (i == cnt) break;
+      v = *ring_at(s, idx);
+      if (to < v) break;
     }
     p.pm = pm_make(pm_state(p.pm), pm_paused(p.pm), idx, cnt - i);
+    p.head = v;
   }
 
   // ---------------------------------------------------------------- log
@@ -396,6 +409,7 @@ struct Lane {
         uint32_t idx = start + cnt;
         if (idx >= S.W) idx -= S.W;
         *ring_at(s, idx) = lastsent;                    // inflights.add
+        if (cnt == 0) p.head = lastsent;
         p.next = lastsent + 1;                          // optimisticUpdate
         p.pm = pm_make(HB_PR_REPLICATE, pm_paused(p.pm), start, cnt + 1);
       } else if (st == HB_PR_PROBE) {
@@ -542,7 +556,7 @@ struct Lane {
               }
             } else if (type == HB_MSG_HEARTBEAT_RESP) {          // :547-554
               if (ps == HB_PR_REPLICATE && pm_count(p.pm) == S.W)
-                free_to(from, p, *ring_at(from, pm_start(p.pm)));  // freeFirstOne
+                free_to(from, p, p.head);                        // freeFirstOne
               if (p.match < last) {
                 send = SEND_ONE;
                 send_to = from;

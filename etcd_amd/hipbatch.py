@@ -57,7 +57,9 @@ def lib():
         "hb_copy_events": (C.c_int, [H, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
         "hb_stats_device": (C.c_int, [H, P(C.c_void_p)]),
         "hb_stats": (C.c_int, [H, C.c_void_p]),
-        "hb_phase_ms": (C.c_int, [H, C.c_void_p]),
+        "hb_phase_ms": (C.c_int, [H, C.c_void_p, P(C.c_uint32)]),
+        "hb_phase_reset": (C.c_int, [H]),
+        "hb_stats_to": (C.c_int, [H, C.c_void_p]),
         "hb_alloc_pinned": (C.c_int, [C.c_size_t, P(C.c_void_p)]),
         "hb_free_pinned": (C.c_int, [C.c_void_p]),
     }
@@ -185,7 +187,17 @@ class Engine:
         _check("hb_stats_device", lib().hb_stats_device(self.h, C.byref(p)))
         return p.value
 
+    def stats_to(self, dev_ptr):
+        """Async D2D copy of the last step's stats to a device buffer (torch tensor or int)."""
+        _check("hb_stats_to", lib().hb_stats_to(self.h, C.c_void_p(_ptr(dev_ptr) if not isinstance(dev_ptr, int)
+                                                                   else dev_ptr)))
+
+    def phase_reset(self):
+        _check("hb_phase_reset", lib().hb_phase_reset(self.h))
+
     def phase_ms(self):
+        """(per-phase average ms, number of profiled steps) since phase_reset()."""
         out = np.zeros(abi.HB_PHASE_COUNT, dtype=np.float32)
-        _check("hb_phase_ms", lib().hb_phase_ms(self.h, out.ctypes.data))
-        return out
+        n = C.c_uint32()
+        _check("hb_phase_ms", lib().hb_phase_ms(self.h, out.ctypes.data, C.byref(n)))
+        return out, n.value

@@ -1,0 +1,54 @@
+"""Multi-GPU sharding of raft groups.
+
+Groups are independent (raft/multinode.go:125-131), so they shard by a hash of
+the group id over the GPUs of a node with no data-path collective:
+gpu = splitmix64(group_id) % world.  The host routes every message by the same
+hash; each GPU owns a dense local slot space.  The only collective is one
+all-reduce of the per-step statistics (RCCL over xGMI on GPUs, gloo in CPU
+tests).
+"""
+import numpy as np
+
+from .synth import splitmix64
+
+
+def owner(group_ids, world):
+    """GPU rank that owns each global group id."""
+    return (splitmix64(np.asarray(group_ids, dtype=np.uint64)) % np.uint64(world)).astype(np.int64)
+
+
+class ShardMap:
+    """Global group id <-> (rank, local slot) for one rank."""
+
+    def __init__(self, group_ids, world, rank):
+        ids = np.asarray(group_ids, dtype=np.uint64)
+        own = owner(ids, world)
+        self.world, self.rank = world, rank
+        self.local_ids = ids[own == rank]               # local slot -> global id
+        self._sorted = np.argsort(self.local_ids, kind="stable")
+        self._keys = self.local_ids[self._sorted]
+
+    def __len__(self):
+        return len(self.local_ids)
+
+    def local_slot(self, gids):
+        """Local slots of global ids owned by this rank (-1 if not owned)."""
+        gids = np.asarray(gids, dtype=np.uint64)
+        pos = np.searchsorted(self._keys, gids)
+        pos = np.minimum(pos, len(self._keys) - 1) if len(self._keys) else pos
+        hit = (len(self._keys) > 0) & (self._keys[pos] == gids) if len(self._keys) else np.zeros(len(gids), bool)
+        out = np.full(len(gids), -1, dtype=np.int64)
+        out[hit] = self._sorted[pos[hit]]
+        return out
+
+    def route(self, gids):
+        """Split a message batch by owner rank: returns rank -> indices (arrival order kept)."""
+        own = owner(gids, self.world)
+        return {r: np.nonzero(own == r)[0] for r in range(self.world)}
+
+
+def reduce_stats(stats_tensor, dist=None):
+    """Sum a per-rank HB_STAT_COUNT u64 vector over ranks (one all-reduce)."""
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(stats_tensor)
+    return stats_tensor

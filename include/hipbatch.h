@@ -291,8 +291,13 @@ int  hb_copy_events(hb_handle* h, hb_event* out, uint64_t cap, uint64_t* n);
  * RCCL all-reduce on the same stream) or a synchronous host copy. */
 int  hb_stats_device(hb_handle* h, uint64_t** dev_stats);
 int  hb_stats(hb_handle* h, uint64_t* out);
-/* Per-phase device time in ms of the last HB_STEP_PROFILE step. */
-int  hb_phase_ms(hb_handle* h, float* out /* [HB_PHASE_COUNT] */);
+/* Asynchronous device-to-device copy of the last step's statistics (on the
+ * handle's stream), e.g. into a buffer that an RCCL all-reduce then sums. */
+int  hb_stats_to(hb_handle* h, uint64_t* dev_dst /* [HB_STAT_COUNT] */);
+/* Per-phase device time (ms) averaged over the HB_STEP_PROFILE steps since
+ * hb_phase_reset (the last 256 of them); *steps = how many (synchronizes). */
+int  hb_phase_ms(hb_handle* h, float* out /* [HB_PHASE_COUNT] */, uint32_t* steps);
+int  hb_phase_reset(hb_handle* h);
 
 /* ---- pinned host memory for cgo callers (Go must not hand Go memory to C
  * that C retains; raft/hipbatch packs batches into these buffers). -------- */
