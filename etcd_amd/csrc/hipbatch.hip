@@ -297,7 +297,7 @@ struct ApplyArgs {
 enum { ST_MSGS, ST_APPRESP, ST_VOTERESP, ST_DROPPED, ST_COMMITS, ST_WON, ST_LOST, ST_FAULTS, ST_ENTRIES, ST_N };
 
 template <int NMAX>
-__global__ void __launch_bounds__(PART, (NMAX <= 3 ? 3 : 2)) k_apply(ApplyArgs a) {
+__global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_APPLY_WAVES3 : 2)) k_apply(ApplyArgs a) {
   __shared__ uint32_t l_info[CHUNK];
   __shared__ uint32_t l_orig[CHUNK];
   __shared__ uint64_t l_term[CHUNK];
@@ -332,37 +332,66 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? 3 : 2)) k_apply(ApplyArgs a
   L.lost = 0;
   L.dirty = 0;
 
-  // A group takes part when its slot is live (n > 0) and not faulted.
+  // ---- issue every load of the lane up front (one memory round trip):
+  // meta, proposal, the whole group state, and the first LDS round of the
+  // partition's messages.
+  const uint32_t seg_lo = a.part_off[part], seg_hi = a.part_off[part + 1];
+  const bool wg_work = a.props_on || seg_hi > seg_lo;  // uniform over the workgroup
   L.meta = gvalid ? a.S.meta[g] : 0;
+  const uint32_t prop_raw = (a.props && gvalid) ? a.props[g] : 0u;
+  if (wg_work && gvalid) L.load_all();
+  constexpr uint32_t PER = CHUNK / PART;
+  const uint32_t len0 = (seg_hi - seg_lo) < CHUNK ? (seg_hi - seg_lo) : CHUNK;
+  uint32_t pf_info[PER], pf_orig[PER];
+  uint64_t pf_term[PER], pf_index[PER];
+#pragma unroll
+  for (uint32_t k = 0; k < PER; ++k) {
+    const uint32_t i = tid + k * PART;
+    if (i < len0) {
+      pf_info[k] = a.p_info[seg_lo + i];
+      pf_orig[k] = a.p_orig[seg_lo + i];
+      pf_term[k] = a.p_term[seg_lo + i];
+      pf_index[k] = a.p_index[seg_lo + i];
+    }
+  }
+  // A group takes part when its slot is live (n > 0) and not faulted.
   const bool live = gvalid && m_n(L.meta) != 0 && m_fault(L.meta) == 0;
-  bool loaded = false;
-  uint64_t commit0 = 0, last0 = 0;
+  const uint64_t commit0 = L.committed, last0 = L.last;
+  bool touched = false;
   uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
 
   __syncthreads();
 
-  const uint32_t prop_k = (a.props && live) ? a.props[g] : 0u;
+  const uint32_t prop_k = live ? prop_raw : 0u;
   if (prop_k) {
-    L.load();
-    loaded = true;
-    commit0 = L.committed;
-    last0 = L.last;
+    touched = true;
     L.arrival = HB_NO_INDEX;
     L.step(HB_MSG_PROP, L.self(), 0, prop_k, false, 0);
   }
 
-  const uint32_t seg_lo = a.part_off[part], seg_hi = a.part_off[part + 1];
   for (uint32_t c0 = seg_lo; c0 < seg_hi; c0 += CHUNK) {
     const uint32_t len = (seg_hi - c0) < CHUNK ? (seg_hi - c0) : CHUNK;
     l_cnt[tid] = 0;
     __syncthreads();
-    for (uint32_t i = tid; i < len; i += PART) {
-      const uint32_t inf = a.p_info[c0 + i];
-      l_info[i] = inf;
-      l_orig[i] = a.p_orig[c0 + i];
-      l_term[i] = a.p_term[c0 + i];
-      l_index[i] = a.p_index[c0 + i];
-      atomicAdd(&l_cnt[inf >> 16], 1u);
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      const uint32_t i = tid + k * PART;
+      if (i < len) {
+        uint32_t inf;
+        if (c0 == seg_lo) {
+          inf = pf_info[k];
+          l_orig[i] = pf_orig[k];
+          l_term[i] = pf_term[k];
+          l_index[i] = pf_index[k];
+        } else {
+          inf = a.p_info[c0 + i];
+          l_orig[i] = a.p_orig[c0 + i];
+          l_term[i] = a.p_term[c0 + i];
+          l_index[i] = a.p_index[c0 + i];
+        }
+        l_info[i] = inf;
+        atomicAdd(&l_cnt[inf >> 16], 1u);
+      }
     }
     __syncthreads();
     const uint32_t my_cnt = l_cnt[tid];
@@ -376,6 +405,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? 3 : 2)) k_apply(ApplyArgs a
     }
     __syncthreads();
     if (my_cnt && live) {
+      touched = true;
       // restore arrival order inside this lane's run (tiny insertion sort)
       for (uint32_t x = 1; x < my_cnt; ++x) {
         const uint16_t v = l_perm[my_start + x];
@@ -385,12 +415,6 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? 3 : 2)) k_apply(ApplyArgs a
           --y;
         }
         l_perm[my_start + y] = v;
-      }
-      if (!loaded) {
-        L.load();
-        loaded = true;
-        commit0 = L.committed;
-        last0 = L.last;
       }
       for (uint32_t j = 0; j < my_cnt; ++j) {
         const uint32_t i = l_perm[my_start + j];
@@ -416,7 +440,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? 3 : 2)) k_apply(ApplyArgs a
 
   uint32_t st_commit = 0, st_fault = 0;
   uint64_t st_entries = 0;
-  if (loaded) {
+  if (touched) {
     L.store();
     st_commit = L.committed > commit0;
     st_fault = L.faulted() != 0;

@@ -21,6 +21,9 @@ namespace hb {
 
 constexpr int PART_LOG = 9;                  // groups per partition = apply workgroup
 constexpr uint32_t PART = 1u << PART_LOG;    // 512 lanes, one group each
+#ifndef HB_APPLY_WAVES3
+#define HB_APPLY_WAVES3 4
+#endif
 constexpr uint32_t CHUNK = 2048;             // messages staged in LDS per round (4 per lane)
 
 // ---- packed group meta (u64) ------------------------------------------------
@@ -226,28 +229,24 @@ struct Lane {
     dirty |= 1u << (D_SLOT0 + s);
   }
 
-  __device__ __forceinline__ void load() {
+  // Load every field of the group (all NMAX slots, independent of meta, so all
+  // loads of a lane are in flight together); slots >= n hold zeros (k_load).
+  // A ring head is read only for a non-empty ring.
+  __device__ __forceinline__ void load_all() {
     term = S.term[g];
     committed = S.commit[g];
     first = S.first[g];
     last = S.last[g];
     tfirst = S.tfirst[g];
     tlast = S.tlast[g];
-    const uint32_t nn = n();
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) {
-      if ((uint32_t)s < nn) {
-        match[s] = S.match[(size_t)s * S.G + g];
-        next[s] = S.next[(size_t)s * S.G + g];
-        pm[s] = S.pm[(size_t)s * S.G + g];
-        head[s] = pm_count(pm[s]) ? *ring_at(s, pm_start(pm[s])) : 0;
-      } else {
-        match[s] = 0;
-        next[s] = 0;
-        pm[s] = 0;
-        head[s] = 0;
-      }
+      match[s] = S.match[(size_t)s * S.G + g];
+      next[s] = S.next[(size_t)s * S.G + g];
+      pm[s] = S.pm[(size_t)s * S.G + g];
     }
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) head[s] = pm_count(pm[s]) ? *ring_at(s, pm_start(pm[s])) : 0;
     dirty = 0;
   }
 

@@ -12,7 +12,7 @@ import numpy as np
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhipbatch.so")
+LIB_PATH = os.environ.get("HB_LIB", os.path.join(_HERE, "libhipbatch.so"))
 _lib = None
 
 
