@@ -59,6 +59,31 @@ def cpu_baseline(n, groups=200_000, budget_s=10.0, max_steps=40):
                       f"{groups} groups x {n}, {steps} cfg2 steps, {acks} MsgAppResp in {spent:.2f} s"}
 
 
+def pmc_traffic(path, kernel, G, n, apply_us):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (FETCH_SIZE x 2 + WRITE_SIZE, tools/prof_summary.py).  Used only when the
+    profile was taken on the same workload and its average duration agrees with
+    the live measurement within 15 % (same build); otherwise None."""
+    import glob
+    if path is None:
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+        if not cands:
+            return None, None
+        path = cands[-1]
+    try:
+        d = json.load(open(path))
+        k = d["kernels"][kernel]
+        cfg = d["bench"]["config"]
+    except (OSError, KeyError, ValueError):
+        return None, None
+    if cfg.get("groups_per_gpu") != G or cfg.get("replicas") != n or "traffic_bytes" not in k:
+        return None, None
+    src = os.path.relpath(path, ROOT)
+    if abs(k["avg_us"] - apply_us) > 0.15 * apply_us:
+        return None, f"{src}: profiled avg {k['avg_us']:.1f} us vs live {apply_us:.1f} us (stale, not used)"
+    return float(k["traffic_bytes"]), f"{src}: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, avg {k['avg_us']:.1f} us"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -70,8 +95,8 @@ def main():
     ap.add_argument("--cpu-groups", type=int, default=200_000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-profile", action="store_true", help="skip per-phase HIP events")
-    ap.add_argument("--traffic-bytes", type=float, default=None,
-                    help="HBM bytes per apply launch from a rocprofv3 PMC pass (profiles/)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="profiles/<tag>_traffic.json from tools/profile_round.sh (default: newest in profiles/)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -164,10 +189,13 @@ def main():
                  "finish_ms": float(ph[abi.HB_PHASE_FINISH]), "steps": nph}
         alg = alg_bytes_per_group(n) * G  # per apply launch on this GPU
         achieved = float(alg / (float(ph[abi.HB_PHASE_APPLY]) * 1e-3) / 1e9)
+        kname = f"k_apply<{3 if n <= 3 else (5 if n <= 5 else 7)}>"
+        traffic, tsrc = pmc_traffic(args.traffic_json, kname, G, n, float(ph[abi.HB_PHASE_APPLY]) * 1e3)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": args.traffic_bytes,
-                "kernel": f"k_apply<{3 if n <= 3 else (5 if n <= 5 else 7)}>",
+                "traffic": traffic,
+                "traffic_source": tsrc,
+                "kernel": kname,
                 "alg_bytes_per_launch": alg,
                 "alg_bytes_note": f"SURVEY.md 8(d): {alg_bytes_per_group(n)} B/group = "
                                   f"{alg_bytes_per_group(n) / (n - 1):.0f} B/MsgAppResp x {G * (n - 1)} MsgAppResp"}

@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_APPLY_WAVES3 : 2)) k_app
   }
   // A group takes part when its slot is live (n > 0) and not faulted.
   const bool live = gvalid && m_n(L.meta) != 0 && m_fault(L.meta) == 0;
-  const uint64_t commit0 = L.committed, last0 = L.last;
+  const uint64_t last0 = L.last;
   bool touched = false;
   uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
 
@@ -365,32 +365,41 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_APPLY_WAVES3 : 2)) k_app
   const uint32_t prop_k = live ? prop_raw : 0u;
   if (prop_k) {
     touched = true;
-    L.arrival = HB_NO_INDEX;
+    L.arrival = 0xFFFFFFFFu;
     L.step(HB_MSG_PROP, L.self(), 0, prop_k, false, 0);
   }
 
+  // The first round is staged from the prefetch registers before the loop, so
+  // they are dead while messages are stepped.
+  l_cnt[tid] = 0;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < PER; ++k) {
+    const uint32_t i = tid + k * PART;
+    if (i < len0) {
+      l_info[i] = pf_info[k];
+      l_orig[i] = pf_orig[k];
+      l_term[i] = pf_term[k];
+      l_index[i] = pf_index[k];
+      atomicAdd(&l_cnt[pf_info[k] >> 16], 1u);
+    }
+  }
   for (uint32_t c0 = seg_lo; c0 < seg_hi; c0 += CHUNK) {
     const uint32_t len = (seg_hi - c0) < CHUNK ? (seg_hi - c0) : CHUNK;
-    l_cnt[tid] = 0;
-    __syncthreads();
+    if (c0 != seg_lo) {
+      l_cnt[tid] = 0;
+      __syncthreads();
 #pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) {
-      const uint32_t i = tid + k * PART;
-      if (i < len) {
-        uint32_t inf;
-        if (c0 == seg_lo) {
-          inf = pf_info[k];
-          l_orig[i] = pf_orig[k];
-          l_term[i] = pf_term[k];
-          l_index[i] = pf_index[k];
-        } else {
-          inf = a.p_info[c0 + i];
+      for (uint32_t k = 0; k < PER; ++k) {
+        const uint32_t i = tid + k * PART;
+        if (i < len) {
+          const uint32_t inf = a.p_info[c0 + i];
+          l_info[i] = inf;
           l_orig[i] = a.p_orig[c0 + i];
           l_term[i] = a.p_term[c0 + i];
           l_index[i] = a.p_index[c0 + i];
+          atomicAdd(&l_cnt[inf >> 16], 1u);
         }
-        l_info[i] = inf;
-        atomicAdd(&l_cnt[inf >> 16], 1u);
       }
     }
     __syncthreads();
@@ -442,7 +451,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_APPLY_WAVES3 : 2)) k_app
   uint64_t st_entries = 0;
   if (touched) {
     L.store();
-    st_commit = L.committed > commit0;
+    st_commit = (L.dirty & D_COMMIT) != 0;  // commitTo only raises committed
     st_fault = L.faulted() != 0;
     st_entries = L.last - last0;
   }

@@ -19,12 +19,15 @@
 
 namespace hb {
 
-constexpr int PART_LOG = 9;                  // groups per partition = apply workgroup
-constexpr uint32_t PART = 1u << PART_LOG;    // 512 lanes, one group each
-#ifndef HB_APPLY_WAVES3
-#define HB_APPLY_WAVES3 4
+#ifndef HB_PART_LOG
+#define HB_PART_LOG 8
 #endif
-constexpr uint32_t CHUNK = 2048;             // messages staged in LDS per round (4 per lane)
+constexpr int PART_LOG = HB_PART_LOG;        // groups per partition = apply workgroup
+constexpr uint32_t PART = 1u << PART_LOG;    // lanes of the apply workgroup, one group each
+#ifndef HB_APPLY_WAVES3
+#define HB_APPLY_WAVES3 3
+#endif
+constexpr uint32_t CHUNK = 4 * PART;         // messages staged in LDS per round (4 per lane)
 
 // ---- packed group meta (u64) ------------------------------------------------
 //  [0:2) state  [2:5) n  [5:9) self slot  [9:13) lead ref  [13:17) vote ref
@@ -168,7 +171,7 @@ struct Lane {
   DevState S;
   EvSink* E;  // LDS
   uint32_t g;
-  uint64_t arrival;
+  uint32_t arrival;  // batch position of the message; 0xFFFFFFFF: props[] proposal
   uint64_t term, committed, first, last, tfirst, tlast, meta;
   typename SlotVec<NMAX>::u64 match, next;
   typename SlotVec<NMAX>::u64 head;  // register copy of each ring's head entry
@@ -199,6 +202,9 @@ struct Lane {
     set_field(32, 0xFF, grant);
   }
 
+  __device__ __forceinline__ uint64_t arrival_x() const {
+    return arrival == 0xFFFFFFFFu ? HB_NO_INDEX : (uint64_t)arrival;
+  }
   __device__ __forceinline__ void ev(uint32_t type, uint32_t to, uint32_t aux, uint64_t x) {
     emit_ev(E, g, tta(type, to, aux), x);
   }
@@ -577,7 +583,7 @@ struct Lane {
         }
       } else if (st == HB_STATE_CANDIDATE) {
         if (type == HB_MSG_PROP) {
-          ev(HB_EV_PROP_DROP, 0, 0, arrival);                    // :587-589
+          ev(HB_EV_PROP_DROP, 0, 0, arrival_x());                    // :587-589
         } else if (type == HB_MSG_VOTE_RESP) {                   // :603-612
           const uint32_t gr = poll(from < nn ? from : 7u, !reject);
           if (q == gr) {
@@ -590,8 +596,8 @@ struct Lane {
           }
         }
       } else if (type == HB_MSG_PROP) {                          // stepFollower :618-624
-        if (lead() == HB_REF_NONE) ev(HB_EV_PROP_DROP, 0, 0, arrival);
-        else ev(HB_EV_PROP_FWD, lead(), 0, arrival);
+        if (lead() == HB_REF_NONE) ev(HB_EV_PROP_DROP, 0, 0, arrival_x());
+        else ev(HB_EV_PROP_FWD, lead(), 0, arrival_x());
       }
     }
     // ---- transition 2: becomeLeader (+ noop entry) or becomeFollower(Term, None)
@@ -652,7 +658,7 @@ struct Lane {
         put(s, p);
       }
     }
-    if (faulted()) ev(HB_EV_FAULT, 0, faulted(), arrival);  // faulted groups are never stepped
+    if (faulted()) ev(HB_EV_FAULT, 0, faulted(), arrival_x());  // faulted groups are never stepped
   }
 };
 

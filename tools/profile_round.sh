@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round profile on the GPU box:  gpurun -- bash tools/profile_round.sh rNN
+#   1. rocprofv3 --kernel-trace --stats over bench.py   (per-kernel average durations)
+#   2. PMC pass FETCH_SIZE  (own run, MI355X_MICROARCH.md: one counter group per pass)
+#   3. PMC pass WRITE_SIZE
+#   4. plain bench.py (the JSON line, with the traffic the passes measured)
+# Outputs under gpurun_out/<tag>/; tools/prof_summary.py folds them into profiles/.
+set -euo pipefail
+TAG=${1:-r01}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd "$ROOT"
+STEPS=${STEPS:-20}
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+    python3 bench.py --steps "$STEPS" --warmup 5 --no-cpu-baseline > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
+echo "trace done"
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
+    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > "$OUT/pmc_fetch.log" 2>&1
+echo "fetch done"
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
+    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > "$OUT/pmc_write.log" 2>&1
+echo "write done"
+python3 tools/prof_summary.py "$OUT" --tag "$TAG" --out "$OUT/summary" > "$OUT/summary.log"
+echo "summary done"
+timeout -k 10 300 python3 bench.py --traffic-json "$OUT/summary/${TAG}_traffic.json" > "$OUT/bench.json" 2> "$OUT/bench.err"
+echo "bench done"
+tail -1 "$OUT/bench.json"
