@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "hipbatch_kernels.h"
+#include "hipbatch_fast.h"
 
 using namespace hb;
 
@@ -291,173 +292,86 @@ struct ApplyArgs {
   uint32_t* ev_counts;      // [NB] records in each chunk
   uint64_t* ev_off;         // [NB] chunk offsets (records)
   uint64_t* stats_part;     // [NB][HB_STAT_COUNT]
+  uint32_t* pflag;          // [NB][PART/32] groups handed from k_apply_fast to k_apply
+  uint32_t* resume;         // [G] messages consumed by k_apply_fast | prop pending << 31
+  uint64_t* commit0;        // [G] committed at batch start (for HB_STAT_COMMITS)
 };
 
 // stats slots reduced per workgroup
 enum { ST_MSGS, ST_APPRESP, ST_VOTERESP, ST_DROPPED, ST_COMMITS, ST_WON, ST_LOST, ST_FAULTS, ST_ENTRIES, ST_N };
 
-template <int NMAX>
-__global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_APPLY_WAVES3 : 2)) k_apply(ApplyArgs a) {
-  __shared__ uint32_t l_info[CHUNK];
-  __shared__ uint32_t l_orig[CHUNK];
-  __shared__ uint64_t l_term[CHUNK];
-  __shared__ uint64_t l_index[CHUNK];
-  __shared__ uint16_t l_perm[CHUNK];
-  __shared__ uint32_t l_cnt[PART];
-  __shared__ uint32_t sh16[16];
-  __shared__ EvSink l_sink;
-  __shared__ uint64_t l_stats[ST_N];
+#ifndef HB_FAST_WAVES
+#define HB_FAST_WAVES 4
+#endif
+constexpr uint32_t FLAG_WORDS = PART / 32;  // per-partition bitmask of groups handed to k_apply
 
-  const uint32_t tid = threadIdx.x;
-  const uint32_t part = blockIdx.x;
-  const uint32_t g = part * PART + tid;
-  const bool gvalid = g < a.S.G;
+// LDS staging of one round (<= CHUNK messages) of a partition's segment.
+struct Stage {
+  uint32_t info[CHUNK];
+  uint32_t orig[CHUNK];
+  uint64_t term[CHUNK];
+  uint64_t index[CHUNK];
+  uint16_t perm[CHUNK];
+  uint32_t cnt[PART];
+  uint32_t sh16[16];
+};
 
-  if (tid == 0) {
-    // Exact chunk: every event is emitted while stepping a message (or the
-    // group's proposal), at most ev_per_msg per message, so the partition's
-    // chunk is ev_per_msg x (its messages + its proposal slots).
-    const uint64_t off = (uint64_t)a.ev_per_msg * ((uint64_t)a.part_off[part] + (uint64_t)part * PART * a.props_on);
-    l_sink.chunk = a.ev + off;
-    l_sink.fill = 0;
-    a.ev_off[part] = off;
-  }
-  if (tid < ST_N) l_stats[tid] = 0;
-
-  Lane<NMAX> L;
-  L.S = a.S;
-  L.E = &l_sink;
-  L.g = g;
-  L.won = 0;
-  L.lost = 0;
-  L.dirty = 0;
-
-  // ---- issue every load of the lane up front (one memory round trip):
-  // meta, proposal, the whole group state, and the first LDS round of the
-  // partition's messages.
-  const uint32_t seg_lo = a.part_off[part], seg_hi = a.part_off[part + 1];
-  const bool wg_work = a.props_on || seg_hi > seg_lo;  // uniform over the workgroup
-  L.meta = gvalid ? a.S.meta[g] : 0;
-  const uint32_t prop_raw = (a.props && gvalid) ? a.props[g] : 0u;
-  if (wg_work && gvalid) L.load_all();
+// Stage messages [c0, c0+len) of the sorted batch and counting-sort them by
+// group lane: on return the lane's messages are perm[*start, *start+*cnt), in
+// arrival order (the segment is arrival-ordered; the per-lane run is
+// re-sorted by position after the atomic placement).
+__device__ __forceinline__ void stage_round(Stage& sl, const ApplyArgs& a, uint32_t c0, uint32_t len, uint32_t* start,
+                                            uint32_t* cnt) {
   constexpr uint32_t PER = CHUNK / PART;
-  const uint32_t len0 = (seg_hi - seg_lo) < CHUNK ? (seg_hi - seg_lo) : CHUNK;
-  uint32_t pf_info[PER], pf_orig[PER];
-  uint64_t pf_term[PER], pf_index[PER];
-#pragma unroll
-  for (uint32_t k = 0; k < PER; ++k) {
-    const uint32_t i = tid + k * PART;
-    if (i < len0) {
-      pf_info[k] = a.p_info[seg_lo + i];
-      pf_orig[k] = a.p_orig[seg_lo + i];
-      pf_term[k] = a.p_term[seg_lo + i];
-      pf_index[k] = a.p_index[seg_lo + i];
-    }
-  }
-  // A group takes part when its slot is live (n > 0) and not faulted.
-  const bool live = gvalid && m_n(L.meta) != 0 && m_fault(L.meta) == 0;
-  const uint64_t last0 = L.last;
-  bool touched = false;
-  uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
-
-  __syncthreads();
-
-  const uint32_t prop_k = live ? prop_raw : 0u;
-  if (prop_k) {
-    touched = true;
-    L.arrival = 0xFFFFFFFFu;
-    L.step(HB_MSG_PROP, L.self(), 0, prop_k, false, 0);
-  }
-
-  // The first round is staged from the prefetch registers before the loop, so
-  // they are dead while messages are stepped.
-  l_cnt[tid] = 0;
+  const uint32_t tid = threadIdx.x;
+  sl.cnt[tid] = 0;
   __syncthreads();
 #pragma unroll
   for (uint32_t k = 0; k < PER; ++k) {
     const uint32_t i = tid + k * PART;
-    if (i < len0) {
-      l_info[i] = pf_info[k];
-      l_orig[i] = pf_orig[k];
-      l_term[i] = pf_term[k];
-      l_index[i] = pf_index[k];
-      atomicAdd(&l_cnt[pf_info[k] >> 16], 1u);
+    if (i < len) {
+      const uint32_t inf = a.p_info[c0 + i];
+      sl.info[i] = inf;
+      sl.orig[i] = a.p_orig[c0 + i];
+      sl.term[i] = a.p_term[c0 + i];
+      sl.index[i] = a.p_index[c0 + i];
+      atomicAdd(&sl.cnt[inf >> 16], 1u);
     }
   }
-  for (uint32_t c0 = seg_lo; c0 < seg_hi; c0 += CHUNK) {
-    const uint32_t len = (seg_hi - c0) < CHUNK ? (seg_hi - c0) : CHUNK;
-    if (c0 != seg_lo) {
-      l_cnt[tid] = 0;
-      __syncthreads();
-#pragma unroll
-      for (uint32_t k = 0; k < PER; ++k) {
-        const uint32_t i = tid + k * PART;
-        if (i < len) {
-          const uint32_t inf = a.p_info[c0 + i];
-          l_info[i] = inf;
-          l_orig[i] = a.p_orig[c0 + i];
-          l_term[i] = a.p_term[c0 + i];
-          l_index[i] = a.p_index[c0 + i];
-          atomicAdd(&l_cnt[inf >> 16], 1u);
-        }
-      }
-    }
-    __syncthreads();
-    const uint32_t my_cnt = l_cnt[tid];
-    uint32_t total;
-    const uint32_t my_start = block_excl_scan(my_cnt, sh16, &total);
-    l_cnt[tid] = my_start;  // becomes the fill cursor
-    __syncthreads();
-    for (uint32_t i = tid; i < len; i += PART) {
-      const uint32_t pos = atomicAdd(&l_cnt[l_info[i] >> 16], 1u);
-      l_perm[pos] = (uint16_t)i;
-    }
-    __syncthreads();
-    if (my_cnt && live) {
-      touched = true;
-      // restore arrival order inside this lane's run (tiny insertion sort)
-      for (uint32_t x = 1; x < my_cnt; ++x) {
-        const uint16_t v = l_perm[my_start + x];
-        uint32_t y = x;
-        while (y > 0 && l_perm[my_start + y - 1] > v) {
-          l_perm[my_start + y] = l_perm[my_start + y - 1];
-          --y;
-        }
-        l_perm[my_start + y] = v;
-      }
-      for (uint32_t j = 0; j < my_cnt; ++j) {
-        const uint32_t i = l_perm[my_start + j];
-        const uint32_t inf = l_info[i];
-        const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
-        const bool reject = (inf >> 8) & 1u;
-        if (L.faulted()) break;
-        const bool response = type == HB_MSG_APP_RESP || type == HB_MSG_VOTE_RESP ||
-                              type == HB_MSG_HEARTBEAT_RESP || type == HB_MSG_UNREACHABLE;
-        if (from >= L.n() && response) {  // raft/multinode.go:235
-          st_drop++;
-          continue;
-        }
-        L.arrival = l_orig[i];
-        L.step(type, from, l_term[i], l_index[i], reject, (reject && a.hint) ? a.hint[l_orig[i]] : 0ull);
-        st_msgs++;
-        st_app += type == HB_MSG_APP_RESP;
-        st_vote += type == HB_MSG_VOTE_RESP;
-      }
-    }
-    __syncthreads();
+  __syncthreads();
+  const uint32_t my_cnt = sl.cnt[tid];
+  uint32_t total;
+  const uint32_t my_start = block_excl_scan(my_cnt, sl.sh16, &total);
+  sl.cnt[tid] = my_start;  // becomes the fill cursor
+  __syncthreads();
+  for (uint32_t i = tid; i < len; i += PART) {
+    const uint32_t pos = atomicAdd(&sl.cnt[sl.info[i] >> 16], 1u);
+    sl.perm[pos] = (uint16_t)i;
   }
+  __syncthreads();
+  for (uint32_t x = 1; x < my_cnt; ++x) {  // tiny insertion sort of the lane's run
+    const uint16_t v = sl.perm[my_start + x];
+    uint32_t y = x;
+    while (y > 0 && sl.perm[my_start + y - 1] > v) {
+      sl.perm[my_start + y] = sl.perm[my_start + y - 1];
+      --y;
+    }
+    sl.perm[my_start + y] = v;
+  }
+  *start = my_start;
+  *cnt = my_cnt;
+}
 
-  uint32_t st_commit = 0, st_fault = 0;
-  uint64_t st_entries = 0;
-  if (touched) {
-    L.store();
-    st_commit = (L.dirty & D_COMMIT) != 0;  // commitTo only raises committed
-    st_fault = L.faulted() != 0;
-    st_entries = L.last - last0;
-  }
+__device__ __forceinline__ bool is_response(uint32_t type) {  // raft/util.go:53-55
+  return type == HB_MSG_APP_RESP || type == HB_MSG_VOTE_RESP || type == HB_MSG_HEARTBEAT_RESP ||
+         type == HB_MSG_UNREACHABLE;
+}
 
-  // workgroup reduction of the statistics
-  uint64_t vals[ST_N] = {st_msgs, st_app, st_vote, st_drop, st_commit, L.won, L.lost, st_fault, st_entries};
+// Reduce the lane statistics into the partition's stats row (accumulate: the
+// general kernel adds to what the fast kernel wrote).
+__device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_stats, const uint64_t (&vals)[ST_N],
+                                             uint32_t part, bool accumulate) {
+  const uint32_t tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < ST_N; ++k) {
     uint64_t v = vals[k];
@@ -466,9 +380,220 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_APPLY_WAVES3 : 2)) k_app
     if ((tid & 63) == 0 && v) atomicAdd((unsigned long long*)&l_stats[k], (unsigned long long)v);
   }
   __syncthreads();
-  if (tid < ST_N) a.stats_part[(size_t)part * ST_N + tid] = l_stats[tid];
-  if (tid == 0) a.ev_counts[part] = l_sink.fill;
-  if (tid == 1) a.stats_part[(size_t)gridDim.x * ST_N + part] = l_sink.fill;  // events reserved
+  if (tid < ST_N) {
+    uint64_t* dst = &a.stats_part[(size_t)part * ST_N + tid];
+    *dst = (accumulate ? *dst : 0ull) + l_stats[tid];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_apply_fast: one workgroup per partition, one lane per group, steady-state
+// leader operations only (FastLane).  The first message a lane cannot take
+// (and everything after it) is handed to k_apply: the lane's bit is set in
+// pflag[part] and resume[g] = messages already consumed | prop-pending bit.
+// ---------------------------------------------------------------------------
+template <int NMAX>
+__global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply_fast(ApplyArgs a) {
+  __shared__ Stage sl;
+  __shared__ uint32_t l_fill;
+  __shared__ uint32_t l_flag[FLAG_WORDS];
+  __shared__ uint64_t l_stats[ST_N];
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t part = blockIdx.x;
+  const uint32_t g = part * PART + tid;
+  const bool gvalid = g < a.S.G;
+
+  // Exact chunk: every event is emitted while stepping a message (or the
+  // group's proposal), at most ev_per_msg per message, so the partition's
+  // chunk is ev_per_msg x (its messages + its proposal slots).
+  const uint64_t ev_off = (uint64_t)a.ev_per_msg * ((uint64_t)a.part_off[part] + (uint64_t)part * PART * a.props_on);
+  if (tid == 0) {
+    l_fill = 0;
+    a.ev_off[part] = ev_off;
+  }
+  if (tid < ST_N) l_stats[tid] = 0;
+  if (tid < FLAG_WORDS) l_flag[tid] = 0;
+
+  FastLane<NMAX> L;
+  L.S = a.S;
+  L.E.chunk = a.ev + ev_off;
+  L.E.fill = &l_fill;
+  L.g = g;
+  const uint32_t seg_lo = a.part_off[part], seg_hi = a.part_off[part + 1];
+  const bool wg_work = a.props_on || seg_hi > seg_lo;  // uniform over the workgroup
+  L.mlo = gvalid ? reinterpret_cast<const uint32_t*>(a.S.meta)[2 * (size_t)g] : 0u;
+  const uint32_t prop_raw = (a.props && gvalid) ? a.props[g] : 0u;
+  // A group takes part when its slot is live (n > 0) and not faulted.
+  const bool live = gvalid && L.n() != 0 && L.faulted() == 0;
+  L.dirty = 0;
+  L.last = L.committed = 0;
+  if (wg_work && live) L.load();
+  const uint64_t last0 = L.last, commit0 = L.committed;
+
+  bool flagged = false;
+  uint32_t resume = 0;
+  uint32_t st_msgs = 0, st_drop = 0;
+
+  const uint32_t prop_k = live ? prop_raw : 0u;
+  if (prop_k) {
+    if (L.prop_ok(prop_k)) {
+      L.arrival = 0xFFFFFFFFu;
+      L.prop(prop_k);
+    } else {
+      flagged = true;
+      resume = 1u << 31;  // the proposal itself is pending
+    }
+  }
+
+  uint32_t j = 0;  // messages of this lane consumed so far (all rounds)
+  for (uint32_t c0 = seg_lo; c0 < seg_hi; c0 += CHUNK) {
+    const uint32_t len = (seg_hi - c0) < CHUNK ? (seg_hi - c0) : CHUNK;
+    uint32_t my_start, my_cnt;
+    stage_round(sl, a, c0, len, &my_start, &my_cnt);
+    if (live) {
+      for (uint32_t x = 0; x < my_cnt; ++x) {
+        if (flagged || L.faulted()) break;
+        const uint32_t i = sl.perm[my_start + x];
+        const uint32_t inf = sl.info[i];
+        const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
+        const bool reject = (inf >> 8) & 1u;
+        if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
+          st_drop++;
+          j++;
+          continue;
+        }
+        const uint64_t mterm = sl.term[i];
+        if (!L.accept_ok(type, from, mterm, reject)) {
+          flagged = true;
+          resume = j;
+          break;
+        }
+        L.arrival = sl.orig[i];
+        L.accept(from, sl.index[i]);
+        st_msgs++;
+        j++;
+      }
+    }
+    __syncthreads();
+  }
+
+  L.store();
+  if (flagged) {
+    atomicOr(&l_flag[tid >> 5], 1u << (tid & 31));
+    a.resume[g] = resume;
+    a.commit0[g] = commit0;
+  }
+  const uint64_t vals[ST_N] = {st_msgs,
+                               st_msgs,  // every fast message is a MsgAppResp
+                               0,
+                               st_drop,
+                               (uint64_t)(!flagged && L.committed != commit0),  // commitTo only raises
+                               0,
+                               0,
+                               (uint64_t)(L.faulted() != 0 && live),
+                               L.last - last0};
+  reduce_stats(a, l_stats, vals, part, false);
+  if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
+  if (tid == 0) a.ev_counts[part] = l_fill;
+  if (tid == 1) a.stats_part[(size_t)gridDim.x * ST_N + part] = l_fill;  // events reserved
+}
+
+// ---------------------------------------------------------------------------
+// k_apply: the general state machine (Lane::step) for the groups k_apply_fast
+// handed over, from their resume point.  Partitions without such groups exit
+// after reading their flag words.
+// ---------------------------------------------------------------------------
+template <int NMAX>
+__global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
+  __shared__ Stage sl;
+  __shared__ uint32_t l_fill;
+  __shared__ uint32_t l_flag[FLAG_WORDS];
+  __shared__ uint64_t l_stats[ST_N];
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t part = blockIdx.x;
+  const uint32_t g = part * PART + tid;
+  if (tid < FLAG_WORDS) l_flag[tid] = a.pflag[(size_t)part * FLAG_WORDS + tid];
+  __syncthreads();
+  uint32_t any = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < FLAG_WORDS; ++w) any |= l_flag[w];
+  if (!any) return;  // uniform
+  const bool flagged = (l_flag[tid >> 5] >> (tid & 31)) & 1u;
+
+  const uint64_t ev_off = a.ev_off[part];
+  if (tid == 0) l_fill = a.ev_counts[part];  // append after the fast kernel's events
+  if (tid < ST_N) l_stats[tid] = 0;
+
+  Lane<NMAX> L;
+  L.S = a.S;
+  L.E.chunk = a.ev + ev_off;
+  L.E.fill = &l_fill;
+  L.g = g;
+  L.won = 0;
+  L.lost = 0;
+  L.dirty = 0;
+  L.meta = 0;
+  L.last = 0;
+  L.committed = 0;
+  uint32_t resume = 0;
+  uint64_t commit0 = 0;
+  if (flagged) {  // live and not faulted when it was handed over
+    L.meta = a.S.meta[g];
+    L.load_all();
+    resume = a.resume[g];
+    commit0 = a.commit0[g];
+  }
+  const uint64_t last0 = L.last;
+  uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
+  const uint32_t seg_lo = a.part_off[part], seg_hi = a.part_off[part + 1];
+
+  if (flagged && (resume >> 31)) {
+    L.arrival = 0xFFFFFFFFu;
+    L.step(HB_MSG_PROP, L.self(), 0, a.props[g], false, 0);
+  }
+  const uint32_t skip = resume & 0x7FFFFFFFu;
+  uint32_t j = 0;
+  for (uint32_t c0 = seg_lo; c0 < seg_hi; c0 += CHUNK) {
+    const uint32_t len = (seg_hi - c0) < CHUNK ? (seg_hi - c0) : CHUNK;
+    uint32_t my_start, my_cnt;
+    stage_round(sl, a, c0, len, &my_start, &my_cnt);
+    if (flagged) {
+      for (uint32_t x = 0; x < my_cnt; ++x, ++j) {
+        if (j < skip) continue;
+        const uint32_t i = sl.perm[my_start + x];
+        const uint32_t inf = sl.info[i];
+        const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
+        const bool reject = (inf >> 8) & 1u;
+        if (L.faulted()) break;
+        if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
+          st_drop++;
+          continue;
+        }
+        L.arrival = sl.orig[i];
+        L.step(type, from, sl.term[i], sl.index[i], reject, (reject && a.hint) ? a.hint[sl.orig[i]] : 0ull);
+        st_msgs++;
+        st_app += type == HB_MSG_APP_RESP;
+        st_vote += type == HB_MSG_VOTE_RESP;
+      }
+    }
+    __syncthreads();
+  }
+
+  if (flagged) L.store();
+  const uint64_t vals[ST_N] = {st_msgs,
+                               st_app,
+                               st_vote,
+                               st_drop,
+                               (uint64_t)(flagged && L.committed != commit0),
+                               L.won,
+                               L.lost,
+                               (uint64_t)(flagged && L.faulted() != 0),
+                               L.last - last0};
+  reduce_stats(a, l_stats, vals, part, true);
+  if (tid == 0) a.ev_counts[part] = l_fill;
+  if (tid == 1) a.stats_part[(size_t)gridDim.x * ST_N + part] = l_fill;  // events reserved
 }
 
 // ============================================================================
@@ -641,6 +766,10 @@ struct hb_handle {
   uint64_t* ev_off = nullptr;     // [NB]
   uint64_t* stats_part = nullptr;
   uint64_t* stats = nullptr;
+  // fast -> general hand-over
+  uint32_t* pflag = nullptr;      // [NB][PART/32]
+  uint32_t* resume = nullptr;     // [G]
+  uint64_t* commit0 = nullptr;    // [G]
   static constexpr uint32_t PROF_RING = 256;
   hipEvent_t ph[PROF_RING][HB_PHASE_COUNT + 1] = {};
   uint32_t prof_n = 0;  // profiled steps since hb_phase_reset
@@ -680,6 +809,7 @@ uint32_t ceil_log2(uint32_t x) {
 
 template <int NMAX>
 void launch_apply(hb_handle* h, const ApplyArgs& a) {
+  hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(h->NB), dim3(PART), 0, h->stream, a);
   hipLaunchKernelGGL(k_apply<NMAX>, dim3(h->NB), dim3(PART), 0, h->stream, a);
 }
 
@@ -770,6 +900,9 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->ev_counts, h->NB);
   ALLOC(h->ev_off, h->NB);
   ALLOC(h->stats_part, (size_t)h->NB * (ST_N + 1) + 16);
+  ALLOC(h->pflag, (size_t)h->NB * FLAG_WORDS);
+  ALLOC(h->resume, G);
+  ALLOC(h->commit0, G);
   ALLOC(h->stats, HB_STAT_COUNT);
 #undef ALLOC
   if (rc != HB_OK) {
@@ -980,6 +1113,9 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.ev_counts = h->ev_counts;
   aa.ev_off = h->ev_off;
   aa.stats_part = h->stats_part;
+  aa.pflag = h->pflag;
+  aa.resume = h->resume;
+  aa.commit0 = h->commit0;
   switch (h->nmax) {
     case 3: launch_apply<3>(h, aa); break;
     case 5: launch_apply<5>(h, aa); break;

@@ -1,0 +1,278 @@
+// hipbatch_fast.h — the steady-state leader fast path of the apply phase.
+//
+// k_apply_fast steps, per group (one lane), exactly the two operations that
+// make up steady-state replication (BASELINE.json cfg2):
+//
+//   * MsgProp on a leader whose own id is in prs
+//       stepLeader raft/raft.go:500-513 -> appendEntry :351-360 ->
+//       maybeCommit :323-332 -> bcastAppend :303-310
+//   * MsgAppResp, Reject = false, from a member whose Progress is Replicate,
+//     on a leader, m.Term == 0 or == Term (the Step gate raft/raft.go:462-490
+//     passes without a transition)
+//       stepLeader raft/raft.go:514-546 (maybeUpdate, freeTo, maybeCommit,
+//       bcastAppend / sendAppend)
+//
+// Every other message (and everything after it for that group) is handed to
+// k_apply<NMAX> (the general state machine in hipbatch_kernels.h) through a
+// per-group resume word, so the two kernels together step every group's
+// messages once, in arrival order.  FastLane is the specialization of
+// Lane::step for these preconditions; the parity tests run both paths
+// against the oracle.
+//
+// Why a separate lane type: the general pipeline is ~4k instructions of
+// mostly-skipped branches and register-indexed slot access.  Here every slot
+// access uses a compile-time slot index (runtime slots become predicated
+// unrolled loops), so the hot lane is a few hundred instructions and needs
+// few registers.
+#pragma once
+
+#include "hipbatch_kernels.h"
+
+namespace hb {
+
+template <int NMAX>
+struct FastLane {
+  DevState S;
+  EvSink E;
+  uint32_t g;
+  uint32_t arrival;  // batch position of the message; 0xFFFFFFFF: props[] proposal
+  uint64_t term, committed, first, last, tfirst, tlast;
+  uint32_t mlo;      // meta bits [0, 32): state, n, self, lead, vote, fault
+  uint64_t match[NMAX], next[NMAX], head[NMAX];
+  uint32_t pm[NMAX];
+  uint32_t dirty;
+
+  __device__ __forceinline__ uint32_t n() const { return (mlo >> 2) & 7; }
+  __device__ __forceinline__ uint32_t state() const { return mlo & 3; }
+  __device__ __forceinline__ uint32_t self() const { return (mlo >> 5) & 0xF; }
+  __device__ __forceinline__ uint32_t faulted() const { return (mlo >> 17) & 0xF; }
+  __device__ __forceinline__ uint64_t arrival_x() const {
+    return arrival == 0xFFFFFFFFu ? HB_NO_INDEX : (uint64_t)arrival;
+  }
+  __device__ __forceinline__ void ev(uint32_t type, uint32_t to, uint32_t aux, uint64_t x) {
+    emit_ev(E, g, tta(type, to, aux), x);
+  }
+  __device__ __forceinline__ void fault(uint32_t code) {
+    if (faulted()) return;
+    mlo = (mlo & ~(0xFu << 17)) | (code << 17);
+    dirty |= D_META;
+  }
+  __device__ __forceinline__ uint64_t* ring_at(uint32_t s, uint32_t idx) const {
+    return S.ring + ((size_t)s * S.W + idx) * S.G + g;
+  }
+
+  // All state loads of the lane are independent, so they are in flight together.
+  __device__ __forceinline__ void load() {
+    term = S.term[g];
+    committed = S.commit[g];
+    first = S.first[g];
+    last = S.last[g];
+    tfirst = S.tfirst[g];
+    tlast = S.tlast[g];
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) {
+      match[s] = S.match[(size_t)s * S.G + g];
+      next[s] = S.next[(size_t)s * S.G + g];
+      pm[s] = S.pm[(size_t)s * S.G + g];
+    }
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) head[s] = pm_count(pm[s]) ? *ring_at(s, pm_start(pm[s])) : 0;
+    dirty = 0;
+  }
+  __device__ __forceinline__ void store() {
+    if (dirty & D_META) reinterpret_cast<uint32_t*>(S.meta)[2 * (size_t)g] = mlo;  // little-endian low word
+    if (dirty & D_COMMIT) S.commit[g] = committed;
+    if (dirty & D_LAST) S.last[g] = last;
+    if (dirty & D_TRUN) {
+      S.tfirst[g] = tfirst;
+      S.tlast[g] = tlast;
+    }
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) {
+      if (dirty & (1u << (D_SLOT0 + s))) {
+        S.match[(size_t)s * S.G + g] = match[s];
+        S.next[(size_t)s * S.G + g] = next[s];
+        S.pm[(size_t)s * S.G + g] = pm[s];
+      }
+    }
+  }
+
+  // isPaused raft/progress.go:147-158
+  __device__ __forceinline__ bool is_paused(uint32_t p) const {
+    const uint32_t st = pm_state(p);
+    if (st == HB_PR_PROBE) return pm_paused(p) != 0;
+    if (st == HB_PR_REPLICATE) return pm_count(p) == S.W;
+    return true;
+  }
+  // inflights.freeTo raft/progress.go:204-224 (head entry from the register copy)
+  // (s is a compile-time constant after the callers' unrolled slot loops)
+  __device__ __forceinline__ void free_to(int s, uint64_t to) {
+    const uint32_t p = pm[s];
+    const uint32_t cnt = pm_count(p);
+    if (cnt == 0) return;
+    uint64_t v = head[s];
+    if (to < v) return;
+    uint32_t idx = pm_start(p);
+    const uint32_t W = S.W;
+    uint32_t i = 0;
+    while (true) {
+      ++i;
+      if (++idx >= W) idx -= W;
+      if (i == cnt) break;
+      v = *ring_at(s, idx);
+      if (to < v) break;
+    }
+    pm[s] = pm_make(pm_state(p), pm_paused(p), idx, cnt - i);
+    head[s] = v;
+  }
+  // raftLog.term(i) == Term over the current-term run (raft/log.go:198-217)
+  __device__ __forceinline__ bool term_eq(uint64_t i) const {
+    if (i + 1 < first || i > last) return term == 0;
+    return tfirst <= i && i <= tlast;
+  }
+  // maybeCommit raft/raft.go:323-332 + raftLog.maybeCommit raft/log.go:241-247 +
+  // commitTo :172-180.  The q-th largest Match by an odd-even transposition
+  // network over the NMAX registers (absent slots read as 0).
+  __device__ __forceinline__ bool maybe_commit() {
+    uint64_t v[NMAX];
+    const uint32_t nn = n();
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) v[s] = ((uint32_t)s < nn) ? match[s] : 0;
+#pragma unroll
+    for (int r = 0; r < NMAX; ++r) {
+#pragma unroll
+      for (int j = (r & 1); j + 1 < NMAX; j += 2) {
+        const uint64_t a = v[j], b = v[j + 1];
+        v[j] = a > b ? a : b;
+        v[j + 1] = a > b ? b : a;
+      }
+    }
+    uint64_t mci = v[0];
+#pragma unroll
+    for (int s = 1; s < NMAX; ++s) mci = ((uint32_t)s == nn / 2) ? v[s] : mci;  // q-1, q = n/2+1
+    if (mci > committed && term_eq(mci)) {
+      if (last < mci) {
+        fault(HB_FAULT_COMMIT_RANGE);
+        return false;
+      }
+      committed = mci;
+      dirty |= D_COMMIT;
+      ev(HB_EV_COMMIT, 0, 0, mci);
+      return true;
+    }
+    return false;
+  }
+  // sendAppend raft/raft.go:239-282 to slot s
+  __device__ __forceinline__ void send_append(int s) {
+    const uint32_t p = pm[s];
+    if (is_paused(p)) return;
+    if (next[s] < first) {  // needSnapshot raft/raft.go:715-717
+      const uint64_t snapi = S.snap[g];
+      if (snapi == 0) {
+        fault(HB_FAULT_EMPTY_SNAPSHOT);
+        return;
+      }
+      pm[s] = pm_make(HB_PR_SNAPSHOT, 0, 0, 0);  // becomeSnapshot
+      S.pending[(size_t)s * S.G + g] = snapi;
+      dirty |= 1u << (D_SLOT0 + s);
+      ev(HB_EV_SNAP, s, 0, snapi);
+      return;
+    }
+    const uint64_t x = next[s] - 1;
+    if (next[s] <= last) {
+      const uint64_t lastsent = S.max_msg_size == 0 ? next[s] : last;
+      const uint32_t st = pm_state(p);
+      if (st == HB_PR_REPLICATE) {
+        const uint32_t cnt = pm_count(p), start = pm_start(p);
+        if (cnt == S.W) {
+          fault(HB_FAULT_INFLIGHTS_FULL);
+          return;
+        }
+        uint32_t idx = start + cnt;
+        if (idx >= S.W) idx -= S.W;
+        *ring_at(s, idx) = lastsent;              // inflights.add
+        if (cnt == 0) head[s] = lastsent;
+        next[s] = lastsent + 1;                   // optimisticUpdate
+        pm[s] = pm_make(HB_PR_REPLICATE, pm_paused(p), start, cnt + 1);
+      } else if (st == HB_PR_PROBE) {
+        pm[s] = p | PM_PAUSED;                    // pause
+      }
+      dirty |= 1u << (D_SLOT0 + s);
+    }
+    ev(HB_EV_APP, s, 0, x);
+  }
+  // bcastAppend raft/raft.go:303-310 (slot order, self skipped)
+  __device__ __forceinline__ void bcast_append() {
+    const uint32_t nn = n(), sf = self();
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s)
+      if ((uint32_t)s < nn && (uint32_t)s != sf && !faulted()) send_append(s);
+  }
+
+  // ---- preconditions (checked per message by the kernel)
+  __device__ __forceinline__ bool prop_ok(uint32_t k) const {
+    return k != 0 && state() == HB_STATE_LEADER && self() != HB_SLOT_NONE;
+  }
+  __device__ __forceinline__ bool accept_ok(uint32_t type, uint32_t from, uint64_t mterm, bool reject) const {
+    bool rep = false;
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) rep = ((uint32_t)s == from) ? (pm_state(pm[s]) == HB_PR_REPLICATE) : rep;
+    return type == HB_MSG_APP_RESP && !reject && state() == HB_STATE_LEADER && (mterm == 0 || mterm == term) &&
+           from < n() && rep;
+  }
+
+  // ---- MsgProp with k entries on a leader (prop_ok)
+  __device__ __forceinline__ void prop(uint32_t k) {
+    const uint64_t old = last;
+    last += k;
+    if (tfirst == HB_NO_INDEX) tfirst = old + 1;
+    tlast = last;
+    dirty |= D_LAST | D_TRUN;
+    ev(HB_EV_LAST, 0, 0, last);
+    const uint32_t sf = self();
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) {
+      if ((uint32_t)s == sf) {  // self maybeUpdate(lastIndex) raft/raft.go:358
+        if (match[s] < last) {
+          match[s] = last;
+          pm[s] &= ~PM_PAUSED;
+        }
+        if (next[s] < last + 1) next[s] = last + 1;
+        dirty |= 1u << (D_SLOT0 + s);
+      }
+    }
+    maybe_commit();
+    bcast_append();
+    if (faulted()) ev(HB_EV_FAULT, 0, faulted(), arrival_x());
+  }
+
+  // ---- accepted MsgAppResp from a Replicate member (accept_ok)
+  __device__ __forceinline__ void accept(uint32_t from, uint64_t index) {
+    bool updated = false, old_paused = false;
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) {
+      if ((uint32_t)s == from) {
+        old_paused = pm_count(pm[s]) == S.W;      // isPaused() in Replicate, before maybeUpdate
+        if (next[s] < index + 1) next[s] = index + 1;
+        if (match[s] < index) {                   // maybeUpdate raft/progress.go:102-113
+          match[s] = index;
+          pm[s] &= ~PM_PAUSED;
+          updated = true;
+          free_to(s, index);                      // Replicate: ins.freeTo(m.Index)
+        }
+        dirty |= 1u << (D_SLOT0 + s);
+      }
+    }
+    if (!updated) return;
+    if (maybe_commit()) {
+      bcast_append();
+    } else if (old_paused && !faulted()) {
+#pragma unroll
+      for (int s = 0; s < NMAX; ++s)
+        if ((uint32_t)s == from) send_append(s);
+    }
+    if (faulted()) ev(HB_EV_FAULT, 0, faulted(), arrival_x());
+  }
+};
+
+}  // namespace hb

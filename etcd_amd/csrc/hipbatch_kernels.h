@@ -81,12 +81,13 @@ struct DevState {
 };
 
 // ---- event sink ---------------------------------------------------------------
-// The sink of the apply workgroup lives in LDS so that emit() needs no
-// per-lane state: the kernel fills g_sink once, emit() reads it.
+// A workgroup appends its events to its own chunk of the event region: the
+// chunk base is computed by every lane from kernel arguments (so it stays a
+// global-address-space pointer and the stores are global_store, not flat),
+// and the fill cursor is one LDS word.
 struct EvSink {
-  hb_event* chunk;            // this workgroup's chunk
-  uint32_t fill;              // records written by the workgroup
-  uint32_t pad;
+  hb_event* chunk;            // this workgroup's chunk (global)
+  uint32_t* fill;             // records written by the workgroup (LDS)
 };
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a > b ? b : a; }
@@ -113,9 +114,11 @@ __host__ __device__ constexpr uint32_t tta(uint32_t type, uint32_t to, uint32_t 
 // so it never overflows.  One LDS atomic per active lane; the compiler's
 // atomic optimizer turns it into one ds_add per wave plus mbcnt, and the
 // lanes of a wave write side by side.  A lane's records keep their order.
-__device__ __forceinline__ void emit_ev(EvSink* sink, uint32_t group, uint32_t ttav, uint64_t x) {
-  const uint32_t pos = atomicAdd(&sink->fill, 1u);
-  store_event(sink->chunk + pos, group, ttav, x);
+__device__ __forceinline__ void emit_ev(const EvSink& sink, uint32_t group, uint32_t ttav, uint64_t x) {
+  const uint32_t pos = atomicAdd(sink.fill, 1u);
+#ifndef HB_X_NOEV
+  store_event(sink.chunk + pos, group, ttav, x);
+#endif
 }
 
 template <int N>
@@ -169,7 +172,7 @@ template <> struct SlotVec<7> {
 template <int NMAX>
 struct Lane {
   DevState S;
-  EvSink* E;  // LDS
+  EvSink E;
   uint32_t g;
   uint32_t arrival;  // batch position of the message; 0xFFFFFFFF: props[] proposal
   uint64_t term, committed, first, last, tfirst, tlast, meta;

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Time diagnostic builds of the engine side by side:  gpurun -- bash tools/variants.sh v1 v2 ...
+# (etcd_amd/libhipbatch_<v>.so, built beforehand; "full" = etcd_amd/libhipbatch.so)
+set -e
+cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out/var
+for v in "$@"; do
+  lib=$PWD/etcd_amd/libhipbatch_$v.so; [ "$v" = full ] && lib=$PWD/etcd_amd/libhipbatch.so
+  HB_LIB=$lib timeout -k 10 120 python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline > gpurun_out/var/$v.json
+  python3 -c "import json;d=json.loads(open('gpurun_out/var/$v.json').read().strip().splitlines()[-1]);print('$v',round(d['value']/1e9,3),{k:round(v*1e3,1) for k,v in d['phases'].items() if k!='steps'},d['parity_sanity'])"
+done
