@@ -68,16 +68,24 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh16, 
 }
 
 // ============================================================================
-// Phase 1: stable partition of the batch
+// Phase 1: partition the batch into buckets
 //
-// LSD radix sort of the messages by partition id (group >> PART_LOG), 6 bits
-// (64 bins) per pass, 2 passes up to 4096 partitions (4M groups).  A 512-lane
-// workgroup owns a tile of 2048 messages: it ranks them stably per digit
-// (ballot matching inside a wave, per-wave counters across waves), stages the
-// tile in LDS in digit order, and writes each digit's run contiguously, so the
-// global stores are coalesced runs (~32 records per digit per tile) instead of
+// A bucket is BK = 4096 consecutive group slots (the groups of SIS = 16 apply
+// partitions).  The batch is sorted by bucket id with a stable LSD radix sort,
+// 8-bit digits: one pass up to 256 buckets (1M groups), two passes up to 64K
+// buckets.  A 512-lane workgroup ranks a 2048-message tile stably (ballot
+// matching inside a wave, per-wave counters across waves), stages it in LDS
+// in digit order and writes each digit's run contiguously, so the global
+// stores are coalesced runs (~8 records per digit per tile) instead of
 // scattered single records.  Messages of groups >= capacity are dropped in
-// the first pass.  Arrival order is preserved within every partition.
+// the first pass.  Arrival order is preserved within every bucket.
+//
+// The final pass writes the apply input: one 24-byte MsgRec per message
+// (info with the group's lane in bits 16-23, arrival index, term, index) and
+// one key byte = the message's partition within its bucket.  Each apply
+// workgroup scans its bucket's key bytes to pick its own messages (the 16
+// sisters of a bucket run on one XCD and share the bucket through its L2),
+// which replaces a second full pass over the batch.
 // ============================================================================
 struct BatchDev {
   const uint32_t* group;
@@ -89,12 +97,22 @@ struct BatchDev {
   uint64_t n;
 };
 
-constexpr uint32_t RDX_BITS = 6;
+constexpr uint32_t SIS_LOG = 4;
+constexpr uint32_t SIS = 1u << SIS_LOG;           // apply partitions per bucket
+constexpr uint32_t BK_LOG = PART_LOG + SIS_LOG;   // groups per bucket = 4096
+constexpr uint32_t RDX_BITS = 8;
 constexpr uint32_t RDX_BINS = 1u << RDX_BITS;
 constexpr uint32_t RDX_THREADS = 512;
 constexpr uint32_t RDX_WAVES = RDX_THREADS / 64;
 constexpr uint32_t RDX_ROUNDS = 4;
 constexpr uint32_t RDX_TILE = RDX_THREADS * RDX_ROUNDS;  // 2048
+
+struct MsgRec {      // apply input record (24 B)
+  uint32_t info;     // type | from << 4 | reject << 8 | lane << 16
+  uint32_t orig;     // arrival index in the batch
+  uint64_t term;
+  uint64_t index;
+};
 
 struct RadixSrc {
   const uint32_t* group;
@@ -106,7 +124,7 @@ struct RadixSrc {
   uint32_t n;
 };
 
-struct RadixDst {
+struct RadixDst {  // intermediate pass output
   uint32_t* group;
   uint32_t* info;
   uint32_t* orig;
@@ -114,7 +132,32 @@ struct RadixDst {
   uint64_t* index;
 };
 
+struct FinalDst {  // final pass output = apply input
+  MsgRec* rec;
+  uint8_t* key;
+  uint32_t* bucket;  // bucket id per message (multi-pass only, for k_bucket_bounds)
+  uint32_t* bk_off;  // [NBK + 1] written by the one-pass scatter
+  uint32_t NBK;
+};
+
 __device__ __forceinline__ uint32_t src_n(const RadixSrc& s) { return s.n_dev ? *s.n_dev : s.n; }
+__device__ __forceinline__ uint32_t rdx_digit(uint32_t g, uint32_t shift) {
+  return ((g >> BK_LOG) >> shift) & (RDX_BINS - 1);
+}
+
+// Exclusive scan over the first 256 threads of the block (all threads call it).
+__device__ __forceinline__ uint32_t excl_scan256(uint32_t v, uint32_t* sh4, uint32_t* total) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t incl = wave_incl_scan(v);
+  if (tid < 256 && lane == 63) sh4[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < 4; ++w) before += (w < wave) ? sh4[w] : 0u;
+  *total = sh4[0] + sh4[1] + sh4[2] + sh4[3];
+  __syncthreads();
+  return before + incl - v;
+}
 
 __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t G, uint32_t shift, uint32_t ntiles,
                                                            uint32_t* hist) {
@@ -129,7 +172,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t
     const uint32_t i = base + r * RDX_THREADS + tid;
     if (i < n) {
       const uint32_t g = s.group[i];
-      if (g < G) atomicAdd(&cnt[((g >> PART_LOG) >> shift) & (RDX_BINS - 1)], 1u);
+      if (g < G) atomicAdd(&cnt[rdx_digit(g, shift)], 1u);
     }
   }
   __syncthreads();
@@ -138,9 +181,12 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t
 
 // Row scan: workgroup b turns row b of hist ([RDX_BINS][ntiles] tile counts)
 // into exclusive per-tile prefixes and writes the row total to totals[b].
-__global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t ntiles, uint32_t* totals) {
+// It also clears the per-bucket event-chunk cursors for the coming apply.
+__global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t ntiles, uint32_t* totals,
+                                                    uint32_t* bk_fill, uint32_t NBK) {
   __shared__ uint32_t sh16[16];
   uint32_t* row = hist + (size_t)blockIdx.x * ntiles;
+  for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < NBK; i += gridDim.x * 1024) bk_fill[i] = 0;
   uint32_t carry = 0;
   for (uint32_t base = 0; base < ntiles; base += 4096) {
     const uint32_t i0 = base + threadIdx.x * 4;
@@ -159,13 +205,14 @@ __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t nti
   if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
-__global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, RadixDst d, uint32_t G, uint32_t shift,
-                                                              uint32_t ntiles, const uint32_t* off,
-                                                              const uint32_t* totals, uint32_t* n_valid,
-                                                              uint32_t final_pass) {
+template <bool FINAL>
+__global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, RadixDst d, FinalDst f, uint32_t G,
+                                                              uint32_t shift, uint32_t ntiles, const uint32_t* off,
+                                                              const uint32_t* totals, uint32_t* n_valid) {
   __shared__ uint32_t s_off[RDX_BINS];
   __shared__ uint32_t s_wcnt[RDX_WAVES][RDX_BINS];
   __shared__ uint32_t s_dstart[RDX_BINS + 1];
+  __shared__ uint32_t sh4[4];
   __shared__ uint32_t st_group[RDX_TILE];
   __shared__ uint32_t st_info[RDX_TILE];
   __shared__ uint32_t st_orig[RDX_TILE];
@@ -173,14 +220,22 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
   __shared__ uint64_t st_index[RDX_TILE];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint32_t tile = blockIdx.x;
-  if (tid < RDX_BINS) {
+  {
     // digit base = exclusive scan of the digit totals; + this tile's row prefix
-    const uint32_t t = totals[tid];
-    const uint32_t incl = wave_incl_scan(t);
-    s_off[tid] = incl - t + off[(size_t)tid * ntiles + tile];
-    if (tile == 0 && tid == RDX_BINS - 1) *n_valid = incl;
+    const uint32_t t = tid < RDX_BINS ? totals[tid] : 0u;
+    uint32_t all;
+    const uint32_t excl = excl_scan256(t, sh4, &all);
+    if (tid < RDX_BINS) {
+      s_off[tid] = excl + off[(size_t)tid * ntiles + tile];
+      if (FINAL && f.bk_off && tile == 0 && tid <= f.NBK) f.bk_off[tid] = excl;
+    }
+    if (tile == 0 && tid == 0) {
+      *n_valid = all;
+      if (FINAL && f.bk_off && f.NBK == RDX_BINS) f.bk_off[RDX_BINS] = all;
+    }
   }
-  (&s_wcnt[0][0])[tid] = 0;  // RDX_WAVES * RDX_BINS == RDX_THREADS
+#pragma unroll
+  for (uint32_t k = 0; k < RDX_WAVES * RDX_BINS / RDX_THREADS; ++k) (&s_wcnt[0][0])[tid + k * RDX_THREADS] = 0;
   __syncthreads();
   const uint32_t n = src_n(s);
   const uint32_t base = tile * RDX_TILE;
@@ -200,7 +255,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
     vo[r] = vv[r] ? (s.orig ? s.orig[i] : i) : 0u;
     vt[r] = vv[r] ? s.term[i] : 0ull;
     vx[r] = vv[r] ? s.index[i] : 0ull;
-    vd[r] = ((vg[r] >> PART_LOG) >> shift) & (RDX_BINS - 1);
+    vd[r] = rdx_digit(vg[r], shift);
   }
   // stable rank inside the wave: rounds in order, lanes in order
 #pragma unroll
@@ -219,17 +274,20 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
   }
   __syncthreads();
   // per digit: prefix over waves, then digit starts inside the tile
+  uint32_t run = 0;
   if (tid < RDX_BINS) {
-    uint32_t run = 0;
 #pragma unroll
     for (uint32_t w = 0; w < RDX_WAVES; ++w) {
       const uint32_t c = s_wcnt[w][tid];
       s_wcnt[w][tid] = run;
       run += c;
     }
-    const uint32_t incl = wave_incl_scan(run);
-    s_dstart[tid] = incl - run;
-    if (tid == RDX_BINS - 1) s_dstart[RDX_BINS] = incl;
+  }
+  {
+    uint32_t all;
+    const uint32_t excl = excl_scan256(tid < RDX_BINS ? run : 0u, sh4, &all);
+    if (tid < RDX_BINS) s_dstart[tid] = excl;
+    if (tid == 0) s_dstart[RDX_BINS] = all;
   }
   __syncthreads();
 #pragma unroll
@@ -250,28 +308,40 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
     const uint32_t p = r * RDX_THREADS + tid;
     if (p < valid) {
       const uint32_t g = st_group[p];
-      const uint32_t dg = ((g >> PART_LOG) >> shift) & (RDX_BINS - 1);
+      const uint32_t dg = rdx_digit(g, shift);
       const uint32_t o = s_off[dg] + (p - s_dstart[dg]);
-      d.group[o] = g;
-      d.info[o] = final_pass ? ((st_info[p] & 0xFFFFu) | ((g & (PART - 1)) << 16)) : st_info[p];
-      d.orig[o] = st_orig[p];
-      d.term[o] = st_term[p];
-      d.index[o] = st_index[p];
+      if (FINAL) {
+        MsgRec m;
+        m.info = (st_info[p] & 0xFFFFu) | ((g & (PART - 1)) << 16);
+        m.orig = st_orig[p];
+        m.term = st_term[p];
+        m.index = st_index[p];
+        f.rec[o] = m;
+        f.key[o] = (uint8_t)((g >> PART_LOG) & (SIS - 1));
+        if (f.bucket) f.bucket[o] = g >> BK_LOG;
+      } else {
+        d.group[o] = g;
+        d.info[o] = st_info[p];
+        d.orig[o] = st_orig[p];
+        d.term[o] = st_term[p];
+        d.index[o] = st_index[p];
+      }
     }
   }
 }
 
-// part_off[b] = first position of partition b in the sorted batch (b <= NB).
-__global__ void k_part_bounds(const uint32_t* sorted_group, const uint32_t* n_dev, uint32_t NB, uint32_t* part_off) {
+// bk_off[b] = first position of bucket b in the sorted batch (b <= NBK); the
+// multi-pass case (the one-pass scatter writes bk_off itself).
+__global__ void k_bucket_bounds(const uint32_t* bucket, const uint32_t* n_dev, uint32_t NBK, uint32_t* bk_off) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b > NB) return;
+  if (b > NBK) return;
   uint32_t lo = 0, hi = *n_dev;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if ((sorted_group[mid] >> PART_LOG) < b) lo = mid + 1;
+    if (bucket[mid] < b) lo = mid + 1;
     else hi = mid;
   }
-  part_off[b] = lo;
+  bk_off[b] = lo;
 }
 
 // ============================================================================
@@ -279,16 +349,16 @@ __global__ void k_part_bounds(const uint32_t* sorted_group, const uint32_t* n_de
 // ============================================================================
 struct ApplyArgs {
   DevState S;
-  const uint32_t* p_info;
-  const uint32_t* p_orig;
-  const uint64_t* p_term;
-  const uint64_t* p_index;
+  const MsgRec* rec;        // sorted batch: bucket order, arrival order inside a bucket
+  const uint8_t* key;       // partition-in-bucket of each record
+  const uint32_t* bk_off;   // [NBK+1] bucket bounds in rec
+  uint32_t* bk_fill;        // [NBK] event records reserved by the bucket's partitions
   const uint64_t* hint;     // original-order RejectHint
   const uint32_t* props;    // dense proposals or null
-  const uint32_t* part_off; // [NB+1]
   hb_event* ev;             // event region base
   uint32_t ev_per_msg;      // bound on events per stepped message (EV_MAX)
   uint32_t props_on;        // 1 if props[] is present (one proposal slot per group)
+  uint32_t NB;              // partitions
   uint32_t* ev_counts;      // [NB] records in each chunk
   uint64_t* ev_off;         // [NB] chunk offsets (records)
   uint64_t* stats_part;     // [NB][HB_STAT_COUNT]
@@ -304,9 +374,20 @@ enum { ST_MSGS, ST_APPRESP, ST_VOTERESP, ST_DROPPED, ST_COMMITS, ST_WON, ST_LOST
 #define HB_FAST_WAVES 4
 #endif
 constexpr uint32_t FLAG_WORDS = PART / 32;  // per-partition bitmask of groups handed to k_apply
+constexpr uint32_t KPL = 64;                // bucket key bytes scanned per lane per segment
+constexpr uint32_t SEG = PART * KPL;        // positions per key-scan segment
 
-// LDS staging of one round (<= CHUNK messages) of a partition's segment.
+// blockIdx -> partition.  The SIS sister partitions of a bucket get block ids
+// with equal blockIdx % 8, i.e. one XCD under the round-robin placement, so
+// the bucket's keys and records are fetched into one L2 (speed only).
+__device__ __forceinline__ uint32_t block_part() {
+  const uint32_t x = blockIdx.x, r = x & 7, q = x >> 3;
+  return ((((q >> SIS_LOG) << 3) | r) << SIS_LOG) | (q & (SIS - 1));
+}
+
+// LDS staging of one round (<= CHUNK messages) of a partition's messages.
 struct Stage {
+  uint32_t rbuf[CHUNK];   // bucket-relative positions, increasing (= arrival order)
   uint32_t info[CHUNK];
   uint32_t orig[CHUNK];
   uint64_t term[CHUNK];
@@ -314,28 +395,113 @@ struct Stage {
   uint16_t perm[CHUNK];
   uint32_t cnt[PART];
   uint32_t sh16[16];
+  uint64_t bcast;
 };
 
-// Stage messages [c0, c0+len) of the sorted batch and counting-sort them by
-// group lane: on return the lane's messages are perm[*start, *start+*cnt), in
-// arrival order (the segment is arrival-ordered; the per-lane run is
-// re-sorted by position after the atomic placement).
-__device__ __forceinline__ void stage_round(Stage& sl, const ApplyArgs& a, uint32_t c0, uint32_t len, uint32_t* start,
-                                            uint32_t* cnt) {
+// This lane's KPL key bytes of segment `seg` (positions seg + tid*KPL + k):
+// bit k set where the key equals `sub` and the position is in [lo, hi).
+// Four keys per dword: a SWAR zero-byte test, then the four byte flags are
+// gathered into a nibble by one multiply.
+__device__ __forceinline__ uint64_t scan_keys(const uint8_t* key, uint32_t seg, uint32_t lo, uint32_t hi,
+                                              uint32_t sub) {
+  const uint32_t base = seg + threadIdx.x * KPL;
+  if (base >= hi || base + KPL <= lo) return 0;
+  const uint4* p = reinterpret_cast<const uint4*>(key + base);
+  const uint32_t rep = sub * 0x01010101u;
+  uint64_t eq = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint4 w4 = p[q];
+    const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x = w[k] ^ rep;
+      const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // 0x80 where byte == sub
+      const uint32_t c = (((z >> 7) * 0x01020408u) >> 24) & 0xFu;                 // bytes 0..3 -> bits 0..3
+      eq |= (uint64_t)c << (16 * q + 4 * k);
+    }
+  }
+  const uint32_t a = lo > base ? lo - base : 0u;                // < KPL
+  const uint32_t b = hi - base < KPL ? hi - base : KPL;          // > a
+  const uint64_t vm = (b >= 64 ? ~0ull : ((1ull << b) - 1)) & (~0ull << a);
+  return eq & vm;
+}
+
+// Walk the partition's messages of bucket [lo, hi) in arrival order, in
+// rounds of at most CHUNK.  on_total(total) runs once (all threads) before
+// the first round with the partition's message count; round(fill) runs per
+// round with sl.rbuf[0, fill) = the round's bucket-relative positions.
+template <class OnTotal, class Round>
+__device__ __forceinline__ void walk_partition(Stage& sl, const ApplyArgs& a, uint32_t lo, uint32_t hi, uint32_t sub,
+                                               OnTotal&& on_total, Round&& round) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t seg0 = lo & ~15u;
+  const uint32_t nseg = hi > lo ? (hi - seg0 + SEG - 1) / SEG : 0u;  // uniform
+  if (nseg != 1) {
+    uint32_t total = 0;
+    for (uint32_t s = 0; s < nseg; ++s) {
+      uint32_t t;
+      (void)block_excl_scan((uint32_t)__popcll(scan_keys(a.key, seg0 + s * SEG, lo, hi, sub)), sl.sh16, &t);
+      total += t;
+    }
+    on_total(total);
+  }
+  uint32_t fill = 0;  // uniform
+  for (uint32_t s = 0; s < nseg; ++s) {
+    const uint32_t seg = seg0 + s * SEG;
+    const uint64_t eq = scan_keys(a.key, seg, lo, hi, sub);
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan((uint32_t)__popcll(eq), sl.sh16, &tot);
+    if (nseg == 1) on_total(tot);
+    const uint32_t base = seg + tid * KPL - lo;
+    for (uint32_t done = 0; done < tot;) {
+      const uint32_t take = (tot - done) < (CHUNK - fill) ? (tot - done) : (CHUNK - fill);
+      uint64_t m = eq;
+      uint32_t idx = pre;
+      while (m) {
+        const uint32_t k = (uint32_t)__ffsll((long long)m) - 1;
+        m &= m - 1;
+        if (idx >= done && idx < done + take) sl.rbuf[fill + idx - done] = base + k;
+        ++idx;
+      }
+      fill += take;
+      done += take;
+      if (fill == CHUNK) {
+        __syncthreads();
+        round(fill);
+        fill = 0;
+      }
+    }
+  }
+  if (fill) {
+    __syncthreads();
+    round(fill);
+  }
+}
+
+// Gather the round's records into LDS and counting-sort them by lane: on
+// return the lane's messages are perm[*start, *start + *cnt), in arrival order.
+__device__ __forceinline__ void gather_round(Stage& sl, const ApplyArgs& a, uint32_t lo, uint32_t fill,
+                                             uint32_t* start, uint32_t* cnt) {
   constexpr uint32_t PER = CHUNK / PART;
   const uint32_t tid = threadIdx.x;
   sl.cnt[tid] = 0;
   __syncthreads();
+  MsgRec m[PER];
 #pragma unroll
   for (uint32_t k = 0; k < PER; ++k) {
     const uint32_t i = tid + k * PART;
-    if (i < len) {
-      const uint32_t inf = a.p_info[c0 + i];
-      sl.info[i] = inf;
-      sl.orig[i] = a.p_orig[c0 + i];
-      sl.term[i] = a.p_term[c0 + i];
-      sl.index[i] = a.p_index[c0 + i];
-      atomicAdd(&sl.cnt[inf >> 16], 1u);
+    if (i < fill) m[k] = a.rec[lo + sl.rbuf[i]];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < PER; ++k) {
+    const uint32_t i = tid + k * PART;
+    if (i < fill) {
+      sl.info[i] = m[k].info;
+      sl.orig[i] = m[k].orig;
+      sl.term[i] = m[k].term;
+      sl.index[i] = m[k].index;
+      atomicAdd(&sl.cnt[(m[k].info >> 16) & (PART - 1)], 1u);
     }
   }
   __syncthreads();
@@ -344,8 +510,8 @@ __device__ __forceinline__ void stage_round(Stage& sl, const ApplyArgs& a, uint3
   const uint32_t my_start = block_excl_scan(my_cnt, sl.sh16, &total);
   sl.cnt[tid] = my_start;  // becomes the fill cursor
   __syncthreads();
-  for (uint32_t i = tid; i < len; i += PART) {
-    const uint32_t pos = atomicAdd(&sl.cnt[sl.info[i] >> 16], 1u);
+  for (uint32_t i = tid; i < fill; i += PART) {
+    const uint32_t pos = atomicAdd(&sl.cnt[(sl.info[i] >> 16) & (PART - 1)], 1u);
     sl.perm[pos] = (uint16_t)i;
   }
   __syncthreads();
@@ -399,58 +565,61 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N];
 
+  const uint32_t part = block_part();
+  if (part >= a.NB) return;  // uniform: grid padding
   const uint32_t tid = threadIdx.x;
-  const uint32_t part = blockIdx.x;
+  const uint32_t bk = part >> SIS_LOG, sub = part & (SIS - 1);
   const uint32_t g = part * PART + tid;
   const bool gvalid = g < a.S.G;
-
-  // Exact chunk: every event is emitted while stepping a message (or the
-  // group's proposal), at most ev_per_msg per message, so the partition's
-  // chunk is ev_per_msg x (its messages + its proposal slots).
-  const uint64_t ev_off = (uint64_t)a.ev_per_msg * ((uint64_t)a.part_off[part] + (uint64_t)part * PART * a.props_on);
-  if (tid == 0) {
-    l_fill = 0;
-    a.ev_off[part] = ev_off;
-  }
+  if (tid == 0) l_fill = 0;
   if (tid < ST_N) l_stats[tid] = 0;
   if (tid < FLAG_WORDS) l_flag[tid] = 0;
 
+  const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
   FastLane<NMAX> L;
   L.S = a.S;
-  L.E.chunk = a.ev + ev_off;
   L.E.fill = &l_fill;
   L.g = g;
-  const uint32_t seg_lo = a.part_off[part], seg_hi = a.part_off[part + 1];
-  const bool wg_work = a.props_on || seg_hi > seg_lo;  // uniform over the workgroup
   L.mlo = gvalid ? reinterpret_cast<const uint32_t*>(a.S.meta)[2 * (size_t)g] : 0u;
   const uint32_t prop_raw = (a.props && gvalid) ? a.props[g] : 0u;
   // A group takes part when its slot is live (n > 0) and not faulted.
   const bool live = gvalid && L.n() != 0 && L.faulted() == 0;
   L.dirty = 0;
   L.last = L.committed = 0;
-  if (wg_work && live) L.load();
+  if ((a.props_on || hi > lo) && live) L.load();
   const uint64_t last0 = L.last, commit0 = L.committed;
 
   bool flagged = false;
   uint32_t resume = 0;
   uint32_t st_msgs = 0, st_drop = 0;
-
-  const uint32_t prop_k = live ? prop_raw : 0u;
-  if (prop_k) {
-    if (L.prop_ok(prop_k)) {
-      L.arrival = 0xFFFFFFFFu;
-      L.prop(prop_k);
-    } else {
-      flagged = true;
-      resume = 1u << 31;  // the proposal itself is pending
-    }
-  }
-
   uint32_t j = 0;  // messages of this lane consumed so far (all rounds)
-  for (uint32_t c0 = seg_lo; c0 < seg_hi; c0 += CHUNK) {
-    const uint32_t len = (seg_hi - c0) < CHUNK ? (seg_hi - c0) : CHUNK;
+
+  auto on_total = [&](uint32_t total) {
+    // Exact chunk: every event is emitted while stepping a message (or the
+    // group's proposal), at most ev_per_msg per message.
+    if (tid == 0) {
+      const uint64_t reg = (uint64_t)a.ev_per_msg * ((uint64_t)lo + (uint64_t)bk * (PART * SIS) * a.props_on);
+      const uint32_t mine = a.ev_per_msg * (total + PART * a.props_on);
+      const uint64_t off = reg + atomicAdd(&a.bk_fill[bk], mine);
+      sl.bcast = off;
+      a.ev_off[part] = off;
+    }
+    __syncthreads();
+    L.E.chunk = a.ev + sl.bcast;
+    const uint32_t prop_k = live ? prop_raw : 0u;
+    if (prop_k) {
+      if (L.prop_ok(prop_k)) {
+        L.arrival = 0xFFFFFFFFu;
+        L.prop(prop_k);
+      } else {
+        flagged = true;
+        resume = 1u << 31;  // the proposal itself is pending
+      }
+    }
+  };
+  auto round = [&](uint32_t fill) {
     uint32_t my_start, my_cnt;
-    stage_round(sl, a, c0, len, &my_start, &my_cnt);
+    gather_round(sl, a, lo, fill, &my_start, &my_cnt);
     if (live) {
       for (uint32_t x = 0; x < my_cnt; ++x) {
         if (flagged || L.faulted()) break;
@@ -476,7 +645,8 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
       }
     }
     __syncthreads();
-  }
+  };
+  walk_partition(sl, a, lo, hi, sub, on_total, round);
 
   L.store();
   if (flagged) {
@@ -496,7 +666,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   reduce_stats(a, l_stats, vals, part, false);
   if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
   if (tid == 0) a.ev_counts[part] = l_fill;
-  if (tid == 1) a.stats_part[(size_t)gridDim.x * ST_N + part] = l_fill;  // events reserved
+  if (tid == 1) a.stats_part[(size_t)a.NB * ST_N + part] = l_fill;  // events reserved
 }
 
 // ---------------------------------------------------------------------------
@@ -511,8 +681,10 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N];
 
+  const uint32_t part = block_part();
+  if (part >= a.NB) return;  // uniform: grid padding
   const uint32_t tid = threadIdx.x;
-  const uint32_t part = blockIdx.x;
+  const uint32_t bk = part >> SIS_LOG, sub = part & (SIS - 1);
   const uint32_t g = part * PART + tid;
   if (tid < FLAG_WORDS) l_flag[tid] = a.pflag[(size_t)part * FLAG_WORDS + tid];
   __syncthreads();
@@ -522,13 +694,12 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
   if (!any) return;  // uniform
   const bool flagged = (l_flag[tid >> 5] >> (tid & 31)) & 1u;
 
-  const uint64_t ev_off = a.ev_off[part];
   if (tid == 0) l_fill = a.ev_counts[part];  // append after the fast kernel's events
   if (tid < ST_N) l_stats[tid] = 0;
 
   Lane<NMAX> L;
   L.S = a.S;
-  L.E.chunk = a.ev + ev_off;
+  L.E.chunk = a.ev + a.ev_off[part];
   L.E.fill = &l_fill;
   L.g = g;
   L.won = 0;
@@ -547,18 +718,20 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
   }
   const uint64_t last0 = L.last;
   uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
-  const uint32_t seg_lo = a.part_off[part], seg_hi = a.part_off[part + 1];
-
-  if (flagged && (resume >> 31)) {
-    L.arrival = 0xFFFFFFFFu;
-    L.step(HB_MSG_PROP, L.self(), 0, a.props[g], false, 0);
-  }
   const uint32_t skip = resume & 0x7FFFFFFFu;
   uint32_t j = 0;
-  for (uint32_t c0 = seg_lo; c0 < seg_hi; c0 += CHUNK) {
-    const uint32_t len = (seg_hi - c0) < CHUNK ? (seg_hi - c0) : CHUNK;
+  const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
+
+  auto on_total = [&](uint32_t) {
+    __syncthreads();  // l_fill
+    if (flagged && (resume >> 31)) {
+      L.arrival = 0xFFFFFFFFu;
+      L.step(HB_MSG_PROP, L.self(), 0, a.props[g], false, 0);
+    }
+  };
+  auto round = [&](uint32_t fill) {
     uint32_t my_start, my_cnt;
-    stage_round(sl, a, c0, len, &my_start, &my_cnt);
+    gather_round(sl, a, lo, fill, &my_start, &my_cnt);
     if (flagged) {
       for (uint32_t x = 0; x < my_cnt; ++x, ++j) {
         if (j < skip) continue;
@@ -579,7 +752,8 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
       }
     }
     __syncthreads();
-  }
+  };
+  walk_partition(sl, a, lo, hi, sub, on_total, round);
 
   if (flagged) L.store();
   const uint64_t vals[ST_N] = {st_msgs,
@@ -593,7 +767,7 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
                                L.last - last0};
   reduce_stats(a, l_stats, vals, part, true);
   if (tid == 0) a.ev_counts[part] = l_fill;
-  if (tid == 1) a.stats_part[(size_t)gridDim.x * ST_N + part] = l_fill;  // events reserved
+  if (tid == 1) a.stats_part[(size_t)a.NB * ST_N + part] = l_fill;  // events reserved
 }
 
 // ============================================================================
@@ -747,9 +921,13 @@ struct hb_handle {
   uint32_t* hist = nullptr;       // [RDX_BINS][tiles]
   uint32_t* n_valid = nullptr;    // messages kept after pass 1 (device)
   uint32_t* totals = nullptr;     // [RDX_BINS] digit totals of the current pass
-  uint32_t* part_off = nullptr;   // [NB + 1]
   RadixDst tmp[2] = {};           // intermediate passes (ping-pong)
-  RadixDst fin = {};              // final pass = apply input
+  MsgRec* rec = nullptr;          // final pass = apply input
+  uint8_t* key = nullptr;         // partition-in-bucket per record (+ SEG bytes of padding)
+  uint32_t* bucket = nullptr;     // bucket id per record (multi-pass only)
+  uint32_t* bk_off = nullptr;     // [NBK + 1]
+  uint32_t* bk_fill = nullptr;    // [NBK]
+  uint32_t NBK = 0;               // buckets
   uint32_t passes = 1;
   // host-pointer staging
   uint32_t* s_group = nullptr;
@@ -809,8 +987,9 @@ uint32_t ceil_log2(uint32_t x) {
 
 template <int NMAX>
 void launch_apply(hb_handle* h, const ApplyArgs& a) {
-  hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(h->NB), dim3(PART), 0, h->stream, a);
-  hipLaunchKernelGGL(k_apply<NMAX>, dim3(h->NB), dim3(PART), 0, h->stream, a);
+  const uint32_t grid = ((h->NBK + 7) & ~7u) * SIS;  // XCD-aware padding, see block_part()
+  hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
+  hipLaunchKernelGGL(k_apply<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
 }
 
 }  // namespace
@@ -871,22 +1050,26 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(s.ring, R * (size_t)max_inflight * G);
   // partition scratch
   const size_t mb = max_batch ? max_batch : 1;
-  const uint32_t pbits = std::max<uint32_t>(ceil_log2(h->NB), 1);
+  h->NBK = (capacity + (1u << BK_LOG) - 1) >> BK_LOG;
+  const uint32_t pbits = std::max<uint32_t>(ceil_log2(h->NBK), 1);
   h->passes = (pbits + RDX_BITS - 1) / RDX_BITS;
   const size_t tiles_max = (mb + RDX_TILE - 1) / RDX_TILE;
   ALLOC(h->hist, (size_t)RDX_BINS * tiles_max);
   ALLOC(h->n_valid, 4);
   ALLOC(h->totals, RDX_BINS);
-  ALLOC(h->part_off, h->NB + 1);
-  for (uint32_t k = 0; k < 3; ++k) {
-    RadixDst& d = k < 2 ? h->tmp[k] : h->fin;
-    if (k < 2 && h->passes < 2 + k) continue;  // ping-pong buffers only when needed
+  ALLOC(h->bk_off, h->NBK + 1);
+  ALLOC(h->bk_fill, h->NBK);
+  for (uint32_t k = 0; k + 1 < h->passes && k < 2; ++k) {  // ping-pong buffers of intermediate passes
+    RadixDst& d = h->tmp[k];
     ALLOC(d.group, mb);
     ALLOC(d.info, mb);
     ALLOC(d.orig, mb);
     ALLOC(d.term, mb);
     ALLOC(d.index, mb);
   }
+  ALLOC(h->rec, mb);
+  ALLOC(h->key, mb + SEG);
+  if (h->passes > 1) ALLOC(h->bucket, mb);
   ALLOC(h->s_group, mb);
   ALLOC(h->s_info, mb);
   ALLOC(h->s_term, mb);
@@ -895,7 +1078,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->s_props, G);
   // events: (batch + one proposal slot per group) x EV_MAX (exact bound)
   h->ev_per_msg = h->nmax + 4;
-  h->ev_region = (mb + (uint64_t)h->NB * PART) * h->ev_per_msg;
+  h->ev_region = (mb + (uint64_t)h->NBK * (PART * SIS)) * h->ev_per_msg;
   ALLOC(h->ev, h->ev_region);
   ALLOC(h->ev_counts, h->NB);
   ALLOC(h->ev_off, h->NB);
@@ -1078,38 +1261,46 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   // ---- phase 1: partition ----------------------------------------------------
   const uint32_t NB = h->NB;
   if (b->n == 0) {
-    HB_CHECK(hipMemsetAsync(h->part_off, 0, (NB + 1) * 4ull, st));
+    HB_CHECK(hipMemsetAsync(h->bk_off, 0, (h->NBK + 1) * 4ull, st));
+    HB_CHECK(hipMemsetAsync(h->bk_fill, 0, h->NBK * 4ull, st));
   } else {
     const uint32_t ntiles = (uint32_t)((b->n + RDX_TILE - 1) / RDX_TILE);
     RadixSrc src{bd.group, bd.info, nullptr, bd.term, bd.index, nullptr, (uint32_t)b->n};
+    const FinalDst fin{h->rec, h->key, h->bucket, h->passes == 1 ? h->bk_off : nullptr, h->NBK};
     for (uint32_t p = 0; p < h->passes; ++p) {
       const bool last_pass = p + 1 == h->passes;
-      const RadixDst& dst = last_pass ? h->fin : h->tmp[p & 1];
+      const RadixDst& dst = h->tmp[p & 1];
       const uint32_t shift = p * RDX_BITS;
       hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(RDX_THREADS), 0, st, src, h->G, shift, ntiles, h->hist);
-      hipLaunchKernelGGL(k_scan_rows, dim3(RDX_BINS), dim3(1024), 0, st, h->hist, ntiles, h->totals);
-      hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(RDX_THREADS), 0, st, src, dst, h->G, shift, ntiles,
-                         (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid, last_pass ? 1u : 0u);
+      hipLaunchKernelGGL(k_scan_rows, dim3(RDX_BINS), dim3(1024), 0, st, h->hist, ntiles, h->totals, h->bk_fill,
+                         h->NBK);
+      if (last_pass)
+        hipLaunchKernelGGL(k_radix_scatter<true>, dim3(ntiles), dim3(RDX_THREADS), 0, st, src, dst, fin, h->G, shift,
+                           ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
+      else
+        hipLaunchKernelGGL(k_radix_scatter<false>, dim3(ntiles), dim3(RDX_THREADS), 0, st, src, dst, fin, h->G, shift,
+                           ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
       src = RadixSrc{dst.group, dst.info, dst.orig, dst.term, dst.index, h->n_valid, (uint32_t)b->n};
     }
-    hipLaunchKernelGGL(k_part_bounds, dim3((NB + 1 + 255) / 256), dim3(256), 0, st, (const uint32_t*)h->fin.group,
-                       (const uint32_t*)h->n_valid, NB, h->part_off);
+    if (h->passes > 1)
+      hipLaunchKernelGGL(k_bucket_bounds, dim3((h->NBK + 1 + 255) / 256), dim3(256), 0, st,
+                         (const uint32_t*)h->bucket, (const uint32_t*)h->n_valid, h->NBK, h->bk_off);
   }
   if (prof) HB_CHECK(hipEventRecord(ev[1], st));
 
   // ---- phase 2: apply ----------------------------------------------------------
   ApplyArgs aa;
   aa.S = h->st;
-  aa.p_info = h->fin.info;
-  aa.p_orig = h->fin.orig;
-  aa.p_term = h->fin.term;
-  aa.p_index = h->fin.index;
+  aa.rec = h->rec;
+  aa.key = h->key;
+  aa.bk_off = h->bk_off;
+  aa.bk_fill = h->bk_fill;
   aa.hint = bd.hint;
   aa.props = bd.props;
-  aa.part_off = h->part_off;
   aa.ev = h->ev;
   aa.ev_per_msg = h->ev_per_msg;
   aa.props_on = bd.props ? 1u : 0u;
+  aa.NB = NB;
   aa.ev_counts = h->ev_counts;
   aa.ev_off = h->ev_off;
   aa.stats_part = h->stats_part;
