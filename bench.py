@@ -139,12 +139,15 @@ def main():
     stats_acc = torch.zeros(abi.HB_STAT_COUNT, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
 
+    if world == 1:
+        eng.set_stats_accum(stats_acc)  # summed in the engine's finish phase, no extra launch
+
     def one_step(k, profile):
         eng.step(d_group, d_info, d_term, d_index[k], None, d_props, host=False, profile=profile)
-        eng.stats_to(stats_step)
         if world > 1:
+            eng.stats_to(stats_step)
             dist.all_reduce(stats_step)  # RCCL over xGMI: the only collective
-        stats_acc.add_(stats_step)
+            stats_acc.add_(stats_step)
 
     for k in range(args.warmup):
         one_step(k, False)

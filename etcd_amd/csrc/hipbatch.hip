@@ -361,7 +361,7 @@ struct ApplyArgs {
   uint32_t NB;              // partitions
   uint32_t* ev_counts;      // [NB] records in each chunk
   uint64_t* ev_off;         // [NB] chunk offsets (records)
-  uint64_t* stats_part;     // [NB][HB_STAT_COUNT]
+  uint64_t* stats_shard;    // [8][16] step statistics, one shard per XCD slot (atomic adds)
   uint32_t* pflag;          // [NB][PART/32] groups handed from k_apply_fast to k_apply
   uint32_t* resume;         // [G] messages consumed by k_apply_fast | prop pending << 31
   uint64_t* commit0;        // [G] committed at batch start (for HB_STAT_COMMITS)
@@ -369,6 +369,27 @@ struct ApplyArgs {
 
 // stats slots reduced per workgroup
 enum { ST_MSGS, ST_APPRESP, ST_VOTERESP, ST_DROPPED, ST_COMMITS, ST_WON, ST_LOST, ST_FAULTS, ST_ENTRIES, ST_N };
+
+// Diagnostic build only (-DHB_X_STAMPS): per-workgroup phase timestamps of
+// k_apply_fast (tid 0, s_memtime cycles + s_memrealtime at start/end).
+#ifdef HB_X_STAMPS
+__device__ uint64_t g_stamps[1 << 20];
+#define XSTAMP(k)                                                                          \
+  do {                                                                                     \
+    if (threadIdx.x == 0) g_stamps[(size_t)block_part() * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define XSTAMP_RT(k)                                                                       \
+  do {                                                                                     \
+    if (threadIdx.x == 0) g_stamps[(size_t)block_part() * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define XSTAMP(k) \
+  do {            \
+  } while (0)
+#define XSTAMP_RT(k) \
+  do {               \
+  } while (0)
+#endif
 
 #ifndef HB_FAST_WAVES
 #define HB_FAST_WAVES 4
@@ -386,16 +407,20 @@ __device__ __forceinline__ uint32_t block_part() {
 }
 
 // LDS staging of one round (<= CHUNK messages) of a partition's messages.
+// w[j][i] = word j of the round's i-th MsgRec (info, orig, term lo/hi, index lo/hi).
+// (Gathering the records by LDS-DMA, global_load_lds_dword x6, measured slower
+// than register staging: 6 requests per record instead of 2-3.)
 struct Stage {
   uint32_t rbuf[CHUNK];   // bucket-relative positions, increasing (= arrival order)
-  uint32_t info[CHUNK];
-  uint32_t orig[CHUNK];
-  uint64_t term[CHUNK];
-  uint64_t index[CHUNK];
+  uint32_t w[6][CHUNK];
   uint16_t perm[CHUNK];
   uint32_t cnt[PART];
   uint32_t sh16[16];
   uint64_t bcast;
+  __device__ __forceinline__ uint32_t info(uint32_t i) const { return w[0][i]; }
+  __device__ __forceinline__ uint32_t orig(uint32_t i) const { return w[1][i]; }
+  __device__ __forceinline__ uint64_t term(uint32_t i) const { return (uint64_t)w[2][i] | ((uint64_t)w[3][i] << 32); }
+  __device__ __forceinline__ uint64_t index(uint32_t i) const { return (uint64_t)w[4][i] | ((uint64_t)w[5][i] << 32); }
 };
 
 // This lane's KPL key bytes of segment `seg` (positions seg + tid*KPL + k):
@@ -497,10 +522,12 @@ __device__ __forceinline__ void gather_round(Stage& sl, const ApplyArgs& a, uint
   for (uint32_t k = 0; k < PER; ++k) {
     const uint32_t i = tid + k * PART;
     if (i < fill) {
-      sl.info[i] = m[k].info;
-      sl.orig[i] = m[k].orig;
-      sl.term[i] = m[k].term;
-      sl.index[i] = m[k].index;
+      sl.w[0][i] = m[k].info;
+      sl.w[1][i] = m[k].orig;
+      sl.w[2][i] = (uint32_t)m[k].term;
+      sl.w[3][i] = (uint32_t)(m[k].term >> 32);
+      sl.w[4][i] = (uint32_t)m[k].index;
+      sl.w[5][i] = (uint32_t)(m[k].index >> 32);
       atomicAdd(&sl.cnt[(m[k].info >> 16) & (PART - 1)], 1u);
     }
   }
@@ -511,7 +538,7 @@ __device__ __forceinline__ void gather_round(Stage& sl, const ApplyArgs& a, uint
   sl.cnt[tid] = my_start;  // becomes the fill cursor
   __syncthreads();
   for (uint32_t i = tid; i < fill; i += PART) {
-    const uint32_t pos = atomicAdd(&sl.cnt[(sl.info[i] >> 16) & (PART - 1)], 1u);
+    const uint32_t pos = atomicAdd(&sl.cnt[(sl.info(i) >> 16) & (PART - 1)], 1u);
     sl.perm[pos] = (uint16_t)i;
   }
   __syncthreads();
@@ -533,10 +560,11 @@ __device__ __forceinline__ bool is_response(uint32_t type) {  // raft/util.go:53
          type == HB_MSG_UNREACHABLE;
 }
 
-// Reduce the lane statistics into the partition's stats row (accumulate: the
-// general kernel adds to what the fast kernel wrote).
+// Reduce the lane statistics of the workgroup and add them (plus the events
+// it reserved) to this XCD slot's shard of the step statistics: one no-return
+// atomic per value per workgroup, spread over 8 shards; k_finish sums them.
 __device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_stats, const uint64_t (&vals)[ST_N],
-                                             uint32_t part, bool accumulate) {
+                                             uint64_t events) {
   const uint32_t tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < ST_N; ++k) {
@@ -546,10 +574,8 @@ __device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_sta
     if ((tid & 63) == 0 && v) atomicAdd((unsigned long long*)&l_stats[k], (unsigned long long)v);
   }
   __syncthreads();
-  if (tid < ST_N) {
-    uint64_t* dst = &a.stats_part[(size_t)part * ST_N + tid];
-    *dst = (accumulate ? *dst : 0ull) + l_stats[tid];
-  }
+  const uint64_t v = tid < ST_N ? l_stats[tid] : (tid == ST_N ? events : 0ull);
+  if (tid <= ST_N && v) atomicAdd((unsigned long long*)&a.stats_shard[(blockIdx.x & 7) * 16 + tid], (unsigned long long)v);
 }
 
 // ---------------------------------------------------------------------------
@@ -567,6 +593,8 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
 
   const uint32_t part = block_part();
   if (part >= a.NB) return;  // uniform: grid padding
+  XSTAMP_RT(6);
+  XSTAMP(0);
   const uint32_t tid = threadIdx.x;
   const uint32_t bk = part >> SIS_LOG, sub = part & (SIS - 1);
   const uint32_t g = part * PART + tid;
@@ -595,6 +623,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   uint32_t j = 0;  // messages of this lane consumed so far (all rounds)
 
   auto on_total = [&](uint32_t total) {
+    XSTAMP(1);
     // Exact chunk: every event is emitted while stepping a message (or the
     // group's proposal), at most ev_per_msg per message.
     if (tid == 0) {
@@ -616,15 +645,17 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
         resume = 1u << 31;  // the proposal itself is pending
       }
     }
+    XSTAMP(2);
   };
   auto round = [&](uint32_t fill) {
     uint32_t my_start, my_cnt;
     gather_round(sl, a, lo, fill, &my_start, &my_cnt);
+    XSTAMP(3);
     if (live) {
       for (uint32_t x = 0; x < my_cnt; ++x) {
         if (flagged || L.faulted()) break;
         const uint32_t i = sl.perm[my_start + x];
-        const uint32_t inf = sl.info[i];
+        const uint32_t inf = sl.info(i);
         const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
         const bool reject = (inf >> 8) & 1u;
         if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
@@ -632,19 +663,20 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
           j++;
           continue;
         }
-        const uint64_t mterm = sl.term[i];
+        const uint64_t mterm = sl.term(i);
         if (!L.accept_ok(type, from, mterm, reject)) {
           flagged = true;
           resume = j;
           break;
         }
-        L.arrival = sl.orig[i];
-        L.accept(from, sl.index[i]);
+        L.arrival = sl.orig(i);
+        L.accept(from, sl.index(i));
         st_msgs++;
         j++;
       }
     }
     __syncthreads();
+    XSTAMP(4);
   };
   walk_partition(sl, a, lo, hi, sub, on_total, round);
 
@@ -663,10 +695,11 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
                                0,
                                (uint64_t)(L.faulted() != 0 && live),
                                L.last - last0};
-  reduce_stats(a, l_stats, vals, part, false);
+  reduce_stats(a, l_stats, vals, l_fill);
   if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
   if (tid == 0) a.ev_counts[part] = l_fill;
-  if (tid == 1) a.stats_part[(size_t)a.NB * ST_N + part] = l_fill;  // events reserved
+  XSTAMP(5);
+  XSTAMP_RT(7);
 }
 
 // ---------------------------------------------------------------------------
@@ -694,7 +727,8 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
   if (!any) return;  // uniform
   const bool flagged = (l_flag[tid >> 5] >> (tid & 31)) & 1u;
 
-  if (tid == 0) l_fill = a.ev_counts[part];  // append after the fast kernel's events
+  const uint32_t fill0 = a.ev_counts[part];
+  if (tid == 0) l_fill = fill0;  // append after the fast kernel's events
   if (tid < ST_N) l_stats[tid] = 0;
 
   Lane<NMAX> L;
@@ -736,7 +770,7 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
       for (uint32_t x = 0; x < my_cnt; ++x, ++j) {
         if (j < skip) continue;
         const uint32_t i = sl.perm[my_start + x];
-        const uint32_t inf = sl.info[i];
+        const uint32_t inf = sl.info(i);
         const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
         const bool reject = (inf >> 8) & 1u;
         if (L.faulted()) break;
@@ -744,8 +778,8 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
           st_drop++;
           continue;
         }
-        L.arrival = sl.orig[i];
-        L.step(type, from, sl.term[i], sl.index[i], reject, (reject && a.hint) ? a.hint[sl.orig[i]] : 0ull);
+        L.arrival = sl.orig(i);
+        L.step(type, from, sl.term(i), sl.index(i), reject, (reject && a.hint) ? a.hint[sl.orig(i)] : 0ull);
         st_msgs++;
         st_app += type == HB_MSG_APP_RESP;
         st_vote += type == HB_MSG_VOTE_RESP;
@@ -765,35 +799,27 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
                                L.lost,
                                (uint64_t)(flagged && L.faulted() != 0),
                                L.last - last0};
-  reduce_stats(a, l_stats, vals, part, true);
+  reduce_stats(a, l_stats, vals, l_fill - fill0);
   if (tid == 0) a.ev_counts[part] = l_fill;
-  if (tid == 1) a.stats_part[(size_t)a.NB * ST_N + part] = l_fill;  // events reserved
 }
 
 // ============================================================================
 // Phase 3: finish
 // ============================================================================
-__global__ void __launch_bounds__(1024) k_finish(const uint64_t* stats_part, uint32_t NB, uint64_t* stats) {
-  __shared__ uint64_t acc[HB_STAT_COUNT];
-  if (threadIdx.x < HB_STAT_COUNT) acc[threadIdx.x] = 0;
-  __syncthreads();
-  uint64_t v[ST_N + 1] = {};
-  for (uint32_t p = threadIdx.x; p < NB; p += blockDim.x) {
-#pragma unroll
-    for (int k = 0; k < ST_N; ++k) v[k] += stats_part[(size_t)p * ST_N + k];
-    v[ST_N] += stats_part[(size_t)NB * ST_N + p];
-  }
+__global__ void __launch_bounds__(64) k_finish(uint64_t* shard, uint64_t* stats, uint64_t* accum) {
   const int map[ST_N + 1] = {HB_STAT_MSGS,  HB_STAT_APPRESP, HB_STAT_VOTERESP, HB_STAT_DROPPED, HB_STAT_COMMITS,
                              HB_STAT_WON,   HB_STAT_LOST,    HB_STAT_FAULTS,   HB_STAT_ENTRIES, HB_STAT_EVENTS};
+  const uint32_t k = threadIdx.x;
+  if (k <= ST_N) {
+    uint64_t v = 0;
 #pragma unroll
-  for (int k = 0; k <= ST_N; ++k) {
-    uint64_t x = v[k];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
-    if ((threadIdx.x & 63) == 0 && x) atomicAdd((unsigned long long*)&acc[map[k]], (unsigned long long)x);
+    for (int x = 0; x < 8; ++x) {
+      v += shard[x * 16 + k];
+      shard[x * 16 + k] = 0;  // ready for the next step
+    }
+    stats[map[k]] = v;
+    if (accum) accum[map[k]] += v;
   }
-  __syncthreads();
-  if (threadIdx.x < HB_STAT_COUNT) stats[threadIdx.x] = acc[threadIdx.x];
 }
 
 // ============================================================================
@@ -942,7 +968,8 @@ struct hb_handle {
   uint32_t ev_per_msg = 0;
   uint32_t* ev_counts = nullptr;  // [NB]
   uint64_t* ev_off = nullptr;     // [NB]
-  uint64_t* stats_part = nullptr;
+  uint64_t* stats_shard = nullptr;  // [8][16]
+  uint64_t* stats_accum = nullptr;  // optional caller buffer (hb_set_stats_accum)
   uint64_t* stats = nullptr;
   // fast -> general hand-over
   uint32_t* pflag = nullptr;      // [NB][PART/32]
@@ -1082,7 +1109,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->ev, h->ev_region);
   ALLOC(h->ev_counts, h->NB);
   ALLOC(h->ev_off, h->NB);
-  ALLOC(h->stats_part, (size_t)h->NB * (ST_N + 1) + 16);
+  ALLOC(h->stats_shard, 8 * 16);
   ALLOC(h->pflag, (size_t)h->NB * FLAG_WORDS);
   ALLOC(h->resume, G);
   ALLOC(h->commit0, G);
@@ -1100,7 +1127,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
       }
   // empty slots (n = 0), zeroed progress
   if (hipMemset(s.meta, 0, G * 8) != hipSuccess || hipMemset(s.pm, 0, R * G * 4) != hipSuccess ||
-      hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess ||
+      hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess || hipMemset(h->stats_shard, 0, 8 * 16 * 8) != hipSuccess ||
       hipMemset(h->ev_counts, 0, h->NB * 4ull) != hipSuccess || hipMemset(h->ev_off, 0, h->NB * 8ull) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     hb_destroy(h);
@@ -1303,7 +1330,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.NB = NB;
   aa.ev_counts = h->ev_counts;
   aa.ev_off = h->ev_off;
-  aa.stats_part = h->stats_part;
+  aa.stats_shard = h->stats_shard;
   aa.pflag = h->pflag;
   aa.resume = h->resume;
   aa.commit0 = h->commit0;
@@ -1314,7 +1341,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   }
   if (prof) HB_CHECK(hipEventRecord(ev[2], st));
   // ---- phase 3: finish -----------------------------------------------------------
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(1024), 0, st, h->stats_part, NB, h->stats);
+  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, h->stats_shard, h->stats, h->stats_accum);
   if (prof) HB_CHECK(hipEventRecord(ev[3], st));
   HB_CHECK(hipGetLastError());
   if (prof) h->prof_n++;
@@ -1389,6 +1416,12 @@ int hb_phase_reset(hb_handle* h) {
   return HB_OK;
 }
 
+int hb_set_stats_accum(hb_handle* h, uint64_t* dev_accum) {
+  if (!h) return HB_EINVAL;
+  h->stats_accum = dev_accum;
+  return HB_OK;
+}
+
 int hb_stats_to(hb_handle* h, uint64_t* dev_dst) {
   if (!h || !dev_dst) return HB_EINVAL;
   DeviceGuard guard(h->device);
@@ -1400,6 +1433,12 @@ int hb_alloc_pinned(size_t bytes, void** out) {
   if (!out) return HB_EINVAL;
   return hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? HB_OK : HB_ENOMEM;
 }
+
+#ifdef HB_X_STAMPS
+int hb_x_stamps(uint64_t* out, uint32_t n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)n * 8) == hipSuccess ? HB_OK : HB_EDEVICE;
+}
+#endif
 
 int hb_free_pinned(void* p) { return hipHostFree(p) == hipSuccess ? HB_OK : HB_EDEVICE; }
 

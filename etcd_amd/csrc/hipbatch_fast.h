@@ -79,22 +79,29 @@ struct FastLane {
     for (int s = 0; s < NMAX; ++s) head[s] = pm_count(pm[s]) ? *ring_at(s, pm_start(pm[s])) : 0;
     dirty = 0;
   }
+  // Dirty bits (hipbatch_kernels.h) plus, lane-local to the fast path:
+  // D_TFIRST (tfirst alone; D_TRUN then means tlast) and per-slot D_PM0 + s
+  // (pm alone; D_SLOT0 + s then means match / next).
+  static constexpr uint32_t D_TFIRST = 1u << 5;
+  static constexpr uint32_t D_PM0 = 16;
   __device__ __forceinline__ void store() {
     if (dirty & D_META) reinterpret_cast<uint32_t*>(S.meta)[2 * (size_t)g] = mlo;  // little-endian low word
     if (dirty & D_COMMIT) S.commit[g] = committed;
     if (dirty & D_LAST) S.last[g] = last;
-    if (dirty & D_TRUN) {
-      S.tfirst[g] = tfirst;
-      S.tlast[g] = tlast;
-    }
+    if (dirty & D_TFIRST) S.tfirst[g] = tfirst;
+    if (dirty & D_TRUN) S.tlast[g] = tlast;
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) {
       if (dirty & (1u << (D_SLOT0 + s))) {
         S.match[(size_t)s * S.G + g] = match[s];
         S.next[(size_t)s * S.G + g] = next[s];
-        S.pm[(size_t)s * S.G + g] = pm[s];
       }
+      if (dirty & (1u << (D_PM0 + s))) S.pm[(size_t)s * S.G + g] = pm[s];
     }
+  }
+  __device__ __forceinline__ void set_pm(int s, uint32_t v) {
+    if (v != pm[s]) dirty |= 1u << (D_PM0 + s);
+    pm[s] = v;
   }
 
   // isPaused raft/progress.go:147-158
@@ -122,7 +129,7 @@ struct FastLane {
       v = *ring_at(s, idx);
       if (to < v) break;
     }
-    pm[s] = pm_make(pm_state(p), pm_paused(p), idx, cnt - i);
+    set_pm(s, pm_make(pm_state(p), pm_paused(p), idx, cnt - i));
     head[s] = v;
   }
   // raftLog.term(i) == Term over the current-term run (raft/log.go:198-217)
@@ -172,9 +179,8 @@ struct FastLane {
         fault(HB_FAULT_EMPTY_SNAPSHOT);
         return;
       }
-      pm[s] = pm_make(HB_PR_SNAPSHOT, 0, 0, 0);  // becomeSnapshot
+      set_pm(s, pm_make(HB_PR_SNAPSHOT, 0, 0, 0));  // becomeSnapshot
       S.pending[(size_t)s * S.G + g] = snapi;
-      dirty |= 1u << (D_SLOT0 + s);
       ev(HB_EV_SNAP, s, 0, snapi);
       return;
     }
@@ -193,11 +199,11 @@ struct FastLane {
         *ring_at(s, idx) = lastsent;              // inflights.add
         if (cnt == 0) head[s] = lastsent;
         next[s] = lastsent + 1;                   // optimisticUpdate
-        pm[s] = pm_make(HB_PR_REPLICATE, pm_paused(p), start, cnt + 1);
+        dirty |= 1u << (D_SLOT0 + s);
+        set_pm(s, pm_make(HB_PR_REPLICATE, pm_paused(p), start, cnt + 1));
       } else if (st == HB_PR_PROBE) {
-        pm[s] = p | PM_PAUSED;                    // pause
+        set_pm(s, p | PM_PAUSED);                 // pause
       }
-      dirty |= 1u << (D_SLOT0 + s);
     }
     ev(HB_EV_APP, s, 0, x);
   }
@@ -225,7 +231,10 @@ struct FastLane {
   __device__ __forceinline__ void prop(uint32_t k) {
     const uint64_t old = last;
     last += k;
-    if (tfirst == HB_NO_INDEX) tfirst = old + 1;
+    if (tfirst == HB_NO_INDEX) {
+      tfirst = old + 1;
+      dirty |= D_TFIRST;
+    }
     tlast = last;
     dirty |= D_LAST | D_TRUN;
     ev(HB_EV_LAST, 0, 0, last);
@@ -235,7 +244,7 @@ struct FastLane {
       if ((uint32_t)s == sf) {  // self maybeUpdate(lastIndex) raft/raft.go:358
         if (match[s] < last) {
           match[s] = last;
-          pm[s] &= ~PM_PAUSED;
+          set_pm(s, pm[s] & ~PM_PAUSED);
         }
         if (next[s] < last + 1) next[s] = last + 1;
         dirty |= 1u << (D_SLOT0 + s);
@@ -256,7 +265,7 @@ struct FastLane {
         if (next[s] < index + 1) next[s] = index + 1;
         if (match[s] < index) {                   // maybeUpdate raft/progress.go:102-113
           match[s] = index;
-          pm[s] &= ~PM_PAUSED;
+          set_pm(s, pm[s] & ~PM_PAUSED);
           updated = true;
           free_to(s, index);                      // Replicate: ins.freeTo(m.Index)
         }

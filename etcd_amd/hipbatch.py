@@ -60,6 +60,7 @@ def lib():
         "hb_phase_ms": (C.c_int, [H, C.c_void_p, P(C.c_uint32)]),
         "hb_phase_reset": (C.c_int, [H]),
         "hb_stats_to": (C.c_int, [H, C.c_void_p]),
+        "hb_set_stats_accum": (C.c_int, [H, C.c_void_p]),
         "hb_alloc_pinned": (C.c_int, [C.c_size_t, P(C.c_void_p)]),
         "hb_free_pinned": (C.c_int, [C.c_void_p]),
     }
@@ -191,6 +192,13 @@ class Engine:
         """Async D2D copy of the last step's stats to a device buffer (torch tensor or int)."""
         _check("hb_stats_to", lib().hb_stats_to(self.h, C.c_void_p(_ptr(dev_ptr) if not isinstance(dev_ptr, int)
                                                                    else dev_ptr)))
+
+    def set_stats_accum(self, dev_ptr):
+        """Accumulate every later step's statistics into a device buffer of
+        HB_STAT_COUNT u64 (torch tensor or raw pointer) inside the finish
+        phase; None turns it off."""
+        p = None if dev_ptr is None else (dev_ptr if isinstance(dev_ptr, int) else _ptr(dev_ptr))
+        _check("hb_set_stats_accum", lib().hb_set_stats_accum(self.h, C.c_void_p(p)))
 
     def phase_reset(self):
         _check("hb_phase_reset", lib().hb_phase_reset(self.h))

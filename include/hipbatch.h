@@ -279,7 +279,7 @@ int  hb_get_inflights(hb_handle* h, uint32_t group, uint32_t slot,
 int  hb_step(hb_handle* h, const hb_batch* b, uint32_t flags);
 
 /* Events of the last step, as written by the device: `n_chunks` chunks (one
- * per 1024-group partition); chunk c holds counts[c] events at
+ * per 256-group partition); chunk c holds counts[c] events at
  * base + chunk_off[c], and all events of a group are in one chunk, in order.
  * Device pointers; valid until the next hb_step. */
 int  hb_events_device(hb_handle* h, const hb_event** base, const uint64_t** chunk_off,
@@ -294,6 +294,10 @@ int  hb_stats(hb_handle* h, uint64_t* out);
 /* Asynchronous device-to-device copy of the last step's statistics (on the
  * handle's stream), e.g. into a buffer that an RCCL all-reduce then sums. */
 int  hb_stats_to(hb_handle* h, uint64_t* dev_dst /* [HB_STAT_COUNT] */);
+/* Optional device accumulator: every later hb_step also adds its statistics
+ * into dev_accum[HB_STAT_COUNT] in its finish phase (no extra launch).
+ * NULL turns it off.  The buffer must outlive its use. */
+int  hb_set_stats_accum(hb_handle* h, uint64_t* dev_accum);
 /* Per-phase device time (ms) averaged over the HB_STEP_PROFILE steps since
  * hb_phase_reset (the last 256 of them); *steps = how many (synchronizes). */
 int  hb_phase_ms(hb_handle* h, float* out /* [HB_PHASE_COUNT] */, uint32_t* steps);
