@@ -423,27 +423,37 @@ struct Stage {
   __device__ __forceinline__ uint64_t index(uint32_t i) const { return (uint64_t)w[4][i] | ((uint64_t)w[5][i] << 32); }
 };
 
-// This lane's KPL key bytes of segment `seg` (positions seg + tid*KPL + k):
-// bit k set where the key equals `sub` and the position is in [lo, hi).
-// Four keys per dword: a SWAR zero-byte test, then the four byte flags are
-// gathered into a nibble by one multiply.
-__device__ __forceinline__ uint64_t scan_keys(const uint8_t* key, uint32_t seg, uint32_t lo, uint32_t hi,
-                                              uint32_t sub) {
-  const uint32_t base = seg + threadIdx.x * KPL;
+// This lane's KPL key bytes of segment `seg` (positions seg + tid*KPL + k).
+// load_keys only issues the loads, so the caller can overlap them with other
+// work; eval_keys returns bit k set where the key equals `sub` and the
+// position is in [lo, hi).  Four keys per dword: a SWAR zero-byte test, then
+// the four byte flags are gathered into a nibble by one multiply.
+struct Keys {
+  uint4 q[KPL / 16];
+  uint32_t base;
+};
+__device__ __forceinline__ Keys load_keys(const uint8_t* key, uint32_t seg, uint32_t lo, uint32_t hi) {
+  Keys k;
+  k.base = seg + threadIdx.x * KPL;
+  const uint4* p = reinterpret_cast<const uint4*>(key + k.base);
+#pragma unroll
+  for (int q = 0; q < (int)(KPL / 16); ++q) k.q[q] = (k.base < hi && k.base + KPL > lo) ? p[q] : make_uint4(0, 0, 0, 0);
+  return k;
+}
+__device__ __forceinline__ uint64_t eval_keys(const Keys& k, uint32_t lo, uint32_t hi, uint32_t sub) {
+  const uint32_t base = k.base;
   if (base >= hi || base + KPL <= lo) return 0;
-  const uint4* p = reinterpret_cast<const uint4*>(key + base);
   const uint32_t rep = sub * 0x01010101u;
   uint64_t eq = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint4 w4 = p[q];
-    const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+  for (int q = 0; q < (int)(KPL / 16); ++q) {
+    const uint32_t w[4] = {k.q[q].x, k.q[q].y, k.q[q].z, k.q[q].w};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t x = w[k] ^ rep;
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t x = w[j] ^ rep;
       const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // 0x80 where byte == sub
       const uint32_t c = (((z >> 7) * 0x01020408u) >> 24) & 0xFu;                 // bytes 0..3 -> bits 0..3
-      eq |= (uint64_t)c << (16 * q + 4 * k);
+      eq |= (uint64_t)c << (16 * q + 4 * j);
     }
   }
   const uint32_t a = lo > base ? lo - base : 0u;                // < KPL
@@ -451,14 +461,19 @@ __device__ __forceinline__ uint64_t scan_keys(const uint8_t* key, uint32_t seg, 
   const uint64_t vm = (b >= 64 ? ~0ull : ((1ull << b) - 1)) & (~0ull << a);
   return eq & vm;
 }
+__device__ __forceinline__ uint64_t scan_keys(const uint8_t* key, uint32_t seg, uint32_t lo, uint32_t hi,
+                                              uint32_t sub) {
+  return eval_keys(load_keys(key, seg, lo, hi), lo, hi, sub);
+}
 
 // Walk the partition's messages of bucket [lo, hi) in arrival order, in
 // rounds of at most CHUNK.  on_total(total) runs once (all threads) before
 // the first round with the partition's message count; round(fill) runs per
 // round with sl.rbuf[0, fill) = the round's bucket-relative positions.
+// `first`: the keys of segment 0, already loaded by the caller (or null).
 template <class OnTotal, class Round>
 __device__ __forceinline__ void walk_partition(Stage& sl, const ApplyArgs& a, uint32_t lo, uint32_t hi, uint32_t sub,
-                                               OnTotal&& on_total, Round&& round) {
+                                               const Keys* first, OnTotal&& on_total, Round&& round) {
   const uint32_t tid = threadIdx.x;
   const uint32_t seg0 = lo & ~15u;
   const uint32_t nseg = hi > lo ? (hi - seg0 + SEG - 1) / SEG : 0u;  // uniform
@@ -474,7 +489,7 @@ __device__ __forceinline__ void walk_partition(Stage& sl, const ApplyArgs& a, ui
   uint32_t fill = 0;  // uniform
   for (uint32_t s = 0; s < nseg; ++s) {
     const uint32_t seg = seg0 + s * SEG;
-    const uint64_t eq = scan_keys(a.key, seg, lo, hi, sub);
+    const uint64_t eq = (s == 0 && first) ? eval_keys(*first, lo, hi, sub) : scan_keys(a.key, seg, lo, hi, sub);
     uint32_t tot;
     const uint32_t pre = block_excl_scan((uint32_t)__popcll(eq), sl.sh16, &tot);
     if (nseg == 1) on_total(tot);
@@ -506,8 +521,10 @@ __device__ __forceinline__ void walk_partition(Stage& sl, const ApplyArgs& a, ui
 
 // Gather the round's records into LDS and counting-sort them by lane: on
 // return the lane's messages are perm[*start, *start + *cnt), in arrival order.
+// `issued()` runs once the round's record loads are in flight.
+template <class Issued>
 __device__ __forceinline__ void gather_round(Stage& sl, const ApplyArgs& a, uint32_t lo, uint32_t fill,
-                                             uint32_t* start, uint32_t* cnt) {
+                                             uint32_t* start, uint32_t* cnt, Issued&& issued) {
   constexpr uint32_t PER = CHUNK / PART;
   const uint32_t tid = threadIdx.x;
   sl.cnt[tid] = 0;
@@ -518,6 +535,7 @@ __device__ __forceinline__ void gather_round(Stage& sl, const ApplyArgs& a, uint
     const uint32_t i = tid + k * PART;
     if (i < fill) m[k] = a.rec[lo + sl.rbuf[i]];
   }
+  issued();
 #pragma unroll
   for (uint32_t k = 0; k < PER; ++k) {
     const uint32_t i = tid + k * PART;
@@ -587,7 +605,7 @@ __device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_sta
 template <int NMAX>
 __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply_fast(ApplyArgs a) {
   __shared__ Stage sl;
-  __shared__ uint32_t l_fill;
+  __shared__ uint32_t l_fill, l_pfill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N];
 
@@ -599,14 +617,15 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   const uint32_t bk = part >> SIS_LOG, sub = part & (SIS - 1);
   const uint32_t g = part * PART + tid;
   const bool gvalid = g < a.S.G;
-  if (tid == 0) l_fill = 0;
+  if (tid == 0) l_fill = l_pfill = 0;
   if (tid < ST_N) l_stats[tid] = 0;
   if (tid < FLAG_WORDS) l_flag[tid] = 0;
 
+  // ---- issue the lane's loads: group state, then this lane's bucket keys of
+  // segment 0 (the proposal below overlaps the key loads).
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
   FastLane<NMAX> L;
   L.S = a.S;
-  L.E.fill = &l_fill;
   L.g = g;
   L.mlo = gvalid ? reinterpret_cast<const uint32_t*>(a.S.meta)[2 * (size_t)g] : 0u;
   const uint32_t prop_raw = (a.props && gvalid) ? a.props[g] : 0u;
@@ -616,25 +635,20 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   L.last = L.committed = 0;
   if ((a.props_on || hi > lo) && live) L.load();
   const uint64_t last0 = L.last, commit0 = L.committed;
+  const Keys k0 = load_keys(a.key, lo & ~15u, lo, hi);
 
   bool flagged = false;
   uint32_t resume = 0;
   uint32_t st_msgs = 0, st_drop = 0;
   uint32_t j = 0;  // messages of this lane consumed so far (all rounds)
 
-  auto on_total = [&](uint32_t total) {
-    XSTAMP(1);
-    // Exact chunk: every event is emitted while stepping a message (or the
-    // group's proposal), at most ev_per_msg per message.
-    if (tid == 0) {
-      const uint64_t reg = (uint64_t)a.ev_per_msg * ((uint64_t)lo + (uint64_t)bk * (PART * SIS) * a.props_on);
-      const uint32_t mine = a.ev_per_msg * (total + PART * a.props_on);
-      const uint64_t off = reg + atomicAdd(&a.bk_fill[bk], mine);
-      sl.bcast = off;
-      a.ev_off[part] = off;
-    }
-    __syncthreads();
-    L.E.chunk = a.ev + sl.bcast;
+  // ---- the dense proposal: its events go to the partition's P chunk (fixed
+  // slot of ev_per_msg x PART records), before any message event of the group.
+  {
+    const uint64_t poff = (uint64_t)part * PART * a.ev_per_msg;
+    if (tid == 0) a.ev_off[2 * part] = poff;
+    L.E.chunk = a.ev + poff;
+    L.E.fill = &l_pfill;
     const uint32_t prop_k = live ? prop_raw : 0u;
     if (prop_k) {
       if (L.prop_ok(prop_k)) {
@@ -642,14 +656,33 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
         L.prop(prop_k);
       } else {
         flagged = true;
-        resume = 1u << 31;  // the proposal itself is pending
+        resume = 1u << 31;  // the proposal itself is pending (stepped by k_apply into the M chunk)
       }
     }
+  }
+  XSTAMP(1);
+
+  // ---- messages: M chunk of ev_per_msg x (messages + PART) records reserved
+  // in the bucket's region (the general kernel may append a pending proposal).
+  uint32_t moff_pending = 0;
+  bool first_round = true;
+  auto on_total = [&](uint32_t total) {
+    if (tid == 0) moff_pending = atomicAdd(&a.bk_fill[bk], a.ev_per_msg * (total + PART * a.props_on));
     XSTAMP(2);
   };
   auto round = [&](uint32_t fill) {
     uint32_t my_start, my_cnt;
-    gather_round(sl, a, lo, fill, &my_start, &my_cnt);
+    gather_round(sl, a, lo, fill, &my_start, &my_cnt, [&]() {
+      if (first_round && tid == 0) sl.bcast = moff_pending;  // waits for the atomic only
+    });
+    if (first_round) {
+      const uint64_t moff = (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + (uint64_t)lo +
+                                                      (uint64_t)bk * (PART * SIS) * a.props_on) + sl.bcast;
+      if (tid == 0) a.ev_off[2 * part + 1] = moff;
+      L.E.chunk = a.ev + moff;
+      L.E.fill = &l_fill;
+      first_round = false;
+    }
     XSTAMP(3);
     if (live) {
       for (uint32_t x = 0; x < my_cnt; ++x) {
@@ -678,7 +711,10 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
     __syncthreads();
     XSTAMP(4);
   };
-  walk_partition(sl, a, lo, hi, sub, on_total, round);
+  walk_partition(sl, a, lo, hi, sub, &k0, on_total, round);
+  if (first_round && tid == 0)  // no message for this partition: the M chunk is only reserved
+    a.ev_off[2 * part + 1] = (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + (uint64_t)lo +
+                                                       (uint64_t)bk * (PART * SIS) * a.props_on) + moff_pending;
 
   L.store();
   if (flagged) {
@@ -695,9 +731,12 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
                                0,
                                (uint64_t)(L.faulted() != 0 && live),
                                L.last - last0};
-  reduce_stats(a, l_stats, vals, l_fill);
+  reduce_stats(a, l_stats, vals, (uint64_t)l_fill + l_pfill);
   if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
-  if (tid == 0) a.ev_counts[part] = l_fill;
+  if (tid == 0) {
+    a.ev_counts[2 * part] = l_pfill;
+    a.ev_counts[2 * part + 1] = l_fill;
+  }
   XSTAMP(5);
   XSTAMP_RT(7);
 }
@@ -727,13 +766,13 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
   if (!any) return;  // uniform
   const bool flagged = (l_flag[tid >> 5] >> (tid & 31)) & 1u;
 
-  const uint32_t fill0 = a.ev_counts[part];
-  if (tid == 0) l_fill = fill0;  // append after the fast kernel's events
+  const uint32_t fill0 = a.ev_counts[2 * part + 1];
+  if (tid == 0) l_fill = fill0;  // append to the M chunk after the fast kernel's events
   if (tid < ST_N) l_stats[tid] = 0;
 
   Lane<NMAX> L;
   L.S = a.S;
-  L.E.chunk = a.ev + a.ev_off[part];
+  L.E.chunk = a.ev + a.ev_off[2 * part + 1];
   L.E.fill = &l_fill;
   L.g = g;
   L.won = 0;
@@ -765,7 +804,7 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
   };
   auto round = [&](uint32_t fill) {
     uint32_t my_start, my_cnt;
-    gather_round(sl, a, lo, fill, &my_start, &my_cnt);
+    gather_round(sl, a, lo, fill, &my_start, &my_cnt, []() {});
     if (flagged) {
       for (uint32_t x = 0; x < my_cnt; ++x, ++j) {
         if (j < skip) continue;
@@ -787,7 +826,7 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
     }
     __syncthreads();
   };
-  walk_partition(sl, a, lo, hi, sub, on_total, round);
+  walk_partition(sl, a, lo, hi, sub, nullptr, on_total, round);
 
   if (flagged) L.store();
   const uint64_t vals[ST_N] = {st_msgs,
@@ -800,7 +839,7 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
                                (uint64_t)(flagged && L.faulted() != 0),
                                L.last - last0};
   reduce_stats(a, l_stats, vals, l_fill - fill0);
-  if (tid == 0) a.ev_counts[part] = l_fill;
+  if (tid == 0) a.ev_counts[2 * part + 1] = l_fill;
 }
 
 // ============================================================================
@@ -917,20 +956,27 @@ __global__ void k_get_ins(DevState S, uint32_t g, uint32_t s, uint64_t* vals, ui
   }
 }
 
-// Dense gather of the chunked events (chunk c at base + c*cap, counts[c]).
-__global__ void __launch_bounds__(256) k_gather_events(const hb_event* base, const uint32_t* counts,
-                                                       const uint64_t* offs, hb_event* out) {
-  __shared__ uint64_t s_off;
-  const uint32_t c = blockIdx.x;
-  if (threadIdx.x == 0) {
-    uint64_t off = 0;
-    for (uint32_t k = 0; k < c; ++k) off += counts[k];
-    s_off = off;
+// Dense gather of the chunked events: chunk c (counts[c] records at
+// base + offs[c]) goes to out + dst[c], dst = exclusive scan of counts
+// (k_scan_counts, one 1024-thread block).
+__global__ void __launch_bounds__(1024) k_scan_counts(const uint32_t* counts, uint32_t n, uint64_t* dst) {
+  __shared__ uint32_t sh16[16];
+  const uint32_t per = (n + 1023) / 1024, b0 = threadIdx.x * per;
+  uint64_t sum = 0;
+  for (uint32_t i = b0; i < b0 + per && i < n; ++i) sum += counts[i];
+  uint32_t tot;
+  uint64_t run = block_excl_scan((uint32_t)sum, sh16, &tot);  // total events < 2^32 (max_batch < 2^31, EV_MAX <= 11)
+  for (uint32_t i = b0; i < b0 + per && i < n; ++i) {
+    dst[i] = run;
+    run += counts[i];
   }
-  __syncthreads();
+}
+__global__ void __launch_bounds__(256) k_gather_events(const hb_event* base, const uint32_t* counts,
+                                                       const uint64_t* offs, const uint64_t* dst, hb_event* out) {
+  const uint32_t c = blockIdx.x;
   const uint32_t cnt = counts[c];
   const hb_event* src = base + offs[c];
-  for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) out[s_off + i] = src[i];
+  for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) out[dst[c] + i] = src[i];
 }
 
 // ============================================================================
@@ -1105,10 +1151,11 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->s_props, G);
   // events: (batch + one proposal slot per group) x EV_MAX (exact bound)
   h->ev_per_msg = h->nmax + 4;
-  h->ev_region = (mb + (uint64_t)h->NBK * (PART * SIS)) * h->ev_per_msg;
+  // P chunks (one per partition, dense proposals) then the bucket regions of M chunks
+  h->ev_region = ((uint64_t)h->NB * PART + mb + (uint64_t)h->NBK * (PART * SIS)) * h->ev_per_msg;
   ALLOC(h->ev, h->ev_region);
-  ALLOC(h->ev_counts, h->NB);
-  ALLOC(h->ev_off, h->NB);
+  ALLOC(h->ev_counts, 2ull * h->NB);
+  ALLOC(h->ev_off, 2ull * h->NB);
   ALLOC(h->stats_shard, 8 * 16);
   ALLOC(h->pflag, (size_t)h->NB * FLAG_WORDS);
   ALLOC(h->resume, G);
@@ -1128,7 +1175,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   // empty slots (n = 0), zeroed progress
   if (hipMemset(s.meta, 0, G * 8) != hipSuccess || hipMemset(s.pm, 0, R * G * 4) != hipSuccess ||
       hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess || hipMemset(h->stats_shard, 0, 8 * 16 * 8) != hipSuccess ||
-      hipMemset(h->ev_counts, 0, h->NB * 4ull) != hipSuccess || hipMemset(h->ev_off, 0, h->NB * 8ull) != hipSuccess ||
+      hipMemset(h->ev_counts, 0, h->NB * 8ull) != hipSuccess || hipMemset(h->ev_off, 0, h->NB * 16ull) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     hb_destroy(h);
     return HB_EDEVICE;
@@ -1355,7 +1402,7 @@ int hb_events_device(hb_handle* h, const hb_event** base, const uint64_t** chunk
   *base = h->ev;
   *chunk_off = h->ev_off;
   *counts = h->ev_counts;
-  *n_chunks = h->NB;
+  *n_chunks = 2 * h->NB;
   return HB_OK;
 }
 
@@ -1370,8 +1417,11 @@ int hb_copy_events(hb_handle* h, hb_event* out, uint64_t cap, uint64_t* n) {
   if (total == 0) return HB_OK;
   if (!out || cap < total) return HB_EINVAL;
   hb_event* d = nullptr;
-  HB_CHECK(hipMalloc(&d, total * sizeof(hb_event)));
-  hipLaunchKernelGGL(k_gather_events, dim3(h->NB), dim3(256), 0, h->stream, h->ev, h->ev_counts, h->ev_off, d);
+  HB_CHECK(hipMalloc(&d, total * sizeof(hb_event) + 16ull * h->NB));
+  uint64_t* dst = reinterpret_cast<uint64_t*>(d + total);
+  hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, h->stream, (const uint32_t*)h->ev_counts, 2 * h->NB, dst);
+  hipLaunchKernelGGL(k_gather_events, dim3(2 * h->NB), dim3(256), 0, h->stream, h->ev, h->ev_counts, h->ev_off,
+                     (const uint64_t*)dst, d);
   hipError_t e = hipMemcpyAsync(out, d, total * sizeof(hb_event), hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   (void)hipFree(d);
