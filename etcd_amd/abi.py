@@ -73,6 +73,8 @@ HB_EV_VOTE = 8
 HB_EV_PROP_FWD = 9
 HB_EV_PROP_DROP = 10
 HB_EV_FAULT = 11
+HB_EVW_BCAST = 12  # device event word: HB_EV_APP to every slot of a mask
+HB_EVW_CONT = 15  # device event word: continuation (x bits 40..63)
 
 HB_STAT_MSGS = 0
 HB_STAT_APPRESP = 1

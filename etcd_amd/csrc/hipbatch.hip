@@ -355,8 +355,8 @@ struct ApplyArgs {
   uint32_t* bk_fill;        // [NBK] event records reserved by the bucket's partitions
   const uint64_t* hint;     // original-order RejectHint
   const uint32_t* props;    // dense proposals or null
-  hb_event* ev;             // event region base
-  uint32_t ev_per_msg;      // bound on events per stepped message (EV_MAX)
+  uint64_t* ev;             // event region base (compact words, hipbatch_kernels.h)
+  uint32_t ev_per_msg;      // bound on event words per stepped message
   uint32_t props_on;        // 1 if props[] is present (one proposal slot per group)
   uint32_t NB;              // partitions
   uint32_t* ev_counts;      // [NB] records in each chunk
@@ -581,18 +581,18 @@ __device__ __forceinline__ bool is_response(uint32_t type) {  // raft/util.go:53
 // Reduce the lane statistics of the workgroup and add them (plus the events
 // it reserved) to this XCD slot's shard of the step statistics: one no-return
 // atomic per value per workgroup, spread over 8 shards; k_finish sums them.
-__device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_stats, const uint64_t (&vals)[ST_N],
-                                             uint64_t events) {
+// vals[ST_N] = the lane's events (public count).
+__device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_stats, const uint64_t (&vals)[ST_N + 1]) {
   const uint32_t tid = threadIdx.x;
 #pragma unroll
-  for (int k = 0; k < ST_N; ++k) {
+  for (int k = 0; k <= ST_N; ++k) {
     uint64_t v = vals[k];
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
     if ((tid & 63) == 0 && v) atomicAdd((unsigned long long*)&l_stats[k], (unsigned long long)v);
   }
   __syncthreads();
-  const uint64_t v = tid < ST_N ? l_stats[tid] : (tid == ST_N ? events : 0ull);
+  const uint64_t v = tid <= ST_N ? l_stats[tid] : 0ull;
   if (tid <= ST_N && v) atomicAdd((unsigned long long*)&a.stats_shard[(blockIdx.x & 7) * 16 + tid], (unsigned long long)v);
 }
 
@@ -607,7 +607,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   __shared__ Stage sl;
   __shared__ uint32_t l_fill, l_pfill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
-  __shared__ uint64_t l_stats[ST_N];
+  __shared__ uint64_t l_stats[ST_N + 1];
 
   const uint32_t part = block_part();
   if (part >= a.NB) return;  // uniform: grid padding
@@ -618,7 +618,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   const uint32_t g = part * PART + tid;
   const bool gvalid = g < a.S.G;
   if (tid == 0) l_fill = l_pfill = 0;
-  if (tid < ST_N) l_stats[tid] = 0;
+  if (tid <= ST_N) l_stats[tid] = 0;
   if (tid < FLAG_WORDS) l_flag[tid] = 0;
 
   // ---- issue the lane's loads: group state, then this lane's bucket keys of
@@ -632,6 +632,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   // A group takes part when its slot is live (n > 0) and not faulted.
   const bool live = gvalid && L.n() != 0 && L.faulted() == 0;
   L.dirty = 0;
+  L.nev = 0;
   L.last = L.committed = 0;
   if ((a.props_on || hi > lo) && live) L.load();
   const uint64_t last0 = L.last, commit0 = L.committed;
@@ -722,16 +723,17 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
     a.resume[g] = resume;
     a.commit0[g] = commit0;
   }
-  const uint64_t vals[ST_N] = {st_msgs,
-                               st_msgs,  // every fast message is a MsgAppResp
-                               0,
-                               st_drop,
-                               (uint64_t)(!flagged && L.committed != commit0),  // commitTo only raises
-                               0,
-                               0,
-                               (uint64_t)(L.faulted() != 0 && live),
-                               L.last - last0};
-  reduce_stats(a, l_stats, vals, (uint64_t)l_fill + l_pfill);
+  const uint64_t vals[ST_N + 1] = {st_msgs,
+                                   st_msgs,  // every fast message is a MsgAppResp
+                                   0,
+                                   st_drop,
+                                   (uint64_t)(!flagged && L.committed != commit0),  // commitTo only raises
+                                   0,
+                                   0,
+                                   (uint64_t)(L.faulted() != 0 && live),
+                                   L.last - last0,
+                                   L.nev};
+  reduce_stats(a, l_stats, vals);
   if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
   if (tid == 0) {
     a.ev_counts[2 * part] = l_pfill;
@@ -751,7 +753,7 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
   __shared__ Stage sl;
   __shared__ uint32_t l_fill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
-  __shared__ uint64_t l_stats[ST_N];
+  __shared__ uint64_t l_stats[ST_N + 1];
 
   const uint32_t part = block_part();
   if (part >= a.NB) return;  // uniform: grid padding
@@ -768,7 +770,7 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
 
   const uint32_t fill0 = a.ev_counts[2 * part + 1];
   if (tid == 0) l_fill = fill0;  // append to the M chunk after the fast kernel's events
-  if (tid < ST_N) l_stats[tid] = 0;
+  if (tid <= ST_N) l_stats[tid] = 0;
 
   Lane<NMAX> L;
   L.S = a.S;
@@ -777,6 +779,7 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
   L.g = g;
   L.won = 0;
   L.lost = 0;
+  L.nev = 0;
   L.dirty = 0;
   L.meta = 0;
   L.last = 0;
@@ -829,16 +832,17 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
   walk_partition(sl, a, lo, hi, sub, nullptr, on_total, round);
 
   if (flagged) L.store();
-  const uint64_t vals[ST_N] = {st_msgs,
-                               st_app,
-                               st_vote,
-                               st_drop,
-                               (uint64_t)(flagged && L.committed != commit0),
-                               L.won,
-                               L.lost,
-                               (uint64_t)(flagged && L.faulted() != 0),
-                               L.last - last0};
-  reduce_stats(a, l_stats, vals, l_fill - fill0);
+  const uint64_t vals[ST_N + 1] = {st_msgs,
+                                   st_app,
+                                   st_vote,
+                                   st_drop,
+                                   (uint64_t)(flagged && L.committed != commit0),
+                                   L.won,
+                                   L.lost,
+                                   (uint64_t)(flagged && L.faulted() != 0),
+                                   L.last - last0,
+                                   L.nev};
+  reduce_stats(a, l_stats, vals);
   if (tid == 0) a.ev_counts[2 * part + 1] = l_fill;
 }
 
@@ -956,27 +960,70 @@ __global__ void k_get_ins(DevState S, uint32_t g, uint32_t s, uint64_t* vals, ui
   }
 }
 
-// Dense gather of the chunked events: chunk c (counts[c] records at
-// base + offs[c]) goes to out + dst[c], dst = exclusive scan of counts
-// (k_scan_counts, one 1024-thread block).
+// Dense gather of the chunked events: chunk c (counts[c] compact words at
+// base + offs[c]; chunk 2p / 2p+1 = partition p's P / M chunk) is expanded
+// into public hb_event records at out + dst[c], dst = exclusive scan of the
+// per-chunk event counts.
+__device__ __forceinline__ uint32_t evc_outputs(uint64_t w) {
+  const uint32_t t = (uint32_t)w & 0xF;
+  if (t == EVC_CONT) return 0;
+  if (t == EVC_BCAST) return __popc((uint32_t)(w >> 4) & 0x7F);
+  return 1;
+}
+__global__ void __launch_bounds__(256) k_chunk_events(const uint64_t* base, const uint32_t* counts,
+                                                      const uint64_t* offs, uint32_t* out_counts) {
+  __shared__ uint32_t sh16[16];
+  const uint32_t c = blockIdx.x, n = counts[c];
+  const uint64_t* src = base + offs[c];
+  uint32_t k = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) k += evc_outputs(src[i]);
+  uint32_t tot;
+  (void)block_excl_scan(k, sh16, &tot);
+  if (threadIdx.x == 0) out_counts[c] = tot;
+}
 __global__ void __launch_bounds__(1024) k_scan_counts(const uint32_t* counts, uint32_t n, uint64_t* dst) {
   __shared__ uint32_t sh16[16];
   const uint32_t per = (n + 1023) / 1024, b0 = threadIdx.x * per;
   uint64_t sum = 0;
   for (uint32_t i = b0; i < b0 + per && i < n; ++i) sum += counts[i];
   uint32_t tot;
-  uint64_t run = block_excl_scan((uint32_t)sum, sh16, &tot);  // total events < 2^32 (max_batch < 2^31, EV_MAX <= 11)
+  uint64_t run = block_excl_scan((uint32_t)sum, sh16, &tot);  // total events < 2^32
   for (uint32_t i = b0; i < b0 + per && i < n; ++i) {
     dst[i] = run;
     run += counts[i];
   }
 }
-__global__ void __launch_bounds__(256) k_gather_events(const hb_event* base, const uint32_t* counts,
+__global__ void __launch_bounds__(256) k_expand_events(const uint64_t* base, const uint32_t* counts,
                                                        const uint64_t* offs, const uint64_t* dst, hb_event* out) {
-  const uint32_t c = blockIdx.x;
-  const uint32_t cnt = counts[c];
-  const hb_event* src = base + offs[c];
-  for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) out[dst[c] + i] = src[i];
+  __shared__ uint32_t sh16[16];
+  const uint32_t c = blockIdx.x, n = counts[c], part = c >> 1;
+  const uint64_t* src = base + offs[c];
+  uint64_t run = dst[c];
+  for (uint32_t t0 = 0; t0 < n; t0 += blockDim.x) {
+    const uint32_t i = t0 + threadIdx.x;
+    const uint64_t w = i < n ? src[i] : (uint64_t)EVC_CONT;
+    const uint32_t k = evc_outputs(w);
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(k, sh16, &tot);
+    if (k) {
+      const uint32_t type = (uint32_t)w & 0xF, to = (uint32_t)(w >> 4) & 0x7F, aux = (uint32_t)(w >> 12) & 0xF;
+      const uint32_t group = part * PART + ((uint32_t)(w >> 16) & 0xFF);
+      uint64_t x = w >> 24;
+      if ((w >> 11) & 1u) x |= (src[i + 1] >> 4) << 40;
+      hb_event* o = out + run + ex;
+      if (type == EVC_BCAST) {
+        uint32_t m = to, r = 0;
+        while (m) {
+          const uint32_t s = __ffs(m) - 1;
+          m &= m - 1;
+          o[r++] = hb_event{x, group, (uint8_t)HB_EV_APP, (uint8_t)s, 0};
+        }
+      } else {
+        o[0] = hb_event{x, group, (uint8_t)type, (uint8_t)to, (uint16_t)aux};
+      }
+    }
+    run += tot;
+  }
 }
 
 // ============================================================================
@@ -1009,7 +1056,7 @@ struct hb_handle {
   uint64_t* s_index = nullptr;
   uint64_t* s_hint = nullptr;
   // events
-  hb_event* ev = nullptr;
+  uint64_t* ev = nullptr;   // compact event words
   uint64_t ev_region = 0;  // records
   uint32_t ev_per_msg = 0;
   uint32_t* ev_counts = nullptr;  // [NB]
@@ -1150,7 +1197,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->s_hint, mb);
   ALLOC(h->s_props, G);
   // events: (batch + one proposal slot per group) x EV_MAX (exact bound)
-  h->ev_per_msg = h->nmax + 4;
+  h->ev_per_msg = EVC_WORDS_MAX * (h->nmax + 4);  // events per message <= nmax + 4, <= 2 words each
   // P chunks (one per partition, dense proposals) then the bucket regions of M chunks
   h->ev_region = ((uint64_t)h->NB * PART + mb + (uint64_t)h->NBK * (PART * SIS)) * h->ev_per_msg;
   ALLOC(h->ev, h->ev_region);
@@ -1396,7 +1443,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   return HB_OK;
 }
 
-int hb_events_device(hb_handle* h, const hb_event** base, const uint64_t** chunk_off, const uint32_t** counts,
+int hb_events_device(hb_handle* h, const uint64_t** base, const uint64_t** chunk_off, const uint32_t** counts,
                      uint32_t* n_chunks) {
   if (!h || !base || !chunk_off || !counts || !n_chunks) return HB_EINVAL;
   *base = h->ev;
@@ -1417,11 +1464,14 @@ int hb_copy_events(hb_handle* h, hb_event* out, uint64_t cap, uint64_t* n) {
   if (total == 0) return HB_OK;
   if (!out || cap < total) return HB_EINVAL;
   hb_event* d = nullptr;
-  HB_CHECK(hipMalloc(&d, total * sizeof(hb_event) + 16ull * h->NB));
+  HB_CHECK(hipMalloc(&d, total * sizeof(hb_event) + 24ull * h->NB));
   uint64_t* dst = reinterpret_cast<uint64_t*>(d + total);
-  hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, h->stream, (const uint32_t*)h->ev_counts, 2 * h->NB, dst);
-  hipLaunchKernelGGL(k_gather_events, dim3(2 * h->NB), dim3(256), 0, h->stream, h->ev, h->ev_counts, h->ev_off,
-                     (const uint64_t*)dst, d);
+  uint32_t* per_chunk = reinterpret_cast<uint32_t*>(dst + 2 * h->NB);
+  hipLaunchKernelGGL(k_chunk_events, dim3(2 * h->NB), dim3(256), 0, h->stream, (const uint64_t*)h->ev,
+                     (const uint32_t*)h->ev_counts, (const uint64_t*)h->ev_off, per_chunk);
+  hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, h->stream, (const uint32_t*)per_chunk, 2 * h->NB, dst);
+  hipLaunchKernelGGL(k_expand_events, dim3(2 * h->NB), dim3(256), 0, h->stream, (const uint64_t*)h->ev,
+                     (const uint32_t*)h->ev_counts, (const uint64_t*)h->ev_off, (const uint64_t*)dst, d);
   hipError_t e = hipMemcpyAsync(out, d, total * sizeof(hb_event), hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   (void)hipFree(d);

@@ -41,6 +41,7 @@ struct FastLane {
   uint64_t match[NMAX], next[NMAX], head[NMAX];
   uint32_t pm[NMAX];
   uint32_t dirty;
+  uint32_t nev;      // public events emitted (an EVC_BCAST word counts once per slot)
 
   __device__ __forceinline__ uint32_t n() const { return (mlo >> 2) & 7; }
   __device__ __forceinline__ uint32_t state() const { return mlo & 3; }
@@ -50,7 +51,8 @@ struct FastLane {
     return arrival == 0xFFFFFFFFu ? HB_NO_INDEX : (uint64_t)arrival;
   }
   __device__ __forceinline__ void ev(uint32_t type, uint32_t to, uint32_t aux, uint64_t x) {
-    emit_ev(E, g, tta(type, to, aux), x);
+    emit_ev(E, g & (PART - 1), type, to, aux, x);
+    nev++;
   }
   __device__ __forceinline__ void fault(uint32_t code) {
     if (faulted()) return;
@@ -169,20 +171,23 @@ struct FastLane {
     }
     return false;
   }
-  // sendAppend raft/raft.go:239-282 to slot s
-  __device__ __forceinline__ void send_append(int s) {
+  // sendAppend raft/raft.go:239-282 to slot s: the progress side effects;
+  // returns the message it sends (SEND_NONE / SEND_APP / SEND_SNAP, index *x)
+  // for the caller to emit.
+  enum : uint32_t { SEND_NONE = 0, SEND_APP = 1, SEND_SNAP = 2 };
+  __device__ __forceinline__ uint32_t send_decide(int s, uint64_t* xo) {
     const uint32_t p = pm[s];
-    if (is_paused(p)) return;
+    if (is_paused(p)) return SEND_NONE;
     if (next[s] < first) {  // needSnapshot raft/raft.go:715-717
       const uint64_t snapi = S.snap[g];
       if (snapi == 0) {
         fault(HB_FAULT_EMPTY_SNAPSHOT);
-        return;
+        return SEND_NONE;
       }
       set_pm(s, pm_make(HB_PR_SNAPSHOT, 0, 0, 0));  // becomeSnapshot
       S.pending[(size_t)s * S.G + g] = snapi;
-      ev(HB_EV_SNAP, s, 0, snapi);
-      return;
+      *xo = snapi;
+      return SEND_SNAP;
     }
     const uint64_t x = next[s] - 1;
     if (next[s] <= last) {
@@ -192,7 +197,7 @@ struct FastLane {
         const uint32_t cnt = pm_count(p), start = pm_start(p);
         if (cnt == S.W) {
           fault(HB_FAULT_INFLIGHTS_FULL);
-          return;
+          return SEND_NONE;
         }
         uint32_t idx = start + cnt;
         if (idx >= S.W) idx -= S.W;
@@ -205,14 +210,45 @@ struct FastLane {
         set_pm(s, p | PM_PAUSED);                 // pause
       }
     }
-    ev(HB_EV_APP, s, 0, x);
+    *xo = x;
+    return SEND_APP;
   }
-  // bcastAppend raft/raft.go:303-310 (slot order, self skipped)
+  __device__ __forceinline__ void send_append(int s) {
+    uint64_t x = 0;
+    const uint32_t k = send_decide(s, &x);
+    if (k != SEND_NONE) ev(k == SEND_APP ? HB_EV_APP : HB_EV_SNAP, s, 0, x);
+  }
+  // bcastAppend raft/raft.go:303-310 (slot order, self skipped).  When every
+  // message it sends is a MsgApp with the same Index (steady state), the sends
+  // are recorded as one EVC_BCAST word; otherwise one event per send, in slot
+  // order.  Nothing else is emitted between the sends, so the order holds.
   __device__ __forceinline__ void bcast_append() {
     const uint32_t nn = n(), sf = self();
+    uint32_t kind[NMAX];
+    uint64_t xs[NMAX];
+    uint32_t mask = 0;
+    uint64_t x0 = 0;
+    bool same = true;
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) {
+      kind[s] = SEND_NONE;
+      xs[s] = 0;
+      if ((uint32_t)s < nn && (uint32_t)s != sf && !faulted()) kind[s] = send_decide(s, &xs[s]);
+      if (kind[s] != SEND_NONE) {
+        if (mask == 0) x0 = xs[s];
+        same = same && kind[s] == SEND_APP && xs[s] == x0;
+        mask |= 1u << s;
+      }
+    }
+    if (mask == 0) return;
+    if (same && (mask & (mask - 1))) {
+      emit_ev(E, g & (PART - 1), EVC_BCAST, mask, 0, x0);
+      nev += __popc(mask);
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < NMAX; ++s)
-      if ((uint32_t)s < nn && (uint32_t)s != sf && !faulted()) send_append(s);
+      if (kind[s] != SEND_NONE) ev(kind[s] == SEND_APP ? HB_EV_APP : HB_EV_SNAP, s, 0, xs[s]);
   }
 
   // ---- preconditions (checked per message by the kernel)

@@ -81,13 +81,28 @@ struct DevState {
 };
 
 // ---- event sink ---------------------------------------------------------------
-// A workgroup appends its events to its own chunk of the event region: the
-// chunk base is computed by every lane from kernel arguments (so it stays a
-// global-address-space pointer and the stores are global_store, not flat),
-// and the fill cursor is one LDS word.
+// Device event records are compact 8-byte words (the public 16-byte hb_event
+// stream is expanded from them by hb_copy_events, see hipbatch.hip):
+//
+//   [0:4)   type: HB_EV_*, or EVC_BCAST (an HB_EV_APP to every slot in the
+//           mask, same x), or EVC_CONT (second word of a long record)
+//   [4:11)  to (slot / node ref), or the slot mask of EVC_BCAST
+//   [11]    long: x >= 2^40, its high 24 bits follow in an EVC_CONT word
+//   [12:16) aux (LAST noop flag, FAULT code)
+//   [16:24) the group's lane in its partition (the chunk names the partition)
+//   [24:64) x bits 0..39
+//   EVC_CONT word: [0:4) = EVC_CONT, [4:28) = x bits 40..63
+//
+// A workgroup appends its words to its own chunk: the chunk base is computed
+// by every lane from kernel arguments (a global-address-space pointer, so the
+// stores are global_store, not flat) and the fill cursor is one LDS word.
+constexpr uint32_t EVC_BCAST = HB_EVW_BCAST;
+constexpr uint32_t EVC_CONT = HB_EVW_CONT;
+constexpr uint32_t EVC_WORDS_MAX = 2;  // words per event (long records)
+
 struct EvSink {
-  hb_event* chunk;            // this workgroup's chunk (global)
-  uint32_t* fill;             // records written by the workgroup (LDS)
+  uint64_t* chunk;            // this workgroup's chunk (global)
+  uint32_t* fill;             // words written by the workgroup (LDS)
 };
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a > b ? b : a; }
@@ -96,29 +111,26 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-__device__ __forceinline__ void store_event(hb_event* dst, uint32_t group, uint32_t tta, uint64_t x) {
-  uint4 v;
-  v.x = (uint32_t)x;
-  v.y = (uint32_t)(x >> 32);
-  v.z = group;
-  v.w = tta;
-  *reinterpret_cast<uint4*>(dst) = v;
+__host__ __device__ constexpr uint64_t evc_word(uint32_t type, uint32_t to, uint32_t aux, uint32_t lane, uint64_t x,
+                                                bool lng) {
+  return (uint64_t)(type & 0xF) | ((uint64_t)(to & 0x7F) << 4) | ((uint64_t)lng << 11) | ((uint64_t)(aux & 0xF) << 12) |
+         ((uint64_t)(lane & 0xFF) << 16) | ((x & 0xFFFFFFFFFFull) << 24);
 }
 
-__host__ __device__ constexpr uint32_t tta(uint32_t type, uint32_t to, uint32_t aux) {
-  return (type & 0xFF) | ((to & 0xFF) << 8) | ((aux & 0xFFFF) << 16);
-}
-
-// Append one 16-byte record to the workgroup's chunk.  The chunk is sized
-// from the partition's exact message count (events per message are bounded),
-// so it never overflows.  One LDS atomic per active lane; the compiler's
-// atomic optimizer turns it into one ds_add per wave plus mbcnt, and the
-// lanes of a wave write side by side.  A lane's records keep their order.
-__device__ __forceinline__ void emit_ev(const EvSink& sink, uint32_t group, uint32_t ttav, uint64_t x) {
-  const uint32_t pos = atomicAdd(sink.fill, 1u);
-#ifndef HB_X_NOEV
-  store_event(sink.chunk + pos, group, ttav, x);
-#endif
+// Append one event.  One LDS atomic per active lane (the compiler's atomic
+// optimizer makes it one ds_add per wave plus mbcnt), so the lanes of a wave
+// write side by side; a lane's events keep their order.  Values of x that
+// need more than 40 bits take a second word (rare path).
+__device__ __forceinline__ void emit_ev(const EvSink& sink, uint32_t lane, uint32_t type, uint32_t to, uint32_t aux,
+                                        uint64_t x) {
+  if (__builtin_expect((x >> 40) == 0, 1)) {
+    const uint32_t pos = atomicAdd(sink.fill, 1u);
+    sink.chunk[pos] = evc_word(type, to, aux, lane, x, false);
+  } else {
+    const uint32_t pos = atomicAdd(sink.fill, 2u);
+    sink.chunk[pos] = evc_word(type, to, aux, lane, x, true);
+    sink.chunk[pos + 1] = (uint64_t)EVC_CONT | ((x >> 40) << 4);
+  }
 }
 
 template <int N>
@@ -181,6 +193,7 @@ struct Lane {
   typename SlotVec<NMAX>::u32 pm;
   uint32_t dirty;
   uint32_t won, lost;
+  uint32_t nev;  // events emitted
 
   // ---------------------------------------------------------------- meta
   __device__ __forceinline__ uint32_t n() const { return m_n(meta); }
@@ -209,7 +222,8 @@ struct Lane {
     return arrival == 0xFFFFFFFFu ? HB_NO_INDEX : (uint64_t)arrival;
   }
   __device__ __forceinline__ void ev(uint32_t type, uint32_t to, uint32_t aux, uint64_t x) {
-    emit_ev(E, g, tta(type, to, aux), x);
+    emit_ev(E, g & (PART - 1), type, to, aux, x);
+    nev++;
   }
   // A reference panic: the group stops; the FAULT event is emitted once, at
   // the end of the message (nothing else is emitted after a fault).

@@ -278,11 +278,25 @@ int  hb_get_inflights(hb_handle* h, uint32_t group, uint32_t slot,
  * are read with the functions below. */
 int  hb_step(hb_handle* h, const hb_batch* b, uint32_t flags);
 
-/* Events of the last step, as written by the device: `n_chunks` chunks (one
- * per 256-group partition); chunk c holds counts[c] events at
- * base + chunk_off[c], and all events of a group are in one chunk, in order.
- * Device pointers; valid until the next hb_step. */
-int  hb_events_device(hb_handle* h, const hb_event** base, const uint64_t** chunk_off,
+/* Events of the last step, as written by the device (zero-copy access for a
+ * consumer on the GPU): `n_chunks` chunks, two per 256-group partition p
+ * (chunk 2p: the events of the dense props[] proposals, chunk 2p+1: the
+ * events of the partition's messages); chunk c holds counts[c] 8-byte words
+ * at base + chunk_off[c].  A group's events are its words in chunk 2p, then
+ * in chunk 2p+1, each in order.  Word format (bit ranges):
+ *   [0:4)   type: HB_EV_*; 12 = an HB_EV_APP to every slot of the mask in
+ *           `to` (same x, aux 0), in slot order; 15 = continuation word
+ *   [4:11)  to (slot / node ref), or the slot mask of type 12
+ *   [11]    x needs 64 bits: the next word is a continuation holding
+ *           x bits 40..63 in its bits [4:28)
+ *   [12:16) aux
+ *   [16:24) group - 256 p
+ *   [24:64) x bits 0..39
+ * hb_copy_events expands them into hb_event records.  Device pointers; valid
+ * until the next hb_step. */
+#define HB_EVW_BCAST 12
+#define HB_EVW_CONT  15
+int  hb_events_device(hb_handle* h, const uint64_t** base, const uint64_t** chunk_off,
                       const uint32_t** counts, uint32_t* n_chunks);
 /* Gather the last step's events densely into host memory (synchronizes).
  * *n = number of events; returns HB_EINVAL if cap is too small. */

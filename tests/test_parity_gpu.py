@@ -97,3 +97,12 @@ def test_out_of_range_groups_and_empty_batch():
     b["group"] = b["group"].copy()
     b["group"][:50] = 5000  # beyond capacity: ignored by both
     pair.step(b, ctx="oob")
+
+
+def test_large_indices_long_event_words():
+    """Indices and terms beyond 2^40 take two device event words (continuation)."""
+    g, runs = synth.steady_groups(2000, 3, seed=21, last_hi=1 << 62, term_hi=1 << 50)
+    pair = Pair(g, runs, 3, 16, max_batch=1 << 14)
+    for step in range(2):
+        _, st, _ = pair.step(synth.cfg2_batch(g, step, seed=31 + step), ctx=f"large step {step}")
+        assert st[abi.HB_STAT_COMMITS] == 2000
