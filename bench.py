@@ -189,10 +189,12 @@ def main():
     if not args.no_profile:
         ph, nph = eng.phase_ms()
         phase = {"partition_ms": float(ph[abi.HB_PHASE_PARTITION]), "apply_ms": float(ph[abi.HB_PHASE_APPLY]),
-                 "finish_ms": float(ph[abi.HB_PHASE_FINISH]), "steps": nph}
-        alg = alg_bytes_per_group(n) * G  # per apply launch on this GPU
+                 "general_ms": float(ph[abi.HB_PHASE_GENERAL]), "finish_ms": float(ph[abi.HB_PHASE_FINISH]),
+                 "steps": nph}
+        alg = alg_bytes_per_group(n) * G  # per k_apply_fast launch on this GPU
+        # HB_PHASE_APPLY brackets exactly the k_apply_fast launch (HIP events on the launch stream)
         achieved = float(alg / (float(ph[abi.HB_PHASE_APPLY]) * 1e-3) / 1e9)
-        kname = f"k_apply<{3 if n <= 3 else (5 if n <= 5 else 7)}>"
+        kname = f"k_apply_fast<{3 if n <= 3 else (5 if n <= 5 else 7)}>"
         traffic, tsrc = pmc_traffic(args.traffic_json, kname, G, n, float(ph[abi.HB_PHASE_APPLY]) * 1e3)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),

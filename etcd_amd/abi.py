@@ -90,8 +90,9 @@ HB_STAT_COUNT = 10
 
 HB_PHASE_PARTITION = 0
 HB_PHASE_APPLY = 1
-HB_PHASE_FINISH = 2
-HB_PHASE_COUNT = 3
+HB_PHASE_GENERAL = 2
+HB_PHASE_FINISH = 3
+HB_PHASE_COUNT = 4
 
 STAT_NAMES = ["msgs", "appresp", "voteresp", "dropped", "commits", "won", "lost",
               "events", "faults", "entries"]

@@ -365,6 +365,13 @@ struct ApplyArgs {
   uint32_t* pflag;          // [NB][PART/32] groups handed from k_apply_fast to k_apply
   uint32_t* resume;         // [G] messages consumed by k_apply_fast | prop pending << 31
   uint64_t* commit0;        // [G] committed at batch start (for HB_STAT_COMMITS)
+  // k_route -> k_apply_fast: each group's first kmax messages, lane-major
+  uint32_t kmax;            // slots per group (= nmax - 1)
+  uint8_t* cnt;             // [G] messages of the group in this batch (saturated at 255)
+  uint32_t* slot_info;      // [kmax][G]
+  uint32_t* slot_orig;      // [kmax][G]
+  uint64_t* slot_term;      // [kmax][G]
+  uint64_t* slot_index;     // [kmax][G]
 };
 
 // stats slots reduced per workgroup
@@ -406,14 +413,16 @@ __device__ __forceinline__ uint32_t block_part() {
   return ((((q >> SIS_LOG) << 3) | r) << SIS_LOG) | (q & (SIS - 1));
 }
 
-// LDS staging of one round (<= CHUNK messages) of a partition's messages.
+// LDS staging of one round (<= CH messages) of a partition's messages.
 // w[j][i] = word j of the round's i-th MsgRec (info, orig, term lo/hi, index lo/hi).
 // (Gathering the records by LDS-DMA, global_load_lds_dword x6, measured slower
 // than register staging: 6 requests per record instead of 2-3.)
+template <uint32_t CH>
 struct Stage {
-  uint32_t rbuf[CHUNK];   // bucket-relative positions, increasing (= arrival order)
-  uint32_t w[6][CHUNK];
-  uint16_t perm[CHUNK];
+  static constexpr uint32_t CHUNK = CH;
+  uint32_t rbuf[CH];      // bucket-relative positions, increasing (= arrival order)
+  uint32_t w[6][CH];
+  uint16_t perm[CH];
   uint32_t cnt[PART];
   uint32_t sh16[16];
   uint64_t bcast;
@@ -471,9 +480,10 @@ __device__ __forceinline__ uint64_t scan_keys(const uint8_t* key, uint32_t seg, 
 // the first round with the partition's message count; round(fill) runs per
 // round with sl.rbuf[0, fill) = the round's bucket-relative positions.
 // `first`: the keys of segment 0, already loaded by the caller (or null).
-template <class OnTotal, class Round>
-__device__ __forceinline__ void walk_partition(Stage& sl, const ApplyArgs& a, uint32_t lo, uint32_t hi, uint32_t sub,
+template <class St, class OnTotal, class Round>
+__device__ __forceinline__ void walk_partition(St& sl, const ApplyArgs& a, uint32_t lo, uint32_t hi, uint32_t sub,
                                                const Keys* first, OnTotal&& on_total, Round&& round) {
+  constexpr uint32_t CHUNK = St::CHUNK;
   const uint32_t tid = threadIdx.x;
   const uint32_t seg0 = lo & ~15u;
   const uint32_t nseg = hi > lo ? (hi - seg0 + SEG - 1) / SEG : 0u;  // uniform
@@ -522,10 +532,10 @@ __device__ __forceinline__ void walk_partition(Stage& sl, const ApplyArgs& a, ui
 // Gather the round's records into LDS and counting-sort them by lane: on
 // return the lane's messages are perm[*start, *start + *cnt), in arrival order.
 // `issued()` runs once the round's record loads are in flight.
-template <class Issued>
-__device__ __forceinline__ void gather_round(Stage& sl, const ApplyArgs& a, uint32_t lo, uint32_t fill,
+template <class St, class Issued>
+__device__ __forceinline__ void gather_round(St& sl, const ApplyArgs& a, uint32_t lo, uint32_t fill,
                                              uint32_t* start, uint32_t* cnt, Issued&& issued) {
-  constexpr uint32_t PER = CHUNK / PART;
+  constexpr uint32_t PER = St::CHUNK / PART;
   const uint32_t tid = threadIdx.x;
   sl.cnt[tid] = 0;
   __syncthreads();
@@ -597,125 +607,156 @@ __device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_sta
 }
 
 // ---------------------------------------------------------------------------
+// k_route: one workgroup per partition.  Picks the partition's messages out
+// of its bucket (key scan), gathers them and sorts them by lane (arrival
+// order kept), and lays each lane's first KMAX messages out lane-major:
+// slot k of group g at slots.*[k][g], so k_apply_fast reads them with
+// coalesced loads in the same round trip as the group state.  cnt[g] =
+// the lane's message count (saturated at 255).  It also reserves the
+// partition's M event chunk (ev_off[2p+1]).  No raft logic runs here.
+// ---------------------------------------------------------------------------
+#ifndef HB_ROUTE_CHUNK
+#define HB_ROUTE_CHUNK 512
+#endif
+__global__ void __launch_bounds__(PART, 8) k_route(ApplyArgs a) {
+  __shared__ Stage<HB_ROUTE_CHUNK> sl;
+  const uint32_t part = block_part();
+  if (part >= a.NB) return;  // uniform: grid padding
+  const uint32_t tid = threadIdx.x;
+  const uint32_t bk = part >> SIS_LOG, sub = part & (SIS - 1);
+  const uint32_t g = part * PART + tid;
+  const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
+  const uint32_t kmax = a.kmax;
+  uint32_t j = 0;  // messages of this lane so far (all rounds)
+  auto on_total = [&](uint32_t total) {
+    if (tid == 0) {
+      const uint32_t r = atomicAdd(&a.bk_fill[bk], a.ev_per_msg * (total + PART * a.props_on));
+      a.ev_off[2 * part + 1] = (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + (uint64_t)lo +
+                                                         (uint64_t)bk * (PART * SIS) * a.props_on) + r;
+    }
+  };
+  auto round = [&](uint32_t fill) {
+    uint32_t my_start, my_cnt;
+    gather_round(sl, a, lo, fill, &my_start, &my_cnt, []() {});
+    for (uint32_t x = 0; x < my_cnt && j + x < kmax; ++x) {
+      const uint32_t i = sl.perm[my_start + x];
+      const size_t o = (size_t)(j + x) * a.S.G + g;
+      a.slot_info[o] = sl.info(i);
+      a.slot_orig[o] = sl.orig(i);
+      a.slot_term[o] = sl.term(i);
+      a.slot_index[o] = sl.index(i);
+    }
+    j += my_cnt;
+    __syncthreads();
+  };
+  walk_partition(sl, a, lo, hi, sub, nullptr, on_total, round);
+  if (g < a.S.G) a.cnt[g] = (uint8_t)(j < 255 ? j : 255);
+}
+
+// ---------------------------------------------------------------------------
 // k_apply_fast: one workgroup per partition, one lane per group, steady-state
-// leader operations only (FastLane).  The first message a lane cannot take
-// (and everything after it) is handed to k_apply: the lane's bit is set in
-// pflag[part] and resume[g] = messages already consumed | prop-pending bit.
+// leader operations only (FastLane).  Every load of the lane (state, its
+// message count, its first KMAX messages) is issued at once; no LDS staging,
+// no barrier until the statistics.  The first message a lane cannot take
+// (and everything after it, and messages beyond KMAX) is handed to k_apply:
+// the lane's bit is set in pflag[part] and resume[g] = messages already
+// consumed | prop-pending bit.
 // ---------------------------------------------------------------------------
 template <int NMAX>
 __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply_fast(ApplyArgs a) {
-  __shared__ Stage sl;
+  constexpr uint32_t KMAX = NMAX - 1;  // one MsgAppResp per follower per batch
   __shared__ uint32_t l_fill, l_pfill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
 
   const uint32_t part = block_part();
   if (part >= a.NB) return;  // uniform: grid padding
-  XSTAMP_RT(6);
-  XSTAMP(0);
   const uint32_t tid = threadIdx.x;
-  const uint32_t bk = part >> SIS_LOG, sub = part & (SIS - 1);
   const uint32_t g = part * PART + tid;
   const bool gvalid = g < a.S.G;
   if (tid == 0) l_fill = l_pfill = 0;
   if (tid <= ST_N) l_stats[tid] = 0;
   if (tid < FLAG_WORDS) l_flag[tid] = 0;
 
-  // ---- issue the lane's loads: group state, then this lane's bucket keys of
-  // segment 0 (the proposal below overlaps the key loads).
-  const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
+  // ---- every load of the lane, one round trip
   FastLane<NMAX> L;
   L.S = a.S;
   L.g = g;
   L.mlo = gvalid ? reinterpret_cast<const uint32_t*>(a.S.meta)[2 * (size_t)g] : 0u;
   const uint32_t prop_raw = (a.props && gvalid) ? a.props[g] : 0u;
+  const uint32_t cnt = gvalid ? a.cnt[g] : 0u;
   // A group takes part when its slot is live (n > 0) and not faulted.
   const bool live = gvalid && L.n() != 0 && L.faulted() == 0;
   L.dirty = 0;
   L.nev = 0;
   L.last = L.committed = 0;
-  if ((a.props_on || hi > lo) && live) L.load();
+  if (live) L.load();
+  uint32_t s_info[KMAX], s_orig[KMAX];
+  uint64_t s_term[KMAX], s_index[KMAX];
+#pragma unroll
+  for (uint32_t k = 0; k < KMAX; ++k) {
+    const size_t o = (size_t)k * a.S.G + g;
+    const bool on = gvalid && k < cnt;
+    s_info[k] = on ? a.slot_info[o] : 0u;
+    s_orig[k] = on ? a.slot_orig[o] : 0u;
+    s_term[k] = on ? a.slot_term[o] : 0ull;
+    s_index[k] = on ? a.slot_index[o] : 0ull;
+  }
+  const uint64_t moff = a.ev_off[2 * part + 1];
   const uint64_t last0 = L.last, commit0 = L.committed;
-  const Keys k0 = load_keys(a.key, lo & ~15u, lo, hi);
 
   bool flagged = false;
   uint32_t resume = 0;
   uint32_t st_msgs = 0, st_drop = 0;
-  uint32_t j = 0;  // messages of this lane consumed so far (all rounds)
 
   // ---- the dense proposal: its events go to the partition's P chunk (fixed
-  // slot of ev_per_msg x PART records), before any message event of the group.
-  {
-    const uint64_t poff = (uint64_t)part * PART * a.ev_per_msg;
-    if (tid == 0) a.ev_off[2 * part] = poff;
-    L.E.chunk = a.ev + poff;
-    L.E.fill = &l_pfill;
-    const uint32_t prop_k = live ? prop_raw : 0u;
-    if (prop_k) {
-      if (L.prop_ok(prop_k)) {
-        L.arrival = 0xFFFFFFFFu;
-        L.prop(prop_k);
-      } else {
-        flagged = true;
-        resume = 1u << 31;  // the proposal itself is pending (stepped by k_apply into the M chunk)
-      }
+  // slot of ev_per_msg x PART words), before any message event of the group.
+  const uint64_t poff = (uint64_t)part * PART * a.ev_per_msg;
+  if (tid == 0) a.ev_off[2 * part] = poff;
+  L.E.chunk = a.ev + poff;
+  L.E.fill = &l_pfill;
+  const uint32_t prop_k = live ? prop_raw : 0u;
+  if (prop_k) {
+    if (L.prop_ok(prop_k)) {
+      L.arrival = 0xFFFFFFFFu;
+      L.prop(prop_k);
+    } else {
+      flagged = true;
+      resume = 1u << 31;  // the proposal itself is pending (stepped by k_apply into the M chunk)
     }
   }
-  XSTAMP(1);
 
-  // ---- messages: M chunk of ev_per_msg x (messages + PART) records reserved
-  // in the bucket's region (the general kernel may append a pending proposal).
-  uint32_t moff_pending = 0;
-  bool first_round = true;
-  auto on_total = [&](uint32_t total) {
-    if (tid == 0) moff_pending = atomicAdd(&a.bk_fill[bk], a.ev_per_msg * (total + PART * a.props_on));
-    XSTAMP(2);
-  };
-  auto round = [&](uint32_t fill) {
-    uint32_t my_start, my_cnt;
-    gather_round(sl, a, lo, fill, &my_start, &my_cnt, [&]() {
-      if (first_round && tid == 0) sl.bcast = moff_pending;  // waits for the atomic only
-    });
-    if (first_round) {
-      const uint64_t moff = (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + (uint64_t)lo +
-                                                      (uint64_t)bk * (PART * SIS) * a.props_on) + sl.bcast;
-      if (tid == 0) a.ev_off[2 * part + 1] = moff;
-      L.E.chunk = a.ev + moff;
-      L.E.fill = &l_fill;
-      first_round = false;
-    }
-    XSTAMP(3);
-    if (live) {
-      for (uint32_t x = 0; x < my_cnt; ++x) {
-        if (flagged || L.faulted()) break;
-        const uint32_t i = sl.perm[my_start + x];
-        const uint32_t inf = sl.info(i);
-        const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
-        const bool reject = (inf >> 8) & 1u;
-        if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
-          st_drop++;
-          j++;
-          continue;
-        }
-        const uint64_t mterm = sl.term(i);
-        if (!L.accept_ok(type, from, mterm, reject)) {
-          flagged = true;
-          resume = j;
-          break;
-        }
-        L.arrival = sl.orig(i);
-        L.accept(from, sl.index(i));
-        st_msgs++;
+  // ---- the lane's messages, arrival order (M chunk reserved by k_route)
+  L.E.chunk = a.ev + moff;
+  L.E.fill = &l_fill;
+  uint32_t j = 0;  // messages consumed
+  if (live) {
+#pragma unroll
+    for (uint32_t k = 0; k < KMAX; ++k) {
+      if (k >= cnt || flagged || L.faulted()) break;
+      const uint32_t inf = s_info[k];
+      const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
+      const bool reject = (inf >> 8) & 1u;
+      if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
+        st_drop++;
         j++;
+        continue;
       }
+      if (!L.accept_ok(type, from, s_term[k], reject)) {
+        flagged = true;
+        resume = j;
+        break;
+      }
+      L.arrival = s_orig[k];
+      L.accept(from, s_index[k]);
+      st_msgs++;
+      j++;
     }
-    __syncthreads();
-    XSTAMP(4);
-  };
-  walk_partition(sl, a, lo, hi, sub, &k0, on_total, round);
-  if (first_round && tid == 0)  // no message for this partition: the M chunk is only reserved
-    a.ev_off[2 * part + 1] = (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + (uint64_t)lo +
-                                                       (uint64_t)bk * (PART * SIS) * a.props_on) + moff_pending;
+    if (!flagged && !L.faulted() && cnt > KMAX) {  // more messages than slots: the rest in k_apply
+      flagged = true;
+      resume = j;
+    }
+  }
 
   L.store();
   if (flagged) {
@@ -739,8 +780,6 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
     a.ev_counts[2 * part] = l_pfill;
     a.ev_counts[2 * part + 1] = l_fill;
   }
-  XSTAMP(5);
-  XSTAMP_RT(7);
 }
 
 // ---------------------------------------------------------------------------
@@ -750,7 +789,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
 // ---------------------------------------------------------------------------
 template <int NMAX>
 __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
-  __shared__ Stage sl;
+  __shared__ Stage<CHUNK> sl;
   __shared__ uint32_t l_fill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
@@ -1068,6 +1107,11 @@ struct hb_handle {
   uint32_t* pflag = nullptr;      // [NB][PART/32]
   uint32_t* resume = nullptr;     // [G]
   uint64_t* commit0 = nullptr;    // [G]
+  uint8_t* cnt = nullptr;         // [G]
+  uint32_t* slot_info = nullptr;  // [nmax-1][G]
+  uint32_t* slot_orig = nullptr;
+  uint64_t* slot_term = nullptr;
+  uint64_t* slot_index = nullptr;
   static constexpr uint32_t PROF_RING = 256;
   hipEvent_t ph[PROF_RING][HB_PHASE_COUNT + 1] = {};
   uint32_t prof_n = 0;  // profiled steps since hb_phase_reset
@@ -1105,11 +1149,17 @@ uint32_t ceil_log2(uint32_t x) {
   return b;
 }
 
+// XCD-aware grid (see block_part()): whole groups of 8 buckets x SIS partitions.
+uint32_t apply_grid(const hb_handle* h) { return ((h->NBK + 7) & ~7u) * SIS; }
+
+// The apply kernels; ev = this step's phase events (HB_STEP_PROFILE) or null.
 template <int NMAX>
-void launch_apply(hb_handle* h, const ApplyArgs& a) {
-  const uint32_t grid = ((h->NBK + 7) & ~7u) * SIS;  // XCD-aware padding, see block_part()
+void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev) {
+  const uint32_t grid = apply_grid(h);
   hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
+  if (ev) (void)hipEventRecord(ev[HB_PHASE_APPLY + 1], h->stream);
   hipLaunchKernelGGL(k_apply<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
+  if (ev) (void)hipEventRecord(ev[HB_PHASE_GENERAL + 1], h->stream);
 }
 
 }  // namespace
@@ -1207,6 +1257,11 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->pflag, (size_t)h->NB * FLAG_WORDS);
   ALLOC(h->resume, G);
   ALLOC(h->commit0, G);
+  ALLOC(h->cnt, G);
+  ALLOC(h->slot_info, (R - 1 ? R - 1 : 1) * G);
+  ALLOC(h->slot_orig, (R - 1 ? R - 1 : 1) * G);
+  ALLOC(h->slot_term, (R - 1 ? R - 1 : 1) * G);
+  ALLOC(h->slot_index, (R - 1 ? R - 1 : 1) * G);
   ALLOC(h->stats, HB_STAT_COUNT);
 #undef ALLOC
   if (rc != HB_OK) {
@@ -1407,9 +1462,8 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
       hipLaunchKernelGGL(k_bucket_bounds, dim3((h->NBK + 1 + 255) / 256), dim3(256), 0, st,
                          (const uint32_t*)h->bucket, (const uint32_t*)h->n_valid, h->NBK, h->bk_off);
   }
-  if (prof) HB_CHECK(hipEventRecord(ev[1], st));
 
-  // ---- phase 2: apply ----------------------------------------------------------
+  // ---- phase 2: route each partition's messages to its lanes; apply -----------
   ApplyArgs aa;
   aa.S = h->st;
   aa.rec = h->rec;
@@ -1428,15 +1482,22 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.pflag = h->pflag;
   aa.resume = h->resume;
   aa.commit0 = h->commit0;
+  aa.kmax = h->nmax - 1;
+  aa.cnt = h->cnt;
+  aa.slot_info = h->slot_info;
+  aa.slot_orig = h->slot_orig;
+  aa.slot_term = h->slot_term;
+  aa.slot_index = h->slot_index;
+  hipLaunchKernelGGL(k_route, dim3(apply_grid(h)), dim3(PART), 0, st, aa);
+  if (prof) HB_CHECK(hipEventRecord(ev[HB_PHASE_PARTITION + 1], st));
   switch (h->nmax) {
-    case 3: launch_apply<3>(h, aa); break;
-    case 5: launch_apply<5>(h, aa); break;
-    default: launch_apply<7>(h, aa); break;
+    case 3: launch_apply<3>(h, aa, prof ? ev : nullptr); break;
+    case 5: launch_apply<5>(h, aa, prof ? ev : nullptr); break;
+    default: launch_apply<7>(h, aa, prof ? ev : nullptr); break;
   }
-  if (prof) HB_CHECK(hipEventRecord(ev[2], st));
   // ---- phase 3: finish -----------------------------------------------------------
   hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, h->stats_shard, h->stats, h->stats_accum);
-  if (prof) HB_CHECK(hipEventRecord(ev[3], st));
+  if (prof) HB_CHECK(hipEventRecord(ev[HB_PHASE_FINISH + 1], st));
   HB_CHECK(hipGetLastError());
   if (prof) h->prof_n++;
   h->stepped = true;

@@ -234,10 +234,11 @@ typedef struct hb_event {
 #define HB_STAT_COUNT      10
 
 /* ---- phases (HB_STEP_PROFILE) -------------------------------------------- */
-#define HB_PHASE_PARTITION 0  /* histogram + scan + stable scatter by partition */
-#define HB_PHASE_APPLY     1  /* per-group apply (the dominant kernel)          */
-#define HB_PHASE_FINISH    2  /* stats reduction + event chunk bookkeeping      */
-#define HB_PHASE_COUNT     3
+#define HB_PHASE_PARTITION 0  /* bucket radix sort + per-partition routing to lanes */
+#define HB_PHASE_APPLY     1  /* steady-state fast path (the dominant kernel)      */
+#define HB_PHASE_GENERAL   2  /* general state machine for handed-over groups      */
+#define HB_PHASE_FINISH    3  /* statistics reduction                              */
+#define HB_PHASE_COUNT     4
 
 typedef struct hb_handle hb_handle;
 
