@@ -1068,9 +1068,32 @@ __global__ void __launch_bounds__(256) k_expand_events(const uint64_t* base, con
 // ============================================================================
 // host side
 // ============================================================================
+// What one step's prep (partition + route) hands to its apply.  Two sets, so
+// the prep of batch k+1 (on the prep stream) can run while batch k applies.
+struct PrepSet {
+  MsgRec* rec = nullptr;          // final pass = apply input
+  uint8_t* key = nullptr;         // partition-in-bucket per record (+ SEG bytes of padding)
+  uint32_t* bucket = nullptr;     // bucket id per record (multi-pass only)
+  uint32_t* bk_off = nullptr;     // [NBK + 1]
+  uint8_t* cnt = nullptr;         // [G]
+  uint32_t* slot_info = nullptr;  // [nmax-1][G]
+  uint32_t* slot_orig = nullptr;
+  uint64_t* slot_term = nullptr;
+  uint64_t* slot_index = nullptr;
+  uint64_t* ev_off = nullptr;     // [2 NB] event chunk offsets (route writes the M chunks)
+  uint32_t* ev_counts = nullptr;  // [2 NB]
+  hipEvent_t prepped = nullptr;   // prep stream: this set is ready
+  hipEvent_t applied = nullptr;   // apply stream: the last apply reading this set is done
+  bool used = false;
+};
+
 struct hb_handle {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // apply stream (hb_set_stream)
+  hipStream_t prep = nullptr;     // partition + route (library-owned)
+  hipStream_t in_stream = nullptr;  // where the batch inputs are produced (hb_set_input_stream)
+  bool in_stream_set = false;
+  hipEvent_t in_ready = nullptr;
   uint32_t G = 0, nmax = 0, W = 0, NB = 0;
   uint64_t max_msg_size = 0, max_batch = 0;
   DevState st{};
@@ -1080,11 +1103,9 @@ struct hb_handle {
   uint32_t* n_valid = nullptr;    // messages kept after pass 1 (device)
   uint32_t* totals = nullptr;     // [RDX_BINS] digit totals of the current pass
   RadixDst tmp[2] = {};           // intermediate passes (ping-pong)
-  MsgRec* rec = nullptr;          // final pass = apply input
-  uint8_t* key = nullptr;         // partition-in-bucket per record (+ SEG bytes of padding)
-  uint32_t* bucket = nullptr;     // bucket id per record (multi-pass only)
-  uint32_t* bk_off = nullptr;     // [NBK + 1]
   uint32_t* bk_fill = nullptr;    // [NBK]
+  PrepSet set[2];
+  uint32_t next_set = 0, cur = 0;  // set of the next / the last step
   uint32_t NBK = 0;               // buckets
   uint32_t passes = 1;
   // host-pointer staging
@@ -1098,8 +1119,6 @@ struct hb_handle {
   uint64_t* ev = nullptr;   // compact event words
   uint64_t ev_region = 0;  // records
   uint32_t ev_per_msg = 0;
-  uint32_t* ev_counts = nullptr;  // [NB]
-  uint64_t* ev_off = nullptr;     // [NB]
   uint64_t* stats_shard = nullptr;  // [8][16]
   uint64_t* stats_accum = nullptr;  // optional caller buffer (hb_set_stats_accum)
   uint64_t* stats = nullptr;
@@ -1107,13 +1126,12 @@ struct hb_handle {
   uint32_t* pflag = nullptr;      // [NB][PART/32]
   uint32_t* resume = nullptr;     // [G]
   uint64_t* commit0 = nullptr;    // [G]
-  uint8_t* cnt = nullptr;         // [G]
-  uint32_t* slot_info = nullptr;  // [nmax-1][G]
-  uint32_t* slot_orig = nullptr;
-  uint64_t* slot_term = nullptr;
-  uint64_t* slot_index = nullptr;
   static constexpr uint32_t PROF_RING = 256;
-  hipEvent_t ph[PROF_RING][HB_PHASE_COUNT + 1] = {};
+  // per profiled step: prep start, prep end (prep stream), apply start, fast end,
+  // general end, finish end (apply stream)
+  static constexpr uint32_t PH_EVENTS = 6;
+  hipEvent_t ph[PROF_RING][PH_EVENTS] = {};
+  bool prof_full[PROF_RING] = {};  // all phases recorded (else only HB_PHASE_APPLY)
   uint32_t prof_n = 0;  // profiled steps since hb_phase_reset
   bool stepped = false;
 };
@@ -1154,12 +1172,13 @@ uint32_t apply_grid(const hb_handle* h) { return ((h->NBK + 7) & ~7u) * SIS; }
 
 // The apply kernels; ev = this step's phase events (HB_STEP_PROFILE) or null.
 template <int NMAX>
-void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev) {
+void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
   const uint32_t grid = apply_grid(h);
+  if (ev) (void)hipEventRecord(ev[2], h->stream);
   hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
-  if (ev) (void)hipEventRecord(ev[HB_PHASE_APPLY + 1], h->stream);
+  if (ev) (void)hipEventRecord(ev[3], h->stream);
   hipLaunchKernelGGL(k_apply<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
-  if (ev) (void)hipEventRecord(ev[HB_PHASE_GENERAL + 1], h->stream);
+  if (ev && full) (void)hipEventRecord(ev[4], h->stream);
 }
 
 }  // namespace
@@ -1227,7 +1246,6 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->hist, (size_t)RDX_BINS * tiles_max);
   ALLOC(h->n_valid, 4);
   ALLOC(h->totals, RDX_BINS);
-  ALLOC(h->bk_off, h->NBK + 1);
   ALLOC(h->bk_fill, h->NBK);
   for (uint32_t k = 0; k + 1 < h->passes && k < 2; ++k) {  // ping-pong buffers of intermediate passes
     RadixDst& d = h->tmp[k];
@@ -1237,9 +1255,19 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
     ALLOC(d.term, mb);
     ALLOC(d.index, mb);
   }
-  ALLOC(h->rec, mb);
-  ALLOC(h->key, mb + SEG);
-  if (h->passes > 1) ALLOC(h->bucket, mb);
+  for (PrepSet& ps : h->set) {
+    ALLOC(ps.rec, mb);
+    ALLOC(ps.key, mb + SEG);
+    if (h->passes > 1) ALLOC(ps.bucket, mb);
+    ALLOC(ps.bk_off, h->NBK + 1);
+    ALLOC(ps.cnt, G);
+    ALLOC(ps.slot_info, (R - 1) * G);
+    ALLOC(ps.slot_orig, (R - 1) * G);
+    ALLOC(ps.slot_term, (R - 1) * G);
+    ALLOC(ps.slot_index, (R - 1) * G);
+    ALLOC(ps.ev_counts, 2ull * h->NB);
+    ALLOC(ps.ev_off, 2ull * h->NB);
+  }
   ALLOC(h->s_group, mb);
   ALLOC(h->s_info, mb);
   ALLOC(h->s_term, mb);
@@ -1251,33 +1279,32 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   // P chunks (one per partition, dense proposals) then the bucket regions of M chunks
   h->ev_region = ((uint64_t)h->NB * PART + mb + (uint64_t)h->NBK * (PART * SIS)) * h->ev_per_msg;
   ALLOC(h->ev, h->ev_region);
-  ALLOC(h->ev_counts, 2ull * h->NB);
-  ALLOC(h->ev_off, 2ull * h->NB);
   ALLOC(h->stats_shard, 8 * 16);
   ALLOC(h->pflag, (size_t)h->NB * FLAG_WORDS);
   ALLOC(h->resume, G);
   ALLOC(h->commit0, G);
-  ALLOC(h->cnt, G);
-  ALLOC(h->slot_info, (R - 1 ? R - 1 : 1) * G);
-  ALLOC(h->slot_orig, (R - 1 ? R - 1 : 1) * G);
-  ALLOC(h->slot_term, (R - 1 ? R - 1 : 1) * G);
-  ALLOC(h->slot_index, (R - 1 ? R - 1 : 1) * G);
   ALLOC(h->stats, HB_STAT_COUNT);
 #undef ALLOC
   if (rc != HB_OK) {
     hb_destroy(h);
     return rc;
   }
+  bool ok = hipStreamCreateWithFlags(&h->prep, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&h->in_ready, hipEventDisableTiming) == hipSuccess;
+  for (PrepSet& ps : h->set)
+    ok = ok && hipEventCreateWithFlags(&ps.prepped, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&ps.applied, hipEventDisableTiming) == hipSuccess;
   for (auto& row : h->ph)
-    for (auto& e : row)
-      if (hipEventCreate(&e) != hipSuccess) {
-        hb_destroy(h);
-        return HB_EDEVICE;
-      }
+    for (auto& e : row) ok = ok && hipEventCreate(&e) == hipSuccess;
+  if (!ok) {
+    hb_destroy(h);
+    return HB_EDEVICE;
+  }
   // empty slots (n = 0), zeroed progress
   if (hipMemset(s.meta, 0, G * 8) != hipSuccess || hipMemset(s.pm, 0, R * G * 4) != hipSuccess ||
       hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess || hipMemset(h->stats_shard, 0, 8 * 16 * 8) != hipSuccess ||
-      hipMemset(h->ev_counts, 0, h->NB * 8ull) != hipSuccess || hipMemset(h->ev_off, 0, h->NB * 16ull) != hipSuccess ||
+      hipMemset(h->set[0].ev_counts, 0, h->NB * 8ull) != hipSuccess ||
+      hipMemset(h->set[0].ev_off, 0, h->NB * 16ull) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     hb_destroy(h);
     return HB_EDEVICE;
@@ -1294,6 +1321,12 @@ int hb_destroy(hb_handle* h) {
   for (auto& row : h->ph)
     for (auto& e : row)
       if (e) (void)hipEventDestroy(e);
+  for (PrepSet& ps : h->set) {
+    if (ps.prepped) (void)hipEventDestroy(ps.prepped);
+    if (ps.applied) (void)hipEventDestroy(ps.applied);
+  }
+  if (h->in_ready) (void)hipEventDestroy(h->in_ready);
+  if (h->prep) (void)hipStreamDestroy(h->prep);
   delete h;
   return HB_OK;
 }
@@ -1307,6 +1340,7 @@ int hb_set_stream(hb_handle* h, void* stream) {
 int hb_sync(hb_handle* h) {
   if (!h) return HB_EINVAL;
   DeviceGuard guard(h->device);
+  HB_CHECK(hipStreamSynchronize(h->prep));
   HB_CHECK(hipStreamSynchronize(h->stream));
   return HB_OK;
 }
@@ -1411,16 +1445,34 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   if (!h || !b || b->n > h->max_batch) return HB_EINVAL;
   if (b->n && (!b->group || !b->info || !b->term || !b->index)) return HB_EINVAL;
   DeviceGuard guard(h->device);
-  hipStream_t st = h->stream;
+  hipStream_t st = h->stream;  // apply stream
+  // prep stream (partition + route): the library's own stream when the caller
+  // named a separate input stream, else the apply stream itself (no hops)
+  const bool two = h->in_stream_set && h->in_stream != h->stream;
+  hipStream_t ps_st = two ? h->prep : st;
   const bool prof = (flags & HB_STEP_PROFILE) != 0;
+  const bool prof_apply = prof || (flags & HB_STEP_PROFILE_APPLY) != 0;
+  PrepSet& ps = h->set[h->next_set];
+  hipEvent_t* ev = h->ph[h->prof_n % hb_handle::PROF_RING];
+
+  // ---- prep inputs.  The prep stream waits for (a) the inputs: the input
+  // stream's work so far (default: the apply stream, i.e. no overlap), (b) the
+  // last apply that read this prep set (two steps ago).
   BatchDev bd{b->group, b->info, b->term, b->index, b->hint, b->props, b->n};
+  if (two) {
+    HB_CHECK(hipEventRecord(h->in_ready, h->in_stream));
+    HB_CHECK(hipStreamWaitEvent(ps_st, h->in_ready, 0));
+    if (ps.used) HB_CHECK(hipStreamWaitEvent(ps_st, ps.applied, 0));
+  }
   if (flags & HB_STEP_HOST_PTRS) {
+    // partition inputs on the prep stream (staging is reused in prep-stream
+    // order); props / hint are read by apply, so they go on the apply stream.
     const size_t n = b->n;
     if (n) {
-      HB_CHECK(hipMemcpyAsync(h->s_group, b->group, n * 4, hipMemcpyHostToDevice, st));
-      HB_CHECK(hipMemcpyAsync(h->s_info, b->info, n * 4, hipMemcpyHostToDevice, st));
-      HB_CHECK(hipMemcpyAsync(h->s_term, b->term, n * 8, hipMemcpyHostToDevice, st));
-      HB_CHECK(hipMemcpyAsync(h->s_index, b->index, n * 8, hipMemcpyHostToDevice, st));
+      HB_CHECK(hipMemcpyAsync(h->s_group, b->group, n * 4, hipMemcpyHostToDevice, ps_st));
+      HB_CHECK(hipMemcpyAsync(h->s_info, b->info, n * 4, hipMemcpyHostToDevice, ps_st));
+      HB_CHECK(hipMemcpyAsync(h->s_term, b->term, n * 8, hipMemcpyHostToDevice, ps_st));
+      HB_CHECK(hipMemcpyAsync(h->s_index, b->index, n * 8, hipMemcpyHostToDevice, ps_st));
       if (b->hint) HB_CHECK(hipMemcpyAsync(h->s_hint, b->hint, n * 8, hipMemcpyHostToDevice, st));
     }
     if (b->props) HB_CHECK(hipMemcpyAsync(h->s_props, b->props, (size_t)h->G * 4, hipMemcpyHostToDevice, st));
@@ -1431,44 +1483,43 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     bd.hint = b->hint ? h->s_hint : nullptr;
     bd.props = b->props ? h->s_props : nullptr;
   }
-  hipEvent_t* ev = h->ph[h->prof_n % hb_handle::PROF_RING];
-  if (prof) HB_CHECK(hipEventRecord(ev[0], st));
+  if (prof) HB_CHECK(hipEventRecord(ev[0], ps_st));
 
-  // ---- phase 1: partition ----------------------------------------------------
+  // ---- phase 1: partition (prep stream) ---------------------------------------
   const uint32_t NB = h->NB;
   if (b->n == 0) {
-    HB_CHECK(hipMemsetAsync(h->bk_off, 0, (h->NBK + 1) * 4ull, st));
-    HB_CHECK(hipMemsetAsync(h->bk_fill, 0, h->NBK * 4ull, st));
+    HB_CHECK(hipMemsetAsync(ps.bk_off, 0, (h->NBK + 1) * 4ull, ps_st));
+    HB_CHECK(hipMemsetAsync(h->bk_fill, 0, h->NBK * 4ull, ps_st));
   } else {
     const uint32_t ntiles = (uint32_t)((b->n + RDX_TILE - 1) / RDX_TILE);
     RadixSrc src{bd.group, bd.info, nullptr, bd.term, bd.index, nullptr, (uint32_t)b->n};
-    const FinalDst fin{h->rec, h->key, h->bucket, h->passes == 1 ? h->bk_off : nullptr, h->NBK};
+    const FinalDst fin{ps.rec, ps.key, ps.bucket, h->passes == 1 ? ps.bk_off : nullptr, h->NBK};
     for (uint32_t p = 0; p < h->passes; ++p) {
       const bool last_pass = p + 1 == h->passes;
       const RadixDst& dst = h->tmp[p & 1];
       const uint32_t shift = p * RDX_BITS;
-      hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(RDX_THREADS), 0, st, src, h->G, shift, ntiles, h->hist);
-      hipLaunchKernelGGL(k_scan_rows, dim3(RDX_BINS), dim3(1024), 0, st, h->hist, ntiles, h->totals, h->bk_fill,
+      hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, h->G, shift, ntiles, h->hist);
+      hipLaunchKernelGGL(k_scan_rows, dim3(RDX_BINS), dim3(1024), 0, ps_st, h->hist, ntiles, h->totals, h->bk_fill,
                          h->NBK);
       if (last_pass)
-        hipLaunchKernelGGL(k_radix_scatter<true>, dim3(ntiles), dim3(RDX_THREADS), 0, st, src, dst, fin, h->G, shift,
-                           ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
+        hipLaunchKernelGGL(k_radix_scatter<true>, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
+                           shift, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
       else
-        hipLaunchKernelGGL(k_radix_scatter<false>, dim3(ntiles), dim3(RDX_THREADS), 0, st, src, dst, fin, h->G, shift,
-                           ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
+        hipLaunchKernelGGL(k_radix_scatter<false>, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
+                           shift, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
       src = RadixSrc{dst.group, dst.info, dst.orig, dst.term, dst.index, h->n_valid, (uint32_t)b->n};
     }
     if (h->passes > 1)
-      hipLaunchKernelGGL(k_bucket_bounds, dim3((h->NBK + 1 + 255) / 256), dim3(256), 0, st,
-                         (const uint32_t*)h->bucket, (const uint32_t*)h->n_valid, h->NBK, h->bk_off);
+      hipLaunchKernelGGL(k_bucket_bounds, dim3((h->NBK + 1 + 255) / 256), dim3(256), 0, ps_st,
+                         (const uint32_t*)ps.bucket, (const uint32_t*)h->n_valid, h->NBK, ps.bk_off);
   }
 
-  // ---- phase 2: route each partition's messages to its lanes; apply -----------
+  // ---- phase 2: route each partition's messages to its lanes (prep stream) ----
   ApplyArgs aa;
   aa.S = h->st;
-  aa.rec = h->rec;
-  aa.key = h->key;
-  aa.bk_off = h->bk_off;
+  aa.rec = ps.rec;
+  aa.key = ps.key;
+  aa.bk_off = ps.bk_off;
   aa.bk_fill = h->bk_fill;
   aa.hint = bd.hint;
   aa.props = bd.props;
@@ -1476,30 +1527,41 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.ev_per_msg = h->ev_per_msg;
   aa.props_on = bd.props ? 1u : 0u;
   aa.NB = NB;
-  aa.ev_counts = h->ev_counts;
-  aa.ev_off = h->ev_off;
+  aa.ev_counts = ps.ev_counts;
+  aa.ev_off = ps.ev_off;
   aa.stats_shard = h->stats_shard;
   aa.pflag = h->pflag;
   aa.resume = h->resume;
   aa.commit0 = h->commit0;
   aa.kmax = h->nmax - 1;
-  aa.cnt = h->cnt;
-  aa.slot_info = h->slot_info;
-  aa.slot_orig = h->slot_orig;
-  aa.slot_term = h->slot_term;
-  aa.slot_index = h->slot_index;
-  hipLaunchKernelGGL(k_route, dim3(apply_grid(h)), dim3(PART), 0, st, aa);
-  if (prof) HB_CHECK(hipEventRecord(ev[HB_PHASE_PARTITION + 1], st));
-  switch (h->nmax) {
-    case 3: launch_apply<3>(h, aa, prof ? ev : nullptr); break;
-    case 5: launch_apply<5>(h, aa, prof ? ev : nullptr); break;
-    default: launch_apply<7>(h, aa, prof ? ev : nullptr); break;
+  aa.cnt = ps.cnt;
+  aa.slot_info = ps.slot_info;
+  aa.slot_orig = ps.slot_orig;
+  aa.slot_term = ps.slot_term;
+  aa.slot_index = ps.slot_index;
+  hipLaunchKernelGGL(k_route, dim3(apply_grid(h)), dim3(PART), 0, ps_st, aa);
+  if (prof) HB_CHECK(hipEventRecord(ev[1], ps_st));
+  if (two) {
+    HB_CHECK(hipEventRecord(ps.prepped, ps_st));
+    // ---- phase 3: apply (apply stream, after the previous step's apply) ------
+    HB_CHECK(hipStreamWaitEvent(st, ps.prepped, 0));
   }
-  // ---- phase 3: finish -----------------------------------------------------------
+  switch (h->nmax) {
+    case 3: launch_apply<3>(h, aa, prof_apply ? ev : nullptr, prof); break;
+    case 5: launch_apply<5>(h, aa, prof_apply ? ev : nullptr, prof); break;
+    default: launch_apply<7>(h, aa, prof_apply ? ev : nullptr, prof); break;
+  }
   hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, h->stats_shard, h->stats, h->stats_accum);
-  if (prof) HB_CHECK(hipEventRecord(ev[HB_PHASE_FINISH + 1], st));
+  if (prof) HB_CHECK(hipEventRecord(ev[5], st));
+  if (two) HB_CHECK(hipEventRecord(ps.applied, st));
   HB_CHECK(hipGetLastError());
-  if (prof) h->prof_n++;
+  ps.used = true;
+  h->cur = h->next_set;
+  h->next_set ^= 1;
+  if (prof_apply) {
+    h->prof_full[h->prof_n % hb_handle::PROF_RING] = prof;
+    h->prof_n++;
+  }
   h->stepped = true;
   return HB_OK;
 }
@@ -1508,8 +1570,8 @@ int hb_events_device(hb_handle* h, const uint64_t** base, const uint64_t** chunk
                      uint32_t* n_chunks) {
   if (!h || !base || !chunk_off || !counts || !n_chunks) return HB_EINVAL;
   *base = h->ev;
-  *chunk_off = h->ev_off;
-  *counts = h->ev_counts;
+  *chunk_off = h->set[h->cur].ev_off;
+  *counts = h->set[h->cur].ev_counts;
   *n_chunks = 2 * h->NB;
   return HB_OK;
 }
@@ -1529,10 +1591,10 @@ int hb_copy_events(hb_handle* h, hb_event* out, uint64_t cap, uint64_t* n) {
   uint64_t* dst = reinterpret_cast<uint64_t*>(d + total);
   uint32_t* per_chunk = reinterpret_cast<uint32_t*>(dst + 2 * h->NB);
   hipLaunchKernelGGL(k_chunk_events, dim3(2 * h->NB), dim3(256), 0, h->stream, (const uint64_t*)h->ev,
-                     (const uint32_t*)h->ev_counts, (const uint64_t*)h->ev_off, per_chunk);
+                     (const uint32_t*)h->set[h->cur].ev_counts, (const uint64_t*)h->set[h->cur].ev_off, per_chunk);
   hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, h->stream, (const uint32_t*)per_chunk, 2 * h->NB, dst);
   hipLaunchKernelGGL(k_expand_events, dim3(2 * h->NB), dim3(256), 0, h->stream, (const uint64_t*)h->ev,
-                     (const uint32_t*)h->ev_counts, (const uint64_t*)h->ev_off, (const uint64_t*)dst, d);
+                     (const uint32_t*)h->set[h->cur].ev_counts, (const uint64_t*)h->set[h->cur].ev_off, (const uint64_t*)dst, d);
   hipError_t e = hipMemcpyAsync(out, d, total * sizeof(hb_event), hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   (void)hipFree(d);
@@ -1560,12 +1622,18 @@ int hb_phase_ms(hb_handle* h, float* out, uint32_t* steps) {
   if (steps) *steps = n;
   for (int i = 0; i < HB_PHASE_COUNT; ++i) out[i] = 0.f;
   if (n == 0) return HB_EINVAL;
+  HB_CHECK(hipStreamSynchronize(h->prep));
   HB_CHECK(hipStreamSynchronize(h->stream));
+  // (start, end) event of each phase in h->ph[k]
+  static const int span[HB_PHASE_COUNT][2] = {{0, 1}, {2, 3}, {3, 4}, {4, 5}};
+  uint32_t nfull = 0;
+  for (uint32_t k = 0; k < n; ++k) nfull += h->prof_full[k] ? 1u : 0u;
   for (uint32_t k = 0; k < n; ++k) {
     for (int i = 0; i < HB_PHASE_COUNT; ++i) {
+      if (i != HB_PHASE_APPLY && !h->prof_full[k]) continue;
       float ms = 0.f;
-      HB_CHECK(hipEventElapsedTime(&ms, h->ph[k][i], h->ph[k][i + 1]));
-      out[i] += ms / (float)n;
+      HB_CHECK(hipEventElapsedTime(&ms, h->ph[k][span[i][0]], h->ph[k][span[i][1]]));
+      out[i] += ms / (float)(i == HB_PHASE_APPLY ? n : nfull);
     }
   }
   return HB_OK;
@@ -1580,6 +1648,13 @@ int hb_phase_reset(hb_handle* h) {
 int hb_set_stats_accum(hb_handle* h, uint64_t* dev_accum) {
   if (!h) return HB_EINVAL;
   h->stats_accum = dev_accum;
+  return HB_OK;
+}
+
+int hb_set_input_stream(hb_handle* h, void* stream) {
+  if (!h) return HB_EINVAL;
+  h->in_stream = reinterpret_cast<hipStream_t>(stream);
+  h->in_stream_set = true;
   return HB_OK;
 }
 

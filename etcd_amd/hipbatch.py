@@ -46,6 +46,7 @@ def lib():
         "hb_create": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, P(H)]),
         "hb_destroy": (C.c_int, [H]),
         "hb_set_stream": (C.c_int, [H, C.c_void_p]),
+        "hb_set_input_stream": (C.c_int, [H, C.c_void_p]),
         "hb_sync": (C.c_int, [H]),
         "hb_load_groups": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
         "hb_get_groups": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
@@ -121,6 +122,13 @@ class Engine:
         raw = getattr(stream, "cuda_stream", stream)
         _check("hb_set_stream", lib().hb_set_stream(self.h, C.c_void_p(raw or 0)))
 
+    def set_input_stream(self, stream):
+        """The stream that produces batch arrays (torch.cuda.Stream / raw hipStream_t / None
+        for the null stream): the prep stage of a step waits only for it, so it can overlap
+        the previous step's apply."""
+        raw = getattr(stream, "cuda_stream", stream)
+        _check("hb_set_input_stream", lib().hb_set_input_stream(self.h, C.c_void_p(raw or 0)))
+
     def sync(self):
         _check("hb_sync", lib().hb_sync(self.h))
 
@@ -152,14 +160,16 @@ class Engine:
 
     # ---- hot path --------------------------------------------------------------
     def step(self, group, info, term, index, hint=None, props=None, host=None, profile=False):
-        """Step one batch.  Arrays are numpy (host) or torch tensors (host or cuda)."""
+        """Step one batch.  Arrays are numpy (host) or torch tensors (host or cuda).
+        profile: False, True (every phase) or "apply" (only HB_PHASE_APPLY)."""
         b = abi.hb_batch()
         b.n = len(group)
         b.group, b.info, b.term, b.index = _ptr(group), _ptr(info), _ptr(term), _ptr(index)
         b.hint, b.props = _ptr(hint), _ptr(props)
         if host is None:
             host = not (hasattr(group, "is_cuda") and group.is_cuda)
-        flags = (abi.HB_STEP_HOST_PTRS if host else 0) | (abi.HB_STEP_PROFILE if profile else 0)
+        prof = {True: abi.HB_STEP_PROFILE, "apply": abi.HB_STEP_PROFILE_APPLY}.get(profile, 0)
+        flags = (abi.HB_STEP_HOST_PTRS if host else 0) | prof
         self._keep = (group, info, term, index, hint, props)
         _check("hb_step", lib().hb_step(self.h, C.byref(b), flags))
 

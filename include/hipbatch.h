@@ -115,6 +115,7 @@ typedef struct hb_batch {
 /* hb_step flags */
 #define HB_STEP_HOST_PTRS 0x1u   /* batch arrays are host pointers (copied H2D) */
 #define HB_STEP_PROFILE   0x2u   /* record per-phase HIP events (hb_phase_ms)   */
+#define HB_STEP_PROFILE_APPLY 0x4u  /* only the HB_PHASE_APPLY events (two, on the apply stream) */
 
 /* ---- per-group state (host view, array-of-structures) --------------------
  * Device keeps this as SoA.  Field meanings follow the reference:
@@ -251,9 +252,23 @@ int  hb_create(int device, uint32_t capacity, uint32_t max_replicas,
                uint32_t max_inflight, uint64_t max_msg_size, uint64_t max_batch,
                hb_handle** out);
 int  hb_destroy(hb_handle* h);
-/* Launch on this HIP stream (hipStream_t as void*); NULL = the null stream. */
+/* Launch on this HIP stream (hipStream_t as void*); NULL = the null stream.
+ * This is the apply stream: the group state, the events and the statistics
+ * are produced on it, in hb_step order. */
 int  hb_set_stream(hb_handle* h, void* hip_stream);
-int  hb_sync(hb_handle* h);
+/* Each hb_step runs in two stages: prep (sort the batch by bucket and route
+ * every group's messages to it; a library-owned stream, double-buffered) and
+ * apply (the raft bookkeeping; the apply stream).  Prep only reads the batch,
+ * so the prep of step k+1 may run while step k applies.  Prep waits for the
+ * work enqueued so far on the INPUT stream, the one that produces the batch
+ * arrays: by default the apply stream (prep k+1 then starts after apply k);
+ * a caller whose batches are ready earlier, or produced on a stream of their
+ * own, names that stream here to let the two stages overlap.  NULL stream
+ * pointer = the null stream.  The caller must keep a batch's arrays intact
+ * until hb_step for it has been followed by hb_sync or by the next hb_step
+ * returning. */
+int  hb_set_input_stream(hb_handle* h, void* hip_stream);
+int  hb_sync(hb_handle* h);   /* waits for both stages of every step so far */
 int  hb_abi_version(void);
 const char* hb_strerror(int code);
 
