@@ -694,13 +694,12 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   uint32_t s_info[KMAX], s_orig[KMAX];
   uint64_t s_term[KMAX], s_index[KMAX];
 #pragma unroll
-  for (uint32_t k = 0; k < KMAX; ++k) {
+  for (uint32_t k = 0; k < KMAX; ++k) {  // independent of cnt: one round trip (unused slots are ignored)
     const size_t o = (size_t)k * a.S.G + g;
-    const bool on = gvalid && k < cnt;
-    s_info[k] = on ? a.slot_info[o] : 0u;
-    s_orig[k] = on ? a.slot_orig[o] : 0u;
-    s_term[k] = on ? a.slot_term[o] : 0ull;
-    s_index[k] = on ? a.slot_index[o] : 0ull;
+    s_info[k] = gvalid ? a.slot_info[o] : 0u;
+    s_orig[k] = gvalid ? a.slot_orig[o] : 0u;
+    s_term[k] = gvalid ? a.slot_term[o] : 0ull;
+    s_index[k] = gvalid ? a.slot_index[o] : 0ull;
   }
   const uint64_t moff = a.ev_off[2 * part + 1];
   const uint64_t last0 = L.last, commit0 = L.committed;
