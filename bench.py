@@ -225,6 +225,9 @@ def main():
                 "traffic": traffic,
                 "traffic_source": tsrc,
                 "kernel": kname,
+                "launch_us_timed": round(apply_ms * 1e3, 2),
+                "launch_us_isolated": round(float(ph2[abi.HB_PHASE_APPLY]) * 1e3, 2),
+                "frac_isolated": round(alg / (float(ph2[abi.HB_PHASE_APPLY]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "alg_bytes_per_launch": alg,
                 "alg_bytes_note": f"SURVEY.md 8(d): {alg_bytes_per_group(n)} B/group = "
                                   f"{alg_bytes_per_group(n) / (n - 1):.0f} B/MsgAppResp x {G * (n - 1)} MsgAppResp"}

@@ -39,7 +39,9 @@ def _runs_for(first, tf, last, term):
 # ---------------------------------------------------------------------------- cfg2
 def steady_groups(G, n=3, seed=0x5EED0002, last_hi=1 << 20, term_hi=1000, with_runs=True):
     """All groups leader (self = slot 0), followers Replicate with empty inflights,
-    every Match = committed = lastIndex; term ~ U[1, term_hi]; termFirst ~ U[1, last]."""
+    every Match = committed = lastIndex; term ~ U[1, term_hi]; termFirst ~ U[1, last].
+    with_runs: True (list of term runs per group), "flat" ((index, term) rows plus
+    per-group offsets, for large G) or False."""
     rng = np.random.default_rng(seed)
     g = np.zeros(G, dtype=A.GROUP_DTYPE)
     term = rng.integers(1, term_hi + 1, G, dtype=np.uint64)
@@ -56,7 +58,12 @@ def steady_groups(G, n=3, seed=0x5EED0002, last_hi=1 << 20, term_hi=1000, with_r
         pr[:, s]["next"] = last + np.uint64(1)
         pr[:, s]["state"] = A.HB_PR_PROBE if s == 0 else A.HB_PR_REPLICATE
     runs = None
-    if with_runs:
+    if with_runs == "flat":  # (flat [2G, 2] (index, term), offsets [G+1]): first = 1 < tf always
+        flat = np.zeros((G, 2, 2), dtype=np.uint64)
+        flat[:, 0, 1] = np.maximum(term.astype(np.int64) - 1, 0).astype(np.uint64)
+        flat[:, 1, 0], flat[:, 1, 1] = tf, term
+        runs = (flat.reshape(-1, 2), np.arange(0, 2 * G + 1, 2, dtype=np.uint64))
+    elif with_runs:
         runs = [_runs_for(1, int(tf[i]), int(last[i]), int(term[i])) for i in range(G)]
     return g, runs
 

@@ -134,6 +134,8 @@ def lib():
             "orc_groups_new": (R, [C.c_uint32]),
             "orc_groups_free": (None, [R, C.c_uint32]),
             "orc_groups_at": (R, [R, C.c_uint32]),
+            "orc_groups_load": (C.c_int, [R, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_uint64]),
+            "orc_groups_export": (None, [R, C.c_uint32, C.c_void_p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -358,6 +360,18 @@ class Raft:
 # ---------------------------------------------------------------------------
 # batch driver (engine format)
 # ---------------------------------------------------------------------------
+def flat_runs(runs):
+    """Log term runs per group as (flat [R, 2] u64 (index, term), offsets [G+1] u64).
+    Accepts the list-of-lists form or an already flat (flat, off) tuple."""
+    if isinstance(runs, tuple):
+        flat, off = runs
+        return np.ascontiguousarray(flat, dtype=np.uint64), np.ascontiguousarray(off, dtype=np.uint64)
+    off = np.zeros(len(runs) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(r) for r in runs])
+    flat = np.array([x for r in runs for x in r], dtype=np.uint64).reshape(-1, 2)
+    return np.ascontiguousarray(flat), off
+
+
 class OracleGroups:
     """ngroups oracle rafts stepped with orc_step_batch (the engine's batch format)."""
 
@@ -368,15 +382,12 @@ class OracleGroups:
         self.G = len(groups)
         self.max_inflight = max_inflight
         self.ptr = L.orc_groups_new(self.G)
-        gbuf = np.ascontiguousarray(groups)
-        for g in range(self.G):
-            rs = runs[g]
-            rr = (orc_run * len(rs))(*[orc_run(int(a), int(b)) for a, b in rs])
-            rec = abi.hb_group.from_buffer_copy(gbuf[g].tobytes())
-            rc = L.orc_raft_from_group(L.orc_groups_at(self.ptr, g), C.byref(rec), rr, len(rs),
-                                       max_inflight, max_msg_size)
-            if rc != 0:
-                raise ValueError(f"orc_raft_from_group({g}) = {rc}")
+        gbuf = np.ascontiguousarray(groups, dtype=abi.GROUP_DTYPE)
+        flat, off = flat_runs(runs)
+        rc = L.orc_groups_load(self.ptr, self.G, gbuf.ctypes.data, flat.ctypes.data, off.ctypes.data,
+                               max_inflight, max_msg_size)
+        if rc != 0:
+            raise ValueError(f"orc_raft_from_group({-rc - 1}) failed")
         for (g, s), vals in (inflights or {}).items():
             v = np.ascontiguousarray(vals, dtype=np.uint64)
             start = int(gbuf[g]["pr"][s]["ins_start"])
@@ -417,12 +428,8 @@ class OracleGroups:
         return ev[: nev.value].copy(), np.array(stats[:], dtype=np.uint64)
 
     def groups(self):
-        L = lib()
         out = np.zeros(self.G, dtype=abi.GROUP_DTYPE)
-        g = abi.hb_group()
-        for i in range(self.G):
-            L.orc_raft_to_group(L.orc_groups_at(self.ptr, i), C.byref(g))
-            out[i] = np.frombuffer(bytes(g), dtype=abi.GROUP_DTYPE)[0]
+        lib().orc_groups_export(self.ptr, self.G, out.ctypes.data)
         return out
 
     def inflights(self, g, slot):

@@ -895,3 +895,20 @@ void orc_groups_free(orc_raft* g, uint32_t ngroups) {
 orc_raft* orc_groups_at(orc_raft* g, uint32_t i) { return &g[i]; }
 
 size_t orc_sizeof_raft(void) { return sizeof(orc_raft); }
+
+/* Bulk CreateGroup / Status for n groups (test infrastructure: lets the
+ * Python harness load and read back a million groups without a per-group
+ * ctypes call).  Group i's log term runs are runs[run_off[i], run_off[i+1]). */
+int orc_groups_load(orc_raft* gs, uint32_t n, const hb_group* recs, const orc_run* runs, const uint64_t* run_off,
+                    int max_inflight, uint64_t max_msg_size) {
+  for (uint32_t i = 0; i < n; i++) {
+    int rc = orc_raft_from_group(&gs[i], &recs[i], runs + run_off[i], (int)(run_off[i + 1] - run_off[i]),
+                                 max_inflight, max_msg_size);
+    if (rc != 0) return -(int)i - 1;
+  }
+  return 0;
+}
+
+void orc_groups_export(const orc_raft* gs, uint32_t n, hb_group* out) {
+  for (uint32_t i = 0; i < n; i++) orc_raft_to_group(&gs[i], &out[i]);
+}

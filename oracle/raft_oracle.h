@@ -195,6 +195,9 @@ int orc_step_batch(orc_raft* groups, uint32_t ngroups, const hb_batch* b,
 /* Flat-array helpers so the Python harness can drive many groups via ctypes. */
 orc_raft* orc_groups_new(uint32_t ngroups);
 void      orc_groups_free(orc_raft* g, uint32_t ngroups);
+int       orc_groups_load(orc_raft* gs, uint32_t n, const hb_group* recs, const orc_run* runs,
+                          const uint64_t* run_off, int max_inflight, uint64_t max_msg_size);
+void      orc_groups_export(const orc_raft* gs, uint32_t n, hb_group* out);
 orc_raft* orc_groups_at(orc_raft* g, uint32_t i);
 size_t    orc_sizeof_raft(void);
 

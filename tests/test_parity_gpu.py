@@ -106,3 +106,71 @@ def test_large_indices_long_event_words():
     for step in range(2):
         _, st, _ = pair.step(synth.cfg2_batch(g, step, seed=31 + step), ctx=f"large step {step}")
         assert st[abi.HB_STAT_COMMITS] == 2000
+
+
+def test_two_pass_partition_over_1m_groups():
+    """> 256 buckets (1M groups): the bucket sort takes two 8-bit radix passes and
+    bucket bounds come from a binary search; cfg2 then a random mix on top."""
+    G = 1_100_000
+    g, runs = synth.steady_groups(G, 3, seed=41, last_hi=1 << 30, with_runs="flat")
+    pair = Pair(g, runs, 3, 256, max_batch=2 * G + 16)
+    _, st, _ = pair.step(synth.cfg2_batch(g, 0, seed=42), ctx="2-pass cfg2", check_inflights=False)
+    assert st[abi.HB_STAT_COMMITS] == G
+    pair.step(synth.random_batch(g, 300_000, seed=43, props=False), ctx="2-pass random", check_inflights=False)
+
+
+def test_hot_bucket_many_segments_and_rounds():
+    """One bucket takes ~54k messages: the key scan spans several segments and
+    every partition of the bucket several routing / general rounds; its groups
+    have more messages than slots and go through the general state machine."""
+    G = 20_000
+    g, runs = synth.steady_groups(G, 3, seed=51, last_hi=5000)
+    pair = Pair(g, runs, 3, 256, max_batch=1 << 17)
+    rng = np.random.default_rng(52)
+    N = 60_000
+    grp = np.where(rng.random(N) < 0.9, rng.integers(0, 4096, N), rng.integers(0, G, N)).astype(np.uint32)
+    slot = rng.integers(1, 3, N).astype(np.uint32)
+    last = g["last_index"][grp].astype(np.int64)
+    index = (last + 1 - rng.integers(0, 4, N)).astype(np.uint64)
+    info = (abi.HB_MSG_APP_RESP | (slot << 4)).astype(np.uint32)
+    b = dict(group=grp, info=info, term=g["term"][grp].astype(np.uint64), index=index, hint=None,
+             props=np.ones(G, np.uint32))
+    pair.step(b, ctx="hot bucket")
+
+
+def test_pipelined_steps_with_input_stream():
+    """Prep of step k+1 overlaps apply of step k (separate input stream, device
+    batches, no sync between steps): the final state and the summed statistics
+    equal stepping the same batches through the oracle."""
+    import torch
+    from etcd_amd.hipbatch import Engine
+    from oracle.pyoracle import OracleGroups
+    G, n = 50_000, 3
+    g, runs = synth.steady_groups(G, n, seed=61, last_hi=1 << 20)
+    og = OracleGroups(g, runs, 256)
+    init = og.groups()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream()
+    eng = Engine(G, max_replicas=n, max_inflight=256, max_batch=4 * G, stream=stream)
+    eng.set_input_stream(torch.cuda.Stream(device=dev))
+    eng.load_groups(init)
+    acc = torch.zeros(abi.HB_STAT_COUNT, dtype=torch.int64, device=dev)
+    eng.set_stats_accum(acc)
+    batches = [synth.cfg2_batch(g, k, seed=62 + k) for k in range(4)]
+    batches.append(synth.random_batch(g, 40_000, seed=70))
+    d = []
+    for b in batches:
+        t = {k: (torch.from_numpy(v.view(np.int32 if v.dtype == np.uint32 else np.int64)).to(dev) if v is not None
+                 else None) for k, v in b.items()}
+        d.append(t)
+    torch.cuda.synchronize()
+    for t in d:  # back to back: no sync, batches stay alive in `d`
+        eng.step(t["group"], t["info"], t["term"], t["index"], t["hint"], t["props"], host=False)
+    eng.sync()
+    ora_sum = np.zeros(abi.HB_STAT_COUNT, dtype=np.uint64)
+    for b in batches:
+        _, st = og.step(b)
+        ora_sum += st
+    assert np.array_equal(acc.cpu().numpy().astype(np.uint64), ora_sum)
+    from .parity_util import assert_groups_equal
+    assert_groups_equal(eng.get_groups(), og.groups(), "pipelined")
