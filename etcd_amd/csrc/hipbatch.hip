@@ -1288,7 +1288,11 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
     hb_destroy(h);
     return rc;
   }
-  bool ok = hipStreamCreateWithFlags(&h->prep, hipStreamNonBlocking) == hipSuccess &&
+  // the prep stream runs at the lowest priority: its kernels fill what the
+  // apply stage leaves idle instead of competing with it
+  int prio_least = 0, prio_greatest = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+  bool ok = hipStreamCreateWithPriority(&h->prep, hipStreamNonBlocking, prio_least) == hipSuccess &&
             hipEventCreateWithFlags(&h->in_ready, hipEventDisableTiming) == hipSuccess;
   for (PrepSet& ps : h->set)
     ok = ok && hipEventCreateWithFlags(&ps.prepped, hipEventDisableTiming) == hipSuccess &&

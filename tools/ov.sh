@@ -2,7 +2,7 @@
 # overlap vs no overlap, with and without apply-phase events:  gpurun -- bash tools/ov.sh
 set -e
 cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out/ov
-for args in "" "--no-profile" "--no-overlap" "--no-overlap --no-profile"; do
+for args in "" "--no-profile" "--overlap" "--overlap --no-profile"; do
   timeout -k 10 120 python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline $args > gpurun_out/ov/o.json
   A="$args" python3 - <<'PY'
 import json, os
