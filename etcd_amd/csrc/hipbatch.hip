@@ -359,6 +359,7 @@ struct ApplyArgs {
   uint32_t ev_per_msg;      // bound on event words per stepped message
   uint32_t props_on;        // 1 if props[] is present (one proposal slot per group)
   uint32_t NB;              // partitions
+  uint32_t NBK;             // buckets
   uint32_t* ev_counts;      // [NB] records in each chunk
   uint64_t* ev_off;         // [NB] chunk offsets (records)
   uint64_t* stats_shard;    // [8][16] step statistics, one shard per XCD slot (atomic adds)
@@ -607,50 +608,105 @@ __device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_sta
 }
 
 // ---------------------------------------------------------------------------
-// k_route: one workgroup per partition.  Picks the partition's messages out
-// of its bucket (key scan), gathers them and sorts them by lane (arrival
-// order kept), and lays each lane's first KMAX messages out lane-major:
-// slot k of group g at slots.*[k][g], so k_apply_fast reads them with
-// coalesced loads in the same round trip as the group state.  cnt[g] =
-// the lane's message count (saturated at 255).  It also reserves the
-// partition's M event chunk (ev_off[2p+1]).  No raft logic runs here.
+// k_route<KMAX>: W = BK / RG workgroups per bucket, each owning RG groups
+// (RG x KMAX message slots fit in LDS: RG = 2048 / 1024 / 512 for KMAX =
+// 2 / 4 / 6).  Each workgroup streams its bucket's records (coalesced; the W
+// sisters of a bucket share one XCD's L2), ranks the messages of its groups
+// with one LDS counter per group, stages each group's first KMAX messages in
+// LDS and writes them out lane-major (slot k of group g at slots.*[k][g]) with
+// coalesced stores, so k_apply_fast reads them in the same round trip as the
+// group state.  Counter ranks follow LDS-atomic order, not arrival order:
+// k_apply_fast sorts a group's slots by arrival index and hands a group with
+// more than KMAX messages to k_apply whole.  cnt[g] = the group's message
+// count (saturated at 255).  Each partition reserves its M event chunk in the
+// bucket's region (one atomic per partition).  No raft logic runs here.
 // ---------------------------------------------------------------------------
-#ifndef HB_ROUTE_CHUNK
-#define HB_ROUTE_CHUNK 512
-#endif
-__global__ void __launch_bounds__(PART, 8) k_route(ApplyArgs a) {
-  __shared__ Stage<HB_ROUTE_CHUNK> sl;
-  const uint32_t part = block_part();
-  if (part >= a.NB) return;  // uniform: grid padding
+constexpr uint32_t ROUTE_THREADS = 1024;
+constexpr uint32_t ROUTE_UNROLL = 4;  // records in flight per lane
+template <int KMAX> struct RouteGeom {
+  static constexpr uint32_t RG_LOG = KMAX <= 2 ? 11 : (KMAX <= 4 ? 10 : 9);
+  static constexpr uint32_t RG = 1u << RG_LOG;     // groups per workgroup
+  static constexpr uint32_t W = (1u << BK_LOG) / RG;  // workgroups per bucket
+};
+
+template <int KMAX>
+__global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
+  using RGm = RouteGeom<KMAX>;
+  constexpr uint32_t RG = RGm::RG, W = RGm::W, NP = RG / PART;
+  __shared__ uint32_t l_cnt[RG];
+  __shared__ uint32_t l_info[KMAX][RG];
+  __shared__ uint32_t l_orig[KMAX][RG];
+  __shared__ uint64_t l_term[KMAX][RG];
+  __shared__ uint64_t l_index[KMAX][RG];
+  __shared__ uint32_t l_ptot[NP];
+  // blockIdx -> (bucket, w): the W sisters of a bucket share blockIdx % 8 (one XCD)
+  const uint32_t x = blockIdx.x, q = x >> 3;
+  const uint32_t bk = ((q / W) << 3) | (x & 7), w = q % W;
+  if (bk >= a.NBK) return;  // uniform: grid padding
   const uint32_t tid = threadIdx.x;
-  const uint32_t bk = part >> SIS_LOG, sub = part & (SIS - 1);
-  const uint32_t g = part * PART + tid;
+  for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) l_cnt[i] = 0;
+  if (tid < NP) l_ptot[tid] = 0;
+  __syncthreads();
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
-  const uint32_t kmax = a.kmax;
-  uint32_t j = 0;  // messages of this lane so far (all rounds)
-  auto on_total = [&](uint32_t total) {
-    if (tid == 0) {
-      const uint32_t r = atomicAdd(&a.bk_fill[bk], a.ev_per_msg * (total + PART * a.props_on));
-      a.ev_off[2 * part + 1] = (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + (uint64_t)lo +
-                                                         (uint64_t)bk * (PART * SIS) * a.props_on) + r;
+  const uint32_t G = a.S.G;
+  const uint32_t lg0 = w * RG;  // first group (in the bucket) of this workgroup
+  for (uint32_t base = lo; base < hi; base += ROUTE_THREADS * ROUTE_UNROLL) {
+    MsgRec m[ROUTE_UNROLL];
+    uint32_t sub[ROUTE_UNROLL];
+#pragma unroll
+    for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
+      const uint32_t p = base + u * ROUTE_THREADS + tid;
+      if (p < hi) {
+        m[u] = a.rec[p];
+        sub[u] = a.key[p];
+      }
     }
-  };
-  auto round = [&](uint32_t fill) {
-    uint32_t my_start, my_cnt;
-    gather_round(sl, a, lo, fill, &my_start, &my_cnt, []() {});
-    for (uint32_t x = 0; x < my_cnt && j + x < kmax; ++x) {
-      const uint32_t i = sl.perm[my_start + x];
-      const size_t o = (size_t)(j + x) * a.S.G + g;
-      a.slot_info[o] = sl.info(i);
-      a.slot_orig[o] = sl.orig(i);
-      a.slot_term[o] = sl.term(i);
-      a.slot_index[o] = sl.index(i);
+#pragma unroll
+    for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
+      const uint32_t p = base + u * ROUTE_THREADS + tid;
+      const uint32_t l = p < hi ? ((sub[u] << PART_LOG) | ((m[u].info >> 16) & (PART - 1))) - lg0 : RG;
+      if (l < RG) {
+        const uint32_t r = atomicAdd(&l_cnt[l], 1u);
+        if (r < (uint32_t)KMAX) {
+          l_info[r][l] = m[u].info;
+          l_orig[r][l] = m[u].orig;
+          l_term[r][l] = m[u].term;
+          l_index[r][l] = m[u].index;
+        }
+      }
     }
-    j += my_cnt;
-    __syncthreads();
-  };
-  walk_partition(sl, a, lo, hi, sub, nullptr, on_total, round);
-  if (g < a.S.G) a.cnt[g] = (uint8_t)(j < 255 ? j : 255);
+  }
+  __syncthreads();
+  const uint32_t gbase = (bk << BK_LOG) + lg0;
+  for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) {
+    const uint32_t c = l_cnt[i], g = gbase + i;
+    if (g < G) {
+      a.cnt[g] = (uint8_t)(c < 255 ? c : 255);
+#pragma unroll
+      for (uint32_t k = 0; k < (uint32_t)KMAX; ++k) {
+        if (k < c) {
+          const size_t o = (size_t)k * G + g;
+          a.slot_info[o] = l_info[k][i];
+          a.slot_orig[o] = l_orig[k][i];
+          a.slot_term[o] = l_term[k][i];
+          a.slot_index[o] = l_index[k][i];
+        }
+      }
+    }
+    uint32_t s = c;  // the wave's 64 groups lie in one partition
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+    if ((tid & 63) == 0 && s) atomicAdd(&l_ptot[i >> PART_LOG], s);
+  }
+  __syncthreads();
+  if (tid < NP) {
+    const uint32_t part = (bk << SIS_LOG) + w * NP + tid;
+    if (part < a.NB) {
+      const uint32_t r = atomicAdd(&a.bk_fill[bk], a.ev_per_msg * (l_ptot[tid] + PART * a.props_on));
+      a.ev_off[2 * part + 1] =
+          (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + lo + (uint64_t)bk * (PART * SIS) * a.props_on) + r;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -725,10 +781,35 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
     }
   }
 
-  // ---- the lane's messages, arrival order (M chunk reserved by k_route)
+  // ---- the lane's messages, arrival order (M chunk reserved by k_route).  The
+  // slots arrive in k_route's counter order: sort them by arrival index
+  // (odd-even transposition over KMAX registers; unused slots sort last).
+#pragma unroll
+  for (uint32_t k = 0; k < KMAX; ++k) s_orig[k] = k < cnt ? s_orig[k] : 0xFFFFFFFFu;
+#pragma unroll
+  for (uint32_t r = 0; r < KMAX; ++r) {
+#pragma unroll
+    for (uint32_t k = (r & 1); k + 1 < KMAX; k += 2) {
+      const bool sw = s_orig[k + 1] < s_orig[k];
+      const uint32_t i0 = s_info[k], o0 = s_orig[k];
+      const uint64_t t0 = s_term[k], x0 = s_index[k];
+      s_info[k] = sw ? s_info[k + 1] : i0;
+      s_orig[k] = sw ? s_orig[k + 1] : o0;
+      s_term[k] = sw ? s_term[k + 1] : t0;
+      s_index[k] = sw ? s_index[k + 1] : x0;
+      s_info[k + 1] = sw ? i0 : s_info[k + 1];
+      s_orig[k + 1] = sw ? o0 : s_orig[k + 1];
+      s_term[k + 1] = sw ? t0 : s_term[k + 1];
+      s_index[k + 1] = sw ? x0 : s_index[k + 1];
+    }
+  }
   L.E.chunk = a.ev + moff;
   L.E.fill = &l_fill;
   uint32_t j = 0;  // messages consumed
+  if (live && cnt > KMAX && !flagged && !L.faulted()) {  // the slots hold an arbitrary KMAX: all to k_apply
+    flagged = true;
+    resume = 0;
+  }
   if (live) {
 #pragma unroll
     for (uint32_t k = 0; k < KMAX; ++k) {
@@ -750,10 +831,6 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
       L.accept(from, s_index[k]);
       st_msgs++;
       j++;
-    }
-    if (!flagged && !L.faulted() && cnt > KMAX) {  // more messages than slots: the rest in k_apply
-      flagged = true;
-      resume = j;
     }
   }
 
@@ -1166,6 +1243,12 @@ uint32_t ceil_log2(uint32_t x) {
   return b;
 }
 
+template <int KMAX>
+void launch_route(hb_handle* h, const ApplyArgs& a, hipStream_t st) {
+  const uint32_t grid = ((h->NBK + 7) & ~7u) * RouteGeom<KMAX>::W;
+  hipLaunchKernelGGL(k_route<KMAX>, dim3(grid), dim3(ROUTE_THREADS), 0, st, a);
+}
+
 // XCD-aware grid (see block_part()): whole groups of 8 buckets x SIS partitions.
 uint32_t apply_grid(const hb_handle* h) { return ((h->NBK + 7) & ~7u) * SIS; }
 
@@ -1530,6 +1613,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.ev_per_msg = h->ev_per_msg;
   aa.props_on = bd.props ? 1u : 0u;
   aa.NB = NB;
+  aa.NBK = h->NBK;
   aa.ev_counts = ps.ev_counts;
   aa.ev_off = ps.ev_off;
   aa.stats_shard = h->stats_shard;
@@ -1542,7 +1626,11 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.slot_orig = ps.slot_orig;
   aa.slot_term = ps.slot_term;
   aa.slot_index = ps.slot_index;
-  hipLaunchKernelGGL(k_route, dim3(apply_grid(h)), dim3(PART), 0, ps_st, aa);
+  switch (h->nmax) {
+    case 3: launch_route<2>(h, aa, ps_st); break;
+    case 5: launch_route<4>(h, aa, ps_st); break;
+    default: launch_route<6>(h, aa, ps_st); break;
+  }
   if (prof) HB_CHECK(hipEventRecord(ev[1], ps_st));
   if (two) {
     HB_CHECK(hipEventRecord(ps.prepped, ps_st));
