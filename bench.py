@@ -37,10 +37,12 @@ def alg_bytes_per_group(n):
 
 def cpu_baseline(n, groups=200_000, budget_s=10.0, max_steps=40):
     """The C oracle (a sequential restatement of the reference loop) on a bounded
-    sample of the same workload, one host core.  Test infrastructure only."""
+    sample of the same workload, one host core: the reference MultiNode steps
+    every group on its single `run` goroutine (raft/multinode.go:166).  Test
+    infrastructure only."""
     from etcd_amd import abi, synth
     from oracle.pyoracle import OracleGroups
-    g, runs = synth.steady_groups(groups, n, seed=0x5EED0002, with_runs=True)
+    g, runs = synth.steady_groups(groups, n, seed=0x5EED0002, with_runs="flat")
     og = OracleGroups(g, runs, 256)
     acks = commits = 0
     spent = 0.0
@@ -56,7 +58,51 @@ def cpu_baseline(n, groups=200_000, budget_s=10.0, max_steps=40):
     return {"value": acks / spent, "unit": "MsgAppResp/s", "cores": 1, "kind": "port",
             "commits_per_s": commits / spent,
             "sample": f"oracle/raft_oracle.c (C restatement of the reference loop, not the Go reference), "
-                      f"{groups} groups x {n}, {steps} cfg2 steps, {acks} MsgAppResp in {spent:.2f} s"}
+                      f"{groups} groups x {n}, {steps} cfg2 steps, {acks} MsgAppResp in {spent:.2f} s, one core"}
+
+
+def cpu_baseline_parallel(n, threads, groups_per_thread=65_536, budget_s=8.0, max_steps=20):
+    """Best case for the CPU: `threads` independent oracle shards (as many
+    MultiNodes as cores, groups partitioned), stepped concurrently from Python
+    threads (each orc_step_batch call releases the GIL).  Test infrastructure only."""
+    import threading
+    from etcd_amd import abi, synth
+    from oracle.pyoracle import OracleGroups, flat_runs
+    G = threads * groups_per_thread
+    g, runs = synth.steady_groups(G, n, seed=0x5EED0002, with_runs="flat")
+    flat, off = flat_runs(runs)
+    shards = []
+    for t in range(threads):
+        a, b = t * groups_per_thread, (t + 1) * groups_per_thread
+        shards.append(OracleGroups(g[a:b], (flat[int(off[a]):int(off[b])], off[a:b + 1] - off[a]), 256))
+    acks = 0
+    spent = 0.0
+    steps = 0
+    while spent < budget_s and steps < max_steps:
+        bt = synth.cfg2_batch(g, steps)
+        sh = bt["group"] // groups_per_thread
+        local = []
+        for t in range(threads):
+            m = sh == t
+            local.append(dict(group=(bt["group"][m] - t * groups_per_thread).astype(np.uint32), info=bt["info"][m],
+                              term=bt["term"][m], index=bt["index"][m], hint=None,
+                              props=bt["props"][t * groups_per_thread:(t + 1) * groups_per_thread]))
+        out = [None] * threads
+
+        def run(t):
+            out[t] = shards[t].step(local[t])[1]
+        th = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+        t0 = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        spent += time.perf_counter() - t0
+        acks += sum(int(o[abi.HB_STAT_APPRESP]) for o in out)
+        steps += 1
+    return {"value": acks / spent, "unit": "MsgAppResp/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} oracle shards x {groups_per_thread} groups x {n} stepped concurrently, "
+                      f"{steps} cfg2 steps, {acks} MsgAppResp in {spent:.2f} s"}
 
 
 def pmc_traffic(path, kernel, G, n, apply_us):
@@ -94,6 +140,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-groups", type=int, default=200_000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
+                    help="shards of the parallel best-case CPU baseline (the GPU box's share is 16 cores)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-phase HIP events")
     ap.add_argument("--overlap", action="store_true",
                     help="batch inputs on their own stream: the prep stage of step k+1 (bucket sort + routing) "
@@ -277,6 +325,11 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(n, args.cpu_groups, args.cpu_seconds)
             except Exception as e:  # report, never fake
                 out["cpu_baseline"] = {"error": repr(e)}
+            if args.cpu_threads > 1:
+                try:
+                    out["cpu_baseline"]["best_case_parallel"] = cpu_baseline_parallel(n, args.cpu_threads)
+                except Exception as e:
+                    out["cpu_baseline"]["best_case_parallel"] = {"error": repr(e)}
         print(json.dumps(out))
 
 

@@ -419,7 +419,9 @@ class OracleGroups:
         b.n = n
         if ev_cap is None:
             ev_cap = (n + self.G) * (abi.HB_MAX_REPLICAS + 6) + 64
-        ev = np.zeros(ev_cap, dtype=abi.EVENT_DTYPE)
+        if getattr(self, "_ev", None) is None or len(self._ev) < ev_cap:
+            self._ev = np.empty(ev_cap, dtype=abi.EVENT_DTYPE)  # reused: the oracle writes what it reports
+        ev = self._ev
         nev = C.c_uint64()
         stats = (C.c_uint64 * abi.HB_STAT_COUNT)()
         rc = L.orc_step_batch(self.ptr, self.G, C.byref(b), ev.ctypes.data, ev_cap, C.byref(nev), stats)
