@@ -196,8 +196,9 @@ def main():
     d_props = torch.from_numpy(batch["props"].view(np.int32)).to(dev)
     base_index = torch.from_numpy(batch["index"].view(np.int64)).to(dev)  # last + 1
     total = args.warmup + args.steps
+    n_iso = 0 if args.no_profile else 10  # steps of the separate per-phase pass after the timed region
     # step k acks index last + k + 1 (prepared before timing: inputs resident in HBM)
-    d_index = [base_index + k for k in range(total)]
+    d_index = [base_index + k for k in range(total + n_iso)]
     stats_step = torch.zeros(abi.HB_STAT_COUNT, dtype=torch.int64, device=dev)
     stats_acc = torch.zeros(abi.HB_STAT_COUNT, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
@@ -259,8 +260,8 @@ def main():
         eng.set_stats_accum(None)
         eng.set_input_stream(stream)
         eng.phase_reset()
-        for k in range(min(10, total)):
-            one_step(k % total, True)
+        for k in range(total, total + n_iso):  # the cfg2 stream continues (fresh indices)
+            one_step(k, True)
         torch.cuda.synchronize()
         ph2, nph2 = eng.phase_ms()
         phase = {"apply_ms": apply_ms, "apply_steps": nph,

@@ -29,6 +29,7 @@ def main():
          for k in ("group", "info", "term", "index", "props")}
     for k in range(6):
         eng.step(d["group"], d["info"], d["term"], d["index"] + k, None, d["props"], host=False)
+        torch.cuda.synchronize()
     torch.cuda.synchronize()
     NB = G // 256
     out = np.zeros(NB * 8, dtype=np.uint64)
@@ -36,8 +37,8 @@ def main():
     L.hb_x_stamps.argtypes = [C.c_void_p, C.c_uint32]
     assert L.hb_x_stamps(out.ctypes.data, NB * 8) == 0
     st = out.reshape(NB, 8).astype(np.int64)
-    names = ["keys+state+scan", "alloc+prop", "gather+sort", "steps", "store+stats"]
-    cols = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5)]
+    names = ["loads landed", "proposal", "messages", "store+stats"]
+    cols = [(0, 1), (1, 2), (2, 3), (3, 5)]
     print("phase cycles per workgroup (median / p10 / p90):")
     for nm, (a, b) in zip(names, cols):
         dd = st[:, b] - st[:, a]
