@@ -12,6 +12,11 @@ step statistics.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
+
+--workload cfg3 / cfg4 runs the other SURVEY.md 8(d) streams (auxiliary lines,
+not the headline metric): cfg3 = 1M x 5 lagging followers (open-loop stream
+generated from the engine's state between steps, each step timed by HIP
+events), cfg4 = 4M x 7 election storm (MsgVoteResp tallied/s).
 """
 import argparse
 import json
@@ -105,6 +110,55 @@ def cpu_baseline_parallel(n, threads, groups_per_thread=65_536, budget_s=8.0, ma
                       f"{steps} cfg2 steps, {acks} MsgAppResp in {spent:.2f} s"}
 
 
+def cpu_baseline_cfg4(n, groups=40_000, W=256, budget_s=10.0, max_steps=20):
+    """The C oracle on a bounded sample of the repeatable cfg4 storm, one core."""
+    from etcd_amd import abi, synth
+    from oracle.pyoracle import OracleGroups
+    g, runs = synth.election_groups(groups, n, seed=0x5EED0004)
+    og = OracleGroups(g, runs, W)
+    b = synth.cfg4_storm_batch(g, seed=0x5EED0004)
+    votes = decided = 0
+    spent = 0.0
+    steps = 0
+    while spent < budget_s and steps < max_steps:
+        bk = dict(b, term=synth.storm_terms(b["term"], steps))
+        t0 = time.perf_counter()
+        _, st = og.step(bk)
+        spent += time.perf_counter() - t0
+        votes += int(st[abi.HB_STAT_VOTERESP])
+        decided += int(st[abi.HB_STAT_WON]) + int(st[abi.HB_STAT_LOST])
+        steps += 1
+    return {"value": votes / spent, "unit": "MsgVoteResp/s", "cores": 1, "kind": "port",
+            "elections_decided_per_s": decided / spent,
+            "sample": f"oracle/raft_oracle.c (C restatement, not the Go reference), {groups} groups x {n}, "
+                      f"{steps} storm steps, {votes} MsgVoteResp in {spent:.2f} s, one core"}
+
+
+def cpu_baseline_cfg3(n, groups=60_000, W=256, budget_s=10.0, max_steps=20):
+    """The C oracle on a bounded sample of the open-loop cfg3 stream, one core
+    (stream generation from the oracle's state between steps is not timed)."""
+    from etcd_amd import abi, synth
+    from oracle.pyoracle import OracleGroups
+    g, runs = synth.lagging_groups(groups, n, seed=0x5EED0003, W=W)
+    og = OracleGroups(g, runs, W)
+    rng = np.random.default_rng(0x5EED0003)
+    acks = msgs = 0
+    spent = 0.0
+    steps = 0
+    while spent < budget_s and steps < max_steps:
+        b = synth.cfg3_open_batch(og.groups(), rng)
+        t0 = time.perf_counter()
+        _, st = og.step(b)
+        spent += time.perf_counter() - t0
+        acks += int(st[abi.HB_STAT_APPRESP])
+        msgs += int(st[abi.HB_STAT_MSGS])
+        steps += 1
+    return {"value": acks / spent, "unit": "MsgAppResp/s", "cores": 1, "kind": "port",
+            "msgs_per_s": msgs / spent,
+            "sample": f"oracle/raft_oracle.c (C restatement, not the Go reference), {groups} groups x {n} (W={W}), "
+                      f"{steps} cfg3 steps, {acks} MsgAppResp in {spent:.2f} s, one core"}
+
+
 def pmc_traffic(path, kernel, G, n, apply_us):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (FETCH_SIZE x 2 + WRITE_SIZE, tools/prof_summary.py).  Used only when the
@@ -135,8 +189,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--groups", type=int, default=1 << 20, help="groups per GPU (cfg2: 1M)")
-    ap.add_argument("--replicas", type=int, default=3)
+    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4"], default="cfg2",
+                    help="cfg2 (headline), cfg3 lagging followers, cfg4 election storm")
+    ap.add_argument("--groups", type=int, default=None, help="groups per GPU (cfg2/cfg3: 1M, cfg4: 4M)")
+    ap.add_argument("--replicas", type=int, default=None, help="cfg2: 3, cfg3: 5, cfg4: 7")
+    ap.add_argument("--inflight", type=int, default=256, help="MaxInflightMsgs W (cfg3/cfg4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-groups", type=int, default=200_000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -149,6 +206,10 @@ def main():
     ap.add_argument("--traffic-json", default=None,
                     help="profiles/<tag>_traffic.json from tools/profile_round.sh (default: newest in profiles/)")
     args = ap.parse_args()
+    if args.groups is None:
+        args.groups = (1 << 22) if args.workload == "cfg4" else (1 << 20)
+    if args.replicas is None:
+        args.replicas = {"cfg2": 3, "cfg3": 5, "cfg4": 7}[args.workload]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -165,6 +226,9 @@ def main():
     from etcd_amd import abi, synth
     from etcd_amd.hipbatch import Engine
     from etcd_amd.shard import ShardMap
+
+    if args.workload != "cfg2":
+        return run_aux(args, world, rank, local, dev, torch, dist)
 
     n = args.replicas
     # ---- this rank's shard of the global groups (weak scaling: ~groups per GPU)
@@ -331,6 +395,108 @@ def main():
                     out["cpu_baseline"]["best_case_parallel"] = cpu_baseline_parallel(n, args.cpu_threads)
                 except Exception as e:
                     out["cpu_baseline"]["best_case_parallel"] = {"error": repr(e)}
+        print(json.dumps(out))
+
+
+def run_aux(args, world, rank, local, dev, torch, dist):
+    """cfg3 / cfg4 lines; same JSON shape as the cfg2 line."""
+    from etcd_amd import abi, synth
+    from etcd_amd.hipbatch import Engine
+    n, W, G = args.replicas, args.inflight, args.groups
+    seed = {"cfg3": 0x5EED0003, "cfg4": 0x5EED0004}[args.workload] + rank
+    stream = torch.cuda.current_stream(dev)
+    total = args.warmup + args.steps
+    st_acc = np.zeros(abi.HB_STAT_COUNT, np.uint64)
+    ms_local = 0.0
+    t_wall = time.perf_counter()
+    if args.workload == "cfg4":
+        g, _ = synth.election_groups(G, n, seed=seed, with_runs=False)
+        b = synth.cfg4_storm_batch(g, seed=seed)
+        nmsg = len(b["group"])
+        eng = Engine(G, max_replicas=n, max_inflight=W, max_batch=nmsg, device=local, stream=stream)
+        eng.load_groups(g)
+        del g
+        d_group = torch.from_numpy(b["group"].view(np.int32)).to(dev)
+        d_info = torch.from_numpy(b["info"].view(np.int32)).to(dev)
+        d_index = torch.from_numpy(b["index"].view(np.int64)).to(dev)
+        t0 = torch.from_numpy(b["term"].view(np.int64)).to(dev)
+        nz = (t0 != 0).to(torch.int64)
+        d_terms = [t0 + nz * (4 * k) for k in range(total)]  # storm_terms(term, k), resident before timing
+        stats = torch.zeros(abi.HB_STAT_COUNT, dtype=torch.int64, device=dev)
+        for k in range(args.warmup):
+            eng.step(d_group, d_info, d_terms[k], d_index, None, None, host=False)
+        eng.set_stats_accum(stats)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for k in range(args.warmup, total):
+            eng.step(d_group, d_info, d_terms[k], d_index, None, None, host=False)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms_local = e0.elapsed_time(e1)
+        st_acc = stats.cpu().numpy().astype(np.uint64)
+        timing = "K steps back to back, inputs resident in HBM"
+    else:
+        g, _ = synth.lagging_groups(G, n, seed=seed, W=W)
+        eng = Engine(G, max_replicas=n, max_inflight=W, max_batch=2 * G * n + G, device=local, stream=stream)
+        eng.load_groups(g)
+        rng = np.random.default_rng(seed)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for k in range(total):
+            now = eng.get_groups()  # the stream is generated from the engine's state (untimed)
+            b = synth.cfg3_open_batch(now, rng)
+            del now
+            d = [torch.from_numpy(b[f].view(np.int32 if b[f].dtype == np.uint32 else np.int64)).to(dev)
+                 for f in ("group", "info", "term", "index", "hint", "props")]
+            torch.cuda.synchronize()
+            e0.record(stream)
+            eng.step(*d, host=False)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if k >= args.warmup:
+                ms_local += e0.elapsed_time(e1)
+                st_acc += eng.stats()
+        timing = "sum of per-step HIP event times (stream generation from the engine state between steps excluded)"
+    ms_t = torch.tensor([ms_local], dtype=torch.float64, device=dev)
+    st_t = torch.from_numpy(st_acc.view(np.int64).copy()).to(dev)
+    if world > 1:
+        dist.all_reduce(ms_t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(st_t)
+    ms = float(ms_t.item())
+    st = st_t.cpu().numpy().view(np.uint64)
+    sec = ms / 1e3
+    if args.workload == "cfg4":
+        metric, unit, val = "MsgVoteResp tallied/sec + elections decided/sec (cfg4 election storm)", "MsgVoteResp/s", \
+            int(st[abi.HB_STAT_VOTERESP]) / sec
+        extra = {"elections_decided_per_s": (int(st[abi.HB_STAT_WON]) + int(st[abi.HB_STAT_LOST])) / sec,
+                 "elections_won": int(st[abi.HB_STAT_WON]), "elections_lost": int(st[abi.HB_STAT_LOST])}
+        ok = int(st[abi.HB_STAT_VOTERESP]) == world * G * (n - 1) * args.steps and int(st[abi.HB_STAT_FAULTS]) == 0
+        wl = f"cfg4: {G} raft groups x {n} per GPU, election storm (step-down, MsgHup, {n - 1} MsgVoteResp per group)"
+        data = "synthetic (seeded cfg4 storm replayed at +4 terms per step)"
+    else:
+        metric, unit, val = "MsgAppResp applied/sec (cfg3 lagging followers)", "MsgAppResp/s", \
+            int(st[abi.HB_STAT_APPRESP]) / sec
+        extra = {"msgs_per_s": int(st[abi.HB_STAT_MSGS]) / sec, "commits_per_s": int(st[abi.HB_STAT_COMMITS]) / sec}
+        ok = int(st[abi.HB_STAT_FAULTS]) == 0
+        wl = f"cfg3: {G} raft groups x {n} per GPU, lagging followers (W={W})"
+        data = "synthetic (seeded open-loop cfg3 stream generated from the engine state each step)"
+    out = {"metric": metric, "value": val, "unit": unit, "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": ms / args.steps, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u64", "data": data,
+           "config": {"workload": wl, "groups_per_gpu": G, "replicas": n, "max_inflight": W},
+           "stats": {nm: int(v) for nm, v in zip(abi.STAT_NAMES, st.tolist())}, "timing": timing,
+           "parity_sanity": bool(ok), "wall_s": time.perf_counter() - t_wall, "cpu_baseline": None, **extra}
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = (cpu_baseline_cfg4 if args.workload == "cfg4" else cpu_baseline_cfg3)(n, W=W)
+            except Exception as e:  # report, never fake
+                out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out))
 
 

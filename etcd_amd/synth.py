@@ -8,8 +8,12 @@ sees only the current-term run.
   steady_groups / cfg2_batch    cfg2: 1M x 3 steady-state replication
   random_groups / random_batch  fuzz: every device message type and state
   election_groups / cfg4_batch  cfg4: election storm (MsgHup + MsgVoteResp)
+  cfg4_storm_batch              cfg4, repeatable: every step first steps each
+                                group down (higher term), then the storm
   FollowerSim                   cfg3: closed-loop lagging followers driven by
                                 the leader's MsgApp events
+  cfg3_open_batch               cfg3, open loop from the engine's current state
+                                (vectorized, for the 1M x 5 bench)
 """
 import numpy as np
 
@@ -203,7 +207,7 @@ def random_batch(groups, nmsg, seed=2, nonmember=0.04, props=True):
 
 
 # ---------------------------------------------------------------------------- cfg4
-def election_groups(G, n=7, seed=0x5EED0004, term_hi=1000):
+def election_groups(G, n=7, seed=0x5EED0004, term_hi=1000, with_runs=True):
     """All groups follower at term T ~ U[1, term_hi], no leader, fresh progress."""
     rng = np.random.default_rng(seed)
     g = np.zeros(G, dtype=A.GROUP_DTYPE)
@@ -216,7 +220,9 @@ def election_groups(G, n=7, seed=0x5EED0004, term_hi=1000):
     for s in range(n):
         g["pr"][:, s]["match"] = last if s == 0 else 0
         g["pr"][:, s]["next"] = last + np.uint64(1)
-    runs = [[(0, 0), (1, max(int(term[i]) - 1, 0))] if term[i] > 1 else [(0, 0)] for i in range(G)]
+    runs = None
+    if with_runs:
+        runs = [[(0, 0), (1, max(int(term[i]) - 1, 0))] if term[i] > 1 else [(0, 0)] for i in range(G)]
     return g, runs
 
 
@@ -242,6 +248,44 @@ def cfg4_batch(groups, seed=0x5EED0004, grant_p=0.5, higher_p=0.05):
     term = np.concatenate([np.zeros(G, np.uint64), vterm])
     index = np.zeros(len(grp), np.uint64)
     return dict(group=grp, info=info.astype(np.uint32), term=term, index=index, hint=None, props=None)
+
+
+def cfg4_storm_batch(groups, seed=0x5EED0004, grant_p=0.5, higher_p=0.05):
+    """Repeatable cfg4 step.  Per group, in arrival order: one MsgHeartbeatResp
+    from slot 1 at Term+1 (term gate: every group, whatever it became in the last
+    storm, steps down to follower, raft/raft.go:474-477), MsgHup (campaign at
+    Term+2), then n-1 MsgVoteResp at Term+2 in random order (granted with p =
+    grant_p; a fraction at Term+3 steps the candidate down, lead = From).
+
+    Terms are relative to groups["term"] = T.  Step k of a bench run adds 4k to
+    every nonzero term (the largest term a group reaches in a step is T+3), so
+    the same arrays replay as a fresh storm each step."""
+    rng = np.random.default_rng(seed)
+    G = len(groups)
+    n = int(groups["n"][0])
+    nv = n - 1
+    t0 = groups["term"].astype(np.uint64)
+    down_g = rng.permutation(G).astype(np.uint32)
+    hup_g = rng.permutation(G).astype(np.uint32)
+    vg = np.repeat(np.arange(G, dtype=np.uint32), nv)
+    vs = np.tile(np.arange(1, n, dtype=np.uint32), G)
+    perm = rng.permutation(G * nv)
+    vg, vs = vg[perm], vs[perm]
+    rej = (rng.random(G * nv) >= grant_p).astype(np.uint32)
+    vterm = t0[vg] + np.uint64(2)
+    vterm[rng.random(G * nv) < higher_p] += np.uint64(1)
+    grp = np.concatenate([down_g, hup_g, vg])
+    info = np.concatenate([np.full(G, A.HB_MSG_HEARTBEAT_RESP | (1 << 4), np.uint32),
+                           np.full(G, A.HB_MSG_HUP, np.uint32),
+                           (np.uint32(A.HB_MSG_VOTE_RESP) | (vs << np.uint32(4)) | (rej << np.uint32(8)))])
+    term = np.concatenate([t0[down_g] + np.uint64(1), np.zeros(G, np.uint64), vterm])
+    index = np.zeros(len(grp), np.uint64)
+    return dict(group=grp, info=info.astype(np.uint32), term=term, index=index, hint=None, props=None)
+
+
+def storm_terms(term, k):
+    """cfg4_storm_batch terms for step k: +4k on every nonzero (non-local) term."""
+    return np.where(term == 0, term, term + np.uint64(4 * k)).astype(np.uint64)
 
 
 # ---------------------------------------------------------------------------- cfg3
@@ -323,3 +367,52 @@ def lagging_groups(G, n=5, seed=0x5EED0003, W=8):
     q = n // 2 + 1
     g["committed"] = np.minimum(mt[:, q - 1], g["committed"])
     return g, runs
+
+
+def cfg3_open_batch(groups_now, rng, lag_p=0.2, stale_p=0.05, reject_p=0.05, hb_p=0.1, unreach_p=0.001,
+                    max_props=4):
+    """One cfg3 step generated open loop from the engine's current group state
+    (SURVEY.md 8(d) cfg3): 1-4 proposed entries per group (dense props), then
+    per follower one MsgAppResp -- 70 % acking the new last index, 20 % lagging
+    (last - U[1, 64]), 5 % stale (<= Match), 5 % rejecting (Index = Next - 1,
+    RejectHint = a follower last index >= Match) -- plus MsgHeartbeatResp from
+    10 % of the followers and MsgUnreachable for 0.1 %, all in one random
+    permutation at the leader's term.  Any stream is valid input (the engine
+    applies the reference semantics to whatever arrives); this one keeps the
+    followers in the Probe/Replicate/pause mix the workload is meant to hit."""
+    G = len(groups_now)
+    n = groups_now["n"].astype(np.int64)
+    nmax = int(n.max())
+    selfs = groups_now["self_slot"].astype(np.int64)
+    term = groups_now["term"].astype(np.uint64)
+    lead = groups_now["state"] == A.HB_STATE_LEADER
+    props = np.where(lead, rng.integers(1, max_props + 1, G), 0).astype(np.uint32)
+    last = groups_now["last_index"].astype(np.int64) + props.astype(np.int64)
+    gs, ss = np.meshgrid(np.arange(G, dtype=np.int64), np.arange(nmax, dtype=np.int64), indexing="ij")
+    fol = (ss < n[:, None]) & (ss != selfs[:, None]) & lead[:, None]
+    g, s = gs[fol], ss[fol]
+    match = groups_now["pr"]["match"][g, s].astype(np.int64)
+    nxt = groups_now["pr"]["next"][g, s].astype(np.int64)
+    L = last[g]
+    r = rng.random(len(g))
+    idx = L.copy()
+    lagm = r < lag_p
+    idx[lagm] = np.maximum(L[lagm] - rng.integers(1, 65, int(lagm.sum())), 0)
+    stm = (r >= lag_p) & (r < lag_p + stale_p)
+    idx[stm] = np.maximum(match[stm] - rng.integers(0, 4, int(stm.sum())), 0)
+    rjm = (r >= lag_p + stale_p) & (r < lag_p + stale_p + reject_p)
+    idx[rjm] = np.maximum(nxt[rjm] - 1, 0)
+    hint = np.zeros(len(g), np.int64)
+    hint[rjm] = np.minimum(match[rjm] + rng.integers(0, 8, int(rjm.sum())), L[rjm])
+    info = (A.HB_MSG_APP_RESP | (s << 4) | (rjm.astype(np.int64) << 8))
+    hbm = rng.random(len(g)) < hb_p
+    urm = rng.random(len(g)) < unreach_p
+    mg = np.concatenate([g, g[hbm], g[urm]])
+    mi = np.concatenate([info, A.HB_MSG_HEARTBEAT_RESP | (s[hbm] << 4), A.HB_MSG_UNREACHABLE | (s[urm] << 4)])
+    mt = np.concatenate([term[g], term[g[hbm]], np.zeros(int(urm.sum()), np.uint64)])
+    mx = np.concatenate([idx, np.zeros(int(hbm.sum()) + int(urm.sum()), np.int64)])
+    mh = np.concatenate([hint, np.zeros(int(hbm.sum()) + int(urm.sum()), np.int64)])
+    order = rng.permutation(len(mg))
+    return dict(group=mg[order].astype(np.uint32), info=mi[order].astype(np.uint32),
+                term=mt[order].astype(np.uint64), index=mx[order].astype(np.uint64),
+                hint=mh[order].astype(np.uint64), props=props)

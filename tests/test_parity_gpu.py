@@ -174,3 +174,29 @@ def test_pipelined_steps_with_input_stream():
     assert np.array_equal(acc.cpu().numpy().astype(np.uint64), ora_sum)
     from .parity_util import assert_groups_equal
     assert_groups_equal(eng.get_groups(), og.groups(), "pipelined")
+
+
+def test_cfg4_storm_repeatable_stream():
+    """The bench's repeatable cfg4 storm: step-down, campaign, n-1 votes, replayed
+    at +4 terms per step on the state the previous storm left."""
+    G = 2500
+    g, runs = synth.election_groups(G, 7, seed=21)
+    pair = Pair(g, runs, 7, 64, max_batch=8 * G)
+    b = synth.cfg4_storm_batch(g, seed=22)
+    for k in range(3):
+        _, st, _ = pair.step(dict(b, term=synth.storm_terms(b["term"], k)), ctx=f"storm {k}")
+        assert st[abi.HB_STAT_VOTERESP] == G * 6 and st[abi.HB_STAT_WON] > 0
+
+
+@pytest.mark.parametrize("W", [8, 256])
+def test_cfg3_open_loop_stream(W):
+    """The bench's open-loop cfg3 stream (lagging / stale / rejecting acks,
+    heartbeats, unreachable, 1-4 entries per group) from the engine's own state."""
+    G = 4000
+    g, runs = synth.lagging_groups(G, 5, seed=0x5EED0003, W=W)
+    pair = Pair(g, runs, 5, W, max_batch=8 * G)
+    rng = np.random.default_rng(23)
+    now = pair.og.groups()
+    for k in range(5):
+        _, st, now = pair.step(synth.cfg3_open_batch(now, rng), ctx=f"cfg3 open {k}")
+        assert st[abi.HB_STAT_FAULTS] == 0
