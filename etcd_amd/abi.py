@@ -62,6 +62,7 @@ HB_FAULT_NIL_PROGRESS = 5
 HB_FAULT_COMMIT_RANGE = 6
 HB_FAULT_NO_SELF = 7
 HB_FAULT_FOLLOWER_LEADER = 8
+HB_FAULT_RAND_EXHAUSTED = 9
 
 HB_EV_TERM = 1
 HB_EV_STATE = 2
@@ -146,6 +147,16 @@ class hb_event(C.Structure):
     ]
 
 
+class hb_timer(C.Structure):
+    _fields_ = [
+        ("elapsed", C.c_uint32),
+        ("rand_pos", C.c_uint32),
+        ("election_tick", C.c_uint16),
+        ("heartbeat_tick", C.c_uint16),
+        ("pad", C.c_uint32),
+    ]
+
+
 class hb_batch(C.Structure):
     _fields_ = [
         ("n", C.c_uint64),
@@ -170,8 +181,11 @@ GROUP_DTYPE = np.dtype([
     ("votes_resp", "<u4"), ("votes_grant", "<u4"), ("fault", "<u4"),
     ("pr", PROGRESS_DTYPE, (HB_MAX_REPLICAS,)),
 ])
+TIMER_DTYPE = np.dtype([("elapsed", "<u4"), ("rand_pos", "<u4"), ("election_tick", "<u2"),
+                        ("heartbeat_tick", "<u2"), ("pad", "<u4")])
 EVENT_DTYPE = np.dtype([("x", "<u8"), ("group", "<u4"), ("type", "u1"), ("to", "u1"), ("aux", "<u2")])
 
 assert GROUP_DTYPE.itemsize == C.sizeof(hb_group)
 assert EVENT_DTYPE.itemsize == C.sizeof(hb_event) == 16
+assert TIMER_DTYPE.itemsize == C.sizeof(hb_timer) == 16
 assert PROGRESS_DTYPE.itemsize == C.sizeof(hb_progress)

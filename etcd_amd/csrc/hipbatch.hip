@@ -961,6 +961,104 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
   if (tid == 0) a.ev_counts[2 * part + 1] = l_fill;
 }
 
+// ---------------------------------------------------------------------------
+// k_tick: one MultiNode.Tick (raft/multinode.go:264-275) — every live group
+// runs tickHeartbeat (leader) or tickElection (raft/raft.go:362-382), the
+// draw of isElectionTimeout (:765-771) read from the node's r.rand stream at
+// the group's own position; a due MsgBeat / MsgHup is stepped at once by the
+// general state machine.  Events go to the partition's P chunk (at most one
+// step per group, so the chunk's ev_per_msg x PART words bound them).
+// ---------------------------------------------------------------------------
+template <int NMAX>
+__global__ void __launch_bounds__(PART, 2) k_tick(ApplyArgs a) {
+  __shared__ uint32_t l_fill;
+  __shared__ uint64_t l_stats[ST_N + 1];
+  const uint32_t part = block_part();
+  if (part >= a.NB) return;  // uniform: grid padding
+  const uint32_t tid = threadIdx.x;
+  const uint32_t g = part * PART + tid;
+  if (tid == 0) l_fill = 0;
+  if (tid <= ST_N) l_stats[tid] = 0;
+  __syncthreads();
+
+  const uint64_t poff = (uint64_t)part * PART * a.ev_per_msg;
+  Lane<NMAX> L;
+  L.S = a.S;
+  L.E.chunk = a.ev + poff;
+  L.E.fill = &l_fill;
+  L.g = g;
+  L.won = 0;
+  L.lost = 0;
+  L.nev = 0;
+  L.dirty = 0;
+  L.meta = 0;
+  L.last = 0;
+  L.committed = 0;
+  L.arrival = 0xFFFFFFFFu;
+  uint32_t type = 0xFF;
+  bool live = false;
+  if (g < a.S.G) {
+    L.meta = a.S.meta[g];
+    live = L.n() != 0 && !L.faulted();
+  }
+  if (live) {
+    const uint32_t cfg = a.S.tcfg[g];
+    const uint32_t et = cfg & 0xFFFFu, ht = cfg >> 16;
+    uint32_t el = a.S.elapsed[g];
+    if (L.state() == HB_STATE_LEADER) {  // tickHeartbeat
+      if (++el >= ht) {
+        el = 0;
+        type = HB_MSG_BEAT;
+      }
+    } else if (L.self() == HB_SLOT_NONE) {  // tickElection: !promotable()
+      el = 0;
+    } else if (++el >= et) {  // isElectionTimeout: d = elapsed - et >= 0 takes a draw
+      const uint32_t pos = a.S.rpos[g];
+      if (pos >= a.S.nrnd) {
+        L.fault(HB_FAULT_RAND_EXHAUSTED);
+        L.dirty |= D_META;
+        L.ev(HB_EV_FAULT, 0, HB_FAULT_RAND_EXHAUSTED, HB_NO_INDEX);
+      } else {
+        a.S.rpos[g] = pos + 1;
+        if ((uint64_t)(el - et) > a.S.rnd[pos] % et) {
+          el = 0;
+          type = HB_MSG_HUP;
+        }
+      }
+    }
+    a.S.elapsed[g] = el;
+  }
+  uint64_t last0 = 0, commit0 = 0;
+  if (type != 0xFF) {
+    L.load_all();
+    last0 = L.last;
+    commit0 = L.committed;
+    L.step(type, L.self(), 0, 0, false, 0);
+  }
+  if (live && L.dirty) {
+    if (type == 0xFF) L.S.meta[g] = L.meta;  // the fault only
+    else L.store();
+  }
+  const bool stepped = type != 0xFF;
+  const uint64_t vals[ST_N + 1] = {(uint64_t)stepped,
+                                   0,
+                                   0,
+                                   0,
+                                   (uint64_t)(stepped && L.committed != commit0),
+                                   L.won,
+                                   L.lost,
+                                   (uint64_t)(live && L.faulted() != 0),
+                                   stepped ? L.last - last0 : 0ull,
+                                   L.nev};
+  reduce_stats(a, l_stats, vals);
+  if (tid == 0) {
+    a.ev_off[2 * part] = poff;
+    a.ev_off[2 * part + 1] = poff;
+    a.ev_counts[2 * part] = l_fill;
+    a.ev_counts[2 * part + 1] = 0;
+  }
+}
+
 // ============================================================================
 // Phase 3: finish
 // ============================================================================
@@ -996,6 +1094,8 @@ __global__ void k_load(DevState S, uint32_t first, uint32_t count, const hb_grou
   S.tlast[g] = r.term_last;
   S.snap[g] = r.snap_index;
   S.meta[g] = meta_make(r.state, r.n, r.self_slot, r.lead, r.vote, r.fault, r.votes_resp, r.votes_grant);
+  S.elapsed[g] = 0;  // newRaft: fresh r.rand, becomeFollower -> reset
+  S.rpos[g] = 0;
   for (uint32_t s = 0; s < S.nmax; ++s) {
     const bool on = s < r.n;
     const size_t o = (size_t)s * S.G + g;
@@ -1202,6 +1302,8 @@ struct hb_handle {
   uint32_t* pflag = nullptr;      // [NB][PART/32]
   uint32_t* resume = nullptr;     // [G]
   uint64_t* commit0 = nullptr;    // [G]
+  uint64_t* rnd = nullptr;        // the r.rand stream (hb_set_rand), grown on demand
+  uint64_t rnd_cap = 0;
   static constexpr uint32_t PROF_RING = 256;
   // per profiled step: prep start, prep end (prep stream), apply start, fast end,
   // general end, finish end (apply stream)
@@ -1319,6 +1421,9 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(s.pending, R * G);
   ALLOC(s.pm, R * G);
   ALLOC(s.ring, R * (size_t)max_inflight * G);
+  ALLOC(s.elapsed, G);
+  ALLOC(s.rpos, G);
+  ALLOC(s.tcfg, G);
   // partition scratch
   const size_t mb = max_batch ? max_batch : 1;
   h->NBK = (capacity + (1u << BK_LOG) - 1) >> BK_LOG;
@@ -1388,6 +1493,8 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   }
   // empty slots (n = 0), zeroed progress
   if (hipMemset(s.meta, 0, G * 8) != hipSuccess || hipMemset(s.pm, 0, R * G * 4) != hipSuccess ||
+      hipMemset(s.elapsed, 0, G * 4) != hipSuccess || hipMemset(s.rpos, 0, G * 4) != hipSuccess ||
+      hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(s.tcfg), 10u | (1u << 16), G) != hipSuccess ||
       hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess || hipMemset(h->stats_shard, 0, 8 * 16 * 8) != hipSuccess ||
       hipMemset(h->set[0].ev_counts, 0, h->NB * 8ull) != hipSuccess ||
       hipMemset(h->set[0].ev_off, 0, h->NB * 16ull) != hipSuccess ||
@@ -1411,6 +1518,7 @@ int hb_destroy(hb_handle* h) {
     if (ps.prepped) (void)hipEventDestroy(ps.prepped);
     if (ps.applied) (void)hipEventDestroy(ps.applied);
   }
+  if (h->rnd) (void)hipFree(h->rnd);
   if (h->in_ready) (void)hipEventDestroy(h->in_ready);
   if (h->prep) (void)hipStreamDestroy(h->prep);
   delete h;
@@ -1502,6 +1610,102 @@ int hb_set_inflights(hb_handle* h, uint32_t group, uint32_t slot, uint32_t start
   }
   (void)hipFree(d);
   return e == hipSuccess ? HB_OK : HB_EDEVICE;
+}
+
+int hb_load_timers(hb_handle* h, uint32_t first, uint32_t count, const hb_timer* timers) {
+  if (!h || !timers || (uint64_t)first + count > h->G) return HB_EINVAL;
+  if (count == 0) return HB_OK;
+  std::vector<uint32_t> el(count), pos(count), cfg(count);
+  for (uint32_t i = 0; i < count; ++i) {
+    if (timers[i].election_tick == 0) return HB_EINVAL;  // r.rand.Int() % 0
+    el[i] = timers[i].elapsed;
+    pos[i] = timers[i].rand_pos;
+    cfg[i] = timers[i].election_tick | ((uint32_t)timers[i].heartbeat_tick << 16);
+  }
+  DeviceGuard guard(h->device);
+  HB_CHECK(hipMemcpyAsync(h->st.elapsed + first, el.data(), count * 4ull, hipMemcpyHostToDevice, h->stream));
+  HB_CHECK(hipMemcpyAsync(h->st.rpos + first, pos.data(), count * 4ull, hipMemcpyHostToDevice, h->stream));
+  HB_CHECK(hipMemcpyAsync(h->st.tcfg + first, cfg.data(), count * 4ull, hipMemcpyHostToDevice, h->stream));
+  HB_CHECK(hipStreamSynchronize(h->stream));
+  return HB_OK;
+}
+
+int hb_get_timers(hb_handle* h, uint32_t first, uint32_t count, hb_timer* out) {
+  if (!h || !out || (uint64_t)first + count > h->G) return HB_EINVAL;
+  if (count == 0) return HB_OK;
+  std::vector<uint32_t> el(count), pos(count), cfg(count);
+  DeviceGuard guard(h->device);
+  HB_CHECK(hipMemcpyAsync(el.data(), h->st.elapsed + first, count * 4ull, hipMemcpyDeviceToHost, h->stream));
+  HB_CHECK(hipMemcpyAsync(pos.data(), h->st.rpos + first, count * 4ull, hipMemcpyDeviceToHost, h->stream));
+  HB_CHECK(hipMemcpyAsync(cfg.data(), h->st.tcfg + first, count * 4ull, hipMemcpyDeviceToHost, h->stream));
+  HB_CHECK(hipStreamSynchronize(h->stream));
+  for (uint32_t i = 0; i < count; ++i) {
+    out[i] = hb_timer{};
+    out[i].elapsed = el[i];
+    out[i].rand_pos = pos[i];
+    out[i].election_tick = (uint16_t)(cfg[i] & 0xFFFFu);
+    out[i].heartbeat_tick = (uint16_t)(cfg[i] >> 16);
+  }
+  return HB_OK;
+}
+
+int hb_set_rand(hb_handle* h, uint64_t first, uint64_t count, const uint64_t* draws) {
+  if (!h || (count && !draws) || first > h->st.nrnd) return HB_EINVAL;  // no holes
+  const uint64_t need = first + count;
+  DeviceGuard guard(h->device);
+  if (need > h->rnd_cap) {
+    const uint64_t cap = need > 2 * h->rnd_cap ? need : 2 * h->rnd_cap;
+    uint64_t* p = nullptr;
+    HB_CHECK(hipMalloc(&p, cap * 8));
+    hipError_t e = hipSuccess;
+    if (h->rnd && first) e = hipMemcpyAsync(p, h->rnd, first * 8, hipMemcpyDeviceToDevice, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);  // no kernel reads the old table any more
+    if (e != hipSuccess) {
+      (void)hipFree(p);
+      return HB_EDEVICE;
+    }
+    if (h->rnd) (void)hipFree(h->rnd);
+    h->rnd = p;
+    h->rnd_cap = cap;
+  }
+  if (count) {
+    HB_CHECK(hipMemcpyAsync(h->rnd + first, draws, count * 8, hipMemcpyHostToDevice, h->stream));
+    HB_CHECK(hipStreamSynchronize(h->stream));
+  }
+  h->st.rnd = h->rnd;
+  if (need > h->st.nrnd) h->st.nrnd = need;
+  return HB_OK;
+}
+
+int hb_tick(hb_handle* h, uint32_t flags) {
+  if (!h || flags) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  hipStream_t st = h->stream;
+  const bool two = h->in_stream_set && h->in_stream != h->stream;
+  PrepSet& ps = h->set[h->next_set];
+  ApplyArgs aa{};
+  aa.S = h->st;
+  aa.ev = h->ev;
+  aa.ev_per_msg = h->ev_per_msg;
+  aa.NB = h->NB;
+  aa.NBK = h->NBK;
+  aa.ev_counts = ps.ev_counts;
+  aa.ev_off = ps.ev_off;
+  aa.stats_shard = h->stats_shard;
+  const uint32_t grid = apply_grid(h);
+  switch (h->nmax) {
+    case 3: hipLaunchKernelGGL(k_tick<3>, dim3(grid), dim3(PART), 0, st, aa); break;
+    case 5: hipLaunchKernelGGL(k_tick<5>, dim3(grid), dim3(PART), 0, st, aa); break;
+    default: hipLaunchKernelGGL(k_tick<7>, dim3(grid), dim3(PART), 0, st, aa); break;
+  }
+  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, h->stats_shard, h->stats, h->stats_accum);
+  if (two) HB_CHECK(hipEventRecord(ps.applied, st));  // a later prep reusing this set waits for it
+  HB_CHECK(hipGetLastError());
+  ps.used = true;
+  h->cur = h->next_set;
+  h->next_set ^= 1;
+  h->stepped = true;
+  return HB_OK;
 }
 
 int hb_get_inflights(hb_handle* h, uint32_t group, uint32_t slot, uint32_t* start, uint32_t* count,

@@ -78,6 +78,11 @@ struct DevState {
   uint64_t* pending;          // [nmax][G] PendingSnapshot (valid in Snapshot state)
   uint32_t* pm;               // [nmax][G] packed progress meta
   uint64_t* ring;             // [nmax][W][G] inflight ring
+  uint32_t* elapsed;          // [G] r.elapsed
+  uint32_t* rpos;             // [G] r.rand.Int() values taken so far
+  uint32_t* tcfg;             // [G] ElectionTick | HeartbeatTick << 16
+  const uint64_t* rnd;        // [nrnd] the node's r.rand.Int() stream (host supplied)
+  uint64_t nrnd;
 };
 
 // ---- event sink ---------------------------------------------------------------
@@ -154,6 +159,7 @@ constexpr uint32_t D_TERM = 1u << 1;
 constexpr uint32_t D_COMMIT = 1u << 2;
 constexpr uint32_t D_LAST = 1u << 3;
 constexpr uint32_t D_TRUN = 1u << 4;
+constexpr uint32_t D_ELAPSED = 1u << 5;  // reset zeroed r.elapsed
 constexpr uint32_t D_SLOT0 = 8;  // bit D_SLOT0 + s: slot s (match, next, pm)
 
 struct Pr {
@@ -282,6 +288,7 @@ struct Lane {
       S.tfirst[g] = tfirst;
       S.tlast[g] = tlast;
     }
+    if (dirty & D_ELAPSED) S.elapsed[g] = 0;
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) {
       if (dirty & (1u << (D_SLOT0 + s))) {
@@ -453,6 +460,7 @@ struct Lane {
       ev(HB_EV_TERM, 0, 0, t);
     }
     set_lead(HB_REF_NONE);
+    dirty |= D_ELAPSED;  // r.elapsed = 0
     set_votes(0, 0);
     const uint32_t nn = n(), sf = self();
 #pragma unroll

@@ -54,6 +54,10 @@ def lib():
         "hb_set_inflights": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
         "hb_get_inflights": (C.c_int, [H, C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32), C.c_void_p]),
         "hb_step": (C.c_int, [H, P(abi.hb_batch), C.c_uint32]),
+        "hb_load_timers": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
+        "hb_get_timers": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
+        "hb_set_rand": (C.c_int, [H, C.c_uint64, C.c_uint64, C.c_void_p]),
+        "hb_tick": (C.c_int, [H, C.c_uint32]),
         "hb_events_device": (C.c_int, [H, P(C.c_void_p), P(C.c_void_p), P(C.c_void_p), P(C.c_uint32)]),
         "hb_copy_events": (C.c_int, [H, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
         "hb_stats_device": (C.c_int, [H, P(C.c_void_p)]),
@@ -172,6 +176,26 @@ class Engine:
         flags = (abi.HB_STEP_HOST_PTRS if host else 0) | prof
         self._keep = (group, info, term, index, hint, props)
         _check("hb_step", lib().hb_step(self.h, C.byref(b), flags))
+
+    # ---- timers (MultiNode.Tick) ----------------------------------------------
+    def load_timers(self, timers, first=0):
+        t = np.ascontiguousarray(timers, dtype=abi.TIMER_DTYPE)
+        _check("hb_load_timers", lib().hb_load_timers(self.h, first, len(t), t.ctypes.data))
+
+    def get_timers(self, first=0, count=None):
+        count = self.capacity - first if count is None else count
+        out = np.zeros(count, dtype=abi.TIMER_DTYPE)
+        _check("hb_get_timers", lib().hb_get_timers(self.h, first, count, out.ctypes.data))
+        return out
+
+    def set_rand(self, draws, first=0):
+        """The node's r.rand.Int() stream (rand.New(rand.NewSource(id)))."""
+        d = np.ascontiguousarray(draws, dtype=np.uint64)
+        _check("hb_set_rand", lib().hb_set_rand(self.h, first, len(d), d.ctypes.data if len(d) else None))
+
+    def tick(self):
+        """One MultiNode.Tick over every group (asynchronous; events/stats as step)."""
+        _check("hb_tick", lib().hb_tick(self.h, 0))
 
     def step_batch(self, batch, **kw):
         return self.step(batch["group"], batch["info"], batch["term"], batch["index"],

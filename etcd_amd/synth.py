@@ -206,6 +206,19 @@ def random_batch(groups, nmsg, seed=2, nonmember=0.04, props=True):
     return dict(group=grp, info=info, term=term, index=index, hint=hint, props=pr)
 
 
+def random_timers(G, seed=1, et_hi=12, ht_hi=4, pos_hi=50):
+    """Per-group timers for tick parity: ElectionTick 1..et_hi, HeartbeatTick
+    1..ht_hi, elapsed anywhere in [0, 2 ElectionTick], rand positions spread."""
+    rng = np.random.default_rng(seed)
+    t = np.zeros(G, dtype=A.TIMER_DTYPE)
+    et = rng.integers(1, et_hi + 1, G)
+    t["election_tick"] = et
+    t["heartbeat_tick"] = rng.integers(1, ht_hi + 1, G)
+    t["elapsed"] = rng.integers(0, 2 * et + 1)
+    t["rand_pos"] = rng.integers(0, pos_hi + 1, G)
+    return t
+
+
 # ---------------------------------------------------------------------------- cfg4
 def election_groups(G, n=7, seed=0x5EED0004, term_hi=1000, with_runs=True):
     """All groups follower at term T ~ U[1, term_hi], no leader, fresh progress."""

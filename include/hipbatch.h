@@ -173,6 +173,8 @@ typedef struct hb_group {
 #define HB_FAULT_COMMIT_RANGE    6  /* "tocommit(%d) is out of range" raft/log.go:175-177       */
 #define HB_FAULT_NO_SELF         7  /* appendEntry with r.id not in prs (nil deref raft.go:358) */
 #define HB_FAULT_FOLLOWER_LEADER 8  /* "invalid transition [follower -> leader]" raft/raft.go:409 (oracle KATs only) */
+#define HB_FAULT_RAND_EXHAUSTED  9  /* engine-defined, no reference panic: hb_tick needed draw
+                                       rand_pos of the group but hb_set_rand supplied fewer */
 
 /* ---- events (the sparse delta list) ---------------------------------------
  * One ordered stream of 16-byte records per group describes everything the
@@ -287,6 +289,39 @@ int  hb_set_inflights(hb_handle* h, uint32_t group, uint32_t slot,
                       uint32_t start, uint32_t count, const uint64_t* vals);
 int  hb_get_inflights(hb_handle* h, uint32_t group, uint32_t slot,
                       uint32_t* start, uint32_t* count, uint64_t* vals /* [max_inflight] */);
+
+/* ---- timers (MultiNode.Tick) ---------------------------------------------
+ * Per group: r.elapsed, Config.ElectionTick / HeartbeatTick, and how many
+ * values the group's r.rand has produced.  Every group of a MultiNode owns a
+ * rand.Rand seeded with the same node id (raft/raft.go:189 with
+ * config.ID = mn.id, raft/multinode.go:182), so all groups read one stream,
+ * each at its own position.  The host supplies that stream (the outputs of
+ * rand.New(rand.NewSource(id)).Int(), in order) with hb_set_rand and keeps it
+ * longer than any group's rand_pos + 1 (one draw per group per tick at most).
+ * hb_create sets election_tick 10, heartbeat_tick 1 (the reference tests'
+ * defaults, raft/raft_test.go:1884-1894); hb_load_groups zeroes elapsed and
+ * rand_pos of the loaded groups (newRaft: fresh rand, becomeFollower -> reset).
+ * Follower-side receipts that reset r.elapsed (MsgApp / MsgHeartbeat /
+ * MsgSnap / granted MsgVote, raft/raft.go:625-640) are handled by the host;
+ * it reports them with hb_load_timers. */
+typedef struct hb_timer {
+  uint32_t elapsed;          /* r.elapsed */
+  uint32_t rand_pos;         /* r.rand.Int() values taken so far */
+  uint16_t election_tick;    /* r.electionTimeout (>= 1) */
+  uint16_t heartbeat_tick;   /* r.heartbeatTimeout */
+  uint32_t pad;
+} hb_timer;
+int  hb_load_timers(hb_handle* h, uint32_t first, uint32_t count, const hb_timer* timers);
+int  hb_get_timers(hb_handle* h, uint32_t first, uint32_t count, hb_timer* out);
+/* draws[i] = the (first + i)-th r.rand.Int() value (0 <= v < 2^63); the table
+ * grows to first + count, earlier entries are kept.  Host memory. */
+int  hb_set_rand(hb_handle* h, uint64_t first, uint64_t count, const uint64_t* draws);
+/* One MultiNode.Tick (raft/multinode.go:264-275): every live group ticks
+ * once, tickHeartbeat for leaders, tickElection otherwise (raft/raft.go:
+ * 362-382, isElectionTimeout :765-771); a due MsgBeat / MsgHup is stepped at
+ * once.  Events and statistics as for hb_step (the stepped MsgBeat / MsgHup
+ * count in HB_STAT_MSGS).  flags: 0. */
+int  hb_tick(hb_handle* h, uint32_t flags);
 
 /* ---- the hot path ----------------------------------------------------------
  * Step one batch (all messages of the batch, per group in arrival order).

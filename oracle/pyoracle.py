@@ -66,6 +66,7 @@ class orc_raft(C.Structure):
         ("log", orc_log), ("max_inflight", C.c_int), ("max_msg_size", C.c_uint64),
         ("n", C.c_int), ("ids", C.c_uint64 * ORC_MAX_PEERS), ("prs_", orc_progress * ORC_MAX_PEERS),
         ("state", C.c_int), ("lead", C.c_uint64), ("pending_conf", C.c_int), ("elapsed", C.c_int),
+        ("election_timeout", C.c_int), ("heartbeat_timeout", C.c_int), ("rand_pos", C.c_uint64),
         ("nvotes", C.c_int), ("vote_ids", C.c_uint64 * (ORC_MAX_PEERS + 1)),
         ("vote_vals", C.c_int * (ORC_MAX_PEERS + 1)),
         ("msgs", C.POINTER(orc_msg)), ("nmsgs", C.c_int), ("msgs_cap", C.c_int),
@@ -136,6 +137,11 @@ def lib():
             "orc_groups_at": (R, [R, C.c_uint32]),
             "orc_groups_load": (C.c_int, [R, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_uint64]),
             "orc_groups_export": (None, [R, C.c_uint32, C.c_void_p]),
+            "orc_raft_tick": (C.c_int, [R, P(C.c_uint64), C.c_uint64]),
+            "orc_tick_batch": (C.c_int, [R, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                         P(C.c_uint64), P(C.c_uint64)]),
+            "orc_groups_load_timers": (None, [R, C.c_uint32, C.c_void_p]),
+            "orc_groups_export_timers": (None, [R, C.c_uint32, C.c_void_p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -230,9 +236,11 @@ class Raft:
     """
 
     def __init__(self, id, peers, ents=(), snapshot=None, hard=None, max_inflight=256,
-                 max_msg_size=NO_LIMIT):
+                 max_msg_size=NO_LIMIT, election=10, heartbeat=1, draws=()):
         L = lib()
         self.r = orc_raft()
+        # r.rand.Int() stream (rand.New(rand.NewSource(id)) in the reference): supplied
+        self.draws = np.ascontiguousarray(draws, dtype=np.uint64)
         if snapshot:
             L.orc_log_init(C.byref(self.r.log), snapshot[0] + 1, snapshot[1])
             self.r.log.snap_index = snapshot[0]
@@ -245,6 +253,7 @@ class Raft:
         L.orc_raft_init(C.byref(self.r), id, arr, len(peers), max_inflight, max_msg_size)
         if hard and any(hard):
             L.orc_raft_load_state(C.byref(self.r), *hard)
+        self.r.election_timeout, self.r.heartbeat_timeout = election, heartbeat
 
     def __del__(self):
         try:
@@ -314,6 +323,15 @@ class Raft:
         out = (orc_msg * max(1, n))()
         lib().orc_raft_read_messages(C.byref(self.r), out, n)
         return [out[i] for i in range(n)]
+
+    @property
+    def elapsed(self):
+        return self.r.elapsed
+
+    def tick(self):
+        """r.tick(): tickHeartbeat / tickElection with the supplied draw stream."""
+        d = self.draws
+        return lib().orc_raft_tick(C.byref(self.r), d.ctypes.data_as(C.POINTER(C.c_uint64)), len(d))
 
     def becomeFollower(self, term, lead):
         lib().orc_raft_become_follower(C.byref(self.r), term, lead)
@@ -428,6 +446,31 @@ class OracleGroups:
         if rc != 0:
             raise RuntimeError("oracle event buffer too small")
         return ev[: nev.value].copy(), np.array(stats[:], dtype=np.uint64)
+
+    def tick(self, draws, ev_cap=None):
+        """One MultiNode.Tick over all groups; draws = the r.rand.Int() stream."""
+        L = lib()
+        d = np.ascontiguousarray(draws, dtype=np.uint64)
+        if ev_cap is None:
+            ev_cap = self.G * (abi.HB_MAX_REPLICAS + 6) + 64
+        ev = np.empty(ev_cap, dtype=abi.EVENT_DTYPE)
+        nev = C.c_uint64()
+        stats = (C.c_uint64 * abi.HB_STAT_COUNT)()
+        rc = L.orc_tick_batch(self.ptr, self.G, d.ctypes.data if len(d) else None, len(d), ev.ctypes.data, ev_cap,
+                              C.byref(nev), stats)
+        if rc != 0:
+            raise RuntimeError("oracle event buffer too small")
+        return ev[: nev.value].copy(), np.array(stats[:], dtype=np.uint64)
+
+    def load_timers(self, timers):
+        t = np.ascontiguousarray(timers, dtype=abi.TIMER_DTYPE)
+        assert len(t) == self.G
+        lib().orc_groups_load_timers(self.ptr, self.G, t.ctypes.data)
+
+    def timers(self):
+        out = np.zeros(self.G, dtype=abi.TIMER_DTYPE)
+        lib().orc_groups_export_timers(self.ptr, self.G, out.ctypes.data)
+        return out
 
     def groups(self):
         out = np.zeros(self.G, dtype=abi.GROUP_DTYPE)

@@ -244,6 +244,8 @@ void orc_raft_init(orc_raft* r, uint64_t id, const uint64_t* peers, int npeers,
   r->id = id;
   r->max_inflight = max_inflight;
   r->max_msg_size = max_msg_size;
+  r->election_timeout = 10;                               /* engine defaults (hb_create) */
+  r->heartbeat_timeout = 1;
   r->n = 0;
   for (int i = 0; i < npeers && i < ORC_MAX_PEERS; i++) {
     r->ids[r->n] = peers[i];
@@ -686,6 +688,8 @@ int orc_raft_from_group(orc_raft* r, const hb_group* g, const orc_run* runs, int
   r->id = g->self_slot == HB_SLOT_NONE ? 100 : (uint64_t)g->self_slot + 1;
   r->max_inflight = max_inflight;
   r->max_msg_size = max_msg_size;
+  r->election_timeout = 10;
+  r->heartbeat_timeout = 1;
   r->term = g->term;
   r->commit = g->committed;
   r->vote = slot_id(g, g->vote);
@@ -780,6 +784,49 @@ static int is_response(int type) {                        /* IsResponseMsg raft/
          type == HB_MSG_HEARTBEAT_RESP || type == HB_MSG_UNREACHABLE;
 }
 
+/* per-batch bookkeeping shared by orc_step_batch and orc_tick_batch */
+typedef struct {
+  uint64_t *commit0, *last0;
+  int* fault0;
+  uint64_t won0, lost0;
+} batch_ctx;
+
+static void batch_begin(batch_ctx* c, orc_raft* groups, uint32_t ngroups, uint64_t stats[HB_STAT_COUNT]) {
+  memset(stats, 0, sizeof(uint64_t) * HB_STAT_COUNT);
+  c->commit0 = (uint64_t*)malloc(sizeof(uint64_t) * (ngroups ? ngroups : 1));
+  c->last0 = (uint64_t*)malloc(sizeof(uint64_t) * (ngroups ? ngroups : 1));
+  c->fault0 = (int*)malloc(sizeof(int) * (ngroups ? ngroups : 1));
+  c->won0 = c->lost0 = 0;
+  for (uint32_t g = 0; g < ngroups; g++) {
+    c->won0 += groups[g].n_won;
+    c->lost0 += groups[g].n_lost;
+    c->commit0[g] = groups[g].log.committed;
+    c->last0[g] = groups[g].log.last_index;
+    c->fault0[g] = groups[g].fault;
+    groups[g].group = g;
+  }
+}
+
+static void batch_end(batch_ctx* c, orc_raft* groups, uint32_t ngroups, uint64_t stats[HB_STAT_COUNT],
+                      uint64_t total) {
+  uint64_t won1 = 0, lost1 = 0;
+  for (uint32_t g = 0; g < ngroups; g++) {
+    orc_raft* r = &groups[g];
+    if (r->log.committed > c->commit0[g]) stats[HB_STAT_COMMITS]++;
+    if (r->fault && !c->fault0[g]) stats[HB_STAT_FAULTS]++;
+    stats[HB_STAT_ENTRIES] += r->log.last_index - c->last0[g];
+    r->nmsgs = 0;                                          /* msgs handed to the app via Ready */
+    won1 += r->n_won;
+    lost1 += r->n_lost;
+  }
+  stats[HB_STAT_WON] = won1 - c->won0;
+  stats[HB_STAT_LOST] = lost1 - c->lost0;
+  stats[HB_STAT_EVENTS] = total;
+  free(c->commit0);
+  free(c->last0);
+  free(c->fault0);
+}
+
 static void account(orc_raft* r, int type, uint64_t stats[HB_STAT_COUNT]) {
   stats[HB_STAT_MSGS]++;
   if (type == HB_MSG_APP_RESP) stats[HB_STAT_APPRESP]++;
@@ -790,20 +837,9 @@ static void account(orc_raft* r, int type, uint64_t stats[HB_STAT_COUNT]) {
 int orc_step_batch(orc_raft* groups, uint32_t ngroups, const hb_batch* b,
                    hb_event* ev, uint64_t ev_cap, uint64_t* nev,
                    uint64_t stats[HB_STAT_COUNT]) {
-  memset(stats, 0, sizeof(uint64_t) * HB_STAT_COUNT);
-  uint64_t* commit0 = (uint64_t*)malloc(sizeof(uint64_t) * (ngroups ? ngroups : 1));
-  uint64_t* last0 = (uint64_t*)malloc(sizeof(uint64_t) * (ngroups ? ngroups : 1));
-  int* fault0 = (int*)malloc(sizeof(int) * (ngroups ? ngroups : 1));
+  batch_ctx cx;
+  batch_begin(&cx, groups, ngroups, stats);
   uint64_t total = 0;
-  uint64_t won0 = 0, lost0 = 0;
-  for (uint32_t g = 0; g < ngroups; g++) {
-    won0 += groups[g].n_won;
-    lost0 += groups[g].n_lost;
-    commit0[g] = groups[g].log.committed;
-    last0[g] = groups[g].log.last_index;
-    fault0[g] = groups[g].fault;
-    groups[g].group = g;
-  }
   /* one sink shared by all groups, appended in processing order */
   #define BIND(r) do { (r)->ev = ev; (r)->ev_cap = ev_cap; (r)->nev = total; } while (0)
   #define UNBIND(r) do { total = (r)->nev; (r)->ev = NULL; } while (0)
@@ -859,28 +895,96 @@ int orc_step_batch(orc_raft* groups, uint32_t ngroups, const hb_batch* b,
     account(r, type, stats);
     UNBIND(r);
   }
-  for (uint32_t g = 0; g < ngroups; g++) {
-    orc_raft* r = &groups[g];
-    if (r->log.committed > commit0[g]) stats[HB_STAT_COMMITS]++;
-    if (r->fault && !fault0[g]) stats[HB_STAT_FAULTS]++;
-    stats[HB_STAT_ENTRIES] += r->log.last_index - last0[g];
-    r->nmsgs = 0;                                          /* msgs handed to the app via Ready */
-  }
-  uint64_t won1 = 0, lost1 = 0;
-  for (uint32_t g = 0; g < ngroups; g++) {
-    won1 += groups[g].n_won;
-    lost1 += groups[g].n_lost;
-  }
-  stats[HB_STAT_WON] = won1 - won0;
-  stats[HB_STAT_LOST] = lost1 - lost0;
-  free(commit0);
-  free(last0);
-  free(fault0);
-  stats[HB_STAT_EVENTS] = total;
+  batch_end(&cx, groups, ngroups, stats, total);
   *nev = total;
   #undef BIND
   #undef UNBIND
   return total <= ev_cap ? 0 : -1;
+}
+
+/* ---- tick (raft/raft.go:362-382, 765-771; raft/multinode.go:264-275) ---- */
+static int is_election_timeout(orc_raft* r, const uint64_t* draws, uint64_t ndraws) {
+  int64_t d = (int64_t)r->elapsed - r->election_timeout;
+  if (d < 0) return 0;
+  if (r->rand_pos >= ndraws) {          /* the host's stream is too short (engine-defined) */
+    fault(r, HB_FAULT_RAND_EXHAUSTED);
+    return 0;
+  }
+  uint64_t v = draws[r->rand_pos++];    /* r.rand.Int() */
+  return d > (int64_t)(v % (uint64_t)r->election_timeout);
+}
+
+static void step_local(orc_raft* r, int type) {
+  orc_msg m;
+  memset(&m, 0, sizeof(m));
+  m.type = type;
+  m.from = r->id;
+  m.to = r->id;
+  orc_raft_step(r, &m);
+}
+
+int orc_raft_tick(orc_raft* r, const uint64_t* draws, uint64_t ndraws) {
+  if (r->state == HB_STATE_LEADER) {    /* tickHeartbeat */
+    r->elapsed++;
+    if (r->elapsed >= r->heartbeat_timeout) {
+      r->elapsed = 0;
+      step_local(r, HB_MSG_BEAT);
+      return HB_MSG_BEAT;
+    }
+    return -1;
+  }
+  if (orc_raft_slot(r, r->id) < 0) {    /* tickElection: !promotable() */
+    r->elapsed = 0;
+    return -1;
+  }
+  r->elapsed++;
+  if (is_election_timeout(r, draws, ndraws)) {
+    r->elapsed = 0;
+    step_local(r, HB_MSG_HUP);
+    return HB_MSG_HUP;
+  }
+  return -1;
+}
+
+int orc_tick_batch(orc_raft* groups, uint32_t ngroups, const uint64_t* draws, uint64_t ndraws,
+                   hb_event* ev, uint64_t ev_cap, uint64_t* nev, uint64_t stats[HB_STAT_COUNT]) {
+  batch_ctx cx;
+  batch_begin(&cx, groups, ngroups, stats);
+  uint64_t total = 0;
+  for (uint32_t g = 0; g < ngroups; g++) {
+    orc_raft* r = &groups[g];
+    if (r->n == 0 || r->fault) continue;
+    r->ev = ev;
+    r->ev_cap = ev_cap;
+    r->nev = total;
+    r->arrival = HB_NO_INDEX;
+    int t = orc_raft_tick(r, draws, ndraws);
+    if (t >= 0) account(r, t, stats);
+    total = r->nev;
+    r->ev = NULL;
+  }
+  batch_end(&cx, groups, ngroups, stats, total);
+  *nev = total;
+  return total <= ev_cap ? 0 : -1;
+}
+
+void orc_groups_load_timers(orc_raft* gs, uint32_t n, const hb_timer* t) {
+  for (uint32_t i = 0; i < n; i++) {
+    gs[i].elapsed = (int)t[i].elapsed;
+    gs[i].rand_pos = t[i].rand_pos;
+    gs[i].election_timeout = t[i].election_tick;
+    gs[i].heartbeat_timeout = t[i].heartbeat_tick;
+  }
+}
+
+void orc_groups_export_timers(const orc_raft* gs, uint32_t n, hb_timer* out) {
+  for (uint32_t i = 0; i < n; i++) {
+    memset(&out[i], 0, sizeof(out[i]));
+    out[i].elapsed = (uint32_t)gs[i].elapsed;
+    out[i].rand_pos = (uint32_t)gs[i].rand_pos;
+    out[i].election_tick = (uint16_t)gs[i].election_timeout;
+    out[i].heartbeat_tick = (uint16_t)gs[i].heartbeat_timeout;
+  }
 }
 
 orc_raft* orc_groups_new(uint32_t ngroups) {

@@ -98,6 +98,9 @@ typedef struct orc_raft {
   uint64_t lead;
   int pending_conf;
   int elapsed;
+  int election_timeout;           /* r.electionTimeout (Config.ElectionTick) */
+  int heartbeat_timeout;          /* r.heartbeatTimeout (Config.HeartbeatTick) */
+  uint64_t rand_pos;              /* r.rand.Int() values taken so far */
   int nvotes;                     /* r.votes map */
   uint64_t vote_ids[ORC_MAX_PEERS + 1];
   int vote_vals[ORC_MAX_PEERS + 1];
@@ -191,6 +194,17 @@ int  orc_raft_get_inflights(const orc_raft* r, int slot, uint64_t* vals /* [coun
 int orc_step_batch(orc_raft* groups, uint32_t ngroups, const hb_batch* b,
                    hb_event* ev, uint64_t ev_cap, uint64_t* nev,
                    uint64_t stats[HB_STAT_COUNT]);
+
+/* Tick (raft/raft.go:362-382, isElectionTimeout :765-771); r.rand.Int() is
+ * draws[r->rand_pos++] (the shared rand.NewSource(id) stream).  Returns the
+ * local message type stepped (HB_MSG_BEAT / HB_MSG_HUP) or -1. */
+int orc_raft_tick(orc_raft* r, const uint64_t* draws, uint64_t ndraws);
+/* MultiNode.Tick over all groups (raft/multinode.go:264-275), events and
+ * statistics as orc_step_batch. */
+int orc_tick_batch(orc_raft* groups, uint32_t ngroups, const uint64_t* draws, uint64_t ndraws,
+                   hb_event* ev, uint64_t ev_cap, uint64_t* nev, uint64_t stats[HB_STAT_COUNT]);
+void orc_groups_load_timers(orc_raft* gs, uint32_t n, const hb_timer* t);
+void orc_groups_export_timers(const orc_raft* gs, uint32_t n, hb_timer* out);
 
 /* Flat-array helpers so the Python harness can drive many groups via ctypes. */
 orc_raft* orc_groups_new(uint32_t ngroups);

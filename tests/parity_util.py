@@ -71,6 +71,30 @@ class Pair:
             self.eng.set_inflights(g, s, int(init[g]["pr"][s]["ins_start"]), vals)
         assert_groups_equal(self.eng.get_groups(), init, "load")
 
+    def set_timers(self, timers, draws):
+        self.draws = np.ascontiguousarray(draws, dtype=np.uint64)
+        self.eng.load_timers(timers)
+        self.og.load_timers(timers)
+        self.eng.set_rand(self.draws)
+
+    def tick(self, ctx="", check_inflights=False):
+        """One MultiNode.Tick on both sides; events, stats, groups and timers equal."""
+        self.eng.tick()
+        dev_ev = self.eng.events()
+        dev_st = self.eng.stats()
+        ora_ev, ora_st = self.og.tick(self.draws)
+        assert_events_equal(dev_ev, ora_ev, ctx)
+        assert np.array_equal(dev_st, ora_st), \
+            f"{ctx}: stats dev {dict(zip(abi.STAT_NAMES, dev_st.tolist()))} ora {dict(zip(abi.STAT_NAMES, ora_st.tolist()))}"
+        ora_g = self.og.groups()
+        assert_groups_equal(self.eng.get_groups(), ora_g, ctx)
+        dt, ot = self.eng.get_timers(), self.og.timers()
+        bad = np.nonzero(dt != ot)[0]
+        assert len(bad) == 0, f"{ctx}: timers differ at {bad[:5]}: dev {dt[bad[:3]]} ora {ot[bad[:3]]}"
+        if check_inflights:
+            assert_inflights_equal(self.eng, self.og, ora_g, ctx)
+        return dev_ev, dev_st, ora_g
+
     def step(self, batch, ctx="", check_inflights=True):
         self.eng.step_batch(batch, host=True)
         dev_ev = self.eng.events()
@@ -83,4 +107,6 @@ class Pair:
         assert_groups_equal(self.eng.get_groups(), ora_g, ctx)
         if check_inflights:
             assert_inflights_equal(self.eng, self.og, ora_g, ctx)
+        if getattr(self, "draws", None) is not None:  # transitions zero r.elapsed
+            assert np.array_equal(self.eng.get_timers(), self.og.timers()), f"{ctx}: timers differ"
         return dev_ev, dev_st, ora_g

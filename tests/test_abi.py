@@ -41,12 +41,13 @@ def _compile_layout():
 #include "hipbatch.h"
 #define P(T, F) printf(#T "." #F " %zu\n", offsetof(T, F));
 int main(void) {
-  printf("hb_progress %zu\nhb_group %zu\nhb_event %zu\nhb_batch %zu\n", sizeof(hb_progress),
-         sizeof(hb_group), sizeof(hb_event), sizeof(hb_batch));
+  printf("hb_progress %zu\nhb_group %zu\nhb_event %zu\nhb_batch %zu\nhb_timer %zu\n", sizeof(hb_progress),
+         sizeof(hb_group), sizeof(hb_event), sizeof(hb_batch), sizeof(hb_timer));
   P(hb_group, term) P(hb_group, snap_index) P(hb_group, state) P(hb_group, fault) P(hb_group, pr)
   P(hb_progress, pending_snapshot) P(hb_progress, ins_count)
   P(hb_event, x) P(hb_event, group) P(hb_event, type) P(hb_event, to) P(hb_event, aux)
   P(hb_batch, n) P(hb_batch, props)
+  P(hb_timer, elapsed) P(hb_timer, rand_pos) P(hb_timer, election_tick) P(hb_timer, heartbeat_tick)
   return 0;
 }
 '''
@@ -65,12 +66,14 @@ def test_record_layouts_match():
     assert lay["hb_group"] == C.sizeof(abi.hb_group) == abi.GROUP_DTYPE.itemsize
     assert lay["hb_event"] == C.sizeof(abi.hb_event) == abi.EVENT_DTYPE.itemsize == 16
     assert lay["hb_batch"] == C.sizeof(abi.hb_batch)
+    assert lay["hb_timer"] == C.sizeof(abi.hb_timer) == abi.TIMER_DTYPE.itemsize
     for key, v in lay.items():
         if "." not in key:
             continue
         t, f = key.split(".")
         assert getattr(getattr(abi, t), f).offset == v, key
-        dt = {"hb_group": abi.GROUP_DTYPE, "hb_progress": abi.PROGRESS_DTYPE, "hb_event": abi.EVENT_DTYPE}.get(t)
+        dt = {"hb_group": abi.GROUP_DTYPE, "hb_progress": abi.PROGRESS_DTYPE, "hb_event": abi.EVENT_DTYPE,
+              "hb_timer": abi.TIMER_DTYPE}.get(t)
         if dt is not None:
             assert dt.fields[f][1] == v, key
 

@@ -200,3 +200,61 @@ def test_cfg3_open_loop_stream(W):
     for k in range(5):
         _, st, now = pair.step(synth.cfg3_open_batch(now, rng), ctx=f"cfg3 open {k}")
         assert st[abi.HB_STAT_FAULTS] == 0
+
+
+# ---------------------------------------------------------------- MultiNode.Tick
+DRAWS = np.random.default_rng(77).integers(0, 1 << 63, 4096, dtype=np.uint64)
+
+
+@pytest.mark.parametrize("seed,nmax,W", [(31, 3, 8), (32, 5, 8), (33, 7, 16)])
+def test_tick_random_states(seed, nmax, W):
+    """Ticks interleaved with batches over every role (leaders beat, followers
+    and candidates time out on their own draw positions, non-promotable nodes
+    stay at 0); steps zero r.elapsed on every reset."""
+    G = 2000
+    g, runs, ins = synth.random_groups(G, nmax, seed=seed, W=W)
+    pair = Pair(g, runs, nmax, W, ins=ins, max_batch=1 << 15)
+    pair.set_timers(synth.random_timers(G, seed=seed + 1, et_hi=6, ht_hi=3), DRAWS)
+    for k in range(12):
+        pair.tick(ctx=f"tick {seed}/{k}")
+        if k % 4 == 3:
+            pair.step(synth.random_batch(g, 3000, seed=1000 * seed + k), ctx=f"tick-step {seed}/{k}")
+
+
+def test_tick_elections_and_heartbeats():
+    """cfg4-shaped followers time out and campaign; the winners then beat."""
+    G = 3000
+    g, runs = synth.election_groups(G, 5, seed=41)
+    pair = Pair(g, runs, 5, 64, max_batch=1 << 16)
+    t = np.zeros(G, abi.TIMER_DTYPE)
+    t["election_tick"], t["heartbeat_tick"] = 4, 2
+    pair.set_timers(t, DRAWS)
+    camp = 0
+    for k in range(10):
+        _, st, _ = pair.tick(ctx=f"tick {k}")
+        camp += int(st[abi.HB_STAT_MSGS])
+    assert camp >= G  # every group campaigned at least once
+    # grant every candidate's votes, then leaders heartbeat on their ticks
+    now = pair.og.groups()
+    cand = np.nonzero(now["state"] == abi.HB_STATE_CANDIDATE)[0].astype(np.uint32)
+    vg = np.repeat(cand, 4)
+    vs = np.tile(np.arange(1, 5, dtype=np.uint32), len(cand))
+    b = dict(group=vg, info=(abi.HB_MSG_VOTE_RESP | (vs << 4)).astype(np.uint32),
+             term=now["term"][vg].astype(np.uint64), index=np.zeros(len(vg), np.uint64), hint=None, props=None)
+    _, st, _ = pair.step(b, ctx="votes")
+    assert st[abi.HB_STAT_WON] == len(cand)
+    for k in range(4):
+        pair.tick(ctx=f"beat {k}")
+
+
+def test_tick_draws_exhausted():
+    G = 600
+    g, runs = synth.election_groups(G, 3, seed=43)
+    pair = Pair(g, runs, 3, 8, max_batch=1 << 12)
+    t = np.zeros(G, abi.TIMER_DTYPE)
+    t["election_tick"], t["heartbeat_tick"] = 2, 1
+    t["rand_pos"] = np.arange(G) % 40
+    pair.set_timers(t, DRAWS[:20])
+    for k in range(4):
+        _, st, _ = pair.tick(ctx=f"exhaust {k}")
+    assert (pair.og.groups()["fault"] == abi.HB_FAULT_RAND_EXHAUSTED).sum() > 0
