@@ -159,6 +159,32 @@ def cpu_baseline_cfg3(n, groups=60_000, W=256, budget_s=10.0, max_steps=20):
                       f"{steps} cfg3 steps, {acks} MsgAppResp in {spent:.2f} s, one core"}
 
 
+def cpu_baseline_tick(n, groups=200_000, W=256, budget_s=10.0, max_steps=50):
+    """The C oracle's MultiNode.Tick (orc_tick_batch) on a bounded sample of the
+    tick workload, one core -- the reference ticks every group on its one run
+    goroutine (raft/multinode.go:268-274)."""
+    from etcd_amd import abi, synth
+    from oracle.pyoracle import OracleGroups
+    g, runs = synth.steady_groups(groups, n, seed=0x5EED0002, with_runs="flat")
+    g["state"][1::2] = abi.HB_STATE_FOLLOWER
+    g["lead"][1::2] = 1
+    og = OracleGroups(g, runs, W)
+    t = synth.random_timers(groups, seed=0x5EED0002, et_hi=10, ht_hi=1, pos_hi=0)
+    t["election_tick"] = 10
+    og.load_timers(t)
+    draws = np.random.default_rng(1).integers(0, 1 << 63, 4 * max_steps + 64, dtype=np.uint64)
+    spent = 0.0
+    steps = 0
+    while spent < budget_s and steps < max_steps:
+        t0 = time.perf_counter()
+        og.tick(draws)
+        spent += time.perf_counter() - t0
+        steps += 1
+    return {"value": groups * steps / spent, "unit": "group-ticks/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/raft_oracle.c orc_tick_batch (C restatement, not the Go reference), {groups} groups x {n}, "
+                      f"{steps} ticks in {spent:.2f} s, one core"}
+
+
 def pmc_traffic(path, kernel, G, n, apply_us):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (FETCH_SIZE x 2 + WRITE_SIZE, tools/prof_summary.py).  Used only when the
@@ -189,8 +215,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4"], default="cfg2",
-                    help="cfg2 (headline), cfg3 lagging followers, cfg4 election storm")
+    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4", "tick"], default="cfg2",
+                    help="cfg2 (headline), cfg3 lagging followers, cfg4 election storm, "
+                         "tick = MultiNode.Tick over the cfg2 groups (SURVEY.md 8(f) rank 1)")
     ap.add_argument("--groups", type=int, default=None, help="groups per GPU (cfg2/cfg3: 1M, cfg4: 4M)")
     ap.add_argument("--replicas", type=int, default=None, help="cfg2: 3, cfg3: 5, cfg4: 7")
     ap.add_argument("--inflight", type=int, default=256, help="MaxInflightMsgs W (cfg3/cfg4)")
@@ -209,7 +236,7 @@ def main():
     if args.groups is None:
         args.groups = (1 << 22) if args.workload == "cfg4" else (1 << 20)
     if args.replicas is None:
-        args.replicas = {"cfg2": 3, "cfg3": 5, "cfg4": 7}[args.workload]
+        args.replicas = {"cfg2": 3, "cfg3": 5, "cfg4": 7, "tick": 3}[args.workload]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -403,7 +430,7 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     from etcd_amd import abi, synth
     from etcd_amd.hipbatch import Engine
     n, W, G = args.replicas, args.inflight, args.groups
-    seed = {"cfg3": 0x5EED0003, "cfg4": 0x5EED0004}[args.workload] + rank
+    seed = {"cfg3": 0x5EED0003, "cfg4": 0x5EED0004, "tick": 0x5EED0002}[args.workload] + rank
     stream = torch.cuda.current_stream(dev)
     total = args.warmup + args.steps
     st_acc = np.zeros(abi.HB_STAT_COUNT, np.uint64)
@@ -438,6 +465,35 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         ms_local = e0.elapsed_time(e1)
         st_acc = stats.cpu().numpy().astype(np.uint64)
         timing = "K steps back to back, inputs resident in HBM"
+    elif args.workload == "tick":
+        g, _ = synth.steady_groups(G, n, seed=seed, with_runs=False)
+        # half the groups lead (HeartbeatTick 1: a MsgBeat every tick), half
+        # follow a leader elsewhere with ElectionTick 10 (draws past elapsed 10)
+        g["state"][1::2] = abi.HB_STATE_FOLLOWER
+        g["lead"][1::2] = 1
+        eng = Engine(G, max_replicas=n, max_inflight=W, max_batch=1, device=local, stream=stream)
+        eng.load_groups(g)
+        del g
+        t = synth.random_timers(G, seed=seed, et_hi=10, ht_hi=1, pos_hi=0)
+        t["election_tick"] = 10
+        eng.load_timers(t)
+        eng.set_rand(np.random.default_rng(seed).integers(0, 1 << 63, 4 * total + 64, dtype=np.uint64))
+        stats = torch.zeros(abi.HB_STAT_COUNT, dtype=torch.int64, device=dev)
+        for k in range(args.warmup):
+            eng.tick()
+        eng.set_stats_accum(stats)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for k in range(args.warmup, total):
+            eng.tick()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms_local = e0.elapsed_time(e1)
+        st_acc = stats.cpu().numpy().astype(np.uint64)
+        timing = "K ticks back to back"
     else:
         g, _ = synth.lagging_groups(G, n, seed=seed, W=W)
         eng = Engine(G, max_replicas=n, max_inflight=W, max_batch=2 * G * n + G, device=local, stream=stream)
@@ -467,7 +523,15 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     ms = float(ms_t.item())
     st = st_t.cpu().numpy().view(np.uint64)
     sec = ms / 1e3
-    if args.workload == "cfg4":
+    if args.workload == "tick":
+        metric, unit, val = "group ticks/sec (MultiNode.Tick over 1M groups x 3)", "group-ticks/s", \
+            world * G * args.steps / sec
+        extra = {"msgs_stepped_per_s": int(st[abi.HB_STAT_MSGS]) / sec, "events_per_s": int(st[abi.HB_STAT_EVENTS]) / sec,
+                 "campaigns": int(st[abi.HB_STAT_MSGS]) - world * (G // 2 + G % 2) * args.steps}
+        ok = int(st[abi.HB_STAT_FAULTS]) == 0
+        wl = f"tick: {G} raft groups x {n} per GPU, half leaders (HeartbeatTick 1), half followers (ElectionTick 10)"
+        data = "synthetic (cfg2 groups; seeded timers and r.rand stream)"
+    elif args.workload == "cfg4":
         metric, unit, val = "MsgVoteResp tallied/sec + elections decided/sec (cfg4 election storm)", "MsgVoteResp/s", \
             int(st[abi.HB_STAT_VOTERESP]) / sec
         extra = {"elections_decided_per_s": (int(st[abi.HB_STAT_WON]) + int(st[abi.HB_STAT_LOST])) / sec,
@@ -494,7 +558,8 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             try:
-                out["cpu_baseline"] = (cpu_baseline_cfg4 if args.workload == "cfg4" else cpu_baseline_cfg3)(n, W=W)
+                out["cpu_baseline"] = {"cfg4": cpu_baseline_cfg4, "cfg3": cpu_baseline_cfg3,
+                                       "tick": cpu_baseline_tick}[args.workload](n, W=W)
             except Exception as e:  # report, never fake
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out))
