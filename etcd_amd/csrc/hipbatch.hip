@@ -1093,7 +1093,11 @@ __global__ void k_load(DevState S, uint32_t first, uint32_t count, const hb_grou
   S.tfirst[g] = r.term_first;
   S.tlast[g] = r.term_last;
   S.snap[g] = r.snap_index;
-  S.meta[g] = meta_make(r.state, r.n, r.self_slot, r.lead, r.vote, r.fault, r.votes_resp, r.votes_grant);
+  uint64_t m = meta_make(r.state, r.n, r.self_slot, r.lead, r.vote, r.fault, r.votes_resp, r.votes_grant);
+  if (r.term_last == r.last_index) m |= M_TL;
+  if (r.self_slot < r.n && r.pr[r.self_slot].match == r.last_index && r.pr[r.self_slot].next == r.last_index + 1)
+    m |= M_SM;
+  S.meta[g] = m;
   S.elapsed[g] = 0;  // newRaft: fresh r.rand, becomeFollower -> reset
   S.rpos[g] = 0;
   for (uint32_t s = 0; s < S.nmax; ++s) {
@@ -1118,7 +1122,7 @@ __global__ void k_gather(DevState S, uint32_t first, uint32_t count, hb_group* d
   r.first_index = S.first[g];
   r.last_index = S.last[g];
   r.term_first = S.tfirst[g];
-  r.term_last = S.tlast[g];
+  r.term_last = (m & M_TL) ? r.last_index : S.tlast[g];
   r.snap_index = S.snap[g];
   r.state = m_state(m);
   r.n = m_n(m);
@@ -1131,8 +1135,9 @@ __global__ void k_gather(DevState S, uint32_t first, uint32_t count, hb_group* d
   for (uint32_t s = 0; s < S.nmax && s < r.n; ++s) {
     const size_t o = (size_t)s * S.G + g;
     const uint32_t p = S.pm[o];
-    r.pr[s].match = S.match[o];
-    r.pr[s].next = S.next[o];
+    const bool kept = !((m & M_SM) && s == r.self_slot);  // M_SM: materialized from last
+    r.pr[s].match = kept ? S.match[o] : r.last_index;
+    r.pr[s].next = kept ? S.next[o] : r.last_index + 1;
     r.pr[s].state = pm_state(p);
     r.pr[s].paused = pm_paused(p);
     r.pr[s].ins_start = pm_start(p);

@@ -70,11 +70,15 @@ struct FastLane {
     first = S.first[g];
     last = S.last[g];
     tfirst = S.tfirst[g];
-    tlast = S.tlast[g];
+    // arrays the meta flags mark as not kept are not read (M_TL / M_SM,
+    // hipbatch_kernels.h); these loads issue once meta is in, beside the
+    // ring heads, which wait for pm anyway
+    tlast = (mlo & (uint32_t)M_TL) ? last : S.tlast[g];
+    const uint32_t sf = (mlo & (uint32_t)M_SM) ? self() : 0xFFu;
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) {
-      match[s] = S.match[(size_t)s * S.G + g];
-      next[s] = S.next[(size_t)s * S.G + g];
+      match[s] = ((uint32_t)s == sf) ? last : S.match[(size_t)s * S.G + g];
+      next[s] = ((uint32_t)s == sf) ? last + 1 : S.next[(size_t)s * S.G + g];
       pm[s] = S.pm[(size_t)s * S.G + g];
     }
 #pragma unroll
@@ -87,14 +91,35 @@ struct FastLane {
   static constexpr uint32_t D_TFIRST = 1u << 5;
   static constexpr uint32_t D_PM0 = 16;
   __device__ __forceinline__ void store() {
+    // keep M_TL / M_SM only while they still hold; a cleared flag makes its
+    // array live again, so it is written
+    const bool tl = (mlo & (uint32_t)M_TL) && tlast == last;
+    if ((mlo & (uint32_t)M_TL) && !tl) {
+      mlo &= ~(uint32_t)M_TL;
+      dirty |= D_META | D_TRUN;
+    }
+    uint32_t sf = 0xFFu;
+    if (mlo & (uint32_t)M_SM) {
+      const uint32_t s0 = self();
+      bool ok = false;
+#pragma unroll
+      for (int s = 0; s < NMAX; ++s)
+        if ((uint32_t)s == s0) ok = match[s] == last && next[s] == last + 1;
+      if (ok) {
+        sf = s0;
+      } else {
+        mlo &= ~(uint32_t)M_SM;
+        dirty |= D_META | (1u << (D_SLOT0 + s0));
+      }
+    }
     if (dirty & D_META) reinterpret_cast<uint32_t*>(S.meta)[2 * (size_t)g] = mlo;  // little-endian low word
     if (dirty & D_COMMIT) S.commit[g] = committed;
     if (dirty & D_LAST) S.last[g] = last;
     if (dirty & D_TFIRST) S.tfirst[g] = tfirst;
-    if (dirty & D_TRUN) S.tlast[g] = tlast;
+    if ((dirty & D_TRUN) && !tl) S.tlast[g] = tlast;
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) {
-      if (dirty & (1u << (D_SLOT0 + s))) {
+      if ((dirty & (1u << (D_SLOT0 + s))) && (uint32_t)s != sf) {
         S.match[(size_t)s * S.G + g] = match[s];
         S.next[(size_t)s * S.G + g] = next[s];
       }

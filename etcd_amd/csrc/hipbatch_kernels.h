@@ -31,13 +31,21 @@ constexpr uint32_t CHUNK = 4 * PART;         // messages staged in LDS per round
 
 // ---- packed group meta (u64) ------------------------------------------------
 //  [0:2) state  [2:5) n  [5:9) self slot  [9:13) lead ref  [13:17) vote ref
-//  [17:21) fault  [24:32) votes responded  [32:40) votes granted
+//  [17:21) fault  [21] M_TL  [22] M_SM  [24:32) votes responded  [32:40) votes granted
+//  M_TL: tlast == last — the tlast array is then not kept (a leader's current-
+//  term run always ends at its last entry).  M_SM: the self slot's Match ==
+//  last and Next == last + 1 — its match / next arrays are then not kept (a
+//  leader's own progress after every append).  The steady-state fast path
+//  neither reads nor writes those 48 bytes per group; every other reader
+//  materializes them from `last`.
 __host__ __device__ inline uint64_t meta_make(uint32_t state, uint32_t n, uint32_t self, uint32_t lead,
                                               uint32_t vote, uint32_t fault, uint32_t resp, uint32_t grant) {
   return (uint64_t)(state & 3) | ((uint64_t)(n & 7) << 2) | ((uint64_t)(self & 0xF) << 5) |
          ((uint64_t)(lead & 0xF) << 9) | ((uint64_t)(vote & 0xF) << 13) | ((uint64_t)(fault & 0xF) << 17) |
          ((uint64_t)(resp & 0xFF) << 24) | ((uint64_t)(grant & 0xFF) << 32);
 }
+constexpr uint64_t M_TL = 1ull << 21;
+constexpr uint64_t M_SM = 1ull << 22;
 __host__ __device__ inline uint32_t m_state(uint64_t m) { return (uint32_t)(m & 3); }
 __host__ __device__ inline uint32_t m_n(uint64_t m) { return (uint32_t)((m >> 2) & 7); }
 __host__ __device__ inline uint32_t m_self(uint64_t m) { return (uint32_t)((m >> 5) & 0xF); }
@@ -194,6 +202,7 @@ struct Lane {
   uint32_t g;
   uint32_t arrival;  // batch position of the message; 0xFFFFFFFF: props[] proposal
   uint64_t term, committed, first, last, tfirst, tlast, meta;
+  uint64_t meta0;  // meta as loaded (which arrays are stale: M_TL / M_SM)
   typename SlotVec<NMAX>::u64 match, next;
   typename SlotVec<NMAX>::u64 head;  // register copy of each ring's head entry
   typename SlotVec<NMAX>::u32 pm;
@@ -276,10 +285,37 @@ struct Lane {
     }
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) head[s] = pm_count(pm[s]) ? *ring_at(s, pm_start(pm[s])) : 0;
+    meta0 = meta;
+    if (meta & M_TL) tlast = last;
+    if (meta & M_SM) {
+      const uint32_t sf = self();
+#pragma unroll
+      for (int s = 0; s < NMAX; ++s) {
+        if ((uint32_t)s == sf) {
+          match[s] = last;
+          next[s] = last + 1;
+        }
+      }
+    }
     dirty = 0;
   }
 
   __device__ __forceinline__ void store() {
+    {  // re-derive M_TL / M_SM; an array that was stale and no longer may be is written
+      const uint32_t sf = self(), nn = n();
+      const bool tl = tlast == last;
+      bool sm = false;
+#pragma unroll
+      for (int s = 0; s < NMAX; ++s)
+        if ((uint32_t)s == sf && (uint32_t)s < nn) sm = match[s] == last && next[s] == last + 1;
+      const uint64_t m2 = (meta & ~(M_TL | M_SM)) | (tl ? M_TL : 0ull) | (sm ? M_SM : 0ull);
+      if (m2 != meta) {
+        meta = m2;
+        dirty |= D_META;
+      }
+      if (!tl && (meta0 & M_TL)) dirty |= D_TRUN;
+      if (!sm && (meta0 & M_SM) && sf < (uint32_t)NMAX) dirty |= 1u << (D_SLOT0 + sf);
+    }
     if (dirty & D_META) S.meta[g] = meta;
     if (dirty & D_TERM) S.term[g] = term;
     if (dirty & D_COMMIT) S.commit[g] = committed;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ-counter pass over a short bench run (one PMC group per rocprofv3 run).
-#   gpurun -- bash tools/pmc_sq.sh <tag>
+#   gpurun -- bash tools/pmc_sq.sh <tag>      (BENCH_ARGS="--workload cfg4 ..." to pick the workload)
 set -euo pipefail
 TAG=${1:-sq}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -8,9 +8,10 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT"
+BA=${BENCH_ARGS:---steps 5 --warmup 2}
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
-  --output-format csv -d "$OUT/sq1" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > "$OUT/sq1.log" 2>&1
+  --output-format csv -d "$OUT/sq1" -o run -- python3 bench.py $BA --no-cpu-baseline --no-profile > "$OUT/sq1.log" 2>&1
 echo sq1 done
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_FLAT \
-  --output-format csv -d "$OUT/sq2" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > "$OUT/sq2.log" 2>&1
+  --output-format csv -d "$OUT/sq2" -o run -- python3 bench.py $BA --no-cpu-baseline --no-profile > "$OUT/sq2.log" 2>&1
 echo sq2 done
