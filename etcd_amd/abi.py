@@ -78,6 +78,14 @@ HB_EV_FAULT = 11
 HB_EVW_BCAST = 12  # device event word: HB_EV_APP to every slot of a mask
 HB_EVW_CONT = 15  # device event word: continuation (x bits 40..63)
 
+# wire ingestion record status (hb_decode)
+HB_WIRE_OK = 0
+HB_WIRE_LOCAL = 1
+HB_WIRE_HOST = 2
+HB_WIRE_ERROR = 3
+HB_WIRE_PANIC = 4
+HB_WIRE_BADGROUP = 5
+
 HB_STAT_MSGS = 0
 HB_STAT_APPRESP = 1
 HB_STAT_VOTERESP = 2

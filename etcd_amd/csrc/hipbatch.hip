@@ -24,6 +24,7 @@
 
 #include "hipbatch_kernels.h"
 #include "hipbatch_fast.h"
+#include "hipbatch_wire.h"
 
 using namespace hb;
 
@@ -1059,6 +1060,60 @@ __global__ void __launch_bounds__(PART, 2) k_tick(ApplyArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_decode: wire ingestion (hb_decode).  One lane per record: Message.Unmarshal
+// (hipbatch_wire.h), multiNode.Step's local-message filter (raft/multinode.go:
+// 432-439), m.From -> slot through the group's peer ids, one batch record out.
+// ---------------------------------------------------------------------------
+struct DecodeArgs {
+  const uint8_t* bytes;
+  const uint64_t* off;
+  const uint32_t* len;
+  const uint32_t* group;
+  uint64_t n;
+  const uint64_t* meta;
+  const uint64_t* peer;  // [nmax][G] or null
+  uint32_t G, nmax;
+  uint32_t* o_group;
+  uint32_t* o_info;
+  uint64_t* o_term;
+  uint64_t* o_index;
+  uint64_t* o_hint;
+  uint8_t* status;
+};
+
+__global__ void __launch_bounds__(256) k_decode(DecodeArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= a.n) return;
+  WireMsg m;
+  const int rc = w_unmarshal_message(a.bytes + a.off[k], (int64_t)a.len[k], &m);
+  const uint32_t g = a.group[k];
+  uint32_t st;
+  if (rc == W_ERR) st = HB_WIRE_ERROR;
+  else if (rc == W_PANIC) st = HB_WIRE_PANIC;
+  else if (rc == W_DEEP) st = HB_WIRE_HOST;
+  else if (m.type == HB_MSG_HUP || m.type == HB_MSG_BEAT || m.type == HB_MSG_UNREACHABLE ||
+           m.type == HB_MSG_SNAP_STATUS)
+    st = HB_WIRE_LOCAL;  // IsLocalMsg raft/util.go:49-51
+  else if (m.type != HB_MSG_APP_RESP && m.type != HB_MSG_VOTE_RESP && m.type != HB_MSG_HEARTBEAT_RESP)
+    st = HB_WIRE_HOST;
+  else if (g >= a.G) st = HB_WIRE_BADGROUP;
+  else st = HB_WIRE_OK;
+  uint32_t slot = HB_SLOT_NONE;
+  if (st == HB_WIRE_OK && a.peer && m.from != 0) {
+    const uint32_t nn = m_n(a.meta[g]);
+    for (uint32_t s = 0; s < a.nmax; ++s)
+      if (s < nn && slot == HB_SLOT_NONE && a.peer[(size_t)s * a.G + g] == m.from) slot = s;
+  }
+  const bool ok = st == HB_WIRE_OK;
+  a.o_group[k] = ok ? g : 0xFFFFFFFFu;
+  a.o_info[k] = ok ? ((uint32_t)m.type | (slot << 4) | ((uint32_t)m.reject << 8)) : 0u;
+  a.o_term[k] = ok ? m.term : 0ull;
+  a.o_index[k] = ok ? m.index : 0ull;
+  a.o_hint[k] = ok ? m.hint : 0ull;
+  a.status[k] = (uint8_t)st;
+}
+
 // ============================================================================
 // Phase 3: finish
 // ============================================================================
@@ -1307,6 +1362,7 @@ struct hb_handle {
   uint32_t* pflag = nullptr;      // [NB][PART/32]
   uint32_t* resume = nullptr;     // [G]
   uint64_t* commit0 = nullptr;    // [G]
+  uint64_t* peer = nullptr;       // [nmax][G] node ids (hb_load_peers), allocated on first use
   uint64_t* rnd = nullptr;        // the r.rand stream (hb_set_rand), grown on demand
   uint64_t rnd_cap = 0;
   static constexpr uint32_t PROF_RING = 256;
@@ -1524,6 +1580,7 @@ int hb_destroy(hb_handle* h) {
     if (ps.applied) (void)hipEventDestroy(ps.applied);
   }
   if (h->rnd) (void)hipFree(h->rnd);
+  if (h->peer) (void)hipFree(h->peer);
   if (h->in_ready) (void)hipEventDestroy(h->in_ready);
   if (h->prep) (void)hipStreamDestroy(h->prep);
   delete h;
@@ -1679,6 +1736,55 @@ int hb_set_rand(hb_handle* h, uint64_t first, uint64_t count, const uint64_t* dr
   }
   h->st.rnd = h->rnd;
   if (need > h->st.nrnd) h->st.nrnd = need;
+  return HB_OK;
+}
+
+int hb_load_peers(hb_handle* h, uint32_t first, uint32_t count, const uint64_t* ids) {
+  if (!h || (count && !ids) || (uint64_t)first + count > h->G) return HB_EINVAL;
+  if (count == 0) return HB_OK;
+  DeviceGuard guard(h->device);
+  const size_t G = h->G;
+  if (!h->peer) {
+    HB_CHECK(hipMalloc(&h->peer, (size_t)h->nmax * G * 8));
+    HB_CHECK(hipMemsetAsync(h->peer, 0, (size_t)h->nmax * G * 8, h->stream));
+  }
+  std::vector<uint64_t> row(count);
+  for (uint32_t s = 0; s < h->nmax; ++s) {
+    for (uint32_t i = 0; i < count; ++i) row[i] = ids[(size_t)i * HB_MAX_REPLICAS + s];
+    HB_CHECK(hipMemcpyAsync(h->peer + s * G + first, row.data(), count * 8ull, hipMemcpyHostToDevice, h->stream));
+    HB_CHECK(hipStreamSynchronize(h->stream));  // row is reused
+  }
+  return HB_OK;
+}
+
+int hb_decode(hb_handle* h, const uint8_t* bytes, const uint64_t* off, const uint32_t* len, const uint32_t* group,
+              uint64_t n, const hb_batch* out, uint8_t* status) {
+  if (!h || !out) return HB_EINVAL;
+  if (n == 0) return HB_OK;
+  if (!bytes || !off || !len || !group || !status || !out->group || !out->info || !out->term || !out->index ||
+      !out->hint)
+    return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  DecodeArgs da;
+  da.bytes = bytes;
+  da.off = off;
+  da.len = len;
+  da.group = group;
+  da.n = n;
+  da.meta = h->st.meta;
+  da.peer = h->peer;
+  da.G = h->G;
+  da.nmax = h->nmax;
+  da.o_group = const_cast<uint32_t*>(out->group);
+  da.o_info = const_cast<uint32_t*>(out->info);
+  da.o_term = const_cast<uint64_t*>(out->term);
+  da.o_index = const_cast<uint64_t*>(out->index);
+  da.o_hint = const_cast<uint64_t*>(out->hint);
+  da.status = status;
+  // on the stream the batches come from, so hb_step's prep orders after it
+  hipStream_t ds = h->in_stream_set ? h->in_stream : h->stream;
+  hipLaunchKernelGGL(k_decode, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ds, da);
+  HB_CHECK(hipGetLastError());
   return HB_OK;
 }
 

@@ -73,6 +73,25 @@ struct FastLane {
     // arrays the meta flags mark as not kept are not read (M_TL / M_SM,
     // hipbatch_kernels.h); these loads issue once meta is in, beside the
     // ring heads, which wait for pm anyway
+#ifdef HB_X_UNCOND
+    {
+      const uint64_t tl0 = S.tlast[g];
+      uint64_t m0[NMAX], n0[NMAX];
+#pragma unroll
+      for (int s = 0; s < NMAX; ++s) {
+        m0[s] = S.match[(size_t)s * S.G + g];
+        n0[s] = S.next[(size_t)s * S.G + g];
+        pm[s] = S.pm[(size_t)s * S.G + g];
+      }
+      tlast = (mlo & (uint32_t)M_TL) ? last : tl0;
+      const uint32_t sf = (mlo & (uint32_t)M_SM) ? self() : 0xFFu;
+#pragma unroll
+      for (int s = 0; s < NMAX; ++s) {
+        match[s] = ((uint32_t)s == sf) ? last : m0[s];
+        next[s] = ((uint32_t)s == sf) ? last + 1 : n0[s];
+      }
+    }
+#else
     tlast = (mlo & (uint32_t)M_TL) ? last : S.tlast[g];
     const uint32_t sf = (mlo & (uint32_t)M_SM) ? self() : 0xFFu;
 #pragma unroll
@@ -81,8 +100,14 @@ struct FastLane {
       next[s] = ((uint32_t)s == sf) ? last + 1 : S.next[(size_t)s * S.G + g];
       pm[s] = S.pm[(size_t)s * S.G + g];
     }
+#endif
+#ifdef HB_X_NOHEAD
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) head[s] = pm_count(pm[s]) ? last : 0;  // diagnostic: no ring read
+#else
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) head[s] = pm_count(pm[s]) ? *ring_at(s, pm_start(pm[s])) : 0;
+#endif
     dirty = 0;
   }
   // Dirty bits (hipbatch_kernels.h) plus, lane-local to the fast path:

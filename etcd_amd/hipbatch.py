@@ -58,6 +58,9 @@ def lib():
         "hb_get_timers": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
         "hb_set_rand": (C.c_int, [H, C.c_uint64, C.c_uint64, C.c_void_p]),
         "hb_tick": (C.c_int, [H, C.c_uint32]),
+        "hb_load_peers": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
+        "hb_decode": (C.c_int, [H, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, P(abi.hb_batch),
+                                C.c_void_p]),
         "hb_events_device": (C.c_int, [H, P(C.c_void_p), P(C.c_void_p), P(C.c_void_p), P(C.c_uint32)]),
         "hb_copy_events": (C.c_int, [H, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
         "hb_stats_device": (C.c_int, [H, P(C.c_void_p)]),
@@ -196,6 +199,23 @@ class Engine:
     def tick(self):
         """One MultiNode.Tick over every group (asynchronous; events/stats as step)."""
         _check("hb_tick", lib().hb_tick(self.h, 0))
+
+    # ---- wire ingestion ----------------------------------------------------------
+    def load_peers(self, ids, first=0):
+        """ids: [count, HB_MAX_REPLICAS] node ids per slot (0 = none)."""
+        a = np.ascontiguousarray(ids, dtype=np.uint64).reshape(-1, abi.HB_MAX_REPLICAS)
+        _check("hb_load_peers", lib().hb_load_peers(self.h, first, len(a), a.ctypes.data))
+
+    def decode(self, data, off, length, group, out, status):
+        """Decode raftpb.Message records (device tensors) into the batch arrays
+        out = {group, info, term, index, hint} (device tensors) + status (u8)."""
+        b = abi.hb_batch()
+        b.n = len(off)
+        b.group, b.info, b.term, b.index = _ptr(out["group"]), _ptr(out["info"]), _ptr(out["term"]), _ptr(out["index"])
+        b.hint, b.props = _ptr(out["hint"]), None
+        self._keep_dec = (data, off, length, group, out, status)
+        _check("hb_decode", lib().hb_decode(self.h, _ptr(data), _ptr(off), _ptr(length), _ptr(group), len(off),
+                                            C.byref(b), _ptr(status)))
 
     def step_batch(self, batch, **kw):
         return self.step(batch["group"], batch["info"], batch["term"], batch["index"],

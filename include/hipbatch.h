@@ -323,6 +323,29 @@ int  hb_set_rand(hb_handle* h, uint64_t first, uint64_t count, const uint64_t* d
  * count in HB_STAT_MSGS).  flags: 0. */
 int  hb_tick(hb_handle* h, uint32_t flags);
 
+/* ---- wire ingestion ------------------------------------------------------
+ * Decode raftpb.Message records (protobuf, raft/raftpb/raft.pb.go:549-799
+ * Message.Unmarshal with its Entry / Snapshot / SnapshotMetadata / ConfState
+ * sub-messages and gogo proto.Skip) straight into a device batch, as
+ * multiNode.Step receives them (raft/multinode.go:432-439).  Record i is
+ * bytes[off[i], off[i] + len[i]) for group slot group[i]; m.From becomes the
+ * group's slot through the node ids set with hb_load_peers (HB_SLOT_NONE when
+ * absent, so hb_step's membership filter applies).  bytes / off / len / group
+ * and every array of `out` are device memory; out->props is ignored.  Record
+ * i of `out` is the batch record (group = 0xFFFFFFFF unless HB_WIRE_OK, so
+ * hb_step drops it); status[i] says what became of it:                      */
+#define HB_WIRE_OK       0  /* MsgAppResp / MsgVoteResp / MsgHeartbeatResp: in the batch      */
+#define HB_WIRE_LOCAL    1  /* local type from the network, dropped by Step (IsLocalMsg)      */
+#define HB_WIRE_HOST     2  /* well-formed, not for the device batch (other types, or unknown
+                               fields nesting groups deeper than 16): the host steps it        */
+#define HB_WIRE_ERROR    3  /* Unmarshal returns an error (truncated, wrong / illegal wire type) */
+#define HB_WIRE_PANIC    4  /* the reference would panic or never return (negative lengths)  */
+#define HB_WIRE_BADGROUP 5  /* group[i] >= capacity                                          */
+/* ids[i * HB_MAX_REPLICAS + s] = node id of slot s of group first + i (host memory). */
+int  hb_load_peers(hb_handle* h, uint32_t first, uint32_t count, const uint64_t* ids);
+int  hb_decode(hb_handle* h, const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
+               const uint32_t* group, uint64_t n, const hb_batch* out, uint8_t* status);
+
 /* ---- the hot path ----------------------------------------------------------
  * Step one batch (all messages of the batch, per group in arrival order).
  * Asynchronous on the handle's stream.  Events and statistics of the step

@@ -60,6 +60,39 @@ class orc_msg(C.Structure):
                 f"reject={self.Reject}, nents={self.nents}, ent_lo={self.ent_lo})")
 
 
+class orc_wire_msg(C.Structure):
+    _fields_ = [("type", C.c_int32), ("to", C.c_uint64), ("from_", C.c_uint64), ("term", C.c_uint64),
+                ("log_term", C.c_uint64), ("index", C.c_uint64), ("commit", C.c_uint64),
+                ("reject_hint", C.c_uint64), ("reject", C.c_int), ("nentries", C.c_uint32)]
+
+
+def unmarshal_message(data):
+    """Message.Unmarshal (raft/raftpb/raft.pb.go:549-799) -> (rc, orc_wire_msg);
+    rc 0 ok, 1 error, 2 Go panic / endless loop, 3 groups nested too deep."""
+    m = orc_wire_msg()
+    rc = lib().orc_unmarshal_message(bytes(data), len(data), C.byref(m))
+    return rc, m
+
+
+def decode_batch(data, off, length, group, capacity, group_n, peers):
+    """hb_decode's contract on the CPU.  Returns dict of batch arrays + status."""
+    n = len(off)
+    d = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray)
+                             else data, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    group = np.ascontiguousarray(group, dtype=np.uint32)
+    group_n = np.ascontiguousarray(group_n, dtype=np.uint32)
+    peers = np.ascontiguousarray(peers, dtype=np.uint64)
+    out = dict(group=np.zeros(n, np.uint32), info=np.zeros(n, np.uint32), term=np.zeros(n, np.uint64),
+               index=np.zeros(n, np.uint64), hint=np.zeros(n, np.uint64), status=np.zeros(n, np.uint8))
+    lib().orc_decode_batch(d.ctypes.data, off.ctypes.data, length.ctypes.data, group.ctypes.data, n, capacity,
+                           group_n.ctypes.data, peers.ctypes.data, out["group"].ctypes.data, out["info"].ctypes.data,
+                           out["term"].ctypes.data, out["index"].ctypes.data, out["hint"].ctypes.data,
+                           out["status"].ctypes.data)
+    return out
+
+
 class orc_raft(C.Structure):
     _fields_ = [
         ("id", C.c_uint64), ("Term", C.c_uint64), ("Vote", C.c_uint64), ("Commit", C.c_uint64),
@@ -138,6 +171,10 @@ def lib():
             "orc_groups_load": (C.c_int, [R, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_uint64]),
             "orc_groups_export": (None, [R, C.c_uint32, C.c_void_p]),
             "orc_raft_tick": (C.c_int, [R, P(C.c_uint64), C.c_uint64]),
+            "orc_unmarshal_message": (C.c_int, [C.c_char_p, C.c_int64, P(orc_wire_msg)]),
+            "orc_decode_batch": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_void_p]),
             "orc_tick_batch": (C.c_int, [R, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                          P(C.c_uint64), P(C.c_uint64)]),
             "orc_groups_load_timers": (None, [R, C.c_uint32, C.c_void_p]),

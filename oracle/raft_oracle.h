@@ -206,6 +206,21 @@ int orc_tick_batch(orc_raft* groups, uint32_t ngroups, const uint64_t* draws, ui
 void orc_groups_load_timers(orc_raft* gs, uint32_t n, const hb_timer* t);
 void orc_groups_export_timers(const orc_raft* gs, uint32_t n, hb_timer* out);
 
+/* ---- wire decoding (wire_oracle.c: raft/raftpb/raft.pb.go Unmarshal) ---- */
+typedef struct orc_wire_msg {
+  int32_t type;
+  uint64_t to, from, term, log_term, index, commit, reject_hint;
+  int reject;
+  uint32_t nentries;
+} orc_wire_msg;
+/* 0 = ok, 1 = Unmarshal error, 2 = Go panic / endless loop, 3 = groups nested too deep */
+int  orc_unmarshal_message(const uint8_t* data, int64_t len, orc_wire_msg* m);
+/* hb_decode's contract on the CPU; peers [capacity][HB_MAX_REPLICAS], group_n [capacity] */
+void orc_decode_batch(const uint8_t* bytes, const uint64_t* off, const uint32_t* len, const uint32_t* group,
+                      uint64_t n, uint32_t capacity, const uint32_t* group_n, const uint64_t* peers,
+                      uint32_t* o_group, uint32_t* o_info, uint64_t* o_term, uint64_t* o_index, uint64_t* o_hint,
+                      uint8_t* status);
+
 /* Flat-array helpers so the Python harness can drive many groups via ctypes. */
 orc_raft* orc_groups_new(uint32_t ngroups);
 void      orc_groups_free(orc_raft* g, uint32_t ngroups);
