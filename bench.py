@@ -185,6 +185,38 @@ def cpu_baseline_tick(n, groups=200_000, W=256, budget_s=10.0, max_steps=50):
                       f"{steps} ticks in {spent:.2f} s, one core"}
 
 
+def cpu_baseline_wire(n, groups=100_000, W=256, budget_s=10.0, max_steps=20):
+    """The C oracle decoding the cfg2 wire records (orc_decode_batch, the
+    reference's Unmarshal restated) and stepping them, one core."""
+    from etcd_amd import abi, synth
+    from oracle.pyoracle import OracleGroups, decode_batch
+    g, runs = synth.steady_groups(groups, n, seed=0x5EED0002, with_runs="flat")
+    og = OracleGroups(g, runs, W)
+    peers = np.zeros((groups, abi.HB_MAX_REPLICAS), np.uint64)
+    peers[:, :n] = np.arange(1, n + 1, dtype=np.uint64)
+    gn = np.full(groups, n, np.uint32)
+    acks, spent, dec, steps = 0, 0.0, 0.0, 0
+    while spent < budget_s and steps < max_steps:
+        b = synth.cfg2_batch(g, steps)
+        frm = ((b["info"] >> 4) & 0xF).astype(np.uint64) + np.uint64(1)
+        data, off, ln = synth.encode_responses(abi.HB_MSG_APP_RESP, np.ones(len(frm), np.uint64), frm, b["term"],
+                                               b["index"])
+        t0 = time.perf_counter()
+        o = decode_batch(data, off, ln, b["group"], groups, gn, peers)
+        t1 = time.perf_counter()
+        _, st = og.step(dict(group=o["group"], info=o["info"], term=o["term"], index=o["index"], hint=o["hint"],
+                             props=b["props"]))
+        t2 = time.perf_counter()
+        spent += t2 - t0
+        dec += t1 - t0
+        acks += int(st[abi.HB_STAT_APPRESP])
+        steps += 1
+    return {"value": acks / spent, "unit": "MsgAppResp/s", "cores": 1, "kind": "port",
+            "decode_records_per_s": acks / dec,
+            "sample": f"oracle/wire_oracle.c + raft_oracle.c (C restatements, not the Go reference), {groups} groups "
+                      f"x {n}, {steps} cfg2 steps from wire records, {acks} MsgAppResp in {spent:.2f} s, one core"}
+
+
 def pmc_traffic(path, kernel, G, n, apply_us):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (FETCH_SIZE x 2 + WRITE_SIZE, tools/prof_summary.py).  Used only when the
@@ -215,9 +247,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4", "tick"], default="cfg2",
+    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4", "tick", "wire"], default="cfg2",
                     help="cfg2 (headline), cfg3 lagging followers, cfg4 election storm, "
-                         "tick = MultiNode.Tick over the cfg2 groups (SURVEY.md 8(f) rank 1)")
+                         "tick = MultiNode.Tick over the cfg2 groups (SURVEY.md 8(f) rank 1), "
+                         "wire = cfg2 from raftpb wire records: hb_decode + hb_step (8(f) rank 3)")
     ap.add_argument("--groups", type=int, default=None, help="groups per GPU (cfg2/cfg3: 1M, cfg4: 4M)")
     ap.add_argument("--replicas", type=int, default=None, help="cfg2: 3, cfg3: 5, cfg4: 7")
     ap.add_argument("--inflight", type=int, default=256, help="MaxInflightMsgs W (cfg3/cfg4)")
@@ -236,7 +269,7 @@ def main():
     if args.groups is None:
         args.groups = (1 << 22) if args.workload == "cfg4" else (1 << 20)
     if args.replicas is None:
-        args.replicas = {"cfg2": 3, "cfg3": 5, "cfg4": 7, "tick": 3}[args.workload]
+        args.replicas = {"cfg2": 3, "cfg3": 5, "cfg4": 7, "tick": 3, "wire": 3}[args.workload]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -430,7 +463,7 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     from etcd_amd import abi, synth
     from etcd_amd.hipbatch import Engine
     n, W, G = args.replicas, args.inflight, args.groups
-    seed = {"cfg3": 0x5EED0003, "cfg4": 0x5EED0004, "tick": 0x5EED0002}[args.workload] + rank
+    seed = {"cfg3": 0x5EED0003, "cfg4": 0x5EED0004, "tick": 0x5EED0002, "wire": 0x5EED0002}[args.workload] + rank
     stream = torch.cuda.current_stream(dev)
     total = args.warmup + args.steps
     st_acc = np.zeros(abi.HB_STAT_COUNT, np.uint64)
@@ -494,6 +527,65 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         ms_local = e0.elapsed_time(e1)
         st_acc = stats.cpu().numpy().astype(np.uint64)
         timing = "K ticks back to back"
+    elif args.workload == "wire":
+        g, _ = synth.steady_groups(G, n, seed=seed, with_runs=False)
+        b0 = synth.cfg2_batch(g, 0, seed=seed)
+        nmsg = len(b0["group"])
+        eng = Engine(G, max_replicas=n, max_inflight=W, max_batch=nmsg, device=local, stream=stream)
+        eng.load_groups(g)
+        del g
+        peers = np.zeros((G, abi.HB_MAX_REPLICAS), np.uint64)
+        peers[:, :n] = np.arange(1, n + 1, dtype=np.uint64)
+        eng.load_peers(peers)
+        frm = ((b0["info"] >> 4) & 0xF).astype(np.uint64) + np.uint64(1)
+
+        def tdev(a):
+            return torch.from_numpy(np.ascontiguousarray(a).view(
+                {1: np.uint8, 4: np.int32, 8: np.int64}[a.dtype.itemsize])).to(dev)
+        recs, wire_bytes = [], 0
+        for k in range(total):  # step k acks last + k + 1, encoded as the reference's MarshalTo writes it
+            data, off, ln = synth.encode_responses(abi.HB_MSG_APP_RESP, np.ones(nmsg, np.uint64), frm, b0["term"],
+                                                   b0["index"] + np.uint64(k))
+            recs.append((tdev(data), tdev(off), tdev(ln)))
+            wire_bytes = len(data)
+        d_group, d_props = tdev(b0["group"]), tdev(b0["props"])
+        out = {"group": torch.empty(nmsg, dtype=torch.int32, device=dev),
+               "info": torch.empty(nmsg, dtype=torch.int32, device=dev),
+               "term": torch.empty(nmsg, dtype=torch.int64, device=dev),
+               "index": torch.empty(nmsg, dtype=torch.int64, device=dev),
+               "hint": torch.empty(nmsg, dtype=torch.int64, device=dev)}
+        status = torch.empty(nmsg, dtype=torch.uint8, device=dev)
+        stats = torch.zeros(abi.HB_STAT_COUNT, dtype=torch.int64, device=dev)
+
+        def one(k):
+            eng.decode(recs[k][0], recs[k][1], recs[k][2], d_group, out, status)
+            eng.step(out["group"], out["info"], out["term"], out["index"], out["hint"], d_props, host=False)
+        for k in range(args.warmup):
+            one(k)
+        eng.set_stats_accum(stats)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for k in range(args.warmup, total):
+            one(k)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms_local = e0.elapsed_time(e1)
+        st_acc = stats.cpu().numpy().astype(np.uint64)
+        bad = int((status != abi.HB_WIRE_OK).sum().item())
+        # the decode kernel alone (it only writes the batch arrays, so it replays)
+        eng.set_stats_accum(None)
+        d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        d0.record(stream)
+        for k in range(args.warmup, total):
+            eng.decode(recs[k][0], recs[k][1], recs[k][2], d_group, out, status)
+        d1.record(stream)
+        torch.cuda.synchronize()
+        dec_us = d0.elapsed_time(d1) * 1e3 / args.steps
+        alg = wire_bytes + nmsg * (8 + 4 + 4) + nmsg * (4 + 4 + 8 + 8 + 8 + 1)
+        timing = "K (hb_decode + hb_step) back to back, wire records resident in HBM"
     else:
         g, _ = synth.lagging_groups(G, n, seed=seed, W=W)
         eng = Engine(G, max_replicas=n, max_inflight=W, max_batch=2 * G * n + G, device=local, stream=stream)
@@ -523,7 +615,22 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     ms = float(ms_t.item())
     st = st_t.cpu().numpy().view(np.uint64)
     sec = ms / 1e3
-    if args.workload == "tick":
+    if args.workload == "wire":
+        metric, unit, val = "MsgAppResp applied/sec from raftpb wire records (hb_decode + hb_step, cfg2)", \
+            "MsgAppResp/s", int(st[abi.HB_STAT_APPRESP]) / sec
+        extra = {"commits_per_s": int(st[abi.HB_STAT_COMMITS]) / sec,
+                 "decode": {"us_per_batch": round(dec_us, 2), "records_per_s": nmsg / (dec_us * 1e-6),
+                            "wire_bytes_per_batch": wire_bytes, "records_not_ok": bad,
+                            "roofline": {"bound": "hbm", "kernel": "k_decode",
+                                         "achieved": round(alg / (dec_us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                                         "unit": "GB/s", "frac": round(alg / (dec_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                                         "alg_bytes_per_launch": alg,
+                                         "alg_bytes_note": "record bytes + off/len/group 16 B + batch record "
+                                                           "32 B + status 1 B per record"}}}
+        ok = int(st[abi.HB_STAT_COMMITS]) == world * G * args.steps and bad == 0 and int(st[abi.HB_STAT_FAULTS]) == 0
+        wl = f"wire: cfg2 ({G} raft groups x {n} per GPU), MsgAppResp as raftpb wire records"
+        data = "synthetic (cfg2 stream encoded with the reference's MarshalTo layout)"
+    elif args.workload == "tick":
         metric, unit, val = "group ticks/sec (MultiNode.Tick over 1M groups x 3)", "group-ticks/s", \
             world * G * args.steps / sec
         extra = {"msgs_stepped_per_s": int(st[abi.HB_STAT_MSGS]) / sec, "events_per_s": int(st[abi.HB_STAT_EVENTS]) / sec,
@@ -559,7 +666,7 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = {"cfg4": cpu_baseline_cfg4, "cfg3": cpu_baseline_cfg3,
-                                       "tick": cpu_baseline_tick}[args.workload](n, W=W)
+                                       "tick": cpu_baseline_tick, "wire": cpu_baseline_wire}[args.workload](n, W=W)
             except Exception as e:  # report, never fake
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out))

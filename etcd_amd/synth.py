@@ -429,3 +429,64 @@ def cfg3_open_batch(groups_now, rng, lag_p=0.2, stale_p=0.05, reject_p=0.05, hb_
     return dict(group=mg[order].astype(np.uint32), info=mi[order].astype(np.uint32),
                 term=mt[order].astype(np.uint64), index=mx[order].astype(np.uint64),
                 hint=mh[order].astype(np.uint64), props=props)
+
+
+# ---------------------------------------------------------------------------- wire
+def _varint_len(v):
+    v = np.asarray(v, dtype=np.uint64)
+    n = np.ones(v.shape, dtype=np.int64)
+    x = v >> np.uint64(7)
+    while np.any(x):
+        n += (x != 0)
+        x = x >> np.uint64(7)
+    return n
+
+
+def encode_responses(mtype, to, frm, term, index, reject=None, hint=None):
+    """Vectorized raftpb.Message encoding of response records exactly as the
+    reference's generated MarshalTo writes them (raft/raftpb/raft.pb.go:
+    1271-1330: every required field in field order, LogTerm / Commit 0, no
+    entries, the empty non-nullable snapshot).  Returns (bytes u8, off u64,
+    len u32)."""
+    N = len(term)
+    reject = np.zeros(N, np.uint64) if reject is None else np.asarray(reject, np.uint64)
+    hint = np.zeros(N, np.uint64) if hint is None else np.asarray(hint, np.uint64)
+    cols = [np.full(N, mtype, np.uint64) if np.isscalar(mtype) else np.asarray(mtype, np.uint64),
+            np.asarray(to, np.uint64), np.asarray(frm, np.uint64), np.asarray(term, np.uint64),
+            np.zeros(N, np.uint64), np.asarray(index, np.uint64),
+            np.zeros(N, np.uint64)]  # commit
+    keys = [0x08, 0x10, 0x18, 0x20, 0x28, 0x30, 0x40]
+    # field 9: the empty snapshot {metadata {conf_state {}, index 0, term 0}}
+    snap = np.frombuffer(bytes([0x4A, 0x08, 0x12, 0x06, 0x0A, 0x00, 0x10, 0x00, 0x18, 0x00]), np.uint8)
+    rej = (reject != 0).astype(np.uint64)
+    lens = [_varint_len(c) for c in cols]
+    hlen = _varint_len(hint)
+    rec_len = sum(1 + l for l in lens) + len(snap) + 2 + 1 + hlen
+    off = np.zeros(N, np.uint64)
+    if N > 1:
+        off[1:] = np.cumsum(rec_len[:-1]).astype(np.uint64)
+    out = np.zeros(max(int(rec_len.sum()), 1), np.uint8)
+    pos = off.astype(np.int64)
+
+    def put_varint(pos, c, l, k):
+        out[pos] = k
+        pos = pos + 1
+        v = c.copy()
+        for b in range(int(l.max()) if N else 0):
+            live = b < l
+            byte = (v & np.uint64(0x7F)).astype(np.uint8) | np.where(b + 1 < l, 0x80, 0).astype(np.uint8)
+            out[pos[live] + b] = byte[live]
+            v = v >> np.uint64(7)
+        return pos + l
+
+    for c, l, k in zip(cols[:6], lens[:6], keys[:6]):
+        pos = put_varint(pos, c, l, k)
+    pos = put_varint(pos, cols[6], lens[6], keys[6])  # commit (field 8), after the absent entries
+    for j, b in enumerate(snap):
+        out[pos + j] = b
+    pos = pos + len(snap)
+    out[pos] = 0x50
+    out[pos + 1] = rej.astype(np.uint8)
+    pos = pos + 2
+    pos = put_varint(pos, hint, hlen, 0x58)
+    return out, off, rec_len.astype(np.uint32)

@@ -57,6 +57,22 @@ def test_gogo_encoder_matches_protobuf_library():
         assert rc == OK and o.index == vals[4] and o.nentries == 1
 
 
+def test_vectorized_encoder_matches_gogo():
+    """synth.encode_responses (the bench's encoder) == the restated MarshalTo."""
+    from etcd_amd import synth
+    rng = np.random.default_rng(2)
+    N = 400
+    t = rng.choice(W.RESP_TYPES, N).astype(np.uint64)
+    to, frm = rng.integers(0, 1 << 20, N), rng.integers(0, 1 << 62, N)
+    term, idx = rng.integers(0, 1 << 40, N), rng.integers(0, 1 << 63, N)
+    rej, hint = rng.integers(0, 2, N), rng.integers(0, 1 << 45, N)
+    data, off, ln = synth.encode_responses(t, to, frm, term, idx, rej, hint)
+    for i in range(N):
+        want = W.gogo_marshal(int(t[i]), to=int(to[i]), frm=int(frm[i]), term=int(term[i]), index=int(idx[i]),
+                              reject=bool(rej[i]), hint=int(hint[i]))
+        assert bytes(data[int(off[i]):int(off[i]) + int(ln[i])]) == want, i
+
+
 def test_appresp_wire_size():
     """A steady-state MsgAppResp as the reference encodes it."""
     b = W.gogo_marshal(abi.HB_MSG_APP_RESP, to=1, frm=2, term=7, index=1 << 20)
