@@ -584,7 +584,8 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         d1.record(stream)
         torch.cuda.synchronize()
         dec_us = d0.elapsed_time(d1) * 1e3 / args.steps
-        alg = wire_bytes + nmsg * (8 + 4 + 4) + nmsg * (4 + 4 + 8 + 8 + 8 + 1)
+        # + the From -> slot lookup: the group's n peer ids and n (one 64-byte row)
+        alg = wire_bytes + nmsg * (8 + 4 + 4) + nmsg * (n + 1) * 8 + nmsg * (4 + 4 + 8 + 8 + 8 + 1)
         timing = "K (hb_decode + hb_step) back to back, wire records resident in HBM"
     else:
         g, _ = synth.lagging_groups(G, n, seed=seed, W=W)
@@ -625,8 +626,9 @@ def run_aux(args, world, rank, local, dev, torch, dist):
                                          "achieved": round(alg / (dec_us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS,
                                          "unit": "GB/s", "frac": round(alg / (dec_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                                          "alg_bytes_per_launch": alg,
-                                         "alg_bytes_note": "record bytes + off/len/group 16 B + batch record "
-                                                           "32 B + status 1 B per record"}}}
+                                         "alg_bytes_note": f"record bytes + off/len/group 16 B + peer ids and "
+                                                           f"n {(n + 1) * 8} B + batch record 32 B + status 1 B "
+                                                           f"per record"}}}
         ok = int(st[abi.HB_STAT_COMMITS]) == world * G * args.steps and bad == 0 and int(st[abi.HB_STAT_FAULTS]) == 0
         wl = f"wire: cfg2 ({G} raft groups x {n} per GPU), MsgAppResp as raftpb wire records"
         data = "synthetic (cfg2 stream encoded with the reference's MarshalTo layout)"

@@ -1072,7 +1072,7 @@ struct DecodeArgs {
   const uint32_t* group;
   uint64_t n;
   const uint64_t* meta;
-  const uint64_t* peer;  // [nmax][G] or null
+  const uint4* peer;  // [G] rows of HB_PEER_ROW node ids (64 B), or null
   uint32_t G, nmax;
   uint32_t* o_group;
   uint32_t* o_info;
@@ -1082,12 +1082,11 @@ struct DecodeArgs {
   uint8_t* status;
 };
 
-__global__ void __launch_bounds__(256) k_decode(DecodeArgs a) {
-  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k >= a.n) return;
-  WireMsg m;
-  const int rc = w_unmarshal_message(a.bytes + a.off[k], (int64_t)a.len[k], &m);
-  const uint32_t g = a.group[k];
+constexpr uint32_t HB_PEER_ROW = 8;  // u64 per group peer row: node ids of slots 0..6, then n
+
+// Outcome of one record -> batch record + status (shared by both passes).
+__device__ __forceinline__ void dec_emit(const DecodeArgs& a, uint64_t k, int rc, const WireMsg& m, uint32_t g, bool gok,
+                                         const uint64_t* ids) {
   uint32_t st;
   if (rc == W_ERR) st = HB_WIRE_ERROR;
   else if (rc == W_PANIC) st = HB_WIRE_PANIC;
@@ -1097,13 +1096,14 @@ __global__ void __launch_bounds__(256) k_decode(DecodeArgs a) {
     st = HB_WIRE_LOCAL;  // IsLocalMsg raft/util.go:49-51
   else if (m.type != HB_MSG_APP_RESP && m.type != HB_MSG_VOTE_RESP && m.type != HB_MSG_HEARTBEAT_RESP)
     st = HB_WIRE_HOST;
-  else if (g >= a.G) st = HB_WIRE_BADGROUP;
+  else if (!gok) st = HB_WIRE_BADGROUP;
   else st = HB_WIRE_OK;
   uint32_t slot = HB_SLOT_NONE;
   if (st == HB_WIRE_OK && a.peer && m.from != 0) {
-    const uint32_t nn = m_n(a.meta[g]);
-    for (uint32_t s = 0; s < a.nmax; ++s)
-      if (s < nn && slot == HB_SLOT_NONE && a.peer[(size_t)s * a.G + g] == m.from) slot = s;
+    const uint32_t nn = (uint32_t)ids[HB_PEER_ROW - 1];
+#pragma unroll
+    for (uint32_t s = 0; s < HB_MAX_REPLICAS; ++s)
+      if (s < nn && slot == HB_SLOT_NONE && ids[s] == m.from) slot = s;
   }
   const bool ok = st == HB_WIRE_OK;
   a.o_group[k] = ok ? g : 0xFFFFFFFFu;
@@ -1112,6 +1112,112 @@ __global__ void __launch_bounds__(256) k_decode(DecodeArgs a) {
   a.o_index[k] = ok ? m.index : 0ull;
   a.o_hint[k] = ok ? m.hint : 0ull;
   a.status[k] = (uint8_t)st;
+}
+
+// Pass 1 (k_decode): a wave's 64 records are contiguous in the usual layout,
+// so the wave copies their span into its own LDS window with coalesced
+// 16-byte loads (bytes at the unaligned ends one by one, so nothing outside
+// the span is read) and each lane runs the straight-line MarshalTo-shape
+// parser (w_fast_message) from LDS.  A record of any other shape (or a wave
+// whose span does not fit the window) is queued for pass 2, k_decode_general,
+// which runs the full Message.Unmarshal restatement over the queue only: its
+// register and scratch footprint never limits the occupancy of pass 1.
+constexpr uint32_t DEC_THREADS = 256;
+constexpr uint32_t DEC_WIN = 4096;  // bytes of records staged per wave
+constexpr uint32_t DEC_GEN_BLOCKS = 128;  // pass 2 is the exception path; scratch-heavy waves are costly to launch
+__global__ void __launch_bounds__(DEC_THREADS) k_decode(DecodeArgs a, uint32_t* q, uint32_t* qn) {
+  __shared__ uint4 l_win[DEC_THREADS / 64][DEC_WIN / 16 + 2];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t k = (uint64_t)blockIdx.x * DEC_THREADS + threadIdx.x;
+  const bool live = k < a.n;
+  const uint64_t o = live ? a.off[k] : 0ull;
+  const uint32_t len = live ? a.len[k] : 0u;
+  uint64_t lo = live ? o : ~0ull, hi = live ? o + len : 0ull;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t l2 = __shfl_xor(lo, d), h2 = __shfl_xor(hi, d);
+    lo = l2 < lo ? l2 : lo;
+    hi = h2 > hi ? h2 : hi;
+  }
+  const bool fits = hi > lo && hi - lo <= DEC_WIN;  // uniform in the wave
+  uint8_t* win = reinterpret_cast<uint8_t*>(&l_win[wave][0]);
+  const uintptr_t A = reinterpret_cast<uintptr_t>(a.bytes) + lo, B = reinterpret_cast<uintptr_t>(a.bytes) + hi;
+  const uintptr_t base = A & ~(uintptr_t)15;
+  if (fits) {
+    const uintptr_t A16 = (A + 15) & ~(uintptr_t)15, B16 = B & ~(uintptr_t)15;
+    if (A16 < B16) {
+      const uint32_t nc = (uint32_t)((B16 - A16) >> 4), c0 = (uint32_t)((A16 - base) >> 4);
+      for (uint32_t c = lane; c < nc; c += 64) l_win[wave][c0 + c] = reinterpret_cast<const uint4*>(A16)[c];
+      for (uintptr_t x = A + lane; x < A16; x += 64) win[x - base] = *reinterpret_cast<const uint8_t*>(x);
+      for (uintptr_t x = B16 + lane; x < B; x += 64) win[x - base] = *reinterpret_cast<const uint8_t*>(x);
+    } else {
+      for (uintptr_t x = A + lane; x < B; x += 64) win[x - base] = *reinterpret_cast<const uint8_t*>(x);
+    }
+  }
+  __syncthreads();
+  if (!live) return;
+  // the group's peer row and meta are random gathers: issue them before the
+  // parse so their latency hides behind it
+  const uint32_t g = a.group[k];
+  const bool gok = g < a.G;
+  uint4 prow[4] = {};
+  if (gok && a.peer) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) prow[j] = a.peer[(size_t)g * 4 + j];
+  }
+  WireMsg m;
+  const bool fast = fits && w_fast_message(win + (reinterpret_cast<uintptr_t>(a.bytes) + o - base), (int64_t)len, &m);
+  // wave-aggregated append of the other records to the pass-2 queue
+  const uint64_t slow = __ballot(!fast);
+  if (slow) {
+    const uint32_t cnt = (uint32_t)__popcll(slow);
+    const uint32_t leader = (uint32_t)__ffsll((long long)slow) - 1;
+    uint32_t b0 = 0;
+    if (lane == leader) b0 = atomicAdd(qn, cnt);
+    b0 = __shfl(b0, (int)leader);
+    if (!fast) q[b0 + (uint32_t)__popcll(slow & ((1ull << lane) - 1))] = (uint32_t)k;
+  }
+  if (!fast) return;
+  dec_emit(a, k, W_OK, m, g, gok, reinterpret_cast<const uint64_t*>(prow));
+}
+
+// row[7] of a group's peer row = its replica count n (from meta), so the
+// From -> slot lookup reads one 64-byte row and no meta.  Refreshed whenever
+// either side (hb_load_groups / hb_load_peers) changes.
+__global__ void k_peer_n(uint64_t* peer, const uint64_t* meta, uint32_t first, uint32_t count) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) peer[(size_t)(first + i) * HB_PEER_ROW + HB_PEER_ROW - 1] = m_n(meta[first + i]);
+}
+
+// Pass 2: Message.Unmarshal (hipbatch_wire.h) for the queued records, read
+// from global memory.  Grid-stride over the queue length written by pass 1;
+// the last workgroup to finish clears the queue for the next hb_decode.
+__global__ void __launch_bounds__(DEC_THREADS) k_decode_general(DecodeArgs a, const uint32_t* q, uint32_t* qn) {
+  const uint32_t total = *(volatile uint32_t*)qn;
+  for (uint32_t j = blockIdx.x * DEC_THREADS + threadIdx.x; j < total; j += gridDim.x * DEC_THREADS) {
+    const uint64_t k = q[j];
+    const uint32_t g = a.group[k];
+    const bool gok = g < a.G;
+    uint64_t ids[HB_PEER_ROW] = {};
+    if (gok && a.peer) {
+      const uint64_t* row = reinterpret_cast<const uint64_t*>(a.peer) + (size_t)g * HB_PEER_ROW;
+#pragma unroll
+      for (uint32_t s = 0; s < HB_PEER_ROW; ++s) ids[s] = row[s];
+    }
+    WireMsg m;
+    const int rc = w_unmarshal_message(a.bytes + a.off[k], (int64_t)a.len[k], &m);
+    dec_emit(a, k, rc, m, g, gok, ids);
+  }
+  // qn[1] counts finished workgroups; the last one resets both words
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(qn + 1, 1u) == gridDim.x - 1) {
+      qn[0] = 0;
+      qn[1] = 0;
+      __threadfence();
+    }
+  }
 }
 
 // ============================================================================
@@ -1362,7 +1468,10 @@ struct hb_handle {
   uint32_t* pflag = nullptr;      // [NB][PART/32]
   uint32_t* resume = nullptr;     // [G]
   uint64_t* commit0 = nullptr;    // [G]
-  uint64_t* peer = nullptr;       // [nmax][G] node ids (hb_load_peers), allocated on first use
+  uint64_t* peer = nullptr;       // [G][HB_PEER_ROW] node ids (hb_load_peers), allocated on first use
+  uint32_t* dec_q = nullptr;      // hb_decode pass-2 queue (record indices)
+  uint64_t dec_cap = 0;
+  uint32_t* dec_qn = nullptr;     // [queue length, finished pass-2 workgroups]
   uint64_t* rnd = nullptr;        // the r.rand stream (hb_set_rand), grown on demand
   uint64_t rnd_cap = 0;
   static constexpr uint32_t PROF_RING = 256;
@@ -1581,6 +1690,8 @@ int hb_destroy(hb_handle* h) {
   }
   if (h->rnd) (void)hipFree(h->rnd);
   if (h->peer) (void)hipFree(h->peer);
+  if (h->dec_q) (void)hipFree(h->dec_q);
+  if (h->dec_qn) (void)hipFree(h->dec_qn);
   if (h->in_ready) (void)hipEventDestroy(h->in_ready);
   if (h->prep) (void)hipStreamDestroy(h->prep);
   delete h;
@@ -1629,6 +1740,9 @@ int hb_load_groups(hb_handle* h, uint32_t first, uint32_t count, const hb_group*
   hipError_t e = hipMemcpyAsync(d, groups, sizeof(hb_group) * count, hipMemcpyHostToDevice, h->stream);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_load, dim3((count + 255) / 256), dim3(256), 0, h->stream, h->st, first, count, d);
+    if (h->peer)
+      hipLaunchKernelGGL(k_peer_n, dim3((count + 255) / 256), dim3(256), 0, h->stream, h->peer, h->st.meta, first,
+                         count);
     e = hipStreamSynchronize(h->stream);
   }
   (void)hipFree(d);
@@ -1745,15 +1859,19 @@ int hb_load_peers(hb_handle* h, uint32_t first, uint32_t count, const uint64_t* 
   DeviceGuard guard(h->device);
   const size_t G = h->G;
   if (!h->peer) {
-    HB_CHECK(hipMalloc(&h->peer, (size_t)h->nmax * G * 8));
-    HB_CHECK(hipMemsetAsync(h->peer, 0, (size_t)h->nmax * G * 8, h->stream));
+    HB_CHECK(hipMalloc(&h->peer, G * HB_PEER_ROW * 8));
+    HB_CHECK(hipMemsetAsync(h->peer, 0, G * HB_PEER_ROW * 8, h->stream));
   }
-  std::vector<uint64_t> row(count);
-  for (uint32_t s = 0; s < h->nmax; ++s) {
-    for (uint32_t i = 0; i < count; ++i) row[i] = ids[(size_t)i * HB_MAX_REPLICAS + s];
-    HB_CHECK(hipMemcpyAsync(h->peer + s * G + first, row.data(), count * 8ull, hipMemcpyHostToDevice, h->stream));
-    HB_CHECK(hipStreamSynchronize(h->stream));  // row is reused
-  }
+  // one 64-byte row per group (k_decode reads it with one gather): slots
+  // 0..nmax-1, zeros, then n (k_peer_n)
+  std::vector<uint64_t> rows((size_t)count * HB_PEER_ROW, 0);
+  for (uint32_t i = 0; i < count; ++i)
+    for (uint32_t s = 0; s < h->nmax; ++s) rows[(size_t)i * HB_PEER_ROW + s] = ids[(size_t)i * HB_MAX_REPLICAS + s];
+  HB_CHECK(hipMemcpyAsync(h->peer + (size_t)first * HB_PEER_ROW, rows.data(), rows.size() * 8, hipMemcpyHostToDevice,
+                          h->stream));
+  hipLaunchKernelGGL(k_peer_n, dim3((count + 255) / 256), dim3(256), 0, h->stream, h->peer, h->st.meta, first, count);
+  HB_CHECK(hipGetLastError());
+  HB_CHECK(hipStreamSynchronize(h->stream));  // rows is freed on return
   return HB_OK;
 }
 
@@ -1761,6 +1879,7 @@ int hb_decode(hb_handle* h, const uint8_t* bytes, const uint64_t* off, const uin
               uint64_t n, const hb_batch* out, uint8_t* status) {
   if (!h || !out) return HB_EINVAL;
   if (n == 0) return HB_OK;
+  if (n >= (1ull << 32)) return HB_EINVAL;  // record indices are 32-bit in the pass-2 queue
   if (!bytes || !off || !len || !group || !status || !out->group || !out->info || !out->term || !out->index ||
       !out->hint)
     return HB_EINVAL;
@@ -1772,7 +1891,7 @@ int hb_decode(hb_handle* h, const uint8_t* bytes, const uint64_t* off, const uin
   da.group = group;
   da.n = n;
   da.meta = h->st.meta;
-  da.peer = h->peer;
+  da.peer = reinterpret_cast<const uint4*>(h->peer);
   da.G = h->G;
   da.nmax = h->nmax;
   da.o_group = const_cast<uint32_t*>(out->group);
@@ -1783,7 +1902,23 @@ int hb_decode(hb_handle* h, const uint8_t* bytes, const uint64_t* off, const uin
   da.status = status;
   // on the stream the batches come from, so hb_step's prep orders after it
   hipStream_t ds = h->in_stream_set ? h->in_stream : h->stream;
-  hipLaunchKernelGGL(k_decode, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ds, da);
+  if (n > h->dec_cap) {  // the pass-2 queue holds up to n record indices
+    if (h->dec_q) (void)hipFree(h->dec_q);
+    h->dec_q = nullptr;
+    h->dec_cap = 0;
+    HB_CHECK(hipMalloc(&h->dec_q, n * sizeof(uint32_t)));
+    h->dec_cap = n;
+  }
+  if (!h->dec_qn) {
+    HB_CHECK(hipMalloc(&h->dec_qn, 2 * sizeof(uint32_t)));
+    HB_CHECK(hipMemsetAsync(h->dec_qn, 0, 2 * sizeof(uint32_t), ds));
+  }
+  hipLaunchKernelGGL(k_decode, dim3((unsigned)((n + DEC_THREADS - 1) / DEC_THREADS)), dim3(DEC_THREADS), 0, ds, da,
+                     h->dec_q, h->dec_qn);
+  HB_CHECK(hipGetLastError());
+  const uint64_t gb = (n + DEC_THREADS - 1) / DEC_THREADS;
+  hipLaunchKernelGGL(k_decode_general, dim3((unsigned)(gb < DEC_GEN_BLOCKS ? gb : DEC_GEN_BLOCKS)), dim3(DEC_THREADS), 0,
+                     ds, da, h->dec_q, h->dec_qn);
   HB_CHECK(hipGetLastError());
   return HB_OK;
 }

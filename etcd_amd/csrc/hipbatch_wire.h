@@ -203,6 +203,63 @@ __device__ __forceinline__ int w_parse_sub(const uint8_t* d, int64_t l) {
   return W_OK;
 }
 
+// Fast path for the record shape Message.MarshalTo writes for the messages
+// the engine consumes (raft/raftpb/raft.pb.go:1271-1330): every scalar field
+// once, in field order, no entries, the empty Snapshot (data absent, empty
+// ConfState, index 0, term 0), each varint at most 10 bytes.  On that shape
+// the general parser runs the same field assignments in the same order, so
+// the result is identical; anything else returns false and the record goes
+// to w_unmarshal_message.  Straight-line code with a handful of registers, so
+// the common case does not pay for the general parser's occupancy.
+__device__ __forceinline__ bool w_fast_varint(const uint8_t* d, int64_t l, int64_t& i, uint64_t& v) {
+  v = 0;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    if (i >= l) return false;
+    const uint32_t b = d[i++];
+    v |= (uint64_t)(b & 0x7F) << (7 * k);  // k = 9: bits past 63 drop, as Go's shift
+    if (b < 0x80) return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool w_fast_message(const uint8_t* d, int64_t l, WireMsg* m) {
+  int64_t i = 0;
+  uint64_t v[9];
+  // keys of fields 1..6, 8 (varint), then the empty snapshot, 10, 11
+  const uint8_t keys[7] = {0x08, 0x10, 0x18, 0x20, 0x28, 0x30, 0x40};
+#pragma unroll
+  for (int f = 0; f < 7; ++f) {
+    if (i >= l || d[i] != keys[f]) return false;
+    ++i;
+    if (!w_fast_varint(d, l, i, v[f])) return false;
+  }
+  // 4a 08 | 12 06 | 0a 00 | 10 00 | 18 00 : Snapshot{Metadata{ConfState{}, 0, 0}}
+  if (i + 10 > l) return false;
+  const uint8_t snap[10] = {0x4a, 0x08, 0x12, 0x06, 0x0a, 0x00, 0x10, 0x00, 0x18, 0x00};
+  bool same = true;
+#pragma unroll
+  for (int j = 0; j < 10; ++j) same &= d[i + j] == snap[j];
+  if (!same) return false;
+  i += 10;
+  if (i >= l || d[i] != 0x50) return false;
+  ++i;
+  if (!w_fast_varint(d, l, i, v[7])) return false;
+  if (i >= l || d[i] != 0x58) return false;
+  ++i;
+  if (!w_fast_varint(d, l, i, v[8])) return false;
+  if (i != l) return false;
+  // MessageType is int32: the low 32 bits of the accumulated varint (shifts
+  // of 28 and more wrap inside int32, exactly the general parser's `t`)
+  m->type = (int32_t)(uint32_t)v[0];
+  m->from = v[2];
+  m->term = v[3];
+  m->index = v[5];
+  m->reject = v[7] != 0;
+  m->hint = v[8];
+  return true;
+}
+
 // Message.Unmarshal (raft/raftpb/raft.pb.go:549-799)
 __device__ int w_unmarshal_message(const uint8_t* d, int64_t l, WireMsg* m) {
   m->type = 0;

@@ -97,3 +97,36 @@ def test_decode_then_step_cfg2():
         assert np.array_equal(dev_st, ora_st)
         assert_groups_equal(pair.eng.get_groups(), pair.og.groups(), f"wire step {step}")
         assert dev_st[abi.HB_STAT_COMMITS] == G
+
+
+def test_decode_slots_beyond_n_and_load_order():
+    """From -> slot looks only at slots < n of the group (raft/multinode.go:235
+    drops the rest as non-members), whichever of hb_load_peers /
+    hb_load_groups came first; groups of different n share one handle."""
+    import torch
+    from etcd_amd.hipbatch import Engine
+    G = 2048
+    rng = np.random.default_rng(9)
+    g3, _ = synth.steady_groups(G // 2, 3, seed=3, with_runs=False)
+    g5, _ = synth.steady_groups(G // 2, 5, seed=4, with_runs=False)
+    eng = Engine(G, max_replicas=5, max_inflight=8, max_batch=1 << 16)
+    peers = np.zeros((G, abi.HB_MAX_REPLICAS), np.uint64)
+    peers[:, :5] = np.arange(1, 6, dtype=np.uint64)  # ids beyond n = 3 are set: they must not match
+    eng.load_peers(peers)       # before the groups (n comes from hb_load_groups)
+    eng.load_groups(g3, first=0)
+    eng.load_groups(g5, first=G // 2)
+    eng.load_peers(peers[G // 2:], first=G // 2)  # and after
+    N = 6 * G
+    grp = rng.integers(0, G, N).astype(np.uint32)
+    frm = rng.integers(1, 7, N)
+    recs = [W.gogo_marshal(abi.HB_MSG_APP_RESP, to=1, frm=int(f), term=7, index=int(i))
+            for f, i in zip(frm, rng.integers(0, 1 << 40, N))]
+    data, off, ln = W.pack(recs)
+    out, status = _decode_dev(eng, torch, data, off, ln, grp)
+    nn = np.where(np.arange(G) < G // 2, 3, 5).astype(np.uint32)
+    ora = decode_batch(data, off, ln, grp, G, nn, peers)
+    assert np.array_equal(status.cpu().numpy(), ora["status"])
+    info = out["info"].cpu().numpy().view(np.uint32)
+    assert np.array_equal(info, ora["info"])
+    slot = (info >> 4) & 0xF
+    assert ((slot == abi.HB_SLOT_NONE) == ((frm > nn[grp]) | (frm > 5))).all()
