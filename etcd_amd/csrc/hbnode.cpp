@@ -1,0 +1,1465 @@
+// hbnode.cpp — host side of raft.MultiNode over the MI355X engine (include/hbnode.h).
+//
+// The device (libhipbatch) steps the leader bookkeeping of every group in one
+// launch per Ready cycle and reports what changed as an ordered event stream
+// per group.  This file is the rest of the reference's `multiNode.run` loop
+// (raft/multinode.go:166-322) that stays on the host:
+//
+//   MemoryStorage        raft/storage.go:63-248
+//   raftLog (host half)  raft/log.go:23-308, unstable raft/log_unstable.go:20-140
+//   newReady / commitReady / containsUpdates
+//                        raft/node.go:82-100, 447-463; raft/multinode.go:137-164
+//   message materialisation from the device's send intents
+//                        raft/raft.go:227-321 (send, sendAppend, sendHeartbeat),
+//                        :429-443 (campaign's MsgVote), :614-624 (MsgProp forward)
+//   pendingConf          raft/raft.go:406-427 (becomeLeader scan), :500-513
+//   CreateGroup          raft/multinode.go:181-217 + newRaft raft/raft.go:157-209
+//   ApplyConfChange      raft/multinode.go:239-262, raft/raft.go:729-750
+//   Status               raft/status.go:34-49
+//
+// Nothing here steps raft: every Step/Campaign/Propose/Report goes into the
+// device batch, and the host only replays the events the device returns.
+#include "../../include/hbnode.h"
+
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+struct Panic {
+  std::string msg;
+};
+[[noreturn]] void panicf(const std::string& m) { throw Panic{m}; }
+
+struct Fail {
+  int code;
+};
+
+// ---------------------------------------------------------------- entries
+struct Ent {
+  uint64_t term = 0, index = 0;
+  uint32_t type = HBN_ENTRY_NORMAL;
+  bool has_data = false;
+  std::string data;
+};
+
+Ent ent_from(const hbn_entry& e) {
+  Ent x;
+  x.term = e.term;
+  x.index = e.index;
+  x.type = e.type;
+  x.has_data = e.has_data != 0;
+  if (x.has_data && e.data_len) x.data.assign(reinterpret_cast<const char*>(e.data), e.data_len);
+  return x;
+}
+
+uint64_t sov(uint64_t x) {  // sovRaft: varint length
+  uint64_t n = 0;
+  do {
+    ++n;
+    x >>= 7;
+  } while (x);
+  return n;
+}
+
+// Entry.Size() (raft/raftpb/raft.pb.go, gogo): Type, Term, Index always, Data if non-nil.
+uint64_t ent_size(uint64_t type, uint64_t term, uint64_t index, bool has_data, uint64_t len) {
+  uint64_t n = 1 + sov(type) + 1 + sov(term) + 1 + sov(index);
+  if (has_data) n += 1 + len + sov(len);
+  return n;
+}
+uint64_t ent_size(const Ent& e) { return ent_size(e.type, e.term, e.index, e.has_data, e.data.size()); }
+
+// limitSize raft/util.go:97-110
+template <class V>
+size_t limit_count(const V& ents, uint64_t max_size) {
+  if (ents.empty()) return 0;
+  uint64_t size = ent_size(ents[0]);
+  size_t limit = 1;
+  for (; limit < ents.size(); ++limit) {
+    size += ent_size(ents[limit]);
+    if (size > max_size) break;
+  }
+  return limit;
+}
+
+std::string marshal_varint(uint64_t v) {
+  std::string s;
+  while (v >= 0x80) {
+    s.push_back((char)(v | 0x80));
+    v >>= 7;
+  }
+  s.push_back((char)v);
+  return s;
+}
+
+// ConfChange.MarshalTo (raft/raftpb/raft.pb.go:1402-1426)
+std::string marshal_conf_change(uint64_t id, uint32_t type, uint64_t node, const uint8_t* ctx, uint64_t ctx_len,
+                                bool has_ctx) {
+  std::string s;
+  s.push_back(0x08);
+  s += marshal_varint(id);
+  s.push_back(0x10);
+  s += marshal_varint(type);
+  s.push_back(0x18);
+  s += marshal_varint(node);
+  if (has_ctx) {
+    s.push_back(0x22);
+    s += marshal_varint(ctx_len);
+    if (ctx_len) s.append(reinterpret_cast<const char*>(ctx), ctx_len);
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------- snapshot
+struct Snap {
+  uint64_t index = 0, term = 0;
+  std::vector<uint64_t> nodes;
+  bool has_data = false;
+  std::string data;
+};
+
+void snap_view(const Snap& s, hbn_snapshot* o) {
+  o->index = s.index;
+  o->term = s.term;
+  o->nodes = s.nodes.empty() ? nullptr : s.nodes.data();
+  o->n_nodes = (uint32_t)s.nodes.size();
+  o->has_data = s.has_data;
+  o->data = s.data.empty() ? nullptr : reinterpret_cast<const uint8_t*>(s.data.data());
+  o->data_len = s.data.size();
+}
+
+Snap snap_from(const hbn_snapshot& s) {
+  Snap x;
+  x.index = s.index;
+  x.term = s.term;
+  if (s.n_nodes) x.nodes.assign(s.nodes, s.nodes + s.n_nodes);
+  x.has_data = s.has_data != 0;
+  if (x.has_data && s.data_len) x.data.assign(reinterpret_cast<const char*>(s.data), s.data_len);
+  return x;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- MemoryStorage
+// raft/storage.go:63-248.  ents[i] has raft log position i + ents[0].Index.
+struct hbn_storage {
+  hbn_hard_state hs{0, 0, 0};
+  Snap snap;
+  std::vector<Ent> ents{Ent{}};
+  std::vector<hbn_entry> view;  // hbn_storage_entries result
+
+  uint64_t offset() const { return ents[0].index; }
+  uint64_t last_index() const { return ents[0].index + ents.size() - 1; }
+  uint64_t first_index() const { return ents[0].index + 1; }
+
+  // Term :117-125
+  int term(uint64_t i, uint64_t* t) const {
+    if (i < offset()) return HBN_ECOMPACTED;
+    if (i - offset() >= ents.size())
+      panicf("runtime error: index out of range");  // ms.ents[i-offset] in Go
+    *t = ents[i - offset()].term;
+    return HB_OK;
+  }
+  // Entries :98-114 (returns the limited range [lo, lo+k))
+  int entries(uint64_t lo, uint64_t hi, uint64_t max_size, size_t* first, size_t* count) const {
+    if (lo <= offset()) return HBN_ECOMPACTED;
+    if (hi > last_index() + 1) panicf("entries's hi(" + std::to_string(hi) + ") is out of bound lastindex(" +
+                                      std::to_string(last_index()) + ")");
+    if (ents.size() == 1) return HBN_EUNAVAILABLE;
+    if (lo > hi) panicf("runtime error: slice bounds out of range");
+    const size_t a = lo - offset(), b = hi - offset();
+    size_t k = 0;
+    if (b > a) {
+      uint64_t size = ent_size(ents[a]);
+      for (k = 1; a + k < b; ++k) {
+        size += ent_size(ents[a + k]);
+        if (size > max_size) break;
+      }
+    }
+    *first = a;
+    *count = k;
+    return HB_OK;
+  }
+  // Append :217-248
+  void append(const std::vector<Ent>& in) {
+    if (in.empty()) return;
+    const uint64_t first = ents[0].index + 1;
+    const uint64_t last = in[0].index + in.size() - 1;
+    if (last < first) return;
+    size_t skip = 0;
+    if (first > in[0].index) skip = first - in[0].index;
+    const uint64_t off = in[skip].index - ents[0].index;
+    if (ents.size() > off) {
+      ents.resize(off);
+      ents.insert(ents.end(), in.begin() + skip, in.end());
+    } else if (ents.size() == off) {
+      ents.insert(ents.end(), in.begin() + skip, in.end());
+    } else {
+      panicf("missing log entry [last: " + std::to_string(last_index()) + ", append at: " +
+             std::to_string(in[skip].index) + "]");
+    }
+  }
+};
+
+namespace {
+
+// ---------------------------------------------------------------- raftLog (host half)
+struct Log {
+  hbn_storage* st = nullptr;
+  std::vector<Ent> unstable;  // unstable.entries, position i + offset
+  uint64_t offset = 0;
+  bool has_usnap = false;     // unstable.snapshot (only set by follower-side restore: not on this path)
+  Snap usnap;
+  uint64_t committed = 0, applied = 0;
+
+  // newLog raft/log.go:41-63
+  void init(hbn_storage* s) {
+    st = s;
+    offset = s->last_index() + 1;
+    committed = s->first_index() - 1;
+    applied = s->first_index() - 1;
+  }
+  uint64_t first_index() const { return has_usnap ? usnap.index + 1 : st->first_index(); }
+  uint64_t last_index() const {
+    if (!unstable.empty()) return offset + unstable.size() - 1;
+    if (has_usnap) return usnap.index;
+    return st->last_index();
+  }
+  // unstable.maybeTerm raft/log_unstable.go:54-73
+  bool u_term(uint64_t i, uint64_t* t) const {
+    if (i < offset) {
+      if (has_usnap && usnap.index == i) {
+        *t = usnap.term;
+        return true;
+      }
+      return false;
+    }
+    if (unstable.empty() && !has_usnap) return false;
+    if (i > last_index()) return false;
+    if (i - offset >= unstable.size()) return false;
+    *t = unstable[i - offset].term;
+    return true;
+  }
+  // term raft/log.go:198-217
+  uint64_t term(uint64_t i) const {
+    const uint64_t dummy = first_index() - 1;
+    if (i < dummy || i > last_index()) return 0;
+    uint64_t t;
+    if (u_term(i, &t)) return t;
+    const int rc = st->term(i, &t);
+    if (rc == HB_OK) return t;
+    if (rc == HBN_ECOMPACTED) return 0;
+    panicf("storage term error");
+  }
+  // append :89-98 + truncateAndAppend raft/log_unstable.go:100-122
+  void append(const std::vector<Ent>& ents) {
+    if (ents.empty()) return;
+    const uint64_t after = ents[0].index - 1;
+    if (after < committed)
+      panicf("after(" + std::to_string(after) + ") is out of range [committed(" + std::to_string(committed) + ")]");
+    if (after == offset + unstable.size() - 1) {
+      unstable.insert(unstable.end(), ents.begin(), ents.end());
+    } else if (after < offset) {
+      offset = after + 1;
+      unstable = ents;
+    } else {
+      unstable.resize(after + 1 - offset);
+      unstable.insert(unstable.end(), ents.begin(), ents.end());
+    }
+  }
+  // slice raft/log.go:253-289 (copies)
+  std::vector<Ent> slice(uint64_t lo, uint64_t hi, uint64_t max_size) const {
+    if (lo > hi) panicf("invalid slice " + std::to_string(lo) + " > " + std::to_string(hi));
+    const uint64_t fi = first_index(), len = last_index() - fi + 1;
+    if (lo < fi || hi > fi + len)
+      panicf("slice[" + std::to_string(lo) + "," + std::to_string(hi) + ") out of bound [" + std::to_string(fi) +
+             "," + std::to_string(last_index()) + "]");
+    std::vector<Ent> out;
+    if (lo == hi) return out;
+    if (lo < offset) {
+      const uint64_t h = std::min(hi, offset);
+      size_t a, k;
+      const int rc = st->entries(lo, h, max_size, &a, &k);
+      if (rc == HBN_ECOMPACTED)
+        panicf("entries[" + std::to_string(lo) + ":" + std::to_string(h) + ") from storage is out of bound");
+      if (rc == HBN_EUNAVAILABLE)
+        panicf("entries[" + std::to_string(lo) + ":" + std::to_string(h) + ") is unavailable from storage");
+      out.assign(st->ents.begin() + a, st->ents.begin() + a + k);
+      if ((uint64_t)k < h - lo) return out;
+    }
+    if (hi > offset) {
+      const uint64_t a = std::max(lo, offset);
+      if (hi > offset + unstable.size())
+        panicf("unstable.slice[" + std::to_string(a) + "," + std::to_string(hi) + ") out of bound");
+      out.insert(out.end(), unstable.begin() + (a - offset), unstable.begin() + (hi - offset));
+    }
+    out.resize(limit_count(out, max_size));
+    return out;
+  }
+  // entries :219-224
+  std::vector<Ent> entries(uint64_t i, uint64_t max_size) const {
+    if (i > last_index()) return {};
+    return slice(i, last_index() + 1, max_size);
+  }
+  // nextEnts :135-141
+  std::vector<Ent> next_ents() const {
+    const uint64_t off = std::max(applied + 1, first_index());
+    if (committed + 1 > off) return slice(off, committed + 1, HB_NO_LIMIT);
+    return {};
+  }
+  Snap snapshot() const { return has_usnap ? usnap : st->snap; }
+  // appliedTo :182-190
+  void applied_to(uint64_t i) {
+    if (i == 0) return;
+    if (committed < i || i < applied)
+      panicf("applied(" + std::to_string(i) + ") is out of range [prevApplied(" + std::to_string(applied) +
+             "), committed(" + std::to_string(committed) + ")]");
+    applied = i;
+  }
+  // stableTo raft/log_unstable.go:75-88
+  void stable_to(uint64_t i, uint64_t t) {
+    uint64_t gt;
+    if (!u_term(i, &gt)) return;
+    if (gt == t && i >= offset) {
+      unstable.erase(unstable.begin(), unstable.begin() + (i + 1 - offset));
+      offset = i + 1;
+    }
+  }
+  void stable_snap_to(uint64_t i) {
+    if (has_usnap && usnap.index == i) has_usnap = false;
+  }
+};
+
+// ---------------------------------------------------------------- messages
+struct Msg {
+  uint32_t type = 0, reject = 0;
+  uint64_t to = 0, from = 0, term = 0, log_term = 0, index = 0, commit = 0, reject_hint = 0;
+  std::vector<Ent> entries;
+  bool has_snap = false;
+  Snap snap;
+};
+
+struct Soft {
+  uint64_t lead = 0;
+  uint32_t state = HB_STATE_FOLLOWER;
+  bool operator==(const Soft& o) const { return lead == o.lead && state == o.state; }
+};
+
+bool hs_equal(const hbn_hard_state& a, const hbn_hard_state& b) {
+  return a.term == b.term && a.vote == b.vote && a.commit == b.commit;
+}
+bool hs_empty(const hbn_hard_state& a) { return a.term == 0 && a.vote == 0 && a.commit == 0; }
+
+constexpr uint32_t NO_SLOT = 0xFFFFFFFFu;
+
+struct Group {
+  uint64_t id = 0;
+  uint32_t slot = NO_SLOT;  // device slot, NO_SLOT while prs is empty (host-only)
+  Log log;
+  std::vector<uint64_t> peers;  // device slot -> node id (prs, in slot order)
+  uint64_t term = 0, vote = 0, lead = 0, hs_commit = 0;
+  uint32_t state = HB_STATE_FOLLOWER;
+  Soft prev_soft;
+  hbn_hard_state prev_hard{0, 0, 0};
+  uint64_t prev_snapi = 0;
+  bool pending_conf = false;
+  uint32_t fault = 0;
+  std::deque<Msg> props;  // MsgProp in flight through the device batch, arrival order
+  std::vector<Msg> msgs;  // r.msgs since the last Ready
+  uint32_t election = 10, heartbeat = 1;
+
+  hbn_hard_state hard() const { return hbn_hard_state{term, vote, hs_commit}; }
+  Soft soft() const { return Soft{lead, state}; }
+  int slot_of(uint64_t node) const {
+    for (size_t s = 0; s < peers.size(); ++s)
+      if (peers[s] == node) return (int)s;
+    return -1;
+  }
+};
+
+struct Delivered {
+  bool has_soft = false;
+  Soft soft;
+  hbn_hard_state hard{0, 0, 0};
+  bool has_last = false;
+  uint64_t last_index = 0, last_term = 0;
+  uint64_t snap_index = 0;
+};
+
+}  // namespace
+
+struct hbn_node {
+  hb_handle* h = nullptr;
+  uint64_t id = 0;
+  uint32_t capacity = 0, nmax = 0, W = 0;
+  uint64_t max_msg = HB_NO_LIMIT, max_batch = 0;
+  std::unordered_map<uint64_t, std::unique_ptr<Group>> groups;
+  std::vector<Group*> by_slot;
+  std::vector<uint32_t> free_slots;
+  // pending device batch (host SoA, HB_STEP_HOST_PTRS)
+  std::vector<uint32_t> b_group, b_info;
+  std::vector<uint64_t> b_term, b_index, b_hint;
+  std::unordered_set<Group*> stepped;  // groups whose raft.Step runs in the pending batch
+  std::vector<hb_event> evbuf;
+  // Ready bookkeeping (raft/multinode.go:166-322)
+  std::unordered_set<uint64_t> touched;      // rds candidates since the last delivery
+  std::unordered_set<uint64_t> has_content;  // groups whose state-derived Ready is non-empty
+  bool awaiting_advance = false;
+  std::unordered_map<uint64_t, Delivered> delivered;
+  // arena of the last Ready (valid until the next call)
+  std::vector<hbn_group_ready> r_out;
+  std::deque<std::vector<hbn_entry>> r_ents;
+  std::deque<std::vector<hbn_message>> r_msgs;
+  std::deque<Ent> r_ent_store;
+  std::deque<Snap> r_snaps;
+  std::vector<Msg> r_msg_store;
+};
+
+namespace {
+
+// ---------------------------------------------------------------- device records
+uint32_t ref_of(const Group& g, uint64_t self, uint64_t node) {
+  if (node == 0) return HB_REF_NONE;
+  const int s = g.slot_of(node);
+  if (s >= 0) return (uint32_t)s;
+  if (node == self) return HB_REF_SELF;
+  return HB_REF_OTHER;
+}
+uint64_t id_of_ref(const Group& g, uint64_t self, uint32_t ref, uint64_t keep) {
+  if (ref == HB_REF_NONE) return 0;
+  if (ref == HB_REF_SELF) return self;
+  if (ref == HB_REF_OTHER) return keep;  // an id outside prs: only the host knows it
+  if (ref < g.peers.size()) return g.peers[ref];
+  return keep;
+}
+
+// [term_first, term_last]: the run of i in [first-1, last] with term(i) == Term.
+void term_run(const Group& g, uint64_t* tf, uint64_t* tl) {
+  const uint64_t lo = g.log.first_index() - 1, last = g.log.last_index();
+  uint64_t i = last + 1;
+  while (i > lo && g.log.term(i - 1) == g.term) --i;
+  if (i == last + 1) {
+    *tf = HB_NO_INDEX;
+    *tl = 0;
+  } else {
+    *tf = i;
+    *tl = last;
+  }
+}
+
+void check(int rc) {
+  if (rc != HB_OK) throw Fail{rc};
+}
+
+// A fresh device record from the host state; prs Progress as given.
+hb_group make_record(const hbn_node* n, const Group& g, const std::vector<hb_progress>& prs) {
+  hb_group r;
+  std::memset(&r, 0, sizeof(r));
+  r.term = g.term;
+  r.committed = g.log.committed;
+  r.first_index = g.log.first_index();
+  r.last_index = g.log.last_index();
+  term_run(g, &r.term_first, &r.term_last);
+  r.snap_index = g.log.snapshot().index;
+  r.state = g.state;
+  r.n = (uint32_t)g.peers.size();
+  const int ss = g.slot_of(n->id);
+  r.self_slot = ss >= 0 ? (uint32_t)ss : HB_SLOT_NONE;
+  r.lead = ref_of(g, n->id, g.lead);
+  r.vote = ref_of(g, n->id, g.vote);
+  for (size_t s = 0; s < prs.size(); ++s) r.pr[s] = prs[s];
+  return r;
+}
+
+void load_timers(hbn_node* n, const Group& g, uint32_t elapsed, uint32_t rand_pos) {
+  hb_timer t;
+  std::memset(&t, 0, sizeof(t));
+  t.elapsed = elapsed;
+  t.rand_pos = rand_pos;
+  t.election_tick = (uint16_t)g.election;
+  t.heartbeat_tick = (uint16_t)g.heartbeat;
+  check(hb_load_timers(n->h, g.slot, 1, &t));
+}
+
+uint32_t alloc_slot(hbn_node* n) {
+  if (n->free_slots.empty()) throw Fail{HB_ENOMEM};
+  const uint32_t s = n->free_slots.back();
+  n->free_slots.pop_back();
+  return s;
+}
+
+// ---------------------------------------------------------------- event replay
+void mark_stepped(hbn_node* n, Group& g) {
+  g.hs_commit = g.log.committed;  // r.Commit = r.raftLog.committed after Step (raft/raft.go:488)
+  n->touched.insert(g.id);
+}
+
+Msg base_msg(const hbn_node* n, const Group& g, uint32_t type, uint64_t to) {
+  Msg m;
+  m.type = type;
+  m.to = to;
+  m.from = n->id;   // raft.send (raft/raft.go:227-236)
+  m.term = g.term;
+  return m;
+}
+
+void on_event(hbn_node* n, Group& g, const hb_event& e) {
+  if (g.fault) return;
+  switch (e.type) {
+    case HB_EV_TERM:  // reset (raft/raft.go:334-349)
+      // Vote, lead and state arrive with the transition's STATE event, which the
+      // device emits only when they differ from before the transition (a
+      // candidate re-campaigning keeps Vote = self, so no STATE follows).
+      g.term = e.x;
+      g.pending_conf = false;
+      break;
+    case HB_EV_STATE: {
+      const uint32_t st = (uint32_t)(e.x & 0xFF), lref = (uint32_t)((e.x >> 8) & 0xFF),
+                     vref = (uint32_t)((e.x >> 16) & 0xFF);
+      g.state = st;
+      g.lead = id_of_ref(g, n->id, lref, g.lead);
+      g.vote = id_of_ref(g, n->id, vref, g.vote);
+      g.pending_conf = false;  // every become* runs reset
+      if (st == HB_STATE_LEADER) {
+        // becomeLeader's scan of the uncommitted tail (raft/raft.go:415-424)
+        for (const Ent& x : g.log.entries(g.log.committed + 1, HB_NO_LIMIT)) {
+          if (x.type != HBN_ENTRY_CONF_CHANGE) continue;
+          if (g.pending_conf) {
+            g.fault = HBN_FAULT_DOUBLE_CONF;
+            return;
+          }
+          g.pending_conf = true;
+        }
+      }
+      break;
+    }
+    case HB_EV_COMMIT:
+      g.log.committed = e.x;
+      break;
+    case HB_EV_LAST: {
+      const uint64_t li = g.log.last_index();
+      std::vector<Ent> ents;
+      if (e.aux == 1) {
+        ents.resize(1);  // becomeLeader's pb.Entry{Data: nil}
+      } else {
+        if (g.props.empty()) panicf("device appended entries without a pending proposal");
+        Msg m = std::move(g.props.front());
+        g.props.pop_front();
+        ents = std::move(m.entries);
+        for (Ent& x : ents) {  // stepLeader MsgProp (raft/raft.go:500-513)
+          if (x.type == HBN_ENTRY_CONF_CHANGE) {
+            if (g.pending_conf) x = Ent{};
+            g.pending_conf = true;
+          }
+        }
+      }
+      if (li + ents.size() != e.x) panicf("device lastIndex disagrees with the host log");
+      for (size_t i = 0; i < ents.size(); ++i) {  // appendEntry (raft/raft.go:351-360)
+        ents[i].term = g.term;
+        ents[i].index = li + 1 + i;
+      }
+      g.log.append(ents);
+      break;
+    }
+    case HB_EV_APP: {  // sendAppend (raft/raft.go:261-281)
+      Msg m = base_msg(n, g, HB_MSG_APP, g.peers.at(e.to));
+      m.index = e.x;
+      m.log_term = g.log.term(e.x);
+      m.entries = g.log.entries(e.x + 1, n->max_msg);
+      m.commit = g.log.committed;
+      g.msgs.push_back(std::move(m));
+      break;
+    }
+    case HB_EV_SNAP: {  // sendAppend, snapshot branch (:246-260)
+      Msg m = base_msg(n, g, HB_MSG_SNAP, g.peers.at(e.to));
+      m.has_snap = true;
+      m.snap = g.log.snapshot();
+      g.msgs.push_back(std::move(m));
+      break;
+    }
+    case HB_EV_HEARTBEAT: {  // sendHeartbeat (:285-299)
+      Msg m = base_msg(n, g, HB_MSG_HEARTBEAT, g.peers.at(e.to));
+      m.commit = e.x;
+      g.msgs.push_back(std::move(m));
+      break;
+    }
+    case HB_EV_VOTE: {  // campaign (:429-443)
+      Msg m = base_msg(n, g, HB_MSG_VOTE, g.peers.at(e.to));
+      m.index = e.x;
+      m.log_term = g.log.term(g.log.last_index());
+      g.msgs.push_back(std::move(m));
+      break;
+    }
+    case HB_EV_PROP_FWD: {  // stepFollower MsgProp (:617-624): m.To = r.lead; r.send(m)
+      if (g.props.empty()) panicf("device forwarded a proposal the host does not hold");
+      Msg m = std::move(g.props.front());
+      g.props.pop_front();
+      m.to = id_of_ref(g, n->id, e.to, g.lead);
+      m.from = n->id;  // MsgProp keeps its own Term
+      g.msgs.push_back(std::move(m));
+      break;
+    }
+    case HB_EV_PROP_DROP:
+      if (!g.props.empty()) g.props.pop_front();
+      break;
+    case HB_EV_FAULT:
+      g.fault = e.aux;
+      g.props.clear();
+      break;
+    default:
+      panicf("unknown device event type " + std::to_string(e.type));
+  }
+}
+
+void consume_events(hbn_node* n) {
+  uint64_t cnt = 0;
+  int rc = hb_copy_events(n->h, nullptr, 0, &cnt);
+  if (rc != HB_OK && rc != HB_EINVAL) throw Fail{rc};
+  if (cnt) {
+    if (n->evbuf.size() < cnt) n->evbuf.resize(cnt);
+    check(hb_copy_events(n->h, n->evbuf.data(), n->evbuf.size(), &cnt));
+  }
+  for (uint64_t i = 0; i < cnt; ++i) {
+    const hb_event& e = n->evbuf[i];
+    if (e.group >= n->by_slot.size() || !n->by_slot[e.group]) continue;
+    Group& g = *n->by_slot[e.group];
+    on_event(n, g, e);
+    mark_stepped(n, g);
+  }
+}
+
+void flush(hbn_node* n) {
+  if (n->b_group.empty()) return;
+  hb_batch b;
+  b.n = n->b_group.size();
+  b.group = n->b_group.data();
+  b.info = n->b_info.data();
+  b.term = n->b_term.data();
+  b.index = n->b_index.data();
+  b.hint = n->b_hint.data();
+  b.props = nullptr;
+  check(hb_step(n->h, &b, HB_STEP_HOST_PTRS));
+  consume_events(n);
+  for (Group* g : n->stepped) mark_stepped(n, *g);
+  n->stepped.clear();
+  n->b_group.clear();
+  n->b_info.clear();
+  n->b_term.clear();
+  n->b_index.clear();
+  n->b_hint.clear();
+}
+
+bool is_response(uint32_t t) {  // IsResponseMsg raft/util.go:53-55
+  return t == HB_MSG_APP_RESP || t == HB_MSG_VOTE_RESP || t == HB_MSG_HEARTBEAT_RESP || t == HB_MSG_UNREACHABLE;
+}
+
+// One message of the Ready cycle into the device batch (raft/multinode.go:224-237).
+void push(hbn_node* n, Group& g, uint32_t type, uint64_t from, bool reject, uint64_t term, uint64_t index,
+          uint64_t hint) {
+  const int s = g.slot_of(from);
+  const uint32_t fs = s >= 0 ? (uint32_t)s : HB_SLOT_NONE;
+  n->touched.insert(g.id);
+  if (g.slot == NO_SLOT) {
+    // prs is empty: every response is filtered (raft/multinode.go:235); anything
+    // else would step a raft with no progress at all.
+    if (is_response(type)) return;
+    throw Fail{HBN_EUNSUPPORTED};
+  }
+  if (n->b_group.size() >= n->max_batch) flush(n);
+  n->b_group.push_back(g.slot);
+  n->b_info.push_back(HB_INFO(type, fs, reject));
+  n->b_term.push_back(term);
+  n->b_index.push_back(index);
+  n->b_hint.push_back(hint);
+  if (s >= 0 || !is_response(type)) n->stepped.insert(&g);
+}
+
+Group& group_of(hbn_node* n, uint64_t id) {
+  auto it = n->groups.find(id);
+  if (it == n->groups.end()) throw Fail{HBN_ENOGROUP};
+  return *it->second;
+}
+
+void propose(hbn_node* n, Group& g, Msg m) {
+  if (g.fault) throw Fail{HBN_EPANIC};
+  m.from = n->id;  // raft/multinode.go:228
+  const uint64_t k = m.entries.size(), term = m.term;
+  if (g.slot != NO_SLOT) g.props.push_back(std::move(m));
+  push(n, g, HB_MSG_PROP, n->id, false, term, k, 0);
+}
+
+// ---------------------------------------------------------------- Ready
+struct ReadyParts {
+  bool has_soft = false;
+  Soft soft;
+  hbn_hard_state hard{0, 0, 0};
+  bool has_snap = false;
+  Snap snap;
+  std::vector<Ent> entries, committed;
+};
+
+// newReady raft/node.go:447-463 (without Messages)
+ReadyParts new_ready(const Group& g) {
+  ReadyParts p;
+  p.entries = g.log.unstable;
+  p.committed = g.log.next_ents();
+  if (!(g.soft() == g.prev_soft)) {
+    p.has_soft = true;
+    p.soft = g.soft();
+  }
+  if (!hs_equal(g.hard(), g.prev_hard)) p.hard = g.hard();
+  if (g.log.has_usnap) {
+    p.has_snap = true;
+    p.snap = g.log.usnap;
+  }
+  return p;
+}
+// containsUpdates raft/node.go:96-100
+bool contains(const ReadyParts& p, size_t nmsgs) {
+  return p.has_soft || !hs_empty(p.hard) || (p.has_snap && p.snap.index != 0) || !p.entries.empty() ||
+         !p.committed.empty() || nmsgs > 0;
+}
+
+const hbn_entry* arena_entries(hbn_node* n, const std::vector<Ent>& src, uint64_t* count) {
+  *count = src.size();
+  if (src.empty()) return nullptr;
+  n->r_ents.emplace_back();
+  std::vector<hbn_entry>& v = n->r_ents.back();
+  v.reserve(src.size());
+  for (const Ent& x : src) {
+    n->r_ent_store.push_back(x);
+    const Ent& s = n->r_ent_store.back();
+    hbn_entry e;
+    e.term = s.term;
+    e.index = s.index;
+    e.type = s.type;
+    e.has_data = s.has_data;
+    e.data = s.data.empty() ? nullptr : reinterpret_cast<const uint8_t*>(s.data.data());
+    e.data_len = s.data.size();
+    v.push_back(e);
+  }
+  return v.data();
+}
+
+void clear_arena(hbn_node* n) {
+  n->r_out.clear();
+  n->r_ents.clear();
+  n->r_msgs.clear();
+  n->r_ent_store.clear();
+  n->r_snaps.clear();
+  n->r_msg_store.clear();
+}
+
+// commitReady raft/multinode.go:137-164
+void commit_ready(Group& g, const Delivered& d) {
+  if (d.has_soft) g.prev_soft = d.soft;
+  if (!hs_empty(d.hard)) g.prev_hard = d.hard;
+  if (g.prev_hard.commit != 0) g.log.applied_to(g.prev_hard.commit);
+  if (d.has_last) g.log.stable_to(d.last_index, d.last_term);
+  if (d.snap_index != 0) {
+    g.prev_snapi = d.snap_index;
+    g.log.stable_snap_to(d.snap_index);
+  }
+}
+
+void refresh_content(hbn_node* n, const Group& g) {
+  if (contains(new_ready(g), 0))
+    n->has_content.insert(g.id);
+  else
+    n->has_content.erase(g.id);
+}
+
+// Rebuild the device record of g after prs changed (ApplyConfChange).
+void reload_prs(hbn_node* n, Group& g, const std::vector<uint64_t>& new_peers,
+                const std::vector<std::pair<uint64_t, uint64_t>>& fresh /* id -> (match 0, next) */) {
+  hb_group old;
+  std::memset(&old, 0, sizeof(old));
+  hb_timer tm;
+  std::memset(&tm, 0, sizeof(tm));
+  std::vector<std::vector<uint64_t>> ins;
+  std::vector<uint32_t> ins_start;
+  const std::vector<uint64_t> old_peers = g.peers;
+  if (g.slot != NO_SLOT) {
+    check(hb_get_groups(n->h, g.slot, 1, &old));
+    check(hb_get_timers(n->h, g.slot, 1, &tm));
+    ins.resize(old_peers.size());
+    ins_start.resize(old_peers.size());
+    std::vector<uint64_t> vals(n->W);
+    for (size_t s = 0; s < old_peers.size(); ++s) {
+      uint32_t st = 0, c = 0;
+      check(hb_get_inflights(n->h, g.slot, (uint32_t)s, &st, &c, vals.data()));
+      ins[s].assign(vals.begin(), vals.begin() + c);
+      ins_start[s] = st;
+    }
+  }
+  if (new_peers.size() > n->nmax) throw Fail{HB_EINVAL};
+  g.peers = new_peers;
+  if (new_peers.empty()) {
+    if (g.slot != NO_SLOT) {
+      check(hb_remove_groups(n->h, g.slot, 1));
+      n->by_slot[g.slot] = nullptr;
+      n->free_slots.push_back(g.slot);
+      g.slot = NO_SLOT;
+    }
+    return;
+  }
+  std::vector<hb_progress> prs(new_peers.size());
+  std::vector<int> from_old(new_peers.size(), -1);
+  for (size_t s = 0; s < new_peers.size(); ++s) {
+    std::memset(&prs[s], 0, sizeof(hb_progress));
+    for (size_t o = 0; o < old_peers.size(); ++o)
+      if (old_peers[o] == new_peers[s] && g.slot != NO_SLOT) from_old[s] = (int)o;
+    if (from_old[s] >= 0) {
+      prs[s] = old.pr[from_old[s]];
+    } else {
+      for (const auto& f : fresh)
+        if (f.first == new_peers[s]) prs[s].next = f.second;
+      prs[s].state = HB_PR_PROBE;
+    }
+  }
+  const bool was_loaded = g.slot != NO_SLOT;
+  hb_group r = make_record(n, g, prs);
+  if (was_loaded) {
+    r.term_first = old.term_first;
+    r.term_last = old.term_last;
+    r.fault = old.fault;
+    // r.votes as slot bitmasks: move each responded peer's bit to its new slot
+    uint32_t resp = 0, grant = 0;
+    for (size_t o = 0; o < old_peers.size() + 1; ++o) {
+      const uint32_t bit = o < old_peers.size() ? (uint32_t)o : 7u;
+      if (!((old.votes_resp >> bit) & 1u)) continue;
+      const uint64_t who = o < old_peers.size() ? old_peers[o] : n->id;
+      const int ns = g.slot_of(who);
+      const uint32_t nb = ns >= 0 ? (uint32_t)ns : (who == n->id ? 7u : 0xFFu);
+      if (nb == 0xFFu) continue;  // a voter that left prs: its vote is still in r.votes, kept by no slot
+      resp |= 1u << nb;
+      if ((old.votes_grant >> bit) & 1u) grant |= 1u << nb;
+    }
+    r.votes_resp = resp;
+    r.votes_grant = grant;
+  } else {
+    g.slot = alloc_slot(n);
+    n->by_slot[g.slot] = &g;
+    tm.elapsed = 0;
+    tm.rand_pos = 0;
+  }
+  check(hb_load_groups(n->h, g.slot, 1, &r));
+  hb_timer t2 = tm;
+  t2.election_tick = (uint16_t)g.election;
+  t2.heartbeat_tick = (uint16_t)g.heartbeat;
+  check(hb_load_timers(n->h, g.slot, 1, &t2));
+  for (size_t s = 0; s < new_peers.size(); ++s)
+    if (from_old[s] >= 0 && !ins[from_old[s]].empty())
+      check(hb_set_inflights(n->h, g.slot, (uint32_t)s, ins_start[from_old[s]], (uint32_t)ins[from_old[s]].size(),
+                             ins[from_old[s]].data()));
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    f();
+    return HB_OK;
+  } catch (const Panic& p) {
+    g_err = p.msg;
+    return HBN_EPANIC;
+  } catch (const Fail& e) {
+    g_err = "failed with code " + std::to_string(e.code);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_err = "out of host memory";
+    return HB_ENOMEM;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return HBN_EPANIC;
+  }
+}
+
+}  // namespace
+
+// ======================================================================= C ABI
+extern "C" {
+
+const char* hbn_last_error(void) { return g_err.c_str(); }
+
+uint64_t hbn_entry_size(const hbn_entry* e) {
+  return e ? ent_size(e->type, e->term, e->index, e->has_data != 0, e->data_len) : 0;
+}
+
+// ---- MemoryStorage ----------------------------------------------------------
+int hbn_storage_new(hbn_storage** out) {
+  if (!out) return HB_EINVAL;
+  return guarded([&] { *out = new hbn_storage(); });
+}
+
+int hbn_storage_new_with_entries(const hbn_entry* ents, uint64_t n, hbn_storage** out) {
+  if (!out || (n && !ents)) return HB_EINVAL;
+  return guarded([&] {
+    auto* s = new hbn_storage();
+    s->ents.clear();
+    for (uint64_t i = 0; i < n; ++i) s->ents.push_back(ent_from(ents[i]));
+    if (s->ents.empty()) s->ents.emplace_back();  // Go would index an empty slice; keep the dummy
+    *out = s;
+  });
+}
+
+int hbn_storage_free(hbn_storage* s) {
+  delete s;
+  return HB_OK;
+}
+
+int hbn_storage_initial_state(hbn_storage* s, hbn_hard_state* hs, uint64_t* nodes, uint32_t cap, uint32_t* n_nodes) {
+  if (!s || !hs || !n_nodes) return HB_EINVAL;
+  *hs = s->hs;
+  *n_nodes = (uint32_t)s->snap.nodes.size();
+  if (s->snap.nodes.size() > cap || (cap && !nodes && !s->snap.nodes.empty())) return HB_EINVAL;
+  for (size_t i = 0; i < s->snap.nodes.size(); ++i) nodes[i] = s->snap.nodes[i];
+  return HB_OK;
+}
+
+int hbn_storage_set_hard_state(hbn_storage* s, const hbn_hard_state* hs) {
+  if (!s || !hs) return HB_EINVAL;
+  s->hs = *hs;
+  return HB_OK;
+}
+
+int hbn_storage_entries(hbn_storage* s, uint64_t lo, uint64_t hi, uint64_t max_size, const hbn_entry** out,
+                        uint64_t* n) {
+  if (!s || !out || !n) return HB_EINVAL;
+  int rc = HB_OK;
+  const int g = guarded([&] {
+    size_t a = 0, k = 0;
+    rc = s->entries(lo, hi, max_size, &a, &k);
+    s->view.clear();
+    if (rc != HB_OK) return;
+    for (size_t i = 0; i < k; ++i) {
+      const Ent& x = s->ents[a + i];
+      s->view.push_back(hbn_entry{x.term, x.index, x.type, x.has_data,
+                                  x.data.empty() ? nullptr : reinterpret_cast<const uint8_t*>(x.data.data()),
+                                  x.data.size()});
+    }
+  });
+  if (g != HB_OK) return g;
+  *out = s->view.empty() ? nullptr : s->view.data();
+  *n = s->view.size();
+  return rc;
+}
+
+int hbn_storage_term(hbn_storage* s, uint64_t i, uint64_t* term) {
+  if (!s || !term) return HB_EINVAL;
+  int rc = HB_OK;
+  *term = 0;
+  const int g = guarded([&] { rc = s->term(i, term); });
+  return g != HB_OK ? g : rc;
+}
+
+int hbn_storage_last_index(hbn_storage* s, uint64_t* out) {
+  if (!s || !out) return HB_EINVAL;
+  *out = s->last_index();
+  return HB_OK;
+}
+
+int hbn_storage_first_index(hbn_storage* s, uint64_t* out) {
+  if (!s || !out) return HB_EINVAL;
+  *out = s->first_index();
+  return HB_OK;
+}
+
+int hbn_storage_snapshot(hbn_storage* s, hbn_snapshot* out) {
+  if (!s || !out) return HB_EINVAL;
+  snap_view(s->snap, out);
+  return HB_OK;
+}
+
+// ApplySnapshot raft/storage.go:150-159
+int hbn_storage_apply_snapshot(hbn_storage* s, const hbn_snapshot* snap) {
+  if (!s || !snap) return HB_EINVAL;
+  return guarded([&] {
+    s->snap = snap_from(*snap);
+    Ent d;
+    d.term = snap->term;
+    d.index = snap->index;
+    s->ents.assign(1, d);
+  });
+}
+
+// CreateSnapshot :161-186
+int hbn_storage_create_snapshot(hbn_storage* s, uint64_t i, const uint64_t* nodes, uint32_t n_nodes,
+                                const uint8_t* data, uint64_t data_len, hbn_snapshot* out) {
+  if (!s) return HB_EINVAL;
+  int rc = HB_OK;
+  const int g = guarded([&] {
+    if (i <= s->snap.index) {
+      rc = HBN_ESNAPOUTOFDATE;
+      return;
+    }
+    if (i > s->last_index())
+      panicf("snapshot " + std::to_string(i) + " is out of bound lastindex(" + std::to_string(s->last_index()) + ")");
+    s->snap.index = i;
+    s->snap.term = s->ents[i - s->offset()].term;
+    if (nodes || n_nodes == 0) {
+      if (nodes) s->snap.nodes.assign(nodes, nodes + n_nodes);
+    }
+    s->snap.has_data = data != nullptr;
+    s->snap.data.assign(data ? reinterpret_cast<const char*>(data) : "", data ? data_len : 0);
+  });
+  if (g != HB_OK) return g;
+  if (out) {
+    if (rc == HB_OK)
+      snap_view(s->snap, out);
+    else
+      std::memset(out, 0, sizeof(*out));
+  }
+  return rc;
+}
+
+// Compact :188-214
+int hbn_storage_compact(hbn_storage* s, uint64_t i) {
+  if (!s) return HB_EINVAL;
+  int rc = HB_OK;
+  const int g = guarded([&] {
+    const uint64_t off = s->offset();
+    if (i <= off) {
+      rc = HBN_ECOMPACTED;
+      return;
+    }
+    if (i > s->last_index())
+      panicf("compact " + std::to_string(i) + " is out of bound lastindex(" + std::to_string(s->last_index()) + ")");
+    const size_t k = i - off;
+    std::vector<Ent> ents(1);
+    ents[0].index = s->ents[k].index;
+    ents[0].term = s->ents[k].term;
+    ents.insert(ents.end(), s->ents.begin() + k + 1, s->ents.end());
+    s->ents.swap(ents);
+  });
+  return g != HB_OK ? g : rc;
+}
+
+int hbn_storage_append(hbn_storage* s, const hbn_entry* ents, uint64_t n) {
+  if (!s || (n && !ents)) return HB_EINVAL;
+  return guarded([&] {
+    std::vector<Ent> v;
+    v.reserve(n);
+    for (uint64_t i = 0; i < n; ++i) v.push_back(ent_from(ents[i]));
+    s->append(v);
+  });
+}
+
+// ---- MultiNode ----------------------------------------------------------------
+int hbn_start(int device, uint64_t id, uint32_t capacity, uint32_t max_replicas, uint32_t max_inflight,
+              uint64_t max_msg_size, uint64_t max_batch, hbn_node** out) {
+  if (!out || id == 0 || capacity == 0 || max_batch == 0) return HB_EINVAL;
+  hb_handle* h = nullptr;
+  const int rc = hb_create(device, capacity, max_replicas, max_inflight, max_msg_size, max_batch, &h);
+  if (rc != HB_OK) return rc;
+  return guarded([&] {
+    auto* n = new hbn_node();
+    n->h = h;
+    n->id = id;
+    n->capacity = capacity;
+    n->nmax = max_replicas;
+    n->W = max_inflight;
+    n->max_msg = max_msg_size;
+    n->max_batch = max_batch;
+    n->by_slot.assign(capacity, nullptr);
+    n->free_slots.reserve(capacity);
+    for (uint32_t s = capacity; s > 0; --s) n->free_slots.push_back(s - 1);
+    *out = n;
+  });
+}
+
+int hbn_stop(hbn_node* n) {
+  if (!n) return HB_EINVAL;
+  const int rc = hb_destroy(n->h);
+  delete n;
+  return rc;
+}
+
+hb_handle* hbn_engine(hbn_node* n) { return n ? n->h : nullptr; }
+
+int hbn_create_group(hbn_node* n, uint64_t group, const hbn_config* cfg, hbn_storage* storage,
+                     const uint64_t* peer_ids, uint32_t n_peers) {
+  if (!n || !cfg || !storage || (n_peers && !peer_ids) || cfg->election_tick == 0 || cfg->heartbeat_tick == 0 ||
+      cfg->election_tick > 0xFFFF || cfg->heartbeat_tick > 0xFFFF)
+    return HB_EINVAL;
+  if (n->groups.count(group)) return HBN_EEXIST;
+  return guarded([&] {
+    flush(n);
+    auto gp = std::make_unique<Group>();
+    Group& g = *gp;
+    g.id = group;
+    g.election = cfg->election_tick;
+    g.heartbeat = cfg->heartbeat_tick;
+    // newRaft raft/raft.go:157-209
+    g.log.init(storage);
+    g.peers = storage->snap.nodes;  // ConfState.Nodes (Config.peers is test-only and not taken here)
+    if (!hs_empty(storage->hs)) {  // loadState :755-763
+      const hbn_hard_state& hs = storage->hs;
+      if (hs.commit < g.log.committed || hs.commit > g.log.last_index())
+        panicf("state.commit " + std::to_string(hs.commit) + " is out of range [" + std::to_string(g.log.committed) +
+               ", " + std::to_string(g.log.last_index()) + "]");
+      g.log.committed = hs.commit;
+      g.term = hs.term;
+      g.vote = hs.vote;
+      g.hs_commit = hs.commit;
+    }
+    if (cfg->applied > 0) g.log.applied_to(cfg->applied);
+    // becomeFollower(r.Term, None)
+    g.state = HB_STATE_FOLLOWER;
+    g.lead = 0;
+    std::vector<std::pair<uint64_t, uint64_t>> fresh;
+    if (storage->last_index() == 0) {
+      // new group (raft/multinode.go:194-211): becomeFollower(1, None), one
+      // ConfChangeAddNode entry per peer, committed = len(peers), addNode each.
+      if (g.term != 1) g.vote = 0;
+      g.term = 1;
+      std::vector<Ent> ents(n_peers);
+      for (uint32_t i = 0; i < n_peers; ++i) {
+        ents[i].type = HBN_ENTRY_CONF_CHANGE;
+        ents[i].term = 1;
+        ents[i].index = i + 1;
+        ents[i].has_data = true;
+        ents[i].data = marshal_conf_change(0, HBN_CC_ADD_NODE, peer_ids[i], nullptr, 0, false);
+      }
+      g.log.append(ents);
+      g.log.committed = n_peers;
+      for (uint32_t i = 0; i < n_peers; ++i) {
+        if (g.slot_of(peer_ids[i]) >= 0) continue;  // addNode ignores a known id
+        g.peers.push_back(peer_ids[i]);
+      }
+    }
+    if (g.peers.size() > n->nmax) throw Fail{HB_EINVAL};
+    // Progress after reset / addNode: Next = lastIndex+1; Match = lastIndex for self
+    // after reset, 0 after addNode (the bootstrap path).
+    std::vector<hb_progress> prs(g.peers.size());
+    const bool boot = storage->last_index() == 0;
+    for (size_t s = 0; s < g.peers.size(); ++s) {
+      std::memset(&prs[s], 0, sizeof(hb_progress));
+      prs[s].next = g.log.last_index() + 1;
+      prs[s].match = (!boot && g.peers[s] == n->id) ? g.log.last_index() : 0;
+      prs[s].state = HB_PR_PROBE;
+    }
+    if (!g.peers.empty()) {
+      g.slot = alloc_slot(n);
+      const hb_group r = make_record(n, g, prs);
+      const int rc = hb_load_groups(n->h, g.slot, 1, &r);
+      if (rc != HB_OK) {
+        n->free_slots.push_back(g.slot);
+        throw Fail{rc};
+      }
+      n->by_slot[g.slot] = &g;
+      load_timers(n, g, 0, 0);
+    }
+    // the initial hard and soft states (:213-215)
+    g.prev_soft = g.soft();
+    g.prev_hard = g.hard();
+    n->touched.insert(group);
+    n->groups.emplace(group, std::move(gp));
+  });
+}
+
+int hbn_remove_group(hbn_node* n, uint64_t group) {
+  if (!n) return HB_EINVAL;
+  return guarded([&] {
+    flush(n);
+    auto it = n->groups.find(group);
+    if (it == n->groups.end()) return;  // delete of a missing key is a no-op in Go
+    Group& g = *it->second;
+    if (g.slot != NO_SLOT) {
+      check(hb_remove_groups(n->h, g.slot, 1));
+      n->by_slot[g.slot] = nullptr;
+      n->free_slots.push_back(g.slot);
+    }
+    n->touched.erase(group);
+    n->has_content.erase(group);
+    n->delivered.erase(group);
+    n->groups.erase(it);
+  });
+}
+
+int hbn_set_rand(hbn_node* n, uint64_t first, uint64_t count, const uint64_t* draws) {
+  if (!n) return HB_EINVAL;
+  return hb_set_rand(n->h, first, count, draws);
+}
+
+// Tick (raft/multinode.go:264-275): every group ticks; every group is then a
+// Ready candidate (those whose Ready was left un-advanced come back).
+int hbn_tick(hbn_node* n) {
+  if (!n) return HB_EINVAL;
+  return guarded([&] {
+    flush(n);
+    check(hb_tick(n->h, 0));
+    consume_events(n);
+    for (uint64_t id : n->has_content) n->touched.insert(id);
+  });
+}
+
+int hbn_campaign(hbn_node* n, uint64_t group) {
+  if (!n) return HB_EINVAL;
+  return guarded([&] {
+    Group& g = group_of(n, group);
+    if (g.fault) throw Fail{HBN_EPANIC};
+    push(n, g, HB_MSG_HUP, 0, false, 0, 0, 0);  // Step(MsgHup) (:369-375)
+  });
+}
+
+int hbn_propose(hbn_node* n, uint64_t group, const uint8_t* data, uint64_t len) {
+  if (!n || (len && !data)) return HB_EINVAL;
+  return guarded([&] {
+    Group& g = group_of(n, group);
+    Msg m;
+    m.type = HB_MSG_PROP;
+    Ent e;
+    e.has_data = data != nullptr;
+    if (len) e.data.assign(reinterpret_cast<const char*>(data), len);
+    m.entries.push_back(std::move(e));
+    propose(n, g, std::move(m));
+  });
+}
+
+int hbn_propose_conf_change(hbn_node* n, uint64_t group, uint64_t cc_id, uint32_t cc_type, uint64_t node_id,
+                            const uint8_t* cc_context, uint64_t context_len) {
+  if (!n) return HB_EINVAL;
+  return guarded([&] {
+    Group& g = group_of(n, group);
+    Msg m;
+    m.type = HB_MSG_PROP;
+    Ent e;
+    e.type = HBN_ENTRY_CONF_CHANGE;
+    e.has_data = true;
+    e.data = marshal_conf_change(cc_id, cc_type, node_id, cc_context, context_len, cc_context != nullptr);
+    m.entries.push_back(std::move(e));
+    propose(n, g, std::move(m));
+  });
+}
+
+int hbn_step(hbn_node* n, uint64_t group, const hbn_message* m) {
+  if (!n || !m || (m->n_entries && !m->entries)) return HB_EINVAL;
+  const uint32_t t = m->type;
+  // IsLocalMsg (raft/util.go:49-51): ignored when received over the network
+  if (t == HB_MSG_HUP || t == HB_MSG_BEAT || t == HB_MSG_UNREACHABLE || t == HB_MSG_SNAP_STATUS) return HB_OK;
+  return guarded([&] {
+    Group& g = group_of(n, group);
+    if (t == HB_MSG_PROP) {
+      Msg p;
+      p.type = t;
+      p.to = m->to;
+      p.term = m->term;
+      p.log_term = m->log_term;
+      p.index = m->index;
+      p.commit = m->commit;
+      p.reject = m->reject;
+      p.reject_hint = m->reject_hint;
+      for (uint64_t i = 0; i < m->n_entries; ++i) p.entries.push_back(ent_from(m->entries[i]));
+      propose(n, g, std::move(p));
+      return;
+    }
+    if (t != HB_MSG_APP_RESP && t != HB_MSG_VOTE_RESP && t != HB_MSG_HEARTBEAT_RESP) throw Fail{HBN_EUNSUPPORTED};
+    if (g.fault) throw Fail{HBN_EPANIC};
+    push(n, g, t, m->from, m->reject != 0, m->term, m->index, m->reject_hint);
+  });
+}
+
+int hbn_report_unreachable(hbn_node* n, uint64_t id, uint64_t group) {
+  if (!n) return HB_EINVAL;
+  return guarded([&] {
+    Group& g = group_of(n, group);
+    if (g.fault) throw Fail{HBN_EPANIC};
+    push(n, g, HB_MSG_UNREACHABLE, id, false, 0, 0, 0);
+  });
+}
+
+int hbn_report_snapshot(hbn_node* n, uint64_t id, uint64_t group, int failure) {
+  if (!n) return HB_EINVAL;
+  return guarded([&] {
+    Group& g = group_of(n, group);
+    if (g.fault) throw Fail{HBN_EPANIC};
+    push(n, g, HB_MSG_SNAP_STATUS, id, failure != 0, 0, 0, 0);
+  });
+}
+
+int hbn_apply_conf_change(hbn_node* n, uint64_t group, uint32_t cc_type, uint64_t node_id, uint64_t* nodes_out,
+                          uint32_t* n_nodes) {
+  if (!n) return HB_EINVAL;
+  return guarded([&] {
+    flush(n);
+    Group& g = group_of(n, group);
+    if (g.fault) throw Fail{HBN_EPANIC};
+    n->touched.insert(group);
+    if (node_id != 0) {
+      std::vector<uint64_t> np = g.peers;
+      switch (cc_type) {
+        case HBN_CC_ADD_NODE:  // addNode raft/raft.go:729-738
+          if (g.slot_of(node_id) < 0) {
+            np.push_back(node_id);
+            reload_prs(n, g, np, {{node_id, g.log.last_index() + 1}});
+            g.pending_conf = false;
+          }
+          break;
+        case HBN_CC_REMOVE_NODE:  // removeNode :740-743
+          np.erase(std::remove(np.begin(), np.end(), node_id), np.end());
+          if (np.size() != g.peers.size()) reload_prs(n, g, np, {});
+          g.pending_conf = false;
+          break;
+        case HBN_CC_UPDATE_NODE:
+          g.pending_conf = false;
+          break;
+        default:
+          panicf("unexpected conf type");
+      }
+    } else {
+      g.pending_conf = false;  // resetPendingConf
+    }
+    std::vector<uint64_t> nodes = g.peers;
+    std::sort(nodes.begin(), nodes.end());
+    if (n_nodes) *n_nodes = (uint32_t)nodes.size();
+    if (nodes_out)
+      for (size_t i = 0; i < nodes.size(); ++i) nodes_out[i] = nodes[i];
+  });
+}
+
+int hbn_ready(hbn_node* n, const hbn_group_ready** out, uint64_t* count) {
+  if (!n || !out || !count) return HB_EINVAL;
+  *out = nullptr;
+  *count = 0;
+  int rc = HB_OK;
+  const int g0 = guarded([&] {
+    flush(n);
+    clear_arena(n);
+    if (n->awaiting_advance) {
+      rc = HBN_EAGAIN;
+      return;
+    }
+    std::vector<uint64_t> ids(n->touched.begin(), n->touched.end());
+    std::sort(ids.begin(), ids.end());
+    n->touched.clear();
+    n->delivered.clear();
+    n->r_out.reserve(ids.size());
+    for (uint64_t id : ids) {
+      auto it = n->groups.find(id);
+      if (it == n->groups.end()) continue;
+      Group& g = *it->second;
+      ReadyParts p = new_ready(g);
+      if (contains(p, 0))
+        n->has_content.insert(id);
+      else
+        n->has_content.erase(id);
+      if (!contains(p, g.msgs.size()) && !g.fault) continue;
+      hbn_group_ready r;
+      std::memset(&r, 0, sizeof(r));
+      r.group = id;
+      r.has_soft_state = p.has_soft;
+      r.raft_state = p.soft.state;
+      r.lead = p.soft.lead;
+      r.hard_state = p.hard;
+      if (p.has_snap) {
+        n->r_snaps.push_back(p.snap);
+        snap_view(n->r_snaps.back(), &r.snapshot);
+      }
+      r.entries = arena_entries(n, p.entries, &r.n_entries);
+      r.committed_entries = arena_entries(n, p.committed, &r.n_committed);
+      // Messages (r.msgs), then cleared (:277-281)
+      if (!g.msgs.empty()) {
+        n->r_msgs.emplace_back();
+        std::vector<hbn_message>& mv = n->r_msgs.back();
+        for (Msg& m : g.msgs) {
+          hbn_message x;
+          std::memset(&x, 0, sizeof(x));
+          x.type = m.type;
+          x.reject = m.reject;
+          x.to = m.to;
+          x.from = m.from;
+          x.term = m.term;
+          x.log_term = m.log_term;
+          x.index = m.index;
+          x.commit = m.commit;
+          x.reject_hint = m.reject_hint;
+          x.entries = arena_entries(n, m.entries, &x.n_entries);
+          if (m.has_snap) {
+            n->r_snaps.push_back(m.snap);
+            snap_view(n->r_snaps.back(), &x.snapshot);
+          }
+          mv.push_back(x);
+        }
+        r.messages = mv.data();
+        r.n_messages = mv.size();
+        g.msgs.clear();
+      }
+      r.fault = g.fault;
+      Delivered d;
+      d.has_soft = p.has_soft;
+      d.soft = p.soft;
+      d.hard = p.hard;
+      if (!p.entries.empty()) {
+        d.has_last = true;
+        d.last_index = p.entries.back().index;
+        d.last_term = p.entries.back().term;
+      }
+      d.snap_index = p.has_snap ? p.snap.index : 0;
+      n->delivered[id] = d;
+      n->r_out.push_back(r);
+    }
+    if (n->r_out.empty()) {
+      rc = HBN_EAGAIN;
+      return;
+    }
+    n->awaiting_advance = true;
+  });
+  if (g0 != HB_OK) return g0;
+  if (rc != HB_OK) return rc;
+  *out = n->r_out.data();
+  *count = n->r_out.size();
+  return HB_OK;
+}
+
+int hbn_advance(hbn_node* n, const uint64_t* groups, uint64_t count) {
+  if (!n || (count && !groups)) return HB_EINVAL;
+  return guarded([&] {
+    flush(n);
+    for (uint64_t i = 0; i < count; ++i) {
+      auto it = n->groups.find(groups[i]);
+      auto dt = n->delivered.find(groups[i]);
+      if (it == n->groups.end() || dt == n->delivered.end()) continue;
+      Group& g = *it->second;
+      commit_ready(g, dt->second);
+      n->delivered.erase(dt);
+      refresh_content(n, g);
+      // the recomputed Ready (:290-295) is a candidate again
+      n->touched.insert(g.id);
+    }
+    n->awaiting_advance = false;
+  });
+}
+
+int hbn_status(hbn_node* n, uint64_t group, hbn_group_status* out) {
+  if (!n || !out) return HB_EINVAL;
+  return guarded([&] {
+    flush(n);
+    Group& g = group_of(n, group);
+    std::memset(out, 0, sizeof(*out));
+    out->id = n->id;
+    out->hard_state = g.hard();
+    out->lead = g.lead;
+    out->raft_state = g.state;
+    out->applied = g.log.applied;
+    if (g.state == HB_STATE_LEADER && g.slot != NO_SLOT) {
+      hb_group r;
+      check(hb_get_groups(n->h, g.slot, 1, &r));
+      out->n_progress = (uint32_t)g.peers.size();
+      for (size_t s = 0; s < g.peers.size(); ++s) {
+        out->progress_id[s] = g.peers[s];
+        out->progress[s] = r.pr[s];
+      }
+    }
+  });
+}
+
+}  // extern "C"

@@ -124,3 +124,53 @@ def test_oracle_has_no_product_dependents():
             if f.endswith((".py", ".hip", ".h", ".cpp", ".c")):
                 txt = open(os.path.join(dirpath, f)).read()
                 assert not pat.search(txt), f"{f} references the oracle"
+
+
+# ---- the MultiNode host library (include/hbnode.h) ------------------------------
+NODE_HDR = os.path.join(ROOT, "include", "hbnode.h")
+
+
+def test_hbnode_exports_every_declared_function():
+    from etcd_amd import multinode
+    L = multinode.lib()  # loads (and pulls in libhipbatch.so) without touching the GPU
+    txt = open(NODE_HDR).read()
+    names = sorted(set(re.findall(r"^\s*(?:int|const char\*|uint64_t|hb_handle\*)\s+(hbn_[a-z_]+)\s*\(", txt, re.M)))
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(L, n), f"libhbnode.so does not export {n}"
+    py = set(re.findall(r'"(hbn_[a-z_]+)"', open(os.path.join(ROOT, "etcd_amd", "multinode.py")).read()))
+    assert set(names) <= py, f"multinode.py lacks bindings for {sorted(set(names) - py)}"
+
+
+def test_hbnode_defines_and_layouts_match():
+    from etcd_amd import multinode as M
+    txt = open(NODE_HDR).read()
+    defs = dict(re.findall(r"^#define\s+(HBN_[A-Z0-9_]+)\s+(-?\d+)\b", txt, re.M))
+    for name, val in defs.items():
+        if hasattr(M, name):
+            assert getattr(M, name) == int(val), name
+    src = r'''
+#include <stdio.h>
+#include "hbnode.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(hbn_entry), sizeof(hbn_hard_state), sizeof(hbn_snapshot),
+         sizeof(hbn_message), sizeof(hbn_group_ready), sizeof(hbn_group_status), sizeof(hbn_config));
+  return 0;
+}
+'''
+    with tempfile.TemporaryDirectory() as d:
+        c, exe = os.path.join(d, "l.c"), os.path.join(d, "l")
+        open(c, "w").write(src)
+        subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(NODE_HDR), c, "-o", exe], check=True)
+        sizes = [int(x) for x in subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()]
+    assert sizes == [C.sizeof(t) for t in (M.hbn_entry, M.hbn_hard_state, M.hbn_snapshot, M.hbn_message,
+                                           M.hbn_group_ready, M.hbn_group_status, M.hbn_config)]
+
+
+def test_hbnode_rejects_bad_arguments_without_device_work():
+    from etcd_amd import multinode as M
+    L = M.lib()
+    p = C.c_void_p()
+    assert L.hbn_start(0, 0, 16, 3, 256, abi.HB_NO_LIMIT, 16, C.byref(p)) == abi.HB_EINVAL  # id 0 = None
+    assert L.hbn_start(0, 1, 0, 3, 256, abi.HB_NO_LIMIT, 16, C.byref(p)) == abi.HB_EINVAL
+    assert L.hbn_ready(None, None, None) == abi.HB_EINVAL

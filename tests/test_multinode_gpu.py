@@ -1,0 +1,341 @@
+"""MultiNode host side (etcd_amd/libhbnode.so over libhipbatch.so) on the GPU.
+
+1. The reference's own MultiNode tests, transcribed (raft/multinode_test.go:
+   29-412): Start, Restart, RestartFromSnapshot, Advance, Status, Propose,
+   ProposeConfig, the Step filter.
+2. Randomised parity: many groups driven through the MultiNode API (Campaign,
+   Propose, MsgVoteResp / MsgAppResp / MsgHeartbeatResp, ReportUnreachable,
+   ReportSnapshot, Tick, Ready / Advance), and beside it one oracle raft per
+   group (oracle/raft_oracle.c) stepped with the same messages.  Every Ready is
+   checked against the oracle: HardState / SoftState, the messages (type, to,
+   term, index, log term, commit, reject, entry count and first index — the
+   oracle's r.msgs in order), the unstable entries and the committed entries
+   (indices and terms), and every payload against what was proposed.
+"""
+import numpy as np
+import pytest
+
+from etcd_amd import abi
+from etcd_amd.multinode import (Config, ConfChangeAddNode, ConfChangeRemoveNode, Entry, EntryConfChange, HardState, Message,
+                                MemoryStorage, Ready, Snapshot, SoftState, StartMultiNode, StateLeader, emptyState)
+
+pytestmark = pytest.mark.gpu
+
+
+def cc_data(node_id, typ=ConfChangeAddNode, id=0):
+    """ConfChange{ID, Type, NodeID}.Marshal() (raft/raftpb/raft.pb.go:1402-1426)."""
+    def v(x):
+        out = bytearray()
+        while x >= 0x80:
+            out.append((x & 0x7F) | 0x80)
+            x >>= 7
+        out.append(x)
+        return bytes(out)
+    return b"\x08" + v(id) + b"\x10" + v(typ) + b"\x18" + v(node_id)
+
+
+def test_multinode_start():  # raft/multinode_test.go:246-300
+    ccdata = cc_data(1)
+    wants = [
+        Ready(SoftState=SoftState(Lead=1, RaftState=StateLeader), HardState=HardState(Term=2, Commit=2, Vote=1),
+              Entries=[Entry(Type=EntryConfChange, Term=1, Index=1, Data=ccdata), Entry(Term=2, Index=2)],
+              CommittedEntries=[Entry(Type=EntryConfChange, Term=1, Index=1, Data=ccdata), Entry(Term=2, Index=2)]),
+        Ready(HardState=HardState(Term=2, Commit=3, Vote=1), Entries=[Entry(Term=2, Index=3, Data=b"foo")],
+              CommittedEntries=[Entry(Term=2, Index=3, Data=b"foo")]),
+    ]
+    mn = StartMultiNode(1)
+    storage = MemoryStorage()
+    mn.CreateGroup(1, Config(10, 1), storage, peers=[1])
+    mn.Campaign(1)
+    gs = mn.Ready()
+    assert gs[1] == wants[0]
+    storage.Append(gs[1].Entries)
+    mn.Advance(gs)
+    mn.Propose(1, b"foo")
+    gs2 = mn.Ready()
+    assert gs2[1] == wants[1]
+    storage.Append(gs2[1].Entries)
+    mn.Advance(gs2)
+    assert mn.Ready() == {}
+    mn.Stop()
+
+
+def test_multinode_restart():  # :302-332
+    entries = [Entry(Term=1, Index=1), Entry(Term=1, Index=2, Data=b"foo")]
+    st = HardState(Term=1, Commit=1)
+    want = Ready(HardState=emptyState, CommittedEntries=entries[:st.Commit])
+    storage = MemoryStorage()
+    storage.SetHardState(st)
+    storage.Append(entries)
+    mn = StartMultiNode(1)
+    mn.CreateGroup(1, Config(10, 1), storage)
+    gs = mn.Ready()
+    assert gs[1] == want
+    mn.Advance(gs)
+    assert mn.Ready() == {}
+    mn.Stop()
+
+
+def test_multinode_restart_from_snapshot():  # :334-370
+    snap = Snapshot(Index=2, Term=1, Nodes=[1, 2])
+    entries = [Entry(Term=1, Index=3, Data=b"foo")]
+    st = HardState(Term=1, Commit=3)
+    want = Ready(HardState=emptyState, CommittedEntries=entries)
+    s = MemoryStorage()
+    s.SetHardState(st)
+    s.ApplySnapshot(snap)
+    s.Append(entries)
+    mn = StartMultiNode(1)
+    mn.CreateGroup(1, Config(10, 1), s)
+    gs = mn.Ready()
+    assert gs[1] == want
+    mn.Advance(gs)
+    assert mn.Ready() == {}
+    # the restarted group is on the device: a campaign sends MsgVote to 2 with the log's last (3, 1)
+    mn.Campaign(1)
+    rd = mn.Ready()[1]
+    assert rd.SoftState == SoftState(0, abi.HB_STATE_CANDIDATE)
+    assert rd.HardState == HardState(Term=2, Vote=1, Commit=3)
+    assert rd.Messages == [Message(Type=abi.HB_MSG_VOTE, To=2, From=1, Term=2, LogTerm=1, Index=3)]
+
+
+def test_multinode_advance():  # :372-394
+    storage = MemoryStorage()
+    mn = StartMultiNode(1)
+    mn.CreateGroup(1, Config(10, 1), storage, peers=[1])
+    mn.Campaign(1)
+    rd1 = mn.Ready()
+    mn.Propose(1, b"foo")
+    assert mn.Ready() == {}, "unexpected Ready before Advance"
+    storage.Append(rd1[1].Entries)
+    mn.Advance(rd1)
+    assert mn.Ready() != {}, "expect Ready after Advance"
+
+
+def test_multinode_status():  # :396-412
+    storage = MemoryStorage()
+    mn = StartMultiNode(1)
+    mn.CreateGroup(1, Config(10, 1), storage, peers=[1])
+    assert mn.Status(1) is not None
+    assert mn.Status(2) is None
+    mn.Campaign(1)
+    st = mn.Status(1)
+    assert st.SoftState == SoftState(1, StateLeader) and st.HardState == HardState(2, 1, 2)
+    assert list(st.Progress) == [1] and st.Progress[1].match == 2 and st.Progress[1].next == 3
+
+
+@pytest.mark.parametrize("conf", [False, True])
+def test_multinode_propose(conf):  # :109-155 (Propose) and :157-215 (ProposeConfig)
+    mn = StartMultiNode(1)
+    s = MemoryStorage()
+    mn.CreateGroup(1, Config(10, 1), s, peers=[1])
+    mn.Campaign(1)
+    proposed = False
+    for _ in range(10):
+        rds = mn.Ready()
+        rd = rds[1]
+        s.Append(rd.Entries)
+        if not proposed and rd.SoftState and rd.SoftState.Lead == mn.id:
+            if conf:
+                mn.ProposeConfChange(1, ConfChangeAddNode, 1)
+            else:
+                mn.Propose(1, b"somedata")
+            proposed = True
+        mn.Advance(rds)
+        if s.LastIndex() >= 3:
+            break
+    last = s.LastIndex()
+    ents, err = s.Entries(last, last + 1)
+    assert err is None and len(ents) == 1
+    if conf:
+        assert ents[0].Type == EntryConfChange and ents[0].Data == cc_data(1)
+    else:
+        assert ents[0].Data == b"somedata"
+
+
+def test_multinode_step_ignores_local_messages():  # :29-61 with raft/util.go:49-51
+    mn = StartMultiNode(1)
+    s = MemoryStorage()
+    mn.CreateGroup(1, Config(10, 1), s, peers=[1, 2, 3])
+    rd = mn.Ready()  # bootstrap entries
+    s.Append(rd[1].Entries)
+    mn.Advance(rd)
+    for t in (abi.HB_MSG_HUP, abi.HB_MSG_BEAT, abi.HB_MSG_UNREACHABLE, abi.HB_MSG_SNAP_STATUS):
+        mn.Step(1, Message(Type=t, From=2))
+    # nothing was stepped: the only content is the bootstrap entries, still not
+    # applied because prevHardSt.Commit is 0 (raft/multinode.go:145-157)
+    rd = mn.Ready()[1]
+    assert rd.Messages == [] and rd.SoftState is None and rd.HardState == emptyState and rd.Entries == []
+    assert [e.Index for e in rd.CommittedEntries] == [1, 2, 3]
+    assert mn.Status(1).SoftState.RaftState == abi.HB_STATE_FOLLOWER
+
+
+def test_conf_change_add_remove_keeps_progress():
+    """ApplyConfChange on a leader (raft/multinode.go:239-262): add a node, its
+    progress starts at (0, last+1); remove one; the leader keeps the others'."""
+    mn = StartMultiNode(1)
+    s = MemoryStorage()
+    mn.CreateGroup(7, Config(10, 1), s, peers=[1, 2, 3])
+    mn.Campaign(7)
+    mn.Step(7, Message(Type=abi.HB_MSG_VOTE_RESP, From=2, Term=2))
+    rd = mn.Ready()
+    s.Append(rd[7].Entries)
+    mn.Advance(rd)
+    mn.Step(7, Message(Type=abi.HB_MSG_APP_RESP, From=2, Term=2, Index=4))
+    assert mn.ApplyConfChange(7, ConfChangeAddNode, 4) == [1, 2, 3, 4]
+    st = mn.Status(7)
+    assert (st.Progress[2].match, st.Progress[2].next, st.Progress[2].state) == (4, 5, abi.HB_PR_REPLICATE)
+    assert (st.Progress[4].match, st.Progress[4].next) == (0, 5)
+    assert mn.ApplyConfChange(7, ConfChangeRemoveNode, 3) == [1, 2, 4]
+    st = mn.Status(7)
+    assert sorted(st.Progress) == [1, 2, 4] and st.Progress[2].match == 4
+
+
+# ---------------------------------------------------------------------------------------
+# randomised parity against the oracle
+# ---------------------------------------------------------------------------------------
+def _orc_msgs(o):
+    return [(m.Type, m.To, m.From, m.Term, m.LogTerm, m.Index, m.Commit, bool(m.Reject), m.nents,
+             m.ent_lo if m.nents else 0) for m in o.readMessages()]
+
+
+def _dev_msgs(rd):
+    out = []
+    for m in rd.Messages:
+        lo = m.Entries[0].Index if m.Entries else 0
+        out.append((m.Type, m.To, m.From, m.Term, m.LogTerm, m.Index, m.Commit, m.Reject, len(m.Entries), lo))
+    return out
+
+
+@pytest.mark.parametrize("seed,n", [(1, 3), (2, 5), (3, 3)])
+def test_random_multinode_vs_oracle(seed, n):
+    from oracle.pyoracle import Msg, Raft
+    rng = np.random.default_rng(seed)
+    G, ROUNDS = 96, 60
+    seen = dict(app_ents=0, leaders=0, commits=0, votes=0, beats=0)
+    peers = list(range(1, n + 1))
+    draws = rng.integers(0, 1 << 62, 1 << 14, dtype=np.uint64)
+    mn = StartMultiNode(1, capacity=128, max_replicas=n, max_inflight=8)
+    mn.SetRand(draws)
+    gids = [1000 + 17 * g for g in range(G)]
+    st = {}
+    for gid in gids:
+        s = MemoryStorage()
+        mn.CreateGroup(gid, Config(election=3, heartbeat=1), s, peers=peers)
+        o = Raft(1, peers, ents=[(i, 1) for i in range(1, n + 1)], hard=(1, 0, n), max_inflight=8,
+                 election=3, heartbeat=1, draws=draws)
+        st[gid] = dict(s=s, o=o, data={}, applied=0, prev_hard=(1, 0, 0), prev_soft=(0, 0), seq=0)
+    for gid in gids:  # one Step first, so HardState.Commit (r.Commit) tracks committed from here on
+        mn.Campaign(gid)
+        st[gid]["o"].Step(Msg(abi.HB_MSG_HUP))
+    for rnd in range(ROUNDS):
+        for gid in gids:
+            d, o = st[gid], st[gid]["o"]
+            if d.get("dead"):
+                continue
+            for _ in range(int(rng.integers(0, 4))):
+                if o.fault:
+                    break
+                a = rng.random()
+                frm = int(rng.integers(1, n + 2))  # n + 1 is a non-member
+                member = frm <= n
+                if a < 0.12 and (o.state != abi.HB_STATE_LEADER or rng.random() < 0.05):
+                    mn.Campaign(gid)  # a leader's campaign panics (raft/raft.go:396): both report it
+                    o.Step(Msg(abi.HB_MSG_HUP))
+                elif a < 0.30:
+                    d["seq"] += 1
+                    data = f"{gid}-{d['seq']}".encode()
+                    mn.Propose(gid, data)
+                    o.Step(Msg(abi.HB_MSG_PROP, From=1, Entries=1))
+                    d.setdefault("props", []).append(data)
+                elif a < 0.45:
+                    term = o.Term + (1 if rng.random() < 0.03 else 0)
+                    rej = bool(rng.random() < 0.3)
+                    mn.Step(gid, Message(Type=abi.HB_MSG_VOTE_RESP, From=frm, Term=term, Reject=rej))
+                    if member:
+                        o.Step(Msg(abi.HB_MSG_VOTE_RESP, From=frm, Term=term, Reject=rej))
+                elif a < 0.80:
+                    rej = bool(rng.random() < 0.15)
+                    idx = int(rng.integers(0, o.lastIndex + 1))
+                    hint = int(rng.integers(0, o.lastIndex + 1))
+                    mn.Step(gid, Message(Type=abi.HB_MSG_APP_RESP, From=frm, Term=o.Term, Index=idx, Reject=rej,
+                                         RejectHint=hint))
+                    if member:
+                        o.Step(Msg(abi.HB_MSG_APP_RESP, From=frm, Term=o.Term, Index=idx, Reject=rej,
+                                   RejectHint=hint))
+                elif a < 0.92:
+                    mn.Step(gid, Message(Type=abi.HB_MSG_HEARTBEAT_RESP, From=frm, Term=o.Term))
+                    if member:
+                        o.Step(Msg(abi.HB_MSG_HEARTBEAT_RESP, From=frm, Term=o.Term))
+                elif a < 0.97:
+                    mn.ReportUnreachable(frm, gid)
+                    if member:
+                        o.Step(Msg(abi.HB_MSG_UNREACHABLE, From=frm))
+                elif member and frm != 1 and o.state == abi.HB_STATE_LEADER and \
+                        o.pr(frm).State == abi.HB_PR_SNAPSHOT:
+                    fail = bool(rng.random() < 0.5)
+                    mn.ReportSnapshot(frm, gid, fail)
+                    o.Step(Msg(abi.HB_MSG_SNAP_STATUS, From=frm, Reject=fail))
+        if rnd % 5 == 4:
+            mn.Tick()
+            for gid in gids:
+                st[gid]["o"].tick()
+        rds = mn.Ready()
+        for gid in gids:
+            d, o = st[gid], st[gid]["o"]
+            if d.get("dead"):
+                continue
+            if o.fault:
+                assert gid in rds and rds[gid].fault == o.fault, f"group {gid}: fault"
+                d["dead"] = True
+                continue
+            om = _orc_msgs(o)
+            hard = (o.Term, o.Vote, o.committed)
+            soft = (o.lead, o.state)
+            unstable_lo = d["s"].LastIndex() + 1
+            committed_lo = max(d["applied"] + 1, d["s"].FirstIndex())
+            want_any = bool(om) or hard != d["prev_hard"] or soft != d["prev_soft"] or \
+                o.lastIndex >= unstable_lo or o.committed >= committed_lo
+            ctx = f"seed {seed} round {rnd} group {gid}"
+            if not want_any:
+                assert gid not in rds, ctx
+                continue
+            rd = rds[gid]
+            assert rd.fault == 0, ctx
+            assert _dev_msgs(rd) == om, f"{ctx}: messages\n dev {_dev_msgs(rd)}\n ora {om}"
+            assert rd.HardState == (HardState(*hard) if hard != d["prev_hard"] else emptyState), ctx
+            assert rd.SoftState == (SoftState(*soft) if soft != d["prev_soft"] else None), ctx
+            assert [(e.Index, e.Term) for e in rd.Entries] == \
+                   [(i, o.term(i)) for i in range(unstable_lo, o.lastIndex + 1)], ctx
+            assert [(e.Index, e.Term) for e in rd.CommittedEntries] == \
+                   [(i, o.term(i)) for i in range(committed_lo, o.committed + 1)], ctx
+            # payloads: proposals in order, noops empty
+            for e in rd.Entries:
+                if e.Data is not None:
+                    d["data"][e.Index] = e.Data
+            for m in rd.Messages:
+                for e in m.Entries:
+                    if m.Type == abi.HB_MSG_APP and e.Data is not None:
+                        assert d["data"][e.Index] == e.Data, ctx
+            seen["app_ents"] += sum(1 for m in rd.Messages if m.Type == abi.HB_MSG_APP and m.Entries)
+            seen["votes"] += sum(1 for m in rd.Messages if m.Type == abi.HB_MSG_VOTE)
+            seen["beats"] += sum(1 for m in rd.Messages if m.Type == abi.HB_MSG_HEARTBEAT)
+            seen["commits"] += len(rd.CommittedEntries)
+            seen["leaders"] += int(rd.SoftState is not None and rd.SoftState.RaftState == StateLeader)
+            d["s"].Append(rd.Entries)
+            if rd.SoftState is not None:
+                d["prev_soft"] = soft
+            if rd.HardState != emptyState:
+                d["prev_hard"] = hard
+            if d["prev_hard"][2]:
+                d["applied"] = d["prev_hard"][2]
+        mn.Advance(rds)
+    assert min(seen.values()) > 0, seen  # every kind of Ready content was compared
+    # every accepted proposal's payload reached storage in proposal order
+    for gid in gids:
+        s = st[gid]["s"]
+        ents, err = s.Entries(n + 1, s.LastIndex() + 1) if s.LastIndex() > n else ([], None)
+        got = [e.Data for e in (ents or []) if e.Data is not None]
+        props = st[gid].get("props", [])
+        it = iter(props)
+        assert all(any(p == g for p in it) for g in got), f"group {gid}: payload order"

@@ -203,3 +203,12 @@ def pack(recs):
         off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
     data = np.frombuffer(b"".join(recs), dtype=np.uint8).copy() if recs else np.zeros(1, np.uint8)
     return data, off, lens
+
+
+def pb_entry(type, term, index, data):
+    """raftpb.Entry through the protobuf library (independent of the gogo Size restatement)."""
+    e = pb_classes()["Entry"]()
+    e.Type, e.Term, e.Index = type, term, index
+    if data is not None:
+        e.Data = data
+    return e.SerializeToString()
