@@ -242,15 +242,56 @@ def pmc_traffic(path, kernel, G, n, apply_us):
     return float(k["traffic_bytes"]), f"{src}: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, avg {k['avg_us']:.1f} us"
 
 
+def run_multinode(args):
+    """The MultiNode API end to end: a C++ application
+    (etcd_amd/csrc/hbnode_bench.cpp, the reference's node_bench_test loop over
+    many groups) steps every follower's MsgAppResp, proposes one entry per
+    group, takes the Ready (host assembly over the device step), appends it to
+    MemoryStorage and advances.  Host-inclusive: value = MsgAppResp/s through
+    the whole API, not the kernel rate."""
+    import ctypes as C
+    G = args.groups or 1000
+    n = args.replicas or 3
+    L = C.CDLL(os.path.join(ROOT, "etcd_amd", "libhbnode_bench.so"))
+    L.hbnb_run.restype = C.c_int
+    L.hbnb_run.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]
+    out = (C.c_double * 8)()
+    t0 = time.perf_counter()
+    rc = L.hbnb_run(int(os.environ.get("LOCAL_RANK", "0")), G, n, args.warmup, args.steps, out)
+    wall = time.perf_counter() - t0
+    if rc != 0:
+        raise SystemExit(f"hbnb_run failed: {rc}")
+    secs, acks, adv = out[0], out[1], out[2]
+    rec = {"metric": "MsgAppResp applied/sec through the MultiNode API (Step + Propose + Ready + Advance)",
+           "value": acks / secs, "unit": "MsgAppResp/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": 1e3 * secs / args.steps, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u64",
+           "data": "synthetic (node_bench_test-style loop: every group proposes 'foo', followers ack last index)",
+           "config": {"workload": f"multinode: {G} groups x {n} through include/hbnode.h (SURVEY.md 8(d) cfg1 "
+                                  f"shape{' = BASELINE.json configs[0]' if G == 1000 and n == 3 else ''})",
+                      "groups": G, "replicas": n, "max_inflight": 256},
+           "commits_per_s": adv / secs,
+           "split_s_per_step": {"ready": out[3] / args.steps, "step_and_propose": out[4] / args.steps,
+                                "append_and_advance": out[5] / args.steps},
+           "parity_sanity": bool(adv == G * args.steps and out[7] == 0),
+           "wall_s": wall}
+    if not args.no_cpu_baseline:
+        cb = cpu_baseline(n, groups=min(G, args.cpu_groups), budget_s=min(args.cpu_seconds, 5.0))
+        cb["sample"] += " (raft steps only: no Ready assembly, no storage)"
+        rec["cpu_baseline"] = cb
+    print(json.dumps(rec), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4", "tick", "wire"], default="cfg2",
+    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4", "tick", "wire", "multinode"], default="cfg2",
                     help="cfg2 (headline), cfg3 lagging followers, cfg4 election storm, "
                          "tick = MultiNode.Tick over the cfg2 groups (SURVEY.md 8(f) rank 1), "
-                         "wire = cfg2 from raftpb wire records: hb_decode + hb_step (8(f) rank 3)")
+                         "wire = cfg2 from raftpb wire records: hb_decode + hb_step (8(f) rank 3), "
+                         "multinode = the MultiNode API end to end (Step/Propose/Ready/Advance, 8(f) rank 2)")
     ap.add_argument("--groups", type=int, default=None, help="groups per GPU (cfg2/cfg3: 1M, cfg4: 4M)")
     ap.add_argument("--replicas", type=int, default=None, help="cfg2: 3, cfg3: 5, cfg4: 7")
     ap.add_argument("--inflight", type=int, default=256, help="MaxInflightMsgs W (cfg3/cfg4)")
@@ -266,6 +307,8 @@ def main():
     ap.add_argument("--traffic-json", default=None,
                     help="profiles/<tag>_traffic.json from tools/profile_round.sh (default: newest in profiles/)")
     args = ap.parse_args()
+    if args.workload == "multinode":
+        return run_multinode(args)
     if args.groups is None:
         args.groups = (1 << 22) if args.workload == "cfg4" else (1 << 20)
     if args.replicas is None:

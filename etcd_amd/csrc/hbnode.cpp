@@ -305,6 +305,30 @@ struct Log {
     out.resize(limit_count(out, max_size));
     return out;
   }
+  // slice(lo, hi, noLimit) as a visit over the entries in place (no copies)
+  template <class F>
+  void visit(uint64_t lo, uint64_t hi, F&& f) const {
+    if (lo > hi) panicf("invalid slice " + std::to_string(lo) + " > " + std::to_string(hi));
+    const uint64_t fi = first_index(), li = last_index();
+    if (lo < fi || hi > li + 1)
+      panicf("slice[" + std::to_string(lo) + "," + std::to_string(hi) + ") out of bound [" + std::to_string(fi) +
+             "," + std::to_string(li) + "]");
+    if (lo == hi) return;
+    if (lo < offset) {
+      const uint64_t h = std::min(hi, offset);
+      size_t a, k;
+      const int rc = st->entries(lo, h, HB_NO_LIMIT, &a, &k);
+      if (rc == HBN_ECOMPACTED)
+        panicf("entries[" + std::to_string(lo) + ":" + std::to_string(h) + ") from storage is out of bound");
+      if (rc == HBN_EUNAVAILABLE)
+        panicf("entries[" + std::to_string(lo) + ":" + std::to_string(h) + ") is unavailable from storage");
+      for (size_t i = 0; i < k; ++i) f(st->ents[a + i]);
+    }
+    if (hi > offset) {
+      const uint64_t a = std::max(lo, offset);
+      for (uint64_t i = a; i < hi; ++i) f(unstable[i - offset]);
+    }
+  }
   // entries :219-224
   std::vector<Ent> entries(uint64_t i, uint64_t max_size) const {
     if (i > last_index()) return {};
@@ -343,7 +367,9 @@ struct Log {
 struct Msg {
   uint32_t type = 0, reject = 0;
   uint64_t to = 0, from = 0, term = 0, log_term = 0, index = 0, commit = 0, reject_hint = 0;
-  std::vector<Ent> entries;
+  std::vector<Ent> entries;  // owned entries (proposals), or
+  uint64_t ent_lo = 0, ent_hi = 0;  // log range [lo, hi) still to be read (MsgApp), when !owned
+  bool owned = true;
   bool has_snap = false;
   Snap snap;
 };
@@ -361,6 +387,16 @@ bool hs_empty(const hbn_hard_state& a) { return a.term == 0 && a.vote == 0 && a.
 
 constexpr uint32_t NO_SLOT = 0xFFFFFFFFu;
 
+struct Delivered {
+  bool has_soft = false;
+  Soft soft;
+  hbn_hard_state hard{0, 0, 0};
+  bool has_last = false;
+  uint64_t last_index = 0, last_term = 0;
+  uint64_t snap_index = 0;
+};
+
+
 struct Group {
   uint64_t id = 0;
   uint32_t slot = NO_SLOT;  // device slot, NO_SLOT while prs is empty (host-only)
@@ -376,6 +412,9 @@ struct Group {
   std::deque<Msg> props;  // MsgProp in flight through the device batch, arrival order
   std::vector<Msg> msgs;  // r.msgs since the last Ready
   uint32_t election = 10, heartbeat = 1;
+  // Ready bookkeeping flags (membership of the node's lists)
+  bool touched = false, stepped = false, content = false, delivered = false;
+  Delivered dlv;  // what the last Ready delivered for this group (commitReady input)
 
   hbn_hard_state hard() const { return hbn_hard_state{term, vote, hs_commit}; }
   Soft soft() const { return Soft{lead, state}; }
@@ -384,15 +423,6 @@ struct Group {
       if (peers[s] == node) return (int)s;
     return -1;
   }
-};
-
-struct Delivered {
-  bool has_soft = false;
-  Soft soft;
-  hbn_hard_state hard{0, 0, 0};
-  bool has_last = false;
-  uint64_t last_index = 0, last_term = 0;
-  uint64_t snap_index = 0;
 };
 
 }  // namespace
@@ -408,20 +438,24 @@ struct hbn_node {
   // pending device batch (host SoA, HB_STEP_HOST_PTRS)
   std::vector<uint32_t> b_group, b_info;
   std::vector<uint64_t> b_term, b_index, b_hint;
-  std::unordered_set<Group*> stepped;  // groups whose raft.Step runs in the pending batch
+  std::vector<Group*> stepped;  // groups whose raft.Step runs in the pending batch
   std::vector<hb_event> evbuf;
+  // CreateGroup loads, coalesced into one hb_load_groups / hb_load_timers per slot run
+  std::vector<std::pair<uint32_t, hb_group>> pend_rec;
+  std::vector<std::pair<uint32_t, hb_timer>> pend_tm;
   // Ready bookkeeping (raft/multinode.go:166-322)
-  std::unordered_set<uint64_t> touched;      // rds candidates since the last delivery
-  std::unordered_set<uint64_t> has_content;  // groups whose state-derived Ready is non-empty
+  std::vector<Group*> touched;    // rds candidates since the last delivery (Group::touched)
+  std::vector<Group*> content;    // groups whose state-derived Ready may be non-empty (lazy, Group::content)
+  std::vector<Group*> delivered;  // groups of the last Ready (Group::delivered)
   bool awaiting_advance = false;
-  std::unordered_map<uint64_t, Delivered> delivered;
-  // arena of the last Ready (valid until the next call)
+  // flat arena of the last Ready (valid until the next call); pointers patched at the end
   std::vector<hbn_group_ready> r_out;
-  std::deque<std::vector<hbn_entry>> r_ents;
-  std::deque<std::vector<hbn_message>> r_msgs;
-  std::deque<Ent> r_ent_store;
+  std::vector<hbn_entry> r_ents;
+  std::vector<uint64_t> r_ent_off;  // byte offset of each r_ents[i].data in r_bytes
+  std::vector<hbn_message> r_msgs;
+  std::vector<uint8_t> r_bytes;
+  std::vector<uint64_t> r_off;  // per r_out: entries, committed, messages offsets; per r_msgs: entries offset
   std::deque<Snap> r_snaps;
-  std::vector<Msg> r_msg_store;
 };
 
 namespace {
@@ -480,16 +514,6 @@ hb_group make_record(const hbn_node* n, const Group& g, const std::vector<hb_pro
   return r;
 }
 
-void load_timers(hbn_node* n, const Group& g, uint32_t elapsed, uint32_t rand_pos) {
-  hb_timer t;
-  std::memset(&t, 0, sizeof(t));
-  t.elapsed = elapsed;
-  t.rand_pos = rand_pos;
-  t.election_tick = (uint16_t)g.election;
-  t.heartbeat_tick = (uint16_t)g.heartbeat;
-  check(hb_load_timers(n->h, g.slot, 1, &t));
-}
-
 uint32_t alloc_slot(hbn_node* n) {
   if (n->free_slots.empty()) throw Fail{HB_ENOMEM};
   const uint32_t s = n->free_slots.back();
@@ -498,9 +522,27 @@ uint32_t alloc_slot(hbn_node* n) {
 }
 
 // ---------------------------------------------------------------- event replay
+void touch(hbn_node* n, Group& g) {
+  if (!g.touched) {
+    g.touched = true;
+    n->touched.push_back(&g);
+  }
+}
+
 void mark_stepped(hbn_node* n, Group& g) {
   g.hs_commit = g.log.committed;  // r.Commit = r.raftLog.committed after Step (raft/raft.go:488)
-  n->touched.insert(g.id);
+  touch(n, g);
+}
+
+// r.msgs entries are read from the log when the Ready is built; before the log
+// can lose them (Advance's stableTo, a Ready withheld until Advance) they are copied.
+void materialize(Group& g) {
+  for (Msg& m : g.msgs) {
+    if (m.owned) continue;
+    m.entries.clear();
+    if (m.ent_hi > m.ent_lo) g.log.visit(m.ent_lo, m.ent_hi, [&](const Ent& x) { m.entries.push_back(x); });
+    m.owned = true;
+  }
 }
 
 Msg base_msg(const hbn_node* n, const Group& g, uint32_t type, uint64_t to) {
@@ -574,7 +616,11 @@ void on_event(hbn_node* n, Group& g, const hb_event& e) {
       Msg m = base_msg(n, g, HB_MSG_APP, g.peers.at(e.to));
       m.index = e.x;
       m.log_term = g.log.term(e.x);
-      m.entries = g.log.entries(e.x + 1, n->max_msg);
+      // entries(Index+1, maxMsgSize): (Index, last] under noLimit, one entry under 0
+      const uint64_t li = g.log.last_index();
+      m.owned = false;
+      m.ent_lo = e.x + 1;
+      m.ent_hi = e.x + 1 > li ? e.x + 1 : (n->max_msg == 0 ? e.x + 2 : li + 1);
       m.commit = g.log.committed;
       g.msgs.push_back(std::move(m));
       break;
@@ -637,7 +683,31 @@ void consume_events(hbn_node* n) {
   }
 }
 
+// Push the queued CreateGroup records and timers to the device, one call per
+// run of consecutive slots (a million groups load in a few calls).
+template <class T, class F>
+void load_runs(std::vector<std::pair<uint32_t, T>>& v, F&& load) {
+  if (v.empty()) return;
+  std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::vector<T> run;
+  size_t i = 0;
+  while (i < v.size()) {
+    size_t j = i;
+    run.clear();
+    while (j < v.size() && v[j].first == v[i].first + (j - i)) run.push_back(v[j++].second);
+    check(load(v[i].first, (uint32_t)run.size(), run.data()));
+    i = j;
+  }
+  v.clear();
+}
+
+void sync_loads(hbn_node* n) {
+  load_runs(n->pend_rec, [&](uint32_t f, uint32_t c, const hb_group* r) { return hb_load_groups(n->h, f, c, r); });
+  load_runs(n->pend_tm, [&](uint32_t f, uint32_t c, const hb_timer* t) { return hb_load_timers(n->h, f, c, t); });
+}
+
 void flush(hbn_node* n) {
+  sync_loads(n);
   if (n->b_group.empty()) return;
   hb_batch b;
   b.n = n->b_group.size();
@@ -649,7 +719,10 @@ void flush(hbn_node* n) {
   b.props = nullptr;
   check(hb_step(n->h, &b, HB_STEP_HOST_PTRS));
   consume_events(n);
-  for (Group* g : n->stepped) mark_stepped(n, *g);
+  for (Group* g : n->stepped) {
+    g->stepped = false;
+    mark_stepped(n, *g);
+  }
   n->stepped.clear();
   n->b_group.clear();
   n->b_info.clear();
@@ -667,7 +740,7 @@ void push(hbn_node* n, Group& g, uint32_t type, uint64_t from, bool reject, uint
           uint64_t hint) {
   const int s = g.slot_of(from);
   const uint32_t fs = s >= 0 ? (uint32_t)s : HB_SLOT_NONE;
-  n->touched.insert(g.id);
+  touch(n, g);
   if (g.slot == NO_SLOT) {
     // prs is empty: every response is filtered (raft/multinode.go:235); anything
     // else would step a raft with no progress at all.
@@ -680,7 +753,10 @@ void push(hbn_node* n, Group& g, uint32_t type, uint64_t from, bool reject, uint
   n->b_term.push_back(term);
   n->b_index.push_back(index);
   n->b_hint.push_back(hint);
-  if (s >= 0 || !is_response(type)) n->stepped.insert(&g);
+  if ((s >= 0 || !is_response(type)) && !g.stepped) {
+    g.stepped = true;
+    n->stepped.push_back(&g);
+  }
 }
 
 Group& group_of(hbn_node* n, uint64_t id) {
@@ -698,65 +774,27 @@ void propose(hbn_node* n, Group& g, Msg m) {
 }
 
 // ---------------------------------------------------------------- Ready
-struct ReadyParts {
-  bool has_soft = false;
-  Soft soft;
-  hbn_hard_state hard{0, 0, 0};
-  bool has_snap = false;
-  Snap snap;
-  std::vector<Ent> entries, committed;
-};
-
-// newReady raft/node.go:447-463 (without Messages)
-ReadyParts new_ready(const Group& g) {
-  ReadyParts p;
-  p.entries = g.log.unstable;
-  p.committed = g.log.next_ents();
-  if (!(g.soft() == g.prev_soft)) {
-    p.has_soft = true;
-    p.soft = g.soft();
-  }
-  if (!hs_equal(g.hard(), g.prev_hard)) p.hard = g.hard();
-  if (g.log.has_usnap) {
-    p.has_snap = true;
-    p.snap = g.log.usnap;
-  }
-  return p;
-}
-// containsUpdates raft/node.go:96-100
-bool contains(const ReadyParts& p, size_t nmsgs) {
-  return p.has_soft || !hs_empty(p.hard) || (p.has_snap && p.snap.index != 0) || !p.entries.empty() ||
-         !p.committed.empty() || nmsgs > 0;
-}
-
-const hbn_entry* arena_entries(hbn_node* n, const std::vector<Ent>& src, uint64_t* count) {
-  *count = src.size();
-  if (src.empty()) return nullptr;
-  n->r_ents.emplace_back();
-  std::vector<hbn_entry>& v = n->r_ents.back();
-  v.reserve(src.size());
-  for (const Ent& x : src) {
-    n->r_ent_store.push_back(x);
-    const Ent& s = n->r_ent_store.back();
-    hbn_entry e;
-    e.term = s.term;
-    e.index = s.index;
-    e.type = s.type;
-    e.has_data = s.has_data;
-    e.data = s.data.empty() ? nullptr : reinterpret_cast<const uint8_t*>(s.data.data());
-    e.data_len = s.data.size();
-    v.push_back(e);
-  }
-  return v.data();
+void arena_entry(hbn_node* n, const Ent& x) {
+  hbn_entry e;
+  e.term = x.term;
+  e.index = x.index;
+  e.type = x.type;
+  e.has_data = x.has_data;
+  e.data = nullptr;
+  e.data_len = x.data.size();
+  n->r_ent_off.push_back(n->r_bytes.size());
+  if (!x.data.empty()) n->r_bytes.insert(n->r_bytes.end(), x.data.begin(), x.data.end());
+  n->r_ents.push_back(e);
 }
 
 void clear_arena(hbn_node* n) {
   n->r_out.clear();
   n->r_ents.clear();
+  n->r_ent_off.clear();
   n->r_msgs.clear();
-  n->r_ent_store.clear();
+  n->r_bytes.clear();
+  n->r_off.clear();
   n->r_snaps.clear();
-  n->r_msg_store.clear();
 }
 
 // commitReady raft/multinode.go:137-164
@@ -771,11 +809,19 @@ void commit_ready(Group& g, const Delivered& d) {
   }
 }
 
-void refresh_content(hbn_node* n, const Group& g) {
-  if (contains(new_ready(g), 0))
-    n->has_content.insert(g.id);
-  else
-    n->has_content.erase(g.id);
+// containsUpdates of newReady(g) without building it
+bool has_updates(const Group& g) {
+  if (!(g.soft() == g.prev_soft) || !hs_equal(g.hard(), g.prev_hard)) {
+    if (!(g.soft() == g.prev_soft) || !hs_empty(g.hard())) return true;
+  }
+  if (!g.log.unstable.empty() || (g.log.has_usnap && g.log.usnap.index != 0)) return true;
+  return g.log.committed + 1 > std::max(g.log.applied + 1, g.log.first_index());
+}
+
+void refresh_content(hbn_node* n, Group& g) {
+  const bool c = has_updates(g);
+  if (c && !g.content) n->content.push_back(&g);
+  g.content = c;
 }
 
 // Rebuild the device record of g after prs changed (ApplyConfChange).
@@ -789,6 +835,7 @@ void reload_prs(hbn_node* n, Group& g, const std::vector<uint64_t>& new_peers,
   std::vector<uint32_t> ins_start;
   const std::vector<uint64_t> old_peers = g.peers;
   if (g.slot != NO_SLOT) {
+    sync_loads(n);
     check(hb_get_groups(n->h, g.slot, 1, &old));
     check(hb_get_timers(n->h, g.slot, 1, &tm));
     ins.resize(old_peers.size());
@@ -1092,7 +1139,6 @@ int hbn_create_group(hbn_node* n, uint64_t group, const hbn_config* cfg, hbn_sto
     return HB_EINVAL;
   if (n->groups.count(group)) return HBN_EEXIST;
   return guarded([&] {
-    flush(n);
     auto gp = std::make_unique<Group>();
     Group& g = *gp;
     g.id = group;
@@ -1149,19 +1195,18 @@ int hbn_create_group(hbn_node* n, uint64_t group, const hbn_config* cfg, hbn_sto
     }
     if (!g.peers.empty()) {
       g.slot = alloc_slot(n);
-      const hb_group r = make_record(n, g, prs);
-      const int rc = hb_load_groups(n->h, g.slot, 1, &r);
-      if (rc != HB_OK) {
-        n->free_slots.push_back(g.slot);
-        throw Fail{rc};
-      }
+      n->pend_rec.emplace_back(g.slot, make_record(n, g, prs));
+      hb_timer t;
+      std::memset(&t, 0, sizeof(t));
+      t.election_tick = (uint16_t)g.election;
+      t.heartbeat_tick = (uint16_t)g.heartbeat;
+      n->pend_tm.emplace_back(g.slot, t);
       n->by_slot[g.slot] = &g;
-      load_timers(n, g, 0, 0);
     }
     // the initial hard and soft states (:213-215)
     g.prev_soft = g.soft();
     g.prev_hard = g.hard();
-    n->touched.insert(group);
+    touch(n, g);
     n->groups.emplace(group, std::move(gp));
   });
 }
@@ -1178,9 +1223,8 @@ int hbn_remove_group(hbn_node* n, uint64_t group) {
       n->by_slot[g.slot] = nullptr;
       n->free_slots.push_back(g.slot);
     }
-    n->touched.erase(group);
-    n->has_content.erase(group);
-    n->delivered.erase(group);
+    for (auto* v : {&n->touched, &n->content, &n->delivered, &n->stepped})
+      v->erase(std::remove(v->begin(), v->end(), &g), v->end());
     n->groups.erase(it);
   });
 }
@@ -1195,10 +1239,16 @@ int hbn_set_rand(hbn_node* n, uint64_t first, uint64_t count, const uint64_t* dr
 int hbn_tick(hbn_node* n) {
   if (!n) return HB_EINVAL;
   return guarded([&] {
-    flush(n);
+    flush(n);  // (also pushes queued loads)
     check(hb_tick(n->h, 0));
     consume_events(n);
-    for (uint64_t id : n->has_content) n->touched.insert(id);
+    size_t k = 0;  // every group with pending content is a Ready candidate again; drop stale entries
+    for (Group* g : n->content)
+      if (g->content) {
+        touch(n, *g);
+        n->content[k++] = g;
+      }
+    n->content.resize(k);
   });
 }
 
@@ -1293,7 +1343,7 @@ int hbn_apply_conf_change(hbn_node* n, uint64_t group, uint32_t cc_type, uint64_
     flush(n);
     Group& g = group_of(n, group);
     if (g.fault) throw Fail{HBN_EPANIC};
-    n->touched.insert(group);
+    touch(n, g);
     if (node_id != 0) {
       std::vector<uint64_t> np = g.peers;
       switch (cc_type) {
@@ -1335,81 +1385,97 @@ int hbn_ready(hbn_node* n, const hbn_group_ready** out, uint64_t* count) {
     flush(n);
     clear_arena(n);
     if (n->awaiting_advance) {
+      // readyc is not selectable; r.msgs keep accumulating, so pin their entries
+      for (Group* g : n->touched) materialize(*g);
       rc = HBN_EAGAIN;
       return;
     }
-    std::vector<uint64_t> ids(n->touched.begin(), n->touched.end());
-    std::sort(ids.begin(), ids.end());
-    n->touched.clear();
+    for (Group* g : n->delivered) g->delivered = false;
     n->delivered.clear();
-    n->r_out.reserve(ids.size());
-    for (uint64_t id : ids) {
-      auto it = n->groups.find(id);
-      if (it == n->groups.end()) continue;
-      Group& g = *it->second;
-      ReadyParts p = new_ready(g);
-      if (contains(p, 0))
-        n->has_content.insert(id);
-      else
-        n->has_content.erase(id);
-      if (!contains(p, g.msgs.size()) && !g.fault) continue;
+    for (Group* gp : n->touched) {
+      Group& g = *gp;
+      g.touched = false;
+      refresh_content(n, g);
+      if (!g.content && g.msgs.empty() && !g.fault) continue;  // containsUpdates (raft/node.go:96-100)
+      // newReady raft/node.go:447-463
       hbn_group_ready r;
       std::memset(&r, 0, sizeof(r));
-      r.group = id;
-      r.has_soft_state = p.has_soft;
-      r.raft_state = p.soft.state;
-      r.lead = p.soft.lead;
-      r.hard_state = p.hard;
-      if (p.has_snap) {
-        n->r_snaps.push_back(p.snap);
+      r.group = g.id;
+      Delivered& d = g.dlv;
+      d = Delivered{};
+      if (!(g.soft() == g.prev_soft)) {
+        r.has_soft_state = 1;
+        r.raft_state = g.state;
+        r.lead = g.lead;
+        d.has_soft = true;
+        d.soft = g.soft();
+      }
+      if (!hs_equal(g.hard(), g.prev_hard)) r.hard_state = d.hard = g.hard();
+      if (g.log.has_usnap) {
+        n->r_snaps.push_back(g.log.usnap);
         snap_view(n->r_snaps.back(), &r.snapshot);
+        d.snap_index = g.log.usnap.index;
       }
-      r.entries = arena_entries(n, p.entries, &r.n_entries);
-      r.committed_entries = arena_entries(n, p.committed, &r.n_committed);
-      // Messages (r.msgs), then cleared (:277-281)
-      if (!g.msgs.empty()) {
-        n->r_msgs.emplace_back();
-        std::vector<hbn_message>& mv = n->r_msgs.back();
-        for (Msg& m : g.msgs) {
-          hbn_message x;
-          std::memset(&x, 0, sizeof(x));
-          x.type = m.type;
-          x.reject = m.reject;
-          x.to = m.to;
-          x.from = m.from;
-          x.term = m.term;
-          x.log_term = m.log_term;
-          x.index = m.index;
-          x.commit = m.commit;
-          x.reject_hint = m.reject_hint;
-          x.entries = arena_entries(n, m.entries, &x.n_entries);
-          if (m.has_snap) {
-            n->r_snaps.push_back(m.snap);
-            snap_view(n->r_snaps.back(), &x.snapshot);
-          }
-          mv.push_back(x);
-        }
-        r.messages = mv.data();
-        r.n_messages = mv.size();
-        g.msgs.clear();
-      }
-      r.fault = g.fault;
-      Delivered d;
-      d.has_soft = p.has_soft;
-      d.soft = p.soft;
-      d.hard = p.hard;
-      if (!p.entries.empty()) {
+      n->r_off.push_back(n->r_ents.size());  // Entries = unstableEntries
+      for (const Ent& x : g.log.unstable) arena_entry(n, x);
+      r.n_entries = g.log.unstable.size();
+      if (r.n_entries) {
         d.has_last = true;
-        d.last_index = p.entries.back().index;
-        d.last_term = p.entries.back().term;
+        d.last_index = g.log.unstable.back().index;
+        d.last_term = g.log.unstable.back().term;
       }
-      d.snap_index = p.has_snap ? p.snap.index : 0;
-      n->delivered[id] = d;
+      n->r_off.push_back(n->r_ents.size());  // CommittedEntries = nextEnts (raft/log.go:135-141)
+      const uint64_t lo = std::max(g.log.applied + 1, g.log.first_index());
+      if (g.log.committed + 1 > lo) g.log.visit(lo, g.log.committed + 1, [&](const Ent& x) { arena_entry(n, x); });
+      r.n_committed = n->r_ents.size() - n->r_off.back();
+      n->r_off.push_back(n->r_msgs.size());  // Messages = r.msgs, then cleared (raft/multinode.go:277-281)
+      for (Msg& m : g.msgs) {
+        hbn_message x;
+        std::memset(&x, 0, sizeof(x));
+        x.type = m.type;
+        x.reject = m.reject;
+        x.to = m.to;
+        x.from = m.from;
+        x.term = m.term;
+        x.log_term = m.log_term;
+        x.index = m.index;
+        x.commit = m.commit;
+        x.reject_hint = m.reject_hint;
+        const size_t e0 = n->r_ents.size();
+        if (m.owned)
+          for (const Ent& e : m.entries) arena_entry(n, e);
+        else if (m.ent_hi > m.ent_lo)
+          g.log.visit(m.ent_lo, m.ent_hi, [&](const Ent& e) { arena_entry(n, e); });
+        x.n_entries = n->r_ents.size() - e0;
+        x.entries = reinterpret_cast<const hbn_entry*>(e0);  // offset, patched below
+        if (m.has_snap) {
+          n->r_snaps.push_back(m.snap);
+          snap_view(n->r_snaps.back(), &x.snapshot);
+        }
+        n->r_msgs.push_back(x);
+      }
+      r.n_messages = g.msgs.size();
+      g.msgs.clear();
+      r.fault = g.fault;
+      g.delivered = true;
+      n->delivered.push_back(&g);
       n->r_out.push_back(r);
     }
+    n->touched.clear();
     if (n->r_out.empty()) {
       rc = HBN_EAGAIN;
       return;
+    }
+    // patch the arena pointers now that no vector grows any more
+    for (size_t i = 0; i < n->r_ents.size(); ++i)
+      if (n->r_ents[i].data_len) n->r_ents[i].data = n->r_bytes.data() + n->r_ent_off[i];
+    for (hbn_message& x : n->r_msgs)
+      x.entries = x.n_entries ? n->r_ents.data() + reinterpret_cast<uintptr_t>(x.entries) : nullptr;
+    for (size_t i = 0; i < n->r_out.size(); ++i) {
+      hbn_group_ready& r = n->r_out[i];
+      r.entries = r.n_entries ? n->r_ents.data() + n->r_off[3 * i] : nullptr;
+      r.committed_entries = r.n_committed ? n->r_ents.data() + n->r_off[3 * i + 1] : nullptr;
+      r.messages = r.n_messages ? n->r_msgs.data() + n->r_off[3 * i + 2] : nullptr;
     }
     n->awaiting_advance = true;
   });
@@ -1426,14 +1492,14 @@ int hbn_advance(hbn_node* n, const uint64_t* groups, uint64_t count) {
     flush(n);
     for (uint64_t i = 0; i < count; ++i) {
       auto it = n->groups.find(groups[i]);
-      auto dt = n->delivered.find(groups[i]);
-      if (it == n->groups.end() || dt == n->delivered.end()) continue;
+      if (it == n->groups.end() || !it->second->delivered) continue;
       Group& g = *it->second;
-      commit_ready(g, dt->second);
-      n->delivered.erase(dt);
+      g.delivered = false;
+      materialize(g);  // messages stepped since the Ready still read the log
+      commit_ready(g, g.dlv);
+      // the recomputed Ready (raft/multinode.go:290-295) is a candidate again
       refresh_content(n, g);
-      // the recomputed Ready (:290-295) is a candidate again
-      n->touched.insert(g.id);
+      touch(n, g);
     }
     n->awaiting_advance = false;
   });
