@@ -367,14 +367,23 @@ struct ApplyArgs {
   uint32_t* pflag;          // [NB][PART/32] groups handed from k_apply_fast to k_apply
   uint32_t* resume;         // [G] messages consumed by k_apply_fast | prop pending << 31
   uint64_t* commit0;        // [G] committed at batch start (for HB_STAT_COMMITS)
-  // k_route -> k_apply_fast: each group's first kmax messages, lane-major
-  uint32_t kmax;            // slots per group (= nmax - 1)
+  // k_route -> k_apply_fast / k_apply: each group's first kmax messages, lane-major
+  uint32_t kmax;            // slots per group (= route_kmax(nmax))
   uint8_t* cnt;             // [G] messages of the group in this batch (saturated at 255)
   uint32_t* slot_info;      // [kmax][G]
   uint32_t* slot_orig;      // [kmax][G]
   uint64_t* slot_term;      // [kmax][G]
   uint64_t* slot_index;     // [kmax][G]
 };
+
+// Message slots k_route keeps per group: n - 1 (one MsgAppResp per follower,
+// what k_apply_fast consumes), plus HB_KS_EXTRA for n >= 5 so that k_apply
+// reads a handed-over group's messages from its slots (an election: MsgHup +
+// n - 1 MsgVoteResp + a step-down) instead of walking the bucket.
+#ifndef HB_KS_EXTRA
+#define HB_KS_EXTRA 2
+#endif
+constexpr uint32_t route_kmax(int nmax) { return nmax <= 3 ? 2u : (uint32_t)(nmax - 1 + HB_KS_EXTRA); }
 
 // stats slots reduced per workgroup
 enum { ST_MSGS, ST_APPRESP, ST_VOTERESP, ST_DROPPED, ST_COMMITS, ST_WON, ST_LOST, ST_FAULTS, ST_ENTRIES, ST_N };
@@ -611,7 +620,7 @@ __device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_sta
 // ---------------------------------------------------------------------------
 // k_route<KMAX>: W = BK / RG workgroups per bucket, each owning RG groups
 // (RG x KMAX message slots fit in LDS: RG = 2048 / 1024 / 512 for KMAX =
-// 2 / 4 / 6).  Each workgroup streams its bucket's records (coalesced; the W
+// 2 / <= 4 / <= 8).  Each workgroup streams its bucket's records (coalesced; the W
 // sisters of a bucket share one XCD's L2), ranks the messages of its groups
 // with one LDS counter per group, stages each group's first KMAX messages in
 // LDS and writes them out lane-major (slot k of group g at slots.*[k][g]) with
@@ -862,10 +871,16 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
 // ---------------------------------------------------------------------------
 // k_apply: the general state machine (Lane::step) for the groups k_apply_fast
 // handed over, from their resume point.  Partitions without such groups exit
-// after reading their flag words.
+// after reading their flag words.  A group whose messages all sit in its
+// k_route slots (count <= route_kmax) steps them from there, in arrival order;
+// the bucket is walked (LDS rounds) only when some group of the partition has
+// more messages than slots.
 // ---------------------------------------------------------------------------
+#ifndef HB_GEN_WAVES
+#define HB_GEN_WAVES 2
+#endif
 template <int NMAX>
-__global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
+__global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
   __shared__ Stage<CHUNK> sl;
   __shared__ uint32_t l_fill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
@@ -914,9 +929,61 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
   uint32_t j = 0;
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
 
+  constexpr uint32_t KS = route_kmax(NMAX);
+  const uint32_t cnt = flagged ? a.cnt[g] : 0u;
+  const bool by_slot = flagged && cnt <= KS;
+  const bool by_walk = flagged && !by_slot;
+  __syncthreads();  // l_fill
+  if (by_slot) {
+    if (resume >> 31) {
+      L.arrival = 0xFFFFFFFFu;
+      L.step(HB_MSG_PROP, L.self(), 0, a.props[g], false, 0);
+    }
+    // arrival order of the slots: odd-even transposition over the arrival
+    // indices, the slot numbers riding along as nibbles of `perm`
+    uint32_t key[KS];
+    uint32_t perm = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < KS; ++k) {
+      key[k] = k < cnt ? a.slot_orig[(size_t)k * a.S.G + g] : 0xFFFFFFFFu;
+      perm |= k << (4 * k);
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < KS; ++r) {
+#pragma unroll
+      for (uint32_t k = (r & 1); k + 1 < KS; k += 2) {
+        const uint32_t k0 = key[k], k1 = key[k + 1];
+        const bool sw = k1 < k0;
+        key[k] = sw ? k1 : k0;
+        key[k + 1] = sw ? k0 : k1;
+        const uint32_t p0 = (perm >> (4 * k)) & 0xF, p1 = (perm >> (4 * (k + 1))) & 0xF;
+        const uint32_t swp = (perm & ~(0xFFu << (4 * k))) | (p1 << (4 * k)) | (p0 << (4 * (k + 1)));
+        perm = sw ? swp : perm;
+      }
+    }
+#pragma unroll
+    for (uint32_t x = 0; x < KS; ++x) {
+      if (x >= cnt || L.faulted()) break;
+      if (x < skip) continue;
+      const size_t o = (size_t)((perm >> (4 * x)) & 0xF) * a.S.G + g;
+      const uint32_t inf = a.slot_info[o];
+      const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
+      const bool reject = (inf >> 8) & 1u;
+      if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
+        st_drop++;
+        continue;
+      }
+      L.arrival = key[x];
+      L.step(type, from, a.slot_term[o], a.slot_index[o], reject, (reject && a.hint) ? a.hint[key[x]] : 0ull);
+      st_msgs++;
+      st_app += type == HB_MSG_APP_RESP;
+      st_vote += type == HB_MSG_VOTE_RESP;
+    }
+  }
+
   auto on_total = [&](uint32_t) {
     __syncthreads();  // l_fill
-    if (flagged && (resume >> 31)) {
+    if (by_walk && (resume >> 31)) {
       L.arrival = 0xFFFFFFFFu;
       L.step(HB_MSG_PROP, L.self(), 0, a.props[g], false, 0);
     }
@@ -924,7 +991,7 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
   auto round = [&](uint32_t fill) {
     uint32_t my_start, my_cnt;
     gather_round(sl, a, lo, fill, &my_start, &my_cnt, []() {});
-    if (flagged) {
+    if (by_walk) {
       for (uint32_t x = 0; x < my_cnt; ++x, ++j) {
         if (j < skip) continue;
         const uint32_t i = sl.perm[my_start + x];
@@ -945,7 +1012,7 @@ __global__ void __launch_bounds__(PART, 2) k_apply(ApplyArgs a) {
     }
     __syncthreads();
   };
-  walk_partition(sl, a, lo, hi, sub, nullptr, on_total, round);
+  if (__syncthreads_or(by_walk)) walk_partition(sl, a, lo, hi, sub, nullptr, on_total, round);
 
   if (flagged) L.store();
   const uint64_t vals[ST_N + 1] = {st_msgs,
@@ -1618,10 +1685,10 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
     if (h->passes > 1) ALLOC(ps.bucket, mb);
     ALLOC(ps.bk_off, h->NBK + 1);
     ALLOC(ps.cnt, G);
-    ALLOC(ps.slot_info, (R - 1) * G);
-    ALLOC(ps.slot_orig, (R - 1) * G);
-    ALLOC(ps.slot_term, (R - 1) * G);
-    ALLOC(ps.slot_index, (R - 1) * G);
+    ALLOC(ps.slot_info, route_kmax(R) * G);
+    ALLOC(ps.slot_orig, route_kmax(R) * G);
+    ALLOC(ps.slot_term, route_kmax(R) * G);
+    ALLOC(ps.slot_index, route_kmax(R) * G);
     ALLOC(ps.ev_counts, 2ull * h->NB);
     ALLOC(ps.ev_off, 2ull * h->NB);
   }
@@ -2070,16 +2137,16 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.pflag = h->pflag;
   aa.resume = h->resume;
   aa.commit0 = h->commit0;
-  aa.kmax = h->nmax - 1;
+  aa.kmax = route_kmax(h->nmax);
   aa.cnt = ps.cnt;
   aa.slot_info = ps.slot_info;
   aa.slot_orig = ps.slot_orig;
   aa.slot_term = ps.slot_term;
   aa.slot_index = ps.slot_index;
   switch (h->nmax) {
-    case 3: launch_route<2>(h, aa, ps_st); break;
-    case 5: launch_route<4>(h, aa, ps_st); break;
-    default: launch_route<6>(h, aa, ps_st); break;
+    case 3: launch_route<route_kmax(3)>(h, aa, ps_st); break;
+    case 5: launch_route<route_kmax(5)>(h, aa, ps_st); break;
+    default: launch_route<route_kmax(7)>(h, aa, ps_st); break;
   }
   if (prof) HB_CHECK(hipEventRecord(ev[1], ps_st));
   if (two) {
