@@ -365,7 +365,7 @@ struct ApplyArgs {
   uint64_t* ev_off;         // [NB] chunk offsets (records)
   uint64_t* stats_shard;    // [8][16] step statistics, one shard per XCD slot (atomic adds)
   uint32_t* pflag;          // [NB][PART/32] groups handed from k_apply_fast to k_apply
-  uint32_t* resume;         // [G] messages consumed by k_apply_fast | prop pending << 31
+  uint32_t* resume;         // [G] messages consumed by k_apply_fast | not loaded << 30 | prop pending << 31
   uint64_t* commit0;        // [G] committed at batch start (for HB_STAT_COMMITS)
   // k_route -> k_apply_fast / k_apply: each group's first kmax messages, lane-major
   uint32_t kmax;            // slots per group (= route_kmax(nmax))
@@ -632,7 +632,10 @@ __device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_sta
 // bucket's region (one atomic per partition).  No raft logic runs here.
 // ---------------------------------------------------------------------------
 constexpr uint32_t ROUTE_THREADS = 1024;
-constexpr uint32_t ROUTE_UNROLL = 4;  // records in flight per lane
+#ifndef HB_ROUTE_UNROLL
+#define HB_ROUTE_UNROLL 4
+#endif
+constexpr uint32_t ROUTE_UNROLL = HB_ROUTE_UNROLL;  // records in flight per lane
 template <int KMAX> struct RouteGeom {
   static constexpr uint32_t RG_LOG = KMAX <= 2 ? 11 : (KMAX <= 4 ? 10 : 9);
   static constexpr uint32_t RG = 1u << RG_LOG;     // groups per workgroup
@@ -660,21 +663,21 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
   const uint32_t G = a.S.G;
   const uint32_t lg0 = w * RG;  // first group (in the bucket) of this workgroup
+  const uint32_t sub_lo = lg0 >> PART_LOG, sub_hi = (lg0 + RG) >> PART_LOG;
   for (uint32_t base = lo; base < hi; base += ROUTE_THREADS * ROUTE_UNROLL) {
     MsgRec m[ROUTE_UNROLL];
     uint32_t sub[ROUTE_UNROLL];
 #pragma unroll
     for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
       const uint32_t p = base + u * ROUTE_THREADS + tid;
-      if (p < hi) {
-        m[u] = a.rec[p];
-        sub[u] = a.key[p];
-      }
+      sub[u] = p < hi ? a.key[p] : 0xFFu;
+      if (p < hi) m[u] = a.rec[p];
     }
 #pragma unroll
     for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
       const uint32_t p = base + u * ROUTE_THREADS + tid;
-      const uint32_t l = p < hi ? ((sub[u] << PART_LOG) | ((m[u].info >> 16) & (PART - 1))) - lg0 : RG;
+      const bool own = p < hi && sub[u] >= sub_lo && sub[u] < sub_hi;
+      const uint32_t l = own ? (((sub[u] - sub_lo) << PART_LOG) | ((m[u].info >> 16) & (PART - 1))) : RG;
       if (l < RG) {
         const uint32_t r = atomicAdd(&l_cnt[l], 1u);
         if (r < (uint32_t)KMAX) {
@@ -753,10 +756,14 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   const uint32_t cnt = gvalid ? a.cnt[g] : 0u;
   // A group takes part when its slot is live (n > 0) and not faulted.
   const bool live = gvalid && L.n() != 0 && L.faulted() == 0;
+  // Only a leader has fast-path work: any other live group is handed to
+  // k_apply whole, without loading its state here (resume bit 30: commit0 =
+  // its committed as k_apply loads it).
+  const bool lead = live && L.state() == HB_STATE_LEADER;
   L.dirty = 0;
   L.nev = 0;
   L.last = L.committed = 0;
-  if (live) L.load();
+  if (lead) L.load();
   uint32_t s_info[KMAX], s_orig[KMAX];
   uint64_t s_term[KMAX], s_index[KMAX];
 #pragma unroll
@@ -816,11 +823,15 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   L.E.chunk = a.ev + moff;
   L.E.fill = &l_fill;
   uint32_t j = 0;  // messages consumed
+  if (live && !lead && cnt > 0 && !flagged) {
+    flagged = true;
+    resume = 0;
+  }
   if (live && cnt > KMAX && !flagged && !L.faulted()) {  // the slots hold an arbitrary KMAX: all to k_apply
     flagged = true;
     resume = 0;
   }
-  if (live) {
+  if (lead) {
 #pragma unroll
     for (uint32_t k = 0; k < KMAX; ++k) {
       if (k >= cnt || flagged || L.faulted()) break;
@@ -844,11 +855,11 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
     }
   }
 
-  L.store();
+  if (lead) L.store();
   if (flagged) {
     atomicOr(&l_flag[tid >> 5], 1u << (tid & 31));
-    a.resume[g] = resume;
-    a.commit0[g] = commit0;
+    a.resume[g] = resume | (lead ? 0u : 1u << 30);
+    if (lead) a.commit0[g] = commit0;
   }
   const uint64_t vals[ST_N + 1] = {st_msgs,
                                    st_msgs,  // every fast message is a MsgAppResp
@@ -921,11 +932,11 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
     L.meta = a.S.meta[g];
     L.load_all();
     resume = a.resume[g];
-    commit0 = a.commit0[g];
+    commit0 = ((resume >> 30) & 1u) ? L.committed : a.commit0[g];
   }
   const uint64_t last0 = L.last;
   uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
-  const uint32_t skip = resume & 0x7FFFFFFFu;
+  const uint32_t skip = resume & 0x3FFFFFFFu;
   uint32_t j = 0;
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
 
@@ -961,12 +972,27 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
         perm = sw ? swp : perm;
       }
     }
+    // the next message's loads are issued before this one is stepped
+    uint32_t inf_n = 0;
+    uint64_t term_n = 0, index_n = 0;
+    if (cnt > skip) {
+      const size_t o = (size_t)((perm >> (4 * skip)) & 0xF) * a.S.G + g;
+      inf_n = a.slot_info[o];
+      term_n = a.slot_term[o];
+      index_n = a.slot_index[o];
+    }
 #pragma unroll
     for (uint32_t x = 0; x < KS; ++x) {
       if (x >= cnt || L.faulted()) break;
       if (x < skip) continue;
-      const size_t o = (size_t)((perm >> (4 * x)) & 0xF) * a.S.G + g;
-      const uint32_t inf = a.slot_info[o];
+      const uint32_t inf = inf_n;
+      const uint64_t mterm = term_n, mindex = index_n;
+      if (x + 1 < cnt) {
+        const size_t o = (size_t)((perm >> (4 * (x + 1))) & 0xF) * a.S.G + g;
+        inf_n = a.slot_info[o];
+        term_n = a.slot_term[o];
+        index_n = a.slot_index[o];
+      }
       const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
       const bool reject = (inf >> 8) & 1u;
       if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
@@ -974,7 +1000,7 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
         continue;
       }
       L.arrival = key[x];
-      L.step(type, from, a.slot_term[o], a.slot_index[o], reject, (reject && a.hint) ? a.hint[key[x]] : 0ull);
+      L.step(type, from, mterm, mindex, reject, (reject && a.hint) ? a.hint[key[x]] : 0ull);
       st_msgs++;
       st_app += type == HB_MSG_APP_RESP;
       st_vote += type == HB_MSG_VOTE_RESP;
