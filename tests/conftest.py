@@ -11,3 +11,15 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: longer CPU test")
+
+
+@pytest.fixture(autouse=True, scope="session")
+def _torch_hip_first(request):
+    """GPU sessions: torch's HIP runtime initialises before the engine's (a
+    test that needs torch after an engine was created in the same process then
+    still finds the device)."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    yield
