@@ -176,11 +176,16 @@ _TYPES = np.array([A.HB_MSG_APP_RESP, A.HB_MSG_HEARTBEAT_RESP, A.HB_MSG_VOTE_RES
 _TYPE_P = np.array([0.42, 0.10, 0.16, 0.04, 0.05, 0.12, 0.05, 0.06])
 
 
-def random_batch(groups, nmsg, seed=2, nonmember=0.04, props=True):
-    """Random messages of every device type against `groups` (ids < len(groups))."""
+def random_batch(groups, nmsg, seed=2, nonmember=0.04, props=True, grp=None):
+    """Random messages of every device type against `groups` (ids < len(groups));
+    `grp`: the message groups in arrival order (default: uniform)."""
     rng = np.random.default_rng(seed)
     G = len(groups)
-    grp = rng.integers(0, G, nmsg).astype(np.uint32)
+    if grp is None:
+        grp = rng.integers(0, G, nmsg).astype(np.uint32)
+    else:
+        grp = np.ascontiguousarray(grp, dtype=np.uint32)
+        nmsg = len(grp)
     t = rng.choice(_TYPES, size=nmsg, p=_TYPE_P / _TYPE_P.sum()).astype(np.uint32)
     n = groups["n"][grp].astype(np.int64)
     slot = (rng.random(nmsg) * n).astype(np.uint32)

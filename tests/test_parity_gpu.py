@@ -258,3 +258,24 @@ def test_tick_draws_exhausted():
     for k in range(4):
         _, st, _ = pair.tick(ctx=f"exhaust {k}")
     assert (pair.og.groups()["fault"] == abi.HB_FAULT_RAND_EXHAUSTED).sum() > 0
+
+
+@pytest.mark.parametrize("nmax", [5, 7])
+def test_general_kernel_slot_boundary(nmax):
+    """Handed-over groups with every message count around the route's slot
+    capacity (route_kmax = n + 1 for n >= 5): counts <= capacity are stepped
+    from the slots, larger ones by the bucket walk, mixed inside partitions,
+    with proposals pending; random states and message types."""
+    ks = nmax + 1
+    G = 2048
+    g, runs, ins = synth.random_groups(G, nmax, seed=40 + nmax, W=8)
+    pair = Pair(g, runs, nmax, 8, ins=ins, max_batch=1 << 16)
+    rng = np.random.default_rng(nmax)
+    for k in range(3):
+        counts = np.array([0, 1, ks - 1, ks, ks + 1, 2 * ks + 3])[rng.integers(0, 6, G)]
+        if k == 1:
+            counts[:256] = ks  # one whole partition on the slot path
+            counts[256:512] = ks + 1  # one whole partition walking
+        grp = rng.permutation(np.repeat(np.arange(G, dtype=np.uint32), counts))
+        pair.step(synth.random_batch(g, 0, seed=500 + 10 * nmax + k, grp=grp),
+                  ctx=f"slot boundary n={nmax}/{k}")
