@@ -923,6 +923,7 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
   L.lost = 0;
   L.nev = 0;
   L.dirty = 0;
+  L.prog = false;
   L.meta = 0;
   L.last = 0;
   L.committed = 0;
@@ -930,7 +931,7 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
   uint64_t commit0 = 0;
   if (flagged) {  // live and not faulted when it was handed over
     L.meta = a.S.meta[g];
-    L.load_all();
+    L.load_group();
     resume = a.resume[g];
     commit0 = ((resume >> 30) & 1u) ? L.committed : a.commit0[g];
   }
@@ -972,24 +973,26 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
         perm = sw ? swp : perm;
       }
     }
-    // the next message's loads are issued before this one is stepped
-    uint32_t inf_n = 0;
+    // the next message's loads are issued before this one is stepped (one
+    // rolled loop: Lane::step is inlined once per call site)
+    uint32_t inf_n = 0, orig_n = 0;
     uint64_t term_n = 0, index_n = 0;
     if (cnt > skip) {
       const size_t o = (size_t)((perm >> (4 * skip)) & 0xF) * a.S.G + g;
       inf_n = a.slot_info[o];
+      orig_n = a.slot_orig[o];
       term_n = a.slot_term[o];
       index_n = a.slot_index[o];
     }
-#pragma unroll
-    for (uint32_t x = 0; x < KS; ++x) {
-      if (x >= cnt || L.faulted()) break;
-      if (x < skip) continue;
-      const uint32_t inf = inf_n;
+#pragma nounroll
+    for (uint32_t x = skip; x < cnt; ++x) {
+      if (L.faulted()) break;
+      const uint32_t inf = inf_n, morig = orig_n;
       const uint64_t mterm = term_n, mindex = index_n;
       if (x + 1 < cnt) {
         const size_t o = (size_t)((perm >> (4 * (x + 1))) & 0xF) * a.S.G + g;
         inf_n = a.slot_info[o];
+        orig_n = a.slot_orig[o];
         term_n = a.slot_term[o];
         index_n = a.slot_index[o];
       }
@@ -999,8 +1002,8 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
         st_drop++;
         continue;
       }
-      L.arrival = key[x];
-      L.step(type, from, mterm, mindex, reject, (reject && a.hint) ? a.hint[key[x]] : 0ull);
+      L.arrival = morig;
+      L.step(type, from, mterm, mindex, reject, (reject && a.hint) ? a.hint[morig] : 0ull);
       st_msgs++;
       st_app += type == HB_MSG_APP_RESP;
       st_vote += type == HB_MSG_VOTE_RESP;

@@ -209,6 +209,7 @@ struct Lane {
   uint32_t dirty;
   uint32_t won, lost;
   uint32_t nev;  // events emitted
+  bool prog;     // match / next / pm / head hold the group's progress (loaded or reset)
 
   // ---------------------------------------------------------------- meta
   __device__ __forceinline__ uint32_t n() const { return m_n(meta); }
@@ -271,12 +272,26 @@ struct Lane {
   // loads of a lane are in flight together); slots >= n hold zeros (k_load).
   // A ring head is read only for a non-empty ring.
   __device__ __forceinline__ void load_all() {
+    load_group();
+    load_progress();
+  }
+  // The per-group fields only; step() loads the progress when a leader first
+  // steps a message.  A vote tally reads none, and an election or a higher
+  // term re-initialises every Progress (raft/raft.go:334-349), so a storm
+  // never loads it.
+  __device__ __forceinline__ void load_group() {
     term = S.term[g];
     committed = S.commit[g];
     first = S.first[g];
     last = S.last[g];
     tfirst = S.tfirst[g];
     tlast = S.tlast[g];
+    meta0 = meta;
+    if (meta & M_TL) tlast = last;
+    dirty = 0;
+    prog = false;
+  }
+  __device__ __forceinline__ void load_progress() {
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) {
       match[s] = S.match[(size_t)s * S.G + g];
@@ -285,10 +300,8 @@ struct Lane {
     }
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) head[s] = pm_count(pm[s]) ? *ring_at(s, pm_start(pm[s])) : 0;
-    meta0 = meta;
-    if (meta & M_TL) tlast = last;
-    if (meta & M_SM) {
-      const uint32_t sf = self();
+    if (meta0 & M_SM) {  // as loaded: the self arrays are stale, last (unchanged so far) is their value
+      const uint32_t sf = m_self(meta0);
 #pragma unroll
       for (int s = 0; s < NMAX; ++s) {
         if ((uint32_t)s == sf) {
@@ -297,17 +310,20 @@ struct Lane {
         }
       }
     }
-    dirty = 0;
+    prog = true;
   }
 
   __device__ __forceinline__ void store() {
     {  // re-derive M_TL / M_SM; an array that was stale and no longer may be is written
       const uint32_t sf = self(), nn = n();
       const bool tl = tlast == last;
-      bool sm = false;
+      bool sm = (meta0 & M_SM) != 0;  // progress never loaded: nothing (incl. last) changed it
+      if (prog) {
+        sm = false;
 #pragma unroll
-      for (int s = 0; s < NMAX; ++s)
-        if ((uint32_t)s == sf && (uint32_t)s < nn) sm = match[s] == last && next[s] == last + 1;
+        for (int s = 0; s < NMAX; ++s)
+          if ((uint32_t)s == sf && (uint32_t)s < nn) sm = match[s] == last && next[s] == last + 1;
+      }
       const uint64_t m2 = (meta & ~(M_TL | M_SM)) | (tl ? M_TL : 0ull) | (sm ? M_SM : 0ull);
       if (m2 != meta) {
         meta = m2;
@@ -508,6 +524,7 @@ struct Lane {
         dirty |= 1u << (D_SLOT0 + s);
       }
     }
+    prog = true;
   }
   // becomeFollower :384-391 / becomeCandidate :393-404 / becomeLeader :406-427.
   // Returns true when the transition happened (false on a reference panic).
@@ -566,6 +583,10 @@ struct Lane {
       }
     }
     if (t1 != 0xFF) transition(t1, tt1, ld1);
+    // Only a leader reads its progress without resetting it first: a candidate
+    // or follower polls, and becomeCandidate / becomeLeader / becomeFollower
+    // reset every Progress before a send or an append touches one.
+    if (!prog && state() == HB_STATE_LEADER) load_progress();
 
     uint32_t send = SEND_NONE, send_to = 0;
     uint64_t append_k = 0;
