@@ -282,18 +282,55 @@ def run_multinode(args):
     print(json.dumps(rec), flush=True)
 
 
+def spawn_ranks(args):
+    """`python bench.py --gpus N` (N > 1) without a launcher: start one child
+    rank per GPU with the variables torchrun sets (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR / MASTER_PORT on 127.0.0.1), before this process
+    touches the GPU; wait for all of them and return the worst exit status
+    (the others are stopped as soon as one fails).  Rank 0 prints the line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            c = p.poll()
+            if c is None:
+                continue
+            alive.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                for q in alive:
+                    q.terminate()
+        time.sleep(0.1)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4", "tick", "wire", "multinode"], default="cfg2",
-                    help="cfg2 (headline), cfg3 lagging followers, cfg4 election storm, "
+    ap.add_argument("--workload", choices=["cfg2", "cfg5", "e2e", "cfg3", "cfg4", "tick", "wire", "multinode"],
+                    default="cfg2",
+                    help="cfg2 (headline: 1M groups x 3 per GPU), cfg5 (8M groups x 3 per GPU = BASELINE.json "
+                         "configs[4] at 8 GPUs), e2e = cfg2 with the batch in host memory and the events copied "
+                         "back every step, cfg3 lagging followers, cfg4 election storm, "
                          "tick = MultiNode.Tick over the cfg2 groups (SURVEY.md 8(f) rank 1), "
                          "wire = cfg2 from raftpb wire records: hb_decode + hb_step (8(f) rank 3), "
                          "multinode = the MultiNode API end to end (Step/Propose/Ready/Advance, 8(f) rank 2)")
-    ap.add_argument("--groups", type=int, default=None, help="groups per GPU (cfg2/cfg3: 1M, cfg4: 4M)")
-    ap.add_argument("--replicas", type=int, default=None, help="cfg2: 3, cfg3: 5, cfg4: 7")
+    ap.add_argument("--groups", type=int, default=None,
+                    help="groups per GPU (cfg2/cfg3/e2e: 1M, cfg5: 8M, cfg4: 4M)")
+    ap.add_argument("--replicas", type=int, default=None, help="cfg2/cfg5: 3, cfg3: 5, cfg4: 7")
     ap.add_argument("--inflight", type=int, default=256, help="MaxInflightMsgs W (cfg3/cfg4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-groups", type=int, default=200_000)
@@ -309,50 +346,99 @@ def main():
     args = ap.parse_args()
     if args.workload == "multinode":
         return run_multinode(args)
-    if args.groups is None:
-        args.groups = (1 << 22) if args.workload == "cfg4" else (1 << 20)
-    if args.replicas is None:
-        args.replicas = {"cfg2": 3, "cfg3": 5, "cfg4": 7, "tick": 3, "wire": 3}[args.workload]
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU)")
+    if args.groups is None:
+        args.groups = {"cfg4": 1 << 22, "cfg5": 1 << 23}.get(args.workload, 1 << 20)
+    if args.replicas is None:
+        args.replicas = {"cfg3": 5, "cfg4": 7}.get(args.workload, 3)
+
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.workload in ("cfg2", "cfg5"):
+        return run_replication(args, world, rank, local)
 
     import torch
     import torch.distributed as dist
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    if args.workload == "e2e":
+        return run_e2e(args, world, rank, local, dev, torch, dist)
+    return run_aux(args, world, rank, local, dev, torch, dist)
+
+
+def routed_batch(G_per_gpu, world, rank, n):
+    """Host side of a cfg2 / cfg5 step on this rank: the shard
+    map of the global group-id space [0, world x G_per_gpu) (splitmix64(id) %
+    world), this rank's groups (steady state, seeded per rank), and ONE global
+    arrival stream (every follower of every group acks, same order on every
+    rank) routed to this rank with ShardMap.route_local — owner hash + select
+    + global id -> local slot, timed on its own.  Term / Index come from the
+    local group state."""
+    from etcd_amd import synth
+    from etcd_amd.shard import ShardMap
+    G_total = G_per_gpu * world
+    sm = ShardMap(np.arange(G_total, dtype=np.uint64), world, rank)
+    G = len(sm)
+    table = sm.dense_slots(G_total)
+    groups, _ = synth.steady_groups(G, n, seed=0x5EED0002 + rank, with_runs=False)
+    gid, frm = synth.global_ack_stream(G_total, n)
+    route_s = 0.0
+    parts_s, parts_f = [], []
+    CH = 1 << 23
+    for c0 in range(0, len(gid), CH):
+        t0 = time.perf_counter()
+        idx, slots = sm.route_local(gid[c0:c0 + CH], table)
+        f = frm[c0:c0 + CH][idx]
+        route_s += time.perf_counter() - t0
+        parts_s.append(slots)
+        parts_f.append(f)
+    n_global = len(gid)
+    del gid, frm, table
+    slots, frm_l = np.concatenate(parts_s), np.concatenate(parts_f)
+    batch = synth.cfg2_local_batch(groups, slots, frm_l, 0)
+    route = {"global_msgs_scanned": n_global, "local_msgs": int(len(slots)), "seconds": round(route_s, 4),
+             "msgs_scanned_per_s": n_global / route_s if route_s > 0 else None, "cores": 1,
+             "note": "host routing of the global arrival stream to this rank (etcd_amd/shard.py route_local: "
+                     "splitmix64 owner hash, select, id -> local slot), numpy on one core, outside the timed "
+                     "region" + ("" if world > 1 else "; one GPU: every message is local, no hash")}
+    return groups, batch, G_total, route
+
+
+def run_replication(args, world, rank, local):
+    """cfg2 (headline) / cfg5: steady-state replication, weak scaling over
+    `world` ranks, one GPU each."""
+    n = args.replicas
+    t_setup = time.perf_counter()
+    groups, batch, G_total, route = routed_batch(args.groups, world, rank, n)
+    G = len(groups)
+    nmsg = len(batch["group"])
+    host_setup_s = time.perf_counter() - t_setup
+
+    import torch
+    import torch.distributed as dist
+    from etcd_amd import abi
+    from etcd_amd.hipbatch import Engine
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from etcd_amd import abi, synth
-    from etcd_amd.hipbatch import Engine
-    from etcd_amd.shard import ShardMap
-
-    if args.workload != "cfg2":
-        return run_aux(args, world, rank, local, dev, torch, dist)
-
-    n = args.replicas
-    # ---- this rank's shard of the global groups (weak scaling: ~groups per GPU)
-    gids = np.arange(world * args.groups, dtype=np.uint64)
-    shard = ShardMap(gids, world, rank) if world > 1 else None
-    G = len(shard) if shard is not None else args.groups
-    groups, _ = synth.steady_groups(G, n, seed=0x5EED0002 + rank, with_runs=False)
-    batch = synth.cfg2_batch(groups, 0, seed=0x5EED0002 + rank)
-    nmsg = len(batch["group"])
-
     # the apply stage runs on a high-priority stream; the engine's prep stream is
-    # its lowest-priority one (they overlap unless --no-overlap)
+    # its lowest-priority one (they overlap only with --overlap)
     lo_prio, hi_prio = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
     stream = torch.cuda.Stream(device=dev, priority=hi_prio)
     torch.cuda.set_stream(stream)
-    eng = Engine(G, max_replicas=n, max_inflight=256, max_batch=nmsg, device=local, stream=stream)
+    eng = Engine(G, max_replicas=n, max_inflight=256, max_batch=max(nmsg, 1), device=local, stream=stream)
     # --overlap: the batches are resident before the timed region, produced on
     # their own (idle) stream, so the engine's prep stage of step k+1 (bucket
     # sort + routing) may overlap the apply stage of step k (hb_set_input_stream).
-    # Measured on MI355X: +0-4 % steps/s, but the apply kernel then shares the
-    # GPU and its in-situ roofline fraction drops; off by default.
     if args.overlap:
         in_stream = torch.cuda.Stream(device=dev)
         eng.set_input_stream(in_stream)
@@ -362,6 +448,7 @@ def main():
     d_term = torch.from_numpy(batch["term"].view(np.int64)).to(dev)
     d_props = torch.from_numpy(batch["props"].view(np.int32)).to(dev)
     base_index = torch.from_numpy(batch["index"].view(np.int64)).to(dev)  # last + 1
+    del groups, batch
     total = args.warmup + args.steps
     n_iso = 0 if args.no_profile else 10  # steps of the separate per-phase pass after the timed region
     # step k acks index last + k + 1 (prepared before timing: inputs resident in HBM)
@@ -409,26 +496,27 @@ def main():
     st = stats_acc.cpu().numpy().astype(np.uint64)  # summed over ranks and steps
     appresp = int(st[abi.HB_STAT_APPRESP])
     commits = int(st[abi.HB_STAT_COMMITS])
-    # sanity: every group commits once per step, nothing faults
-    g_all = torch.tensor([G], dtype=torch.int64, device=dev)
+    # sanity: every group of every rank commits once per step, nothing faults
+    ok = commits == G_total * args.steps and int(st[abi.HB_STAT_FAULTS]) == 0 and \
+        appresp == G_total * (n - 1) * args.steps
+    route_t = torch.tensor([route["seconds"]], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(g_all)
-    g_total = int(g_all.item())
-    ok = commits == g_total * args.steps and int(st[abi.HB_STAT_FAULTS]) == 0 and \
-        appresp == g_total * (n - 1) * args.steps
+        dist.all_reduce(route_t, op=dist.ReduceOp.MAX)
+    route["seconds_max_over_ranks"] = float(route_t.item())
 
     phase = {}
     roof = None
+    alg = alg_bytes_per_group(n) * G  # per k_apply_fast launch on this GPU
     if not args.no_profile:
         ph, nph = eng.phase_ms()  # timed region: HB_PHASE_APPLY only
         apply_ms = float(ph[abi.HB_PHASE_APPLY])
         # per-phase breakdown: a separate, untimed pass with every phase event and
-        # the stages serialized on one stream (the timed run overlaps them)
+        # the stages serialized on one stream
         eng.set_stats_accum(None)
         eng.set_input_stream(stream)
         eng.phase_reset()
-        for k in range(total, total + n_iso):  # the cfg2 stream continues (fresh indices)
-            one_step(k, True)
+        for k in range(total, total + n_iso):  # the stream continues (fresh indices)
+            eng.step(d_group, d_info, d_term, d_index[k], None, d_props, host=False, profile=True)
         torch.cuda.synchronize()
         ph2, nph2 = eng.phase_ms()
         phase = {"apply_ms": apply_ms, "apply_steps": nph,
@@ -436,13 +524,10 @@ def main():
                               "apply_ms": float(ph2[abi.HB_PHASE_APPLY]),
                               "general_ms": float(ph2[abi.HB_PHASE_GENERAL]),
                               "finish_ms": float(ph2[abi.HB_PHASE_FINISH]), "steps": nph2}}
-        ph = ph.copy()
-        ph[abi.HB_PHASE_APPLY] = apply_ms
-        alg = alg_bytes_per_group(n) * G  # per k_apply_fast launch on this GPU
         # HB_PHASE_APPLY brackets exactly the k_apply_fast launch (HIP events on the launch stream)
-        achieved = float(alg / (float(ph[abi.HB_PHASE_APPLY]) * 1e-3) / 1e9)
+        achieved = float(alg / (apply_ms * 1e-3) / 1e9)
         kname = f"k_apply_fast<{3 if n <= 3 else (5 if n <= 5 else 7)}>"
-        traffic, tsrc = pmc_traffic(args.traffic_json, kname, G, n, float(ph[abi.HB_PHASE_APPLY]) * 1e3)
+        traffic, tsrc = pmc_traffic(args.traffic_json, kname, G, n, apply_ms * 1e3)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
@@ -453,11 +538,18 @@ def main():
                 "frac_isolated": round(alg / (float(ph2[abi.HB_PHASE_APPLY]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "alg_bytes_per_launch": alg,
                 "alg_bytes_note": f"SURVEY.md 8(d): {alg_bytes_per_group(n)} B/group = "
-                                  f"{alg_bytes_per_group(n) / (n - 1):.0f} B/MsgAppResp x {G * (n - 1)} MsgAppResp"}
+                                  f"{alg_bytes_per_group(n) / (n - 1):.0f} B/MsgAppResp x {G * (n - 1)} MsgAppResp",
+                # the whole step (partition + route + apply + finish) against the same bytes
+                "step_frac": round(alg / (ms / args.steps * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
     out = None
     if rank == 0:
         sec = ms / 1e3
+        cfg5 = args.workload == "cfg5"
+        wl = (f"cfg5: {G_total} raft groups x {n} sharded by splitmix64(group id) % {world} "
+              f"({args.groups} per GPU; BASELINE.json configs[4] is 64M x 3 on 8 GPUs)") if cfg5 else \
+            (f"cfg2: {args.groups} raft groups x {n} per GPU steady-state replication (BASELINE.json configs[1])"
+             + (f", {world} GPUs, sharded by splitmix64(group id) % {world}" if world > 1 else ""))
         out = {
             "metric": METRIC,
             "value": appresp / sec,
@@ -470,15 +562,19 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (seeded cfg2 stream: steady-state leaders, 1 proposal + all follower acks per group per step)",
-            "config": {"workload": "cfg2: 1M raft groups x 3 replicas steady-state replication per GPU "
-                                   "(BASELINE.json configs[1])",
-                       "groups_per_gpu": G, "groups_total": g_total, "replicas": n,
-                       "msgappresp_per_step": g_total * (n - 1), "max_inflight": 256,
-                       "max_msg_size": "noLimit", "sharding": "splitmix64(group id) % N" if world > 1 else "none"},
+            "data": "synthetic (seeded global ack stream routed to each rank: steady-state leaders, "
+                    "1 proposal + all follower acks per group per step)",
+            "config": {"workload": wl,
+                       "groups_per_gpu": args.groups, "groups_rank0": G, "groups_total": G_total, "replicas": n,
+                       "msgappresp_per_step": G_total * (n - 1), "max_inflight": 256,
+                       "max_msg_size": "noLimit", "sharding": f"splitmix64(group id) % {world}" if world > 1 else "none",
+                       "parallelism": f"groups sharded over {world} GPU(s), one rank per GPU"},
             "commits_per_s": commits / sec,
             "parity_sanity": bool(ok),
             "wall_s": wall,
+            "host_setup_s": round(host_setup_s, 2),
+            "host_route": route,
+            "collective": "one RCCL all-reduce (sum) of the 10 step statistics per step" if world > 1 else "none",
             "phases": phase,
             "pipeline": "prep(k+1) || apply(k): batch inputs on their own stream" if args.overlap else "stages serialized",
             "roofline": roof,
@@ -498,7 +594,87 @@ def main():
                     out["cpu_baseline"]["best_case_parallel"] = cpu_baseline_parallel(n, args.cpu_threads)
                 except Exception as e:
                     out["cpu_baseline"]["best_case_parallel"] = {"error": repr(e)}
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
+
+
+def run_e2e(args, world, rank, local, dev, torch, dist):
+    """cfg2 end to end (SURVEY.md 7 "End-to-end vs kernel"; reported apart from
+    the HBM-resident headline): every step's batch starts in pinned host memory
+    (hb_step with HB_STEP_HOST_PTRS copies group / info / term / index and the
+    dense props to the device) and the step's events come back to pinned host
+    memory as public hb_event records (hb_copy_events), i.e. what a host
+    MultiNode hands over and gets back per Ready cycle.  Wall clock per step,
+    synchronised."""
+    from etcd_amd import abi
+    from etcd_amd.hipbatch import Engine
+    n = args.replicas
+    groups, batch, G_total, route = routed_batch(args.groups, world, rank, n)
+    G = len(groups)
+    nmsg = len(batch["group"])
+    stream = torch.cuda.current_stream(dev)
+    eng = Engine(G, max_replicas=n, max_inflight=256, max_batch=nmsg, device=local, stream=stream)
+    eng.load_groups(groups)
+
+    def pinned(a):
+        t = torch.from_numpy(np.ascontiguousarray(a).view({4: np.int32, 8: np.int64}[a.dtype.itemsize]))
+        return t.pin_memory()
+    h_group, h_info, h_term, h_props = (pinned(batch[k]) for k in ("group", "info", "term", "props"))
+    total = args.warmup + args.steps
+    h_index = [pinned(batch["index"] + np.uint64(k)) for k in range(total)]
+    ev_cap = G * (2 * n + 4)
+    h_ev = torch.empty(ev_cap * abi.EVENT_DTYPE.itemsize, dtype=torch.uint8).pin_memory()
+    torch.cuda.synchronize()
+    st_acc = np.zeros(abi.HB_STAT_COUNT, np.uint64)
+    nev_total = 0
+    t_step = t_ev = 0.0
+    for k in range(total):
+        if k == args.warmup:
+            if world > 1:
+                dist.barrier()
+            st_acc[:] = 0
+            nev_total = 0
+            t_step = t_ev = 0.0
+        t0 = time.perf_counter()
+        eng.step(h_group, h_info, h_term, h_index[k], None, h_props, host=True)
+        eng.sync()
+        t1 = time.perf_counter()
+        nev = eng.events_into(h_ev.data_ptr(), ev_cap)
+        t2 = time.perf_counter()
+        t_step += t1 - t0
+        t_ev += t2 - t1
+        nev_total += nev
+        st_acc += eng.stats()
+    sec_t = torch.tensor([t_step + t_ev], dtype=torch.float64)
+    if world > 1:
+        sec_t = sec_t.to(dev)
+        dist.all_reduce(sec_t, op=dist.ReduceOp.MAX)
+    sec = float(sec_t.item())
+    appresp = int(st_acc[abi.HB_STAT_APPRESP])
+    st_t = torch.from_numpy(st_acc.view(np.int64).copy()).to(dev)
+    if world > 1:
+        dist.all_reduce(st_t)
+    st = st_t.cpu().numpy().view(np.uint64)
+    ok = int(st[abi.HB_STAT_COMMITS]) == G_total * args.steps and int(st[abi.HB_STAT_FAULTS]) == 0
+    h2d = nmsg * 24 + G * 4
+    out = {"metric": "MsgAppResp applied/sec end to end (cfg2 batch from host memory + events back to host)",
+           "value": int(st[abi.HB_STAT_APPRESP]) / sec, "unit": "MsgAppResp/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * sec / args.steps,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+           "data": "synthetic (cfg2 stream in pinned host memory)",
+           "config": {"workload": f"e2e: cfg2 {args.groups} raft groups x {n} per GPU, batch H2D + events D2H "
+                                  f"every step", "groups_per_gpu": args.groups, "replicas": n},
+           "split_ms_per_step": {"h2d_and_step": 1e3 * t_step / args.steps,
+                                 "events_d2h": 1e3 * t_ev / args.steps},
+           "bytes_per_step": {"h2d_batch": h2d, "d2h_events": nev_total // max(args.steps, 1) * 16},
+           "pcie_gbs": round((h2d + nev_total / args.steps * 16) / (sec / args.steps) / 1e9, 2),
+           "events_per_step": nev_total // max(args.steps, 1), "parity_sanity": bool(ok),
+           "timing": "wall clock per step: hb_step (H2D inside) + hb_sync, then hb_copy_events into pinned memory",
+           "cpu_baseline": None}
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def run_aux(args, world, rank, local, dev, torch, dist):

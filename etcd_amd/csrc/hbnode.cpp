@@ -156,6 +156,12 @@ struct hbn_storage {
   Snap snap;
   std::vector<Ent> ents{Ent{}};
   std::vector<hbn_entry> view;  // hbn_storage_entries result
+  // (node, group id) of every group whose raftLog reads this storage: Compact /
+  // CreateSnapshot / ApplySnapshot first step the node's pending batch (the
+  // reference stepped those messages before the call) and copy the entries of
+  // the group's pending MsgApps, then the device's firstIndex / snapshot index
+  // of the group is refreshed before its next step.
+  std::vector<std::pair<hbn_node*, uint64_t>> users;
 
   uint64_t offset() const { return ents[0].index; }
   uint64_t last_index() const { return ents[0].index + ents.size() - 1; }
@@ -414,6 +420,7 @@ struct Group {
   uint32_t election = 10, heartbeat = 1;
   // Ready bookkeeping flags (membership of the node's lists)
   bool touched = false, stepped = false, content = false, delivered = false;
+  bool bounds = false;  // storage changed: device firstIndex / snapshot index to refresh (hbn_node::bounds)
   Delivered dlv;  // what the last Ready delivered for this group (commitReady input)
 
   hbn_hard_state hard() const { return hbn_hard_state{term, vote, hs_commit}; }
@@ -443,6 +450,7 @@ struct hbn_node {
   // CreateGroup loads, coalesced into one hb_load_groups / hb_load_timers per slot run
   std::vector<std::pair<uint32_t, hb_group>> pend_rec;
   std::vector<std::pair<uint32_t, hb_timer>> pend_tm;
+  std::vector<Group*> bounds;  // groups whose storage changed since the last device sync (Group::bounds)
   // Ready bookkeeping (raft/multinode.go:166-322)
   std::vector<Group*> touched;    // rds candidates since the last delivery (Group::touched)
   std::vector<Group*> content;    // groups whose state-derived Ready may be non-empty (lazy, Group::content)
@@ -704,6 +712,20 @@ void load_runs(std::vector<std::pair<uint32_t, T>>& v, F&& load) {
 void sync_loads(hbn_node* n) {
   load_runs(n->pend_rec, [&](uint32_t f, uint32_t c, const hb_group* r) { return hb_load_groups(n->h, f, c, r); });
   load_runs(n->pend_tm, [&](uint32_t f, uint32_t c, const hb_timer* t) { return hb_load_timers(n->h, f, c, t); });
+  if (!n->bounds.empty()) {  // storage compactions / snapshots since the last step, one call
+    std::vector<uint32_t> slots;
+    std::vector<uint64_t> first, snap;
+    for (Group* g : n->bounds) {
+      g->bounds = false;
+      if (g->slot == NO_SLOT) continue;
+      slots.push_back(g->slot);
+      first.push_back(g->log.first_index());
+      snap.push_back(g->log.snapshot().index);
+    }
+    n->bounds.clear();
+    if (!slots.empty())
+      check(hb_set_log_bounds(n->h, (uint32_t)slots.size(), slots.data(), first.data(), snap.data()));
+  }
 }
 
 void flush(hbn_node* n) {
@@ -910,6 +932,37 @@ void reload_prs(hbn_node* n, Group& g, const std::vector<uint64_t>& new_peers,
                              ins[from_old[s]].data()));
 }
 
+// Before the application mutates storage `s` (Compact / CreateSnapshot /
+// ApplySnapshot): the messages already handed to MultiNode.Step were stepped
+// by the reference before this call, so a node with a pending batch steps it
+// now; every MsgApp a group sent copied its entries at send time
+// (raft/raft.go:265), so pending lazy messages are materialized.
+void before_storage_change(hbn_storage* s) {
+  for (auto& u : s->users) {
+    if (!u.first->b_group.empty()) flush(u.first);
+    auto it = u.first->groups.find(u.second);
+    if (it != u.first->groups.end() && it->second->log.st == s) materialize(*it->second);
+  }
+}
+// After it: the group's device firstIndex / snapshot index are refreshed
+// before its next step (sync_loads).
+void after_storage_change(hbn_storage* s) {
+  for (auto& u : s->users) {
+    auto it = u.first->groups.find(u.second);
+    if (it == u.first->groups.end() || it->second->log.st != s) continue;
+    Group& g = *it->second;
+    if (!g.bounds) {
+      g.bounds = true;
+      u.first->bounds.push_back(&g);
+    }
+  }
+}
+
+void drop_user(hbn_storage* s, hbn_node* n, uint64_t group) {
+  auto& v = s->users;
+  v.erase(std::remove(v.begin(), v.end(), std::make_pair(n, group)), v.end());
+}
+
 template <class F>
 int guarded(F&& f) {
   try {
@@ -959,6 +1012,11 @@ int hbn_storage_new_with_entries(const hbn_entry* ents, uint64_t n, hbn_storage*
 }
 
 int hbn_storage_free(hbn_storage* s) {
+  if (s)  // groups still reading it keep no dangling back-reference
+    for (auto& u : s->users) {
+      auto it = u.first->groups.find(u.second);
+      if (it != u.first->groups.end() && it->second->log.st == s) it->second->log.st = nullptr;
+    }
   delete s;
   return HB_OK;
 }
@@ -1030,11 +1088,13 @@ int hbn_storage_snapshot(hbn_storage* s, hbn_snapshot* out) {
 int hbn_storage_apply_snapshot(hbn_storage* s, const hbn_snapshot* snap) {
   if (!s || !snap) return HB_EINVAL;
   return guarded([&] {
+    before_storage_change(s);
     s->snap = snap_from(*snap);
     Ent d;
     d.term = snap->term;
     d.index = snap->index;
     s->ents.assign(1, d);
+    after_storage_change(s);
   });
 }
 
@@ -1050,6 +1110,7 @@ int hbn_storage_create_snapshot(hbn_storage* s, uint64_t i, const uint64_t* node
     }
     if (i > s->last_index())
       panicf("snapshot " + std::to_string(i) + " is out of bound lastindex(" + std::to_string(s->last_index()) + ")");
+    before_storage_change(s);
     s->snap.index = i;
     s->snap.term = s->ents[i - s->offset()].term;
     if (nodes || n_nodes == 0) {
@@ -1057,6 +1118,7 @@ int hbn_storage_create_snapshot(hbn_storage* s, uint64_t i, const uint64_t* node
     }
     s->snap.has_data = data != nullptr;
     s->snap.data.assign(data ? reinterpret_cast<const char*>(data) : "", data ? data_len : 0);
+    after_storage_change(s);
   });
   if (g != HB_OK) return g;
   if (out) {
@@ -1080,12 +1142,14 @@ int hbn_storage_compact(hbn_storage* s, uint64_t i) {
     }
     if (i > s->last_index())
       panicf("compact " + std::to_string(i) + " is out of bound lastindex(" + std::to_string(s->last_index()) + ")");
+    before_storage_change(s);
     const size_t k = i - off;
     std::vector<Ent> ents(1);
     ents[0].index = s->ents[k].index;
     ents[0].term = s->ents[k].term;
     ents.insert(ents.end(), s->ents.begin() + k + 1, s->ents.end());
     s->ents.swap(ents);
+    after_storage_change(s);
   });
   return g != HB_OK ? g : rc;
 }
@@ -1125,6 +1189,8 @@ int hbn_start(int device, uint64_t id, uint32_t capacity, uint32_t max_replicas,
 
 int hbn_stop(hbn_node* n) {
   if (!n) return HB_EINVAL;
+  for (auto& kv : n->groups)
+    if (kv.second->log.st) drop_user(kv.second->log.st, n, kv.first);
   const int rc = hb_destroy(n->h);
   delete n;
   return rc;
@@ -1207,6 +1273,7 @@ int hbn_create_group(hbn_node* n, uint64_t group, const hbn_config* cfg, hbn_sto
     g.prev_soft = g.soft();
     g.prev_hard = g.hard();
     touch(n, g);
+    storage->users.emplace_back(n, group);
     n->groups.emplace(group, std::move(gp));
   });
 }
@@ -1223,7 +1290,8 @@ int hbn_remove_group(hbn_node* n, uint64_t group) {
       n->by_slot[g.slot] = nullptr;
       n->free_slots.push_back(g.slot);
     }
-    for (auto* v : {&n->touched, &n->content, &n->delivered, &n->stepped})
+    if (g.log.st) drop_user(g.log.st, n, group);
+    for (auto* v : {&n->touched, &n->content, &n->delivered, &n->stepped, &n->bounds})
       v->erase(std::remove(v->begin(), v->end(), &g), v->end());
     n->groups.erase(it);
   });

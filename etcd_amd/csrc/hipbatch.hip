@@ -1404,6 +1404,15 @@ __global__ void k_gather(DevState S, uint32_t first, uint32_t count, hb_group* d
   dst[i] = r;
 }
 
+__global__ void k_set_bounds(DevState S, uint32_t count, const uint32_t* groups, const uint64_t* first,
+                             const uint64_t* snap) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint32_t g = groups[i];
+  S.first[g] = first[i];
+  S.snap[g] = snap[i];
+}
+
 __global__ void k_remove(DevState S, uint32_t first, uint32_t count) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < count) S.meta[first + i] = 0;
@@ -1568,6 +1577,8 @@ struct hb_handle {
   uint32_t* dec_q = nullptr;      // hb_decode pass-2 queue (record indices)
   uint64_t dec_cap = 0;
   uint32_t* dec_qn = nullptr;     // [queue length, finished pass-2 workgroups]
+  void* evx = nullptr;            // hb_copy_events expansion scratch, grown on demand
+  uint64_t evx_cap = 0;
   uint64_t* rnd = nullptr;        // the r.rand stream (hb_set_rand), grown on demand
   uint64_t rnd_cap = 0;
   static constexpr uint32_t PROF_RING = 256;
@@ -1785,6 +1796,7 @@ int hb_destroy(hb_handle* h) {
     if (ps.applied) (void)hipEventDestroy(ps.applied);
   }
   if (h->rnd) (void)hipFree(h->rnd);
+  if (h->evx) (void)hipFree(h->evx);
   if (h->peer) (void)hipFree(h->peer);
   if (h->dec_q) (void)hipFree(h->dec_q);
   if (h->dec_qn) (void)hipFree(h->dec_qn);
@@ -1865,6 +1877,31 @@ int hb_remove_groups(hb_handle* h, uint32_t first, uint32_t count) {
   hipLaunchKernelGGL(k_remove, dim3((count + 255) / 256), dim3(256), 0, h->stream, h->st, first, count);
   HB_CHECK(hipStreamSynchronize(h->stream));
   return HB_OK;
+}
+
+int hb_set_log_bounds(hb_handle* h, uint32_t count, const uint32_t* groups, const uint64_t* first_index,
+                      const uint64_t* snap_index) {
+  if (!h || (count && (!groups || !first_index || !snap_index))) return HB_EINVAL;
+  if (count == 0) return HB_OK;
+  for (uint32_t i = 0; i < count; ++i)
+    if (groups[i] >= h->G || first_index[i] == 0) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  char* d = nullptr;
+  const size_t bytes = (size_t)count * (4 + 8 + 8);
+  HB_CHECK(hipMalloc(&d, bytes));
+  uint64_t* dfirst = reinterpret_cast<uint64_t*>(d);
+  uint64_t* dsnap = dfirst + count;
+  uint32_t* dgroup = reinterpret_cast<uint32_t*>(dsnap + count);
+  hipError_t e = hipMemcpyAsync(dfirst, first_index, count * 8ull, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dsnap, snap_index, count * 8ull, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dgroup, groups, count * 4ull, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_set_bounds, dim3((count + 255) / 256), dim3(256), 0, h->stream, h->st, count,
+                       (const uint32_t*)dgroup, (const uint64_t*)dfirst, (const uint64_t*)dsnap);
+    e = hipStreamSynchronize(h->stream);
+  }
+  (void)hipFree(d);
+  return e == hipSuccess ? HB_OK : HB_EDEVICE;
 }
 
 int hb_set_inflights(hb_handle* h, uint32_t group, uint32_t slot, uint32_t start, uint32_t count,
@@ -2223,8 +2260,17 @@ int hb_copy_events(hb_handle* h, hb_event* out, uint64_t cap, uint64_t* n) {
   *n = total;
   if (total == 0) return HB_OK;
   if (!out || cap < total) return HB_EINVAL;
-  hb_event* d = nullptr;
-  HB_CHECK(hipMalloc(&d, total * sizeof(hb_event) + 24ull * h->NB));
+  // expansion scratch (records + per-chunk scan), kept across calls and grown on demand
+  const uint64_t need = total * sizeof(hb_event) + 24ull * h->NB;
+  if (need > h->evx_cap) {
+    if (h->evx) (void)hipFree(h->evx);
+    h->evx = nullptr;
+    h->evx_cap = 0;
+    const uint64_t cap = need + need / 4;
+    HB_CHECK(hipMalloc(&h->evx, cap));
+    h->evx_cap = cap;
+  }
+  hb_event* d = reinterpret_cast<hb_event*>(h->evx);
   uint64_t* dst = reinterpret_cast<uint64_t*>(d + total);
   uint32_t* per_chunk = reinterpret_cast<uint32_t*>(dst + 2 * h->NB);
   hipLaunchKernelGGL(k_chunk_events, dim3(2 * h->NB), dim3(256), 0, h->stream, (const uint64_t*)h->ev,
@@ -2234,7 +2280,6 @@ int hb_copy_events(hb_handle* h, hb_event* out, uint64_t cap, uint64_t* n) {
                      (const uint32_t*)h->set[h->cur].ev_counts, (const uint64_t*)h->set[h->cur].ev_off, (const uint64_t*)dst, d);
   hipError_t e = hipMemcpyAsync(out, d, total * sizeof(hb_event), hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-  (void)hipFree(d);
   return e == hipSuccess ? HB_OK : HB_EDEVICE;
 }
 

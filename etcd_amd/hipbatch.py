@@ -52,6 +52,7 @@ def lib():
         "hb_get_groups": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
         "hb_remove_groups": (C.c_int, [H, C.c_uint32, C.c_uint32]),
         "hb_set_inflights": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
+        "hb_set_log_bounds": (C.c_int, [H, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
         "hb_get_inflights": (C.c_int, [H, C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32), C.c_void_p]),
         "hb_step": (C.c_int, [H, P(abi.hb_batch), C.c_uint32]),
         "hb_load_timers": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
@@ -158,6 +159,16 @@ class Engine:
         _check("hb_set_inflights", lib().hb_set_inflights(self.h, group, slot, start, len(v),
                                                           v.ctypes.data if len(v) else None))
 
+    def set_log_bounds(self, groups, first_index, snap_index):
+        """Refresh firstIndex / snapshot index of the given group slots after
+        the application compacted or snapshotted their storage."""
+        g = np.ascontiguousarray(groups, dtype=np.uint32)
+        f = np.ascontiguousarray(first_index, dtype=np.uint64)
+        s = np.ascontiguousarray(snap_index, dtype=np.uint64)
+        assert len(g) == len(f) == len(s)
+        _check("hb_set_log_bounds", lib().hb_set_log_bounds(self.h, len(g), g.ctypes.data, f.ctypes.data,
+                                                            s.ctypes.data))
+
     def get_inflights(self, group, slot):
         out = np.zeros(self.max_inflight, dtype=np.uint64)
         s, c = C.c_uint32(), C.c_uint32()
@@ -231,6 +242,13 @@ class Engine:
         out = np.zeros(max(n.value, 1), dtype=abi.EVENT_DTYPE)
         _check("hb_copy_events", L.hb_copy_events(self.h, out.ctypes.data, len(out), C.byref(n)))
         return out[: n.value]
+
+    def events_into(self, host_ptr, cap):
+        """Dense events of the last step into caller memory (e.g. pinned) of
+        `cap` hb_event records; returns the count (synchronizes)."""
+        n = C.c_uint64()
+        _check("hb_copy_events", lib().hb_copy_events(self.h, C.c_void_p(host_ptr), cap, C.byref(n)))
+        return n.value
 
     def stats(self):
         out = np.zeros(abi.HB_STAT_COUNT, dtype=np.uint64)

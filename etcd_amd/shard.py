@@ -14,6 +14,8 @@ from .synth import splitmix64
 
 def owner(group_ids, world):
     """GPU rank that owns each global group id."""
+    if world == 1:
+        return np.zeros(len(group_ids), dtype=np.int64)
     return (splitmix64(np.asarray(group_ids, dtype=np.uint64)) % np.uint64(world)).astype(np.int64)
 
 
@@ -45,6 +47,24 @@ class ShardMap:
         """Split a message batch by owner rank: returns rank -> indices (arrival order kept)."""
         own = owner(gids, self.world)
         return {r: np.nonzero(own == r)[0] for r in range(self.world)}
+
+    def dense_slots(self, id_space):
+        """Lookup table global id -> local slot (-1 when another rank owns it) for
+        the dense id space [0, id_space): one gather per routed message instead
+        of a binary search."""
+        t = np.full(id_space, -1, dtype=np.int32)
+        t[self.local_ids.astype(np.int64)] = np.arange(len(self.local_ids), dtype=np.int32)
+        return t
+
+    def route_local(self, gids, table=None):
+        """This rank's messages of an arrival-ordered batch: (indices into the
+        batch, local slots), arrival order kept.  `table` = dense_slots() for a
+        dense id space (else the sorted-id search of local_slot)."""
+        gids = np.asarray(gids, dtype=np.uint64)
+        idx = np.nonzero(owner(gids, self.world) == self.rank)[0]
+        sel = gids[idx]
+        slots = table[sel.astype(np.int64)] if table is not None else self.local_slot(sel)
+        return idx, slots.astype(np.uint32)
 
 
 def reduce_stats(stats_tensor, dist=None):

@@ -90,6 +90,30 @@ def cfg2_batch(groups, step, seed=0x5EED0002, xp=np):
     return dict(group=grp, info=info, term=term, index=index, hint=None, props=props)
 
 
+def global_ack_stream(G_total, n=3, seed=0x5EED0005):
+    """The arrival stream of one cfg2/cfg5 step over a GLOBAL group-id space
+    [0, G_total): every follower of every group acks once, in a random order
+    (the same on every rank).  Returns (group id u64, from slot u32); a rank
+    routes it to its own shard (ShardMap.route_local) and fills Term / Index
+    from its groups' state (cfg2_local_batch)."""
+    nf = n - 1
+    perm = np.random.default_rng(seed).permutation(G_total * nf)
+    gid = (perm // nf).astype(np.uint64)
+    frm = (perm % nf + 1).astype(np.uint32)
+    return gid, frm
+
+
+def cfg2_local_batch(groups, slots, frm, step):
+    """A rank's routed cfg2 step: MsgAppResp from `frm` for local group `slots`
+    (arrival order as routed), Term = the group's term, Index = last + step + 1,
+    plus one dense proposal per group."""
+    info = (np.uint32(A.HB_MSG_APP_RESP) | (frm.astype(np.uint32) << np.uint32(4))).astype(np.uint32)
+    term = groups["term"][slots].astype(np.uint64)
+    index = (groups["last_index"][slots] + np.uint64(step + 1)).astype(np.uint64)
+    return dict(group=slots.astype(np.uint32), info=info, term=term, index=index, hint=None,
+                props=np.ones(len(groups), dtype=np.uint32))
+
+
 # ---------------------------------------------------------------------------- fuzz
 def random_groups(G, nmax=3, seed=1, W=8, state_mix=(0.6, 0.2, 0.2)):
     """Diverse, internally consistent group states for fuzz parity.
@@ -239,7 +263,17 @@ def election_groups(G, n=7, seed=0x5EED0004, term_hi=1000, with_runs=True):
         g["pr"][:, s]["match"] = last if s == 0 else 0
         g["pr"][:, s]["next"] = last + np.uint64(1)
     runs = None
-    if with_runs:
+    if with_runs == "flat":  # (0, 0) then (1, T-1) when T > 1
+        two = term > 1
+        cnt = np.where(two, 2, 1).astype(np.uint64)
+        off = np.zeros(G + 1, dtype=np.uint64)
+        off[1:] = np.cumsum(cnt)
+        flat = np.zeros((int(off[-1]), 2), dtype=np.uint64)
+        pos = off[:-1][two].astype(np.int64) + 1
+        flat[pos, 0] = 1
+        flat[pos, 1] = term[two] - np.uint64(1)
+        runs = (flat, off)
+    elif with_runs:
         runs = [[(0, 0), (1, max(int(term[i]) - 1, 0))] if term[i] > 1 else [(0, 0)] for i in range(G)]
     return g, runs
 
@@ -369,9 +403,9 @@ class FollowerSim:
                     hint=arr[:, 6].astype(np.uint64), props=props)
 
 
-def lagging_groups(G, n=5, seed=0x5EED0003, W=8):
+def lagging_groups(G, n=5, seed=0x5EED0003, W=8, with_runs=True):
     """cfg3 start: leaders with followers spread over Probe/Replicate and lag."""
-    g, runs = steady_groups(G, n=n, seed=seed, last_hi=1 << 12, term_hi=100)
+    g, runs = steady_groups(G, n=n, seed=seed, last_hi=1 << 12, term_hi=100, with_runs=with_runs)
     rng = np.random.default_rng(seed + 1)
     for s in range(1, n):
         lag = rng.integers(0, 64, G).astype(np.uint64)

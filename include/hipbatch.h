@@ -284,6 +284,13 @@ int  hb_get_groups(hb_handle* h, uint32_t first, uint32_t count, hb_group* out);
 /* RemoveGroup (raft/multinode.go:219-222): mark slots empty (all messages to
  * them are ignored until reloaded). */
 int  hb_remove_groups(hb_handle* h, uint32_t first, uint32_t count);
+/* The application changed a group's Storage (MemoryStorage.Compact /
+ * CreateSnapshot / ApplySnapshot, raft/storage.go:150-214): refresh the
+ * device copies of raftLog.firstIndex() and raftLog.snapshot().Metadata.Index
+ * that sendAppend reads (needSnapshot, raft/raft.go:246-260, 715-717) for
+ * `count` group slots (host arrays). */
+int  hb_set_log_bounds(hb_handle* h, uint32_t count, const uint32_t* groups,
+                       const uint64_t* first_index, const uint64_t* snap_index);
 /* Inflight window of (group, slot): buffer[(start + i) % max_inflight] = vals[i]. */
 int  hb_set_inflights(hb_handle* h, uint32_t group, uint32_t slot,
                       uint32_t start, uint32_t count, const uint64_t* vals);

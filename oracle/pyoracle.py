@@ -17,7 +17,7 @@ import numpy as np
 from etcd_amd import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_LIB_PATH = os.environ.get("ORC_LIB", os.path.join(_HERE, "build", "liboracle.so"))
 _lib = None
 
 ORC_MAX_PEERS = 8

@@ -313,7 +313,8 @@ static void send(orc_raft* r, orc_msg m) {                /* send raft/raft.go:2
 
 int orc_raft_read_messages(orc_raft* r, orc_msg* out, int cap) {
   int n = r->nmsgs;
-  if (out) memcpy(out, r->msgs, sizeof(orc_msg) * (size_t)(n < cap ? n : cap));
+  const int k = n < cap ? n : cap;
+  if (out && k > 0) memcpy(out, r->msgs, sizeof(orc_msg) * (size_t)k);
   r->nmsgs = 0;
   return n;
 }

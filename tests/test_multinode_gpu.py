@@ -339,3 +339,84 @@ def test_random_multinode_vs_oracle(seed, n):
         props = st[gid].get("props", [])
         it = iter(props)
         assert all(any(p == g for p in it) for g in got), f"group {gid}: payload order"
+
+
+# ---------------------------------------------------------------- storage compaction / snapshots
+def _lagging_leader():
+    """Group 1 on node 1 with peers 1, 2, 3: node 1 leads at term 2, follower 2
+    acks every entry, follower 3 never answers (Probe, paused, Next 4).  Four
+    proposals later the log is 1..8, all committed, all in storage."""
+    s = MemoryStorage()
+    mn = StartMultiNode(1)
+    mn.CreateGroup(1, Config(10, 1), s, peers=[1, 2, 3])
+
+    def cycle():
+        rds = mn.Ready()
+        if 1 in rds:
+            s.Append(rds[1].Entries)
+            mn.Advance(rds)
+        return rds.get(1)
+    cycle()
+    mn.Campaign(1)
+    cycle()
+    mn.Step(1, Message(Type=abi.HB_MSG_VOTE_RESP, From=2, To=1, Term=2))
+    cycle()  # leader: noop 4, MsgApp(3, [4]) to 2 and 3
+    mn.Step(1, Message(Type=abi.HB_MSG_APP_RESP, From=2, To=1, Term=2, Index=4))
+    cycle()
+    for k in range(4):
+        mn.Propose(1, b"x%d" % k)
+        cycle()
+        mn.Step(1, Message(Type=abi.HB_MSG_APP_RESP, From=2, To=1, Term=2, Index=5 + k))
+        cycle()
+    st = mn.Status(1)
+    assert st.HardState.Commit == 8 and st.Progress[3].state == abi.HB_PR_PROBE and st.Progress[3].next == 4
+    return mn, s, cycle
+
+
+def test_compacted_log_sends_snapshot_to_lagging_follower():
+    """Compact + CreateSnapshot on the leader's storage after CreateGroup: the
+    next sendAppend to the lagging follower needs a snapshot (Next 4 <
+    firstIndex 9, raft/raft.go:246-260, 715-717) — a MsgSnap carrying the
+    storage's snapshot, and the follower's Progress becomes Snapshot(8)."""
+    mn, s, cycle = _lagging_leader()
+    snap, err = s.CreateSnapshot(8, [1, 2, 3], b"state@8")
+    assert err is None and snap.Index == 8 and snap.Term == 2
+    assert s.Compact(8) is None
+    mn.Tick()  # MsgBeat -> bcastHeartbeat resumes every peer
+    rd = cycle()
+    assert [(m.Type, m.To) for m in rd.Messages] == [(abi.HB_MSG_HEARTBEAT, 2), (abi.HB_MSG_HEARTBEAT, 3)]
+    mn.Step(1, Message(Type=abi.HB_MSG_HEARTBEAT_RESP, From=3, To=1, Term=2))
+    rd = cycle()
+    assert rd.Messages == [Message(Type=abi.HB_MSG_SNAP, To=3, From=1, Term=2,
+                                   Snapshot=Snapshot(Index=8, Term=2, Nodes=[1, 2, 3], Data=b"state@8"))]
+    p3 = mn.Status(1).Progress[3]
+    assert p3.state == abi.HB_PR_SNAPSHOT and p3.pending_snapshot == 8
+    mn.Stop()
+
+
+def test_compaction_after_send_keeps_the_sent_entries():
+    """A MsgApp is built from the log when the reference sends it (raft.go:265):
+    a heartbeat response stepped before Compact makes the leader send entries
+    4..8 to the lagging follower; compacting them away before the Ready must not
+    change that message.  The follower's next sendAppend is then a MsgSnap."""
+    mn, s, cycle = _lagging_leader()
+    mn.Tick()
+    cycle()
+    mn.Step(1, Message(Type=abi.HB_MSG_HEARTBEAT_RESP, From=3, To=1, Term=2))
+    snap, err = s.CreateSnapshot(8, [1, 2, 3], None)
+    assert err is None
+    assert s.Compact(8) is None
+    rd = cycle()
+    assert len(rd.Messages) == 1
+    m = rd.Messages[0]
+    assert (m.Type, m.To, m.Index, m.LogTerm, m.Commit) == (abi.HB_MSG_APP, 3, 3, 1, 8)
+    assert [(e.Index, e.Term) for e in m.Entries] == [(4, 2), (5, 2), (6, 2), (7, 2), (8, 2)]
+    assert [e.Data for e in m.Entries] == [None, b"x0", b"x1", b"x2", b"x3"]
+    # Probe: paused after the send; the next heartbeat round resumes it and the
+    # response finds Next 4 below firstIndex 9
+    mn.Tick()
+    cycle()
+    mn.Step(1, Message(Type=abi.HB_MSG_HEARTBEAT_RESP, From=3, To=1, Term=2))
+    rd = cycle()
+    assert [(m.Type, m.To, m.Snapshot.Index) for m in rd.Messages] == [(abi.HB_MSG_SNAP, 3, 8)]
+    mn.Stop()

@@ -100,3 +100,28 @@ def test_owner_is_a_partition():
         assert np.array_equal(slots, np.arange(len(m)))
         other = ids[own != world - 1][:10]
         assert (m.local_slot(other) == -1).all()
+
+
+def test_routed_batch_partitions_the_global_stream():
+    """bench.py's host routing (cfg2 / cfg5 at N GPUs): every rank scans one
+    global arrival stream and keeps its own messages; over all ranks each
+    group gets exactly one ack per follower, and a rank's messages keep their
+    global arrival order."""
+    import bench
+    from etcd_amd.synth import global_ack_stream
+    G_per, n = 5000, 3
+    for world in (1, 2, 4):
+        gid, frm = global_ack_stream(G_per * world, n)
+        total = 0
+        for rank in range(world):
+            groups, batch, G_total, route = bench.routed_batch(G_per, world, rank, n)
+            assert G_total == G_per * world and route["local_msgs"] == len(batch["group"])
+            cnt = np.bincount(batch["group"], minlength=len(groups))
+            assert (cnt == n - 1).all()
+            sm = ShardMap(np.arange(G_total, dtype=np.uint64), world, rank)
+            mine = np.nonzero(owner(gid, world) == rank)[0]
+            assert np.array_equal(sm.local_ids[batch["group"]], gid[mine])  # arrival order kept
+            assert np.array_equal((batch["info"] >> 4) & 0xF, frm[mine])
+            assert np.array_equal(batch["index"], groups["last_index"][batch["group"]] + np.uint64(1))
+            total += len(batch["group"])
+        assert total == G_per * world * (n - 1)
