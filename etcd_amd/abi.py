@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-HB_ABI_VERSION = 1
+HB_ABI_VERSION = 2
 
 HB_OK = 0
 HB_EINVAL = -1
@@ -20,6 +20,8 @@ HB_MAX_REPLICAS = 7
 HB_MAX_INFLIGHT = 1024
 HB_NO_LIMIT = (1 << 64) - 1
 HB_NO_INDEX = (1 << 64) - 1
+HB_SIZE_WINDOW = 1024
+HB_ENT_MAX_DATA = 0x3FFFFFFF
 
 # StateType raft/raft.go:35-39
 HB_STATE_FOLLOWER = 0
@@ -63,6 +65,7 @@ HB_FAULT_COMMIT_RANGE = 6
 HB_FAULT_NO_SELF = 7
 HB_FAULT_FOLLOWER_LEADER = 8
 HB_FAULT_RAND_EXHAUSTED = 9
+HB_FAULT_SIZE_WINDOW = 10
 
 HB_EV_TERM = 1
 HB_EV_STATE = 2
@@ -110,6 +113,28 @@ STAT_NAMES = ["msgs", "appresp", "voteresp", "dropped", "commits", "won", "lost"
 
 def hb_info(mtype, from_slot, reject=False):
     return (mtype & 0xF) | ((from_slot & 0xF) << 4) | ((1 if reject else 0) << 8)
+
+
+def hb_ent_desc(data_len, etype=0, has_data=True):
+    """Entry descriptor (HB_ENT_DESC): len(Data) | Type << 30 | (Data != nil) << 31."""
+    return (int(data_len) & HB_ENT_MAX_DATA) | ((int(etype) & 1) << 30) | ((1 if has_data else 0) << 31)
+
+
+def _sov(x):
+    n = 1
+    while x >= 0x80:
+        x >>= 7
+        n += 1
+    return n
+
+
+def entry_size(desc, term, index):
+    """gogo Entry.Size() (raft/raftpb/raft.pb.go:1030-1043) of the entry a descriptor describes."""
+    n = 1 + _sov((desc >> 30) & 1) + 1 + _sov(term) + 1 + _sov(index)
+    if desc >> 31:
+        ln = desc & HB_ENT_MAX_DATA
+        n += 1 + ln + _sov(ln)
+    return n
 
 
 class hb_progress(C.Structure):
@@ -174,6 +199,10 @@ class hb_batch(C.Structure):
         ("index", C.c_void_p),
         ("hint", C.c_void_p),
         ("props", C.c_void_p),
+        ("n_edesc", C.c_uint64),
+        ("edesc", C.c_void_p),
+        ("eoff", C.c_void_p),
+        ("peoff", C.c_void_p),
     ]
 
 

@@ -22,6 +22,7 @@
 #include "../../include/hbnode.h"
 
 #include <algorithm>
+#include <stdexcept>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -77,6 +78,10 @@ uint64_t ent_size(uint64_t type, uint64_t term, uint64_t index, bool has_data, u
   return n;
 }
 uint64_t ent_size(const Ent& e) { return ent_size(e.type, e.term, e.index, e.has_data, e.data.size()); }
+uint32_t ent_desc(const Ent& e) {  // HB_ENT_DESC: the engine computes Entry.Size() from it
+  if (e.data.size() > HB_ENT_MAX_DATA) throw std::length_error("entry data longer than HB_ENT_MAX_DATA");
+  return HB_ENT_DESC(e.data.size(), e.type, e.has_data);
+}
 
 // limitSize raft/util.go:97-110
 template <class V>
@@ -335,6 +340,27 @@ struct Log {
       for (uint64_t i = a; i < hi; ++i) f(unstable[i - offset]);
     }
   }
+  // How many entries limitSize (raft/util.go:97-110) keeps of (lo-1, last]:
+  // the first always, then each while the running Entry.Size() sum <= max.
+  uint64_t limit_count_from(uint64_t lo, uint64_t max_size) const {
+    const uint64_t li = last_index();
+    if (lo > li) return 0;
+    uint64_t size = 0, k = 0;
+    bool stop = false;
+    auto take = [&](const Ent& x) {
+      if (stop) return;
+      size += ent_size(x);
+      if (k == 0 || size <= max_size) ++k;
+      else stop = true;
+    };
+    uint64_t i = lo;  // storage part then unstable part, stopping early
+    while (!stop && i <= li) {
+      const uint64_t h = std::min(li + 1, i + 256);
+      visit(i, h, take);
+      i = h;
+    }
+    return k;
+  }
   // entries :219-224
   std::vector<Ent> entries(uint64_t i, uint64_t max_size) const {
     if (i > last_index()) return {};
@@ -445,6 +471,11 @@ struct hbn_node {
   // pending device batch (host SoA, HB_STEP_HOST_PTRS)
   std::vector<uint32_t> b_group, b_info;
   std::vector<uint64_t> b_term, b_index, b_hint;
+  // finite MaxSizePerMsg: entry descriptors of the batched proposals (hb_batch edesc / eoff)
+  bool sized = false;
+  std::vector<uint32_t> b_edesc;
+  std::vector<uint64_t> b_eoff;
+  std::vector<Group*> pend_sz;  // groups (re)loaded on the device whose entry sizes are still to push
   std::vector<Group*> stepped;  // groups whose raft.Step runs in the pending batch
   std::vector<hb_event> evbuf;
   // CreateGroup loads, coalesced into one hb_load_groups / hb_load_timers per slot run
@@ -628,7 +659,10 @@ void on_event(hbn_node* n, Group& g, const hb_event& e) {
       const uint64_t li = g.log.last_index();
       m.owned = false;
       m.ent_lo = e.x + 1;
-      m.ent_hi = e.x + 1 > li ? e.x + 1 : (n->max_msg == 0 ? e.x + 2 : li + 1);
+      if (e.x + 1 > li) m.ent_hi = e.x + 1;
+      else if (n->max_msg == 0) m.ent_hi = e.x + 2;
+      else if (n->max_msg == HB_NO_LIMIT) m.ent_hi = li + 1;
+      else m.ent_hi = e.x + 1 + g.log.limit_count_from(e.x + 1, n->max_msg);  // limitSize, as the device cut it
       m.commit = g.log.committed;
       g.msgs.push_back(std::move(m));
       break;
@@ -709,9 +743,29 @@ void load_runs(std::vector<std::pair<uint32_t, T>>& v, F&& load) {
   v.clear();
 }
 
+// Finite MaxSizePerMsg: the sizes of the latest entries of groups whose device
+// record was (re)loaded, so the device's limitSize can reach back
+// HB_SIZE_WINDOW - 1 entries.
+void push_sizes(hbn_node* n) {
+  if (n->pend_sz.empty()) return;
+  std::vector<uint32_t> slots, cnt, sizes;
+  for (Group* g : n->pend_sz) {
+    if (g->slot == NO_SLOT) continue;
+    const uint64_t li = g->log.last_index(), fi = g->log.first_index();
+    const uint64_t k = std::min<uint64_t>(li + 1 - fi, HB_SIZE_WINDOW - 1);
+    slots.push_back(g->slot);
+    cnt.push_back((uint32_t)k);
+    g->log.visit(li + 1 - k, li + 1, [&](const Ent& x) { sizes.push_back((uint32_t)ent_size(x)); });
+  }
+  n->pend_sz.clear();
+  if (!slots.empty())
+    check(hb_load_entry_sizes(n->h, (uint32_t)slots.size(), slots.data(), cnt.data(), sizes.data()));
+}
+
 void sync_loads(hbn_node* n) {
   load_runs(n->pend_rec, [&](uint32_t f, uint32_t c, const hb_group* r) { return hb_load_groups(n->h, f, c, r); });
   load_runs(n->pend_tm, [&](uint32_t f, uint32_t c, const hb_timer* t) { return hb_load_timers(n->h, f, c, t); });
+  push_sizes(n);
   if (!n->bounds.empty()) {  // storage compactions / snapshots since the last step, one call
     std::vector<uint32_t> slots;
     std::vector<uint64_t> first, snap;
@@ -731,7 +785,7 @@ void sync_loads(hbn_node* n) {
 void flush(hbn_node* n) {
   sync_loads(n);
   if (n->b_group.empty()) return;
-  hb_batch b;
+  hb_batch b{};
   b.n = n->b_group.size();
   b.group = n->b_group.data();
   b.info = n->b_info.data();
@@ -739,6 +793,11 @@ void flush(hbn_node* n) {
   b.index = n->b_index.data();
   b.hint = n->b_hint.data();
   b.props = nullptr;
+  if (n->sized) {
+    b.n_edesc = n->b_edesc.size();
+    b.edesc = n->b_edesc.data();
+    b.eoff = n->b_eoff.data();
+  }
   check(hb_step(n->h, &b, HB_STEP_HOST_PTRS));
   consume_events(n);
   for (Group* g : n->stepped) {
@@ -751,6 +810,8 @@ void flush(hbn_node* n) {
   n->b_term.clear();
   n->b_index.clear();
   n->b_hint.clear();
+  n->b_edesc.clear();
+  n->b_eoff.clear();
 }
 
 bool is_response(uint32_t t) {  // IsResponseMsg raft/util.go:53-55
@@ -775,6 +836,7 @@ void push(hbn_node* n, Group& g, uint32_t type, uint64_t from, bool reject, uint
   n->b_term.push_back(term);
   n->b_index.push_back(index);
   n->b_hint.push_back(hint);
+  if (n->sized) n->b_eoff.push_back(n->b_edesc.size());  // a MsgProp's descriptors follow (propose)
   if ((s >= 0 || !is_response(type)) && !g.stepped) {
     g.stepped = true;
     n->stepped.push_back(&g);
@@ -793,6 +855,8 @@ void propose(hbn_node* n, Group& g, Msg m) {
   const uint64_t k = m.entries.size(), term = m.term;
   if (g.slot != NO_SLOT) g.props.push_back(std::move(m));
   push(n, g, HB_MSG_PROP, n->id, false, term, k, 0);
+  if (n->sized && g.slot != NO_SLOT)
+    for (const Ent& x : g.props.back().entries) n->b_edesc.push_back(ent_desc(x));
 }
 
 // ---------------------------------------------------------------- Ready
@@ -922,6 +986,10 @@ void reload_prs(hbn_node* n, Group& g, const std::vector<uint64_t>& new_peers,
     tm.rand_pos = 0;
   }
   check(hb_load_groups(n->h, g.slot, 1, &r));
+  if (n->sized) {
+    n->pend_sz.push_back(&g);
+    push_sizes(n);
+  }
   hb_timer t2 = tm;
   t2.election_tick = (uint16_t)g.election;
   t2.heartbeat_tick = (uint16_t)g.heartbeat;
@@ -1179,6 +1247,7 @@ int hbn_start(int device, uint64_t id, uint32_t capacity, uint32_t max_replicas,
     n->nmax = max_replicas;
     n->W = max_inflight;
     n->max_msg = max_msg_size;
+    n->sized = max_msg_size != 0 && max_msg_size != HB_NO_LIMIT;
     n->max_batch = max_batch;
     n->by_slot.assign(capacity, nullptr);
     n->free_slots.reserve(capacity);
@@ -1268,6 +1337,7 @@ int hbn_create_group(hbn_node* n, uint64_t group, const hbn_config* cfg, hbn_sto
       t.heartbeat_tick = (uint16_t)g.heartbeat;
       n->pend_tm.emplace_back(g.slot, t);
       n->by_slot[g.slot] = &g;
+      if (n->sized) n->pend_sz.push_back(&g);
     }
     // the initial hard and soft states (:213-215)
     g.prev_soft = g.soft();
@@ -1291,7 +1361,7 @@ int hbn_remove_group(hbn_node* n, uint64_t group) {
       n->free_slots.push_back(g.slot);
     }
     if (g.log.st) drop_user(g.log.st, n, group);
-    for (auto* v : {&n->touched, &n->content, &n->delivered, &n->stepped, &n->bounds})
+    for (auto* v : {&n->touched, &n->content, &n->delivered, &n->stepped, &n->bounds, &n->pend_sz})
       v->erase(std::remove(v->begin(), v->end(), &g), v->end());
     n->groups.erase(it);
   });

@@ -177,33 +177,37 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t
     }
   }
   __syncthreads();
-  if (tid < RDX_BINS) hist[(size_t)tid * ntiles + blockIdx.x] = cnt[tid];
+  if (tid < RDX_BINS) hist[(size_t)blockIdx.x * RDX_BINS + tid] = cnt[tid];  // [tile][digit]: one 1 KB row per tile
 }
 
-// Row scan: workgroup b turns row b of hist ([RDX_BINS][ntiles] tile counts)
-// into exclusive per-tile prefixes and writes the row total to totals[b].
-// It also clears the per-bucket event-chunk cursors for the coming apply.
+// Column scan: workgroup b turns column d of hist ([ntiles][RDX_BINS] tile
+// counts) into exclusive per-tile prefixes and writes the column total to
+// totals[d].  The 32 digits of one 128-byte line of every tile row are
+// scanned by workgroups of one XCD (blockIdx % 8), so each line is fetched
+// into one L2 once.  It also clears the per-bucket event-chunk cursors for
+// the coming apply.
 __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t ntiles, uint32_t* totals,
                                                     uint32_t* bk_fill, uint32_t NBK) {
   __shared__ uint32_t sh16[16];
-  uint32_t* row = hist + (size_t)blockIdx.x * ntiles;
+  const uint32_t d = (blockIdx.x & 7) * (RDX_BINS / 8) + (blockIdx.x >> 3);
+  uint32_t* col = hist + d;
   for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < NBK; i += gridDim.x * 1024) bk_fill[i] = 0;
   uint32_t carry = 0;
   for (uint32_t base = 0; base < ntiles; base += 4096) {
     const uint32_t i0 = base + threadIdx.x * 4;
     uint32_t v[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = i0 + k < ntiles ? row[i0 + k] : 0u;
+    for (int k = 0; k < 4; ++k) v[k] = i0 + k < ntiles ? col[(size_t)(i0 + k) * RDX_BINS] : 0u;
     uint32_t tot;
     uint32_t run = carry + block_excl_scan(v[0] + v[1] + v[2] + v[3], sh16, &tot);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (i0 + k < ntiles) row[i0 + k] = run;
+      if (i0 + k < ntiles) col[(size_t)(i0 + k) * RDX_BINS] = run;
       run += v[k];
     }
     carry += tot;
   }
-  if (threadIdx.x == 0) totals[blockIdx.x] = carry;
+  if (threadIdx.x == 0) totals[d] = carry;
 }
 
 template <bool FINAL>
@@ -227,7 +231,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
     uint32_t all;
     const uint32_t excl = excl_scan256(t, sh4, &all);
     if (tid < RDX_BINS) {
-      s_off[tid] = excl + off[(size_t)tid * ntiles + tile];
+      s_off[tid] = excl + off[(size_t)tile * RDX_BINS + tid];
       if (FINAL && f.bk_off && tile == 0 && tid <= f.NBK) f.bk_off[tid] = excl;
     }
     if (tile == 0 && tid == 0) {
@@ -1357,6 +1361,10 @@ __global__ void k_load(DevState S, uint32_t first, uint32_t count, const hb_grou
   S.meta[g] = m;
   S.elapsed[g] = 0;  // newRaft: fresh r.rand, becomeFollower -> reset
   S.rpos[g] = 0;
+  if (S.szp) {  // finite max_msg_size: no entry sizes yet (hb_load_entry_sizes)
+    S.szlo[g] = r.last_index;
+    *szp_at(S, g, r.last_index) = 0;
+  }
   for (uint32_t s = 0; s < S.nmax; ++s) {
     const bool on = s < r.n;
     const size_t o = (size_t)s * S.G + g;
@@ -1411,6 +1419,24 @@ __global__ void k_set_bounds(DevState S, uint32_t count, const uint32_t* groups,
   const uint32_t g = groups[i];
   S.first[g] = first[i];
   S.snap[g] = snap[i];
+}
+
+// hb_load_entry_sizes: group groups[i] takes the sizes of its entries
+// (last - n_i, last], concatenated at sizes + off[i]
+__global__ void k_load_sizes(DevState S, uint32_t count, const uint32_t* groups, const uint32_t* n_sizes,
+                             const uint64_t* off, const uint32_t* sizes) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint32_t g = groups[i], k = n_sizes[i];
+  const uint64_t last = S.last[g], lo = last - k;
+  const uint32_t* z = sizes + off[i];
+  uint64_t acc = 0;
+  *szp_at(S, g, lo) = 0;
+  for (uint32_t j = 1; j <= k; ++j) {
+    acc += z[j - 1];
+    *szp_at(S, g, lo + j) = acc;
+  }
+  S.szlo[g] = lo;
 }
 
 __global__ void k_remove(DevState S, uint32_t first, uint32_t count) {
@@ -1546,7 +1572,7 @@ struct hb_handle {
   DevState st{};
   std::vector<void*> allocs;
   // partition scratch
-  uint32_t* hist = nullptr;       // [RDX_BINS][tiles]
+  uint32_t* hist = nullptr;       // [tiles][RDX_BINS]
   uint32_t* n_valid = nullptr;    // messages kept after pass 1 (device)
   uint32_t* totals = nullptr;     // [RDX_BINS] digit totals of the current pass
   RadixDst tmp[2] = {};           // intermediate passes (ping-pong)
@@ -1562,6 +1588,10 @@ struct hb_handle {
   uint64_t* s_term = nullptr;
   uint64_t* s_index = nullptr;
   uint64_t* s_hint = nullptr;
+  uint64_t* s_eoff = nullptr;     // [max_batch] (finite max_msg_size)
+  uint64_t* s_peoff = nullptr;    // [G]
+  uint32_t* s_edesc = nullptr;    // grown on demand
+  uint64_t s_edesc_cap = 0;
   // events
   uint64_t* ev = nullptr;   // compact event words
   uint64_t ev_region = 0;  // records
@@ -1662,8 +1692,7 @@ const char* hb_strerror(int code) {
 int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max_inflight,
               uint64_t max_msg_size, uint64_t max_batch, hb_handle** out) {
   if (!out || capacity == 0 || max_replicas < 1 || max_replicas > HB_MAX_REPLICAS || max_inflight < 1 ||
-      max_inflight > HB_MAX_INFLIGHT || (max_msg_size != 0 && max_msg_size != HB_NO_LIMIT) ||
-      max_batch >= (1ull << 31) || capacity > (1u << 24))
+      max_inflight > HB_MAX_INFLIGHT || max_batch >= (1ull << 31) || capacity > (1u << 24))
     return HB_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return HB_EDEVICE;
@@ -1701,6 +1730,10 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(s.elapsed, G);
   ALLOC(s.rpos, G);
   ALLOC(s.tcfg, G);
+  if (sz_on(max_msg_size)) {  // limitSize needs the latest entries' sizes
+    ALLOC(s.szp, (size_t)HB_SIZE_WINDOW * G);
+    ALLOC(s.szlo, G);
+  }
   // partition scratch
   const size_t mb = max_batch ? max_batch : 1;
   h->NBK = (capacity + (1u << BK_LOG) - 1) >> BK_LOG;
@@ -1738,6 +1771,10 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->s_index, mb);
   ALLOC(h->s_hint, mb);
   ALLOC(h->s_props, G);
+  if (sz_on(max_msg_size)) {
+    ALLOC(h->s_eoff, mb);
+    ALLOC(h->s_peoff, G);
+  }
   // events: (batch + one proposal slot per group) x EV_MAX (exact bound)
   h->ev_per_msg = EVC_WORDS_MAX * (h->nmax + 4);  // events per message <= nmax + 4, <= 2 words each
   // P chunks (one per partition, dense proposals) then the bucket regions of M chunks
@@ -1797,6 +1834,7 @@ int hb_destroy(hb_handle* h) {
   }
   if (h->rnd) (void)hipFree(h->rnd);
   if (h->evx) (void)hipFree(h->evx);
+  if (h->s_edesc) (void)hipFree(h->s_edesc);
   if (h->peer) (void)hipFree(h->peer);
   if (h->dec_q) (void)hipFree(h->dec_q);
   if (h->dec_qn) (void)hipFree(h->dec_qn);
@@ -1898,6 +1936,40 @@ int hb_set_log_bounds(hb_handle* h, uint32_t count, const uint32_t* groups, cons
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_set_bounds, dim3((count + 255) / 256), dim3(256), 0, h->stream, h->st, count,
                        (const uint32_t*)dgroup, (const uint64_t*)dfirst, (const uint64_t*)dsnap);
+    e = hipStreamSynchronize(h->stream);
+  }
+  (void)hipFree(d);
+  return e == hipSuccess ? HB_OK : HB_EDEVICE;
+}
+
+int hb_load_entry_sizes(hb_handle* h, uint32_t count, const uint32_t* groups, const uint32_t* n_sizes,
+                        const uint32_t* sizes) {
+  if (!h || (count && (!groups || !n_sizes))) return HB_EINVAL;
+  if (!sz_on(h->max_msg_size)) return HB_EINVAL;
+  if (count == 0) return HB_OK;
+  std::vector<uint64_t> off(count);
+  uint64_t tot = 0;
+  for (uint32_t i = 0; i < count; ++i) {
+    if (groups[i] >= h->G || n_sizes[i] >= HB_SIZE_WINDOW) return HB_EINVAL;
+    off[i] = tot;
+    tot += n_sizes[i];
+  }
+  if (tot && !sizes) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  char* d = nullptr;
+  const size_t bytes = count * (4ull + 4 + 8) + tot * 4 + 16;
+  HB_CHECK(hipMalloc(&d, bytes));
+  uint64_t* doff = reinterpret_cast<uint64_t*>(d);
+  uint32_t* dgrp = reinterpret_cast<uint32_t*>(doff + count);
+  uint32_t* dn = dgrp + count;
+  uint32_t* dsz = dn + count;
+  hipError_t e = hipMemcpyAsync(doff, off.data(), count * 8ull, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dgrp, groups, count * 4ull, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dn, n_sizes, count * 4ull, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess && tot) e = hipMemcpyAsync(dsz, sizes, tot * 4ull, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_load_sizes, dim3((count + 255) / 256), dim3(256), 0, h->stream, h->st, count,
+                       (const uint32_t*)dgrp, (const uint32_t*)dn, (const uint64_t*)doff, (const uint32_t*)dsz);
     e = hipStreamSynchronize(h->stream);
   }
   (void)hipFree(d);
@@ -2113,6 +2185,8 @@ int hb_get_inflights(hb_handle* h, uint32_t group, uint32_t slot, uint32_t* star
 int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   if (!h || !b || b->n > h->max_batch) return HB_EINVAL;
   if (b->n && (!b->group || !b->info || !b->term || !b->index)) return HB_EINVAL;
+  const bool sized = sz_on(h->max_msg_size);  // appended entries carry descriptors
+  if (sized && ((b->n && !b->eoff) || (b->props && !b->peoff) || (b->n_edesc && !b->edesc))) return HB_EINVAL;
   DeviceGuard guard(h->device);
   hipStream_t st = h->stream;  // apply stream
   // prep stream (partition + route): the library's own stream when the caller
@@ -2128,6 +2202,9 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   // stream's work so far (default: the apply stream, i.e. no overlap), (b) the
   // last apply that read this prep set (two steps ago).
   BatchDev bd{b->group, b->info, b->term, b->index, b->hint, b->props, b->n};
+  const uint32_t* bd_edesc = b->edesc;
+  const uint64_t* bd_eoff = b->eoff;
+  const uint64_t* bd_peoff = b->peoff;
   if (two) {
     HB_CHECK(hipEventRecord(h->in_ready, h->in_stream));
     HB_CHECK(hipStreamWaitEvent(ps_st, h->in_ready, 0));
@@ -2151,6 +2228,22 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     bd.index = h->s_index;
     bd.hint = b->hint ? h->s_hint : nullptr;
     bd.props = b->props ? h->s_props : nullptr;
+    if (sized) {  // entry descriptors are read by apply: apply stream
+      if (b->n_edesc > h->s_edesc_cap) {
+        HB_CHECK(hipStreamSynchronize(st));  // the old staging may still be read
+        if (h->s_edesc) (void)hipFree(h->s_edesc);
+        h->s_edesc = nullptr;
+        h->s_edesc_cap = 0;
+        HB_CHECK(hipMalloc(&h->s_edesc, b->n_edesc * 4));
+        h->s_edesc_cap = b->n_edesc;
+      }
+      if (b->n_edesc) HB_CHECK(hipMemcpyAsync(h->s_edesc, b->edesc, b->n_edesc * 4, hipMemcpyHostToDevice, st));
+      if (n) HB_CHECK(hipMemcpyAsync(h->s_eoff, b->eoff, n * 8, hipMemcpyHostToDevice, st));
+      if (b->props) HB_CHECK(hipMemcpyAsync(h->s_peoff, b->peoff, (size_t)h->G * 8, hipMemcpyHostToDevice, st));
+      bd_edesc = h->s_edesc;
+      bd_eoff = h->s_eoff;
+      bd_peoff = b->props ? h->s_peoff : nullptr;
+    }
   }
   if (prof) HB_CHECK(hipEventRecord(ev[0], ps_st));
 
@@ -2186,6 +2279,9 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   // ---- phase 2: route each partition's messages to its lanes (prep stream) ----
   ApplyArgs aa;
   aa.S = h->st;
+  aa.S.edesc = bd_edesc;
+  aa.S.eoff = bd_eoff;
+  aa.S.peoff = bd_peoff;
   aa.rec = ps.rec;
   aa.key = ps.key;
   aa.bk_off = ps.bk_off;

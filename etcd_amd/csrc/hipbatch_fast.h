@@ -241,7 +241,12 @@ struct FastLane {
     }
     const uint64_t x = next[s] - 1;
     if (next[s] <= last) {
-      const uint64_t lastsent = S.max_msg_size == 0 ? next[s] : last;
+      bool ok = true;
+      const uint64_t lastsent = sz_limit(S, g, next[s], last, &ok);
+      if (!ok) {
+        fault(HB_FAULT_SIZE_WINDOW);
+        return SEND_NONE;
+      }
       const uint32_t st = pm_state(p);
       if (st == HB_PR_REPLICATE) {
         const uint32_t cnt = pm_count(p), start = pm_start(p);
@@ -316,6 +321,7 @@ struct FastLane {
   // ---- MsgProp with k entries on a leader (prop_ok)
   __device__ __forceinline__ void prop(uint32_t k) {
     const uint64_t old = last;
+    if (sz_on(S.max_msg_size)) sz_append(S, g, old, k, term, S.edesc + S.peoff[g]);  // dense proposal entries
     last += k;
     if (tfirst == HB_NO_INDEX) {
       tfirst = old + 1;

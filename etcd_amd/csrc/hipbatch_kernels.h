@@ -91,7 +91,66 @@ struct DevState {
   uint32_t* tcfg;             // [G] ElectionTick | HeartbeatTick << 16
   const uint64_t* rnd;        // [nrnd] the node's r.rand.Int() stream (host supplied)
   uint64_t nrnd;
+  // finite max_msg_size only (sz_on): sizes of the latest entries, for limitSize
+  uint64_t* szp;              // [HB_SIZE_WINDOW][G] szp[i % R] = sum of Entry.Size() of (szlo, i]
+  uint64_t* szlo;             // [G] oldest index i whose szp(i) is kept (szp(szlo) = the base)
+  const uint32_t* edesc;      // this step's entry descriptors (hb_batch.edesc / eoff / peoff)
+  const uint64_t* eoff;
+  const uint64_t* peoff;
 };
+
+// ---- entry sizes (finite MaxSizePerMsg) -----------------------------------------
+static_assert((HB_SIZE_WINDOW & (HB_SIZE_WINDOW - 1)) == 0, "size window is a power of two");
+constexpr uint64_t SZ_MASK = HB_SIZE_WINDOW - 1;
+__host__ __device__ inline bool sz_on(uint64_t max_msg_size) { return max_msg_size != 0 && max_msg_size != HB_NO_LIMIT; }
+// sovRaft: varint length (raft/raftpb/raft.pb.go)
+__device__ __forceinline__ uint64_t sov(uint64_t x) { return x ? (uint64_t)(70 - __clzll(x)) / 7 : 1; }
+// Entry.Size() raft/raftpb/raft.pb.go:1030-1043 of the entry a descriptor (HB_ENT_DESC) describes
+__device__ __forceinline__ uint64_t ent_size(uint32_t desc, uint64_t term, uint64_t index) {
+  uint64_t n = 1 + sov((desc >> 30) & 1u) + 1 + sov(term) + 1 + sov(index);
+  if (desc >> 31) {
+    const uint64_t l = desc & HB_ENT_MAX_DATA;
+    n += 1 + l + sov(l);
+  }
+  return n;
+}
+__device__ __forceinline__ uint64_t* szp_at(const DevState& S, uint32_t g, uint64_t i) {
+  return S.szp + (size_t)(i & SZ_MASK) * S.G + g;
+}
+// appendEntry's entries (last0, last0 + k] at Term `term`: their sizes enter the
+// window (d = their descriptors; null = the becomeLeader noop, pb.Entry{})
+__device__ __forceinline__ void sz_append(const DevState& S, uint32_t g, uint64_t last0, uint64_t k, uint64_t term,
+                                          const uint32_t* d) {
+  if (!sz_on(S.max_msg_size)) return;
+  uint64_t acc = *szp_at(S, g, last0);
+  for (uint64_t j = 1; j <= k; ++j) {
+    acc += ent_size(d ? d[j - 1] : 0u, term, last0 + j);
+    if (j + HB_SIZE_WINDOW > k) *szp_at(S, g, last0 + j) = acc;
+  }
+  const uint64_t last = last0 + k;
+  if (last >= HB_SIZE_WINDOW && S.szlo[g] < last - (HB_SIZE_WINDOW - 1)) S.szlo[g] = last - (HB_SIZE_WINDOW - 1);
+}
+// sendAppend's entries(next, maxMsgSize) (raft/raft.go:265, raft/log.go:219-224)
+// cut by limitSize (raft/util.go:97-110): the last index sent, next <= last.
+// The first entry always goes; each further one while the running sum of
+// Entry.Size() stays <= maxSize (a binary search over the cumulative sizes).
+// *ok = false when the window does not reach back to next - 1.
+__device__ __forceinline__ uint64_t sz_limit(const DevState& S, uint32_t g, uint64_t next, uint64_t last, bool* ok) {
+  if (S.max_msg_size == 0) return next;
+  if (S.max_msg_size == HB_NO_LIMIT) return last;
+  if (next - 1 < S.szlo[g]) {
+    *ok = false;
+    return next;
+  }
+  const uint64_t base = *szp_at(S, g, next - 1);
+  uint64_t lo = next, hi = last;
+  while (lo < hi) {
+    const uint64_t mid = lo + (hi - lo + 1) / 2;
+    if (*szp_at(S, g, mid) - base <= S.max_msg_size) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
 
 // ---- event sink ---------------------------------------------------------------
 // Device event records are compact 8-byte words (the public 16-byte hb_event
@@ -479,7 +538,12 @@ struct Lane {
     }
     const uint64_t x = p.next - 1;
     if (p.next <= last) {
-      const uint64_t lastsent = S.max_msg_size == 0 ? p.next : last;
+      bool ok = true;
+      const uint64_t lastsent = sz_limit(S, g, p.next, last, &ok);
+      if (!ok) {
+        fault(HB_FAULT_SIZE_WINDOW);
+        return;
+      }
       const uint32_t st = pm_state(p.pm);
       if (st == HB_PR_REPLICATE) {
         const uint32_t cnt = pm_count(p.pm), start = pm_start(p.pm);
@@ -693,6 +757,10 @@ struct Lane {
     bool check_commit = resolve_accept;
     if (append_k && !faulted()) {
       const uint64_t old = last;
+      if (sz_on(S.max_msg_size))  // the entries' sizes: noop, dense proposal, or MsgProp message
+        sz_append(S, g, old, append_k, term, noop ? nullptr
+                                                  : (arrival == 0xFFFFFFFFu ? S.edesc + S.peoff[g]
+                                                                            : S.edesc + S.eoff[arrival]));
       last += append_k;
       if (tfirst == HB_NO_INDEX) tfirst = old + 1;
       tlast = last;

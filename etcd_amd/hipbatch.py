@@ -53,6 +53,7 @@ def lib():
         "hb_remove_groups": (C.c_int, [H, C.c_uint32, C.c_uint32]),
         "hb_set_inflights": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
         "hb_set_log_bounds": (C.c_int, [H, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
+        "hb_load_entry_sizes": (C.c_int, [H, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
         "hb_get_inflights": (C.c_int, [H, C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32), C.c_void_p]),
         "hb_step": (C.c_int, [H, P(abi.hb_batch), C.c_uint32]),
         "hb_load_timers": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
@@ -169,6 +170,15 @@ class Engine:
         _check("hb_set_log_bounds", lib().hb_set_log_bounds(self.h, len(g), g.ctypes.data, f.ctypes.data,
                                                             s.ctypes.data))
 
+    def load_entry_sizes(self, sizes):
+        """Finite max_msg_size: {group slot: Entry.Size() of its last n entries, oldest first}."""
+        gs = np.ascontiguousarray(sorted(sizes), dtype=np.uint32)
+        ns = np.ascontiguousarray([len(sizes[int(g)]) for g in gs], dtype=np.uint32)
+        flat = np.ascontiguousarray(np.concatenate([np.asarray(sizes[int(g)], dtype=np.uint32) for g in gs])
+                                    if len(gs) else np.zeros(1, np.uint32), dtype=np.uint32)
+        _check("hb_load_entry_sizes", lib().hb_load_entry_sizes(self.h, len(gs), gs.ctypes.data, ns.ctypes.data,
+                                                                flat.ctypes.data))
+
     def get_inflights(self, group, slot):
         out = np.zeros(self.max_inflight, dtype=np.uint64)
         s, c = C.c_uint32(), C.c_uint32()
@@ -177,18 +187,22 @@ class Engine:
         return s.value, out[: c.value].copy()
 
     # ---- hot path --------------------------------------------------------------
-    def step(self, group, info, term, index, hint=None, props=None, host=None, profile=False):
+    def step(self, group, info, term, index, hint=None, props=None, host=None, profile=False, edesc=None,
+             eoff=None, peoff=None):
         """Step one batch.  Arrays are numpy (host) or torch tensors (host or cuda).
-        profile: False, True (every phase) or "apply" (only HB_PHASE_APPLY)."""
+        profile: False, True (every phase) or "apply" (only HB_PHASE_APPLY).
+        edesc / eoff / peoff: entry descriptors (finite max_msg_size, include/hipbatch.h)."""
         b = abi.hb_batch()
         b.n = len(group)
         b.group, b.info, b.term, b.index = _ptr(group), _ptr(info), _ptr(term), _ptr(index)
         b.hint, b.props = _ptr(hint), _ptr(props)
+        b.n_edesc = 0 if edesc is None else len(edesc)
+        b.edesc, b.eoff, b.peoff = _ptr(edesc), _ptr(eoff), _ptr(peoff)
         if host is None:
             host = not (hasattr(group, "is_cuda") and group.is_cuda)
         prof = {True: abi.HB_STEP_PROFILE, "apply": abi.HB_STEP_PROFILE_APPLY}.get(profile, 0)
         flags = (abi.HB_STEP_HOST_PTRS if host else 0) | prof
-        self._keep = (group, info, term, index, hint, props)
+        self._keep = (group, info, term, index, hint, props, edesc, eoff, peoff)
         _check("hb_step", lib().hb_step(self.h, C.byref(b), flags))
 
     # ---- timers (MultiNode.Tick) ----------------------------------------------
@@ -230,7 +244,8 @@ class Engine:
 
     def step_batch(self, batch, **kw):
         return self.step(batch["group"], batch["info"], batch["term"], batch["index"],
-                         batch.get("hint"), batch.get("props"), **kw)
+                         batch.get("hint"), batch.get("props"), edesc=batch.get("edesc"), eoff=batch.get("eoff"),
+                         peoff=batch.get("peoff"), **kw)
 
     def events(self):
         """Dense events of the last step (host copy, synchronizes)."""

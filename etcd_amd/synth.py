@@ -235,6 +235,51 @@ def random_batch(groups, nmsg, seed=2, nonmember=0.04, props=True, grp=None):
     return dict(group=grp, info=info, term=term, index=index, hint=hint, props=pr)
 
 
+def attach_entry_descs(batch, G, seed=3, max_len=64, nil_p=0.2, conf_p=0.1):
+    """Finite MaxSizePerMsg batches: random entry descriptors (HB_ENT_DESC) for
+    every entry a batch may append — each MsgProp message's index[i] entries
+    (eoff) and each dense proposal's props[g] entries (peoff)."""
+    rng = np.random.default_rng(seed)
+    t = batch["info"] & np.uint32(0xF)
+    k = np.where(t == A.HB_MSG_PROP, batch["index"], 0).astype(np.uint64)
+    pk = batch["props"].astype(np.uint64) if batch.get("props") is not None else np.zeros(G, np.uint64)
+    eoff = np.zeros(len(k), np.uint64)
+    eoff[1:] = np.cumsum(k)[:-1]
+    peoff = (k.sum() + np.concatenate([[0], np.cumsum(pk)[:-1]])).astype(np.uint64)
+    total = int(k.sum() + pk.sum())
+    ln = rng.integers(0, max_len + 1, total).astype(np.uint32)
+    has = (rng.random(total) >= nil_p).astype(np.uint32)
+    et = (rng.random(total) < conf_p).astype(np.uint32)
+    edesc = np.where(has == 1, ln, 0).astype(np.uint32) | (et << np.uint32(30)) | (has << np.uint32(31))
+    return dict(batch, edesc=edesc.astype(np.uint32), eoff=eoff, peoff=peoff if batch.get("props") is not None
+                else None)
+
+
+def window_sizes(groups, runs, seed=4, max_len=64, frac_full=0.7):
+    """Entry.Size() of each group's latest entries (hb_load_entry_sizes): random
+    payloads for the entries the log already holds, their Term from the log's
+    term runs; most groups get their whole log (up to HB_SIZE_WINDOW - 1), the
+    rest only a few entries (sends further back fault HB_FAULT_SIZE_WINDOW)."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    for g in range(len(groups)):
+        first, last = int(groups["first_index"][g]), int(groups["last_index"][g])
+        avail = min(last - (first - 1), A.HB_SIZE_WINDOW - 1)
+        k = avail if rng.random() < frac_full else int(rng.integers(0, avail + 1))
+        rr = runs[g]
+        z = []
+        for i in range(last - k + 1, last + 1):
+            term = 0
+            for idx, t in rr:
+                if idx <= i:
+                    term = t
+            ln = int(rng.integers(0, max_len + 1))
+            d = A.hb_ent_desc(ln, int(rng.random() < 0.1), rng.random() >= 0.2)
+            z.append(A.entry_size(d, term, i))
+        out[g] = z
+    return out
+
+
 def random_timers(G, seed=1, et_hi=12, ht_hi=4, pos_hi=50):
     """Per-group timers for tick parity: ElectionTick 1..et_hi, HeartbeatTick
     1..ht_hi, elapsed anywhere in [0, 2 ElectionTick], rand positions spread."""

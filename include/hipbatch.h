@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define HB_ABI_VERSION 1
+#define HB_ABI_VERSION 2
 
 /* ---- error codes -------------------------------------------------------- */
 #define HB_OK          0
@@ -48,6 +48,7 @@ extern "C" {
 #define HB_MAX_INFLIGHT   1024   /* Config.MaxInflightMsgs upper bound on device       */
 #define HB_NO_LIMIT       UINT64_MAX  /* raft noLimit (raft/raft.go:30)                */
 #define HB_NO_INDEX       UINT64_MAX
+#define HB_SIZE_WINDOW    1024   /* entries whose sizes the device keeps per group (finite MaxSizePerMsg) */
 
 /* ---- raft enums (values equal the reference's) --------------------------- */
 /* StateType raft/raft.go:35-39 */
@@ -98,9 +99,23 @@ extern "C" {
  * props    = optional dense [capacity] entry counts: group g first steps one
  *            MsgProp carrying props[g] entries (if > 0), before its messages
  *            in this batch.  NULL = none.
+ *
+ * Entry descriptors — read only when the handle's max_msg_size is finite
+ * (neither HB_NO_LIMIT nor 0): sendAppend then sends entries(Next,
+ * maxMsgSize) cut by limitSize (raft/raft.go:265, raft/util.go:97-110), which
+ * needs every appended entry's protobuf size (raft/raftpb/raft.pb.go:1030-
+ * 1043).  The device computes Entry.Size() from the descriptor plus the Term
+ * and Index it assigns (appendEntry, raft/raft.go:351-360):
+ *   edesc[k] = HB_ENT_DESC(len(Data), Type, Data != nil)
+ *   eoff[i]  = first descriptor of MsgProp message i (its index[i] entries)
+ *   peoff[g] = first descriptor of the dense proposal props[g]
+ * n_edesc = number of descriptors (bytes copied with HB_STEP_HOST_PTRS).
  */
 #define HB_INFO(type, from_slot, reject) \
   ((uint32_t)(type) | ((uint32_t)(from_slot) << 4) | ((uint32_t)((reject) ? 1 : 0) << 8))
+#define HB_ENT_MAX_DATA   0x3FFFFFFF
+#define HB_ENT_DESC(data_len, type, has_data) \
+  ((uint32_t)(data_len) | ((uint32_t)(type) << 30) | ((uint32_t)((has_data) ? 1 : 0) << 31))
 
 typedef struct hb_batch {
   uint64_t        n;
@@ -110,6 +125,10 @@ typedef struct hb_batch {
   const uint64_t* index;
   const uint64_t* hint;
   const uint32_t* props;
+  uint64_t        n_edesc;
+  const uint32_t* edesc;
+  const uint64_t* eoff;
+  const uint64_t* peoff;
 } hb_batch;
 
 /* hb_step flags */
@@ -175,6 +194,9 @@ typedef struct hb_group {
 #define HB_FAULT_FOLLOWER_LEADER 8  /* "invalid transition [follower -> leader]" raft/raft.go:409 (oracle KATs only) */
 #define HB_FAULT_RAND_EXHAUSTED  9  /* engine-defined, no reference panic: hb_tick needed draw
                                        rand_pos of the group but hb_set_rand supplied fewer */
+#define HB_FAULT_SIZE_WINDOW    10  /* engine-defined, no reference panic: with a finite
+                                       max_msg_size, sendAppend needed the size of an entry
+                                       older than the device's HB_SIZE_WINDOW - 1 latest */
 
 /* ---- events (the sparse delta list) ---------------------------------------
  * One ordered stream of 16-byte records per group describes everything the
@@ -190,9 +212,10 @@ typedef struct hb_group {
  *   HB_EV_LAST      x = new lastIndex, aux = 1 for the becomeLeader noop entry,
  *                   0 for proposal entries        (raft.appendEntry, raft/raft.go:351-360)
  *   HB_EV_APP       to, x = m.Index (= Next-1).  Entries are (x, L] where L is
- *                   the current lastIndex (max_msg_size noLimit) or x+1
- *                   (max_msg_size 0); none if x+1 > L.  m.Commit = current
- *                   committed, m.Term = current term, m.LogTerm = term(x).
+ *                   the current lastIndex (max_msg_size noLimit), x+1
+ *                   (max_msg_size 0), or limitSize's cut of (x, lastIndex]
+ *                   (finite max_msg_size); none if x+1 > lastIndex.  m.Commit =
+ *                   current committed, m.Term = current term, m.LogTerm = term(x).
  *                   (raft.sendAppend, raft/raft.go:261-281)
  *   HB_EV_SNAP      to, x = snapshot index         (raft/raft.go:246-260)
  *   HB_EV_HEARTBEAT to, x = m.Commit              (raft.sendHeartbeat, raft/raft.go:285-299)
@@ -248,8 +271,10 @@ typedef struct hb_handle hb_handle;
 /* ---- lifecycle ------------------------------------------------------------ */
 /* Create a handle on `device` holding up to `capacity` groups of at most
  * `max_replicas` peers, MaxInflightMsgs = max_inflight (Config.MaxInflightMsgs,
- * raft/raft.go:98) and MaxSizePerMsg = max_msg_size (HB_NO_LIMIT or 0 on the
- * device; raft/raft.go:93).  `max_batch` bounds hb_step's n. */
+ * raft/raft.go:98) and MaxSizePerMsg = max_msg_size (raft/raft.go:93; any
+ * value: HB_NO_LIMIT, 0, or a finite size, for which the device keeps the
+ * sizes of each group's last HB_SIZE_WINDOW entries, see
+ * hb_load_entry_sizes).  `max_batch` bounds hb_step's n. */
 int  hb_create(int device, uint32_t capacity, uint32_t max_replicas,
                uint32_t max_inflight, uint64_t max_msg_size, uint64_t max_batch,
                hb_handle** out);
@@ -291,6 +316,15 @@ int  hb_remove_groups(hb_handle* h, uint32_t first, uint32_t count);
  * `count` group slots (host arrays). */
 int  hb_set_log_bounds(hb_handle* h, uint32_t count, const uint32_t* groups,
                        const uint64_t* first_index, const uint64_t* snap_index);
+/* Finite max_msg_size only: the protobuf sizes (Entry.Size()) of the latest
+ * entries of `count` loaded groups, so that sendAppend can cut entries(Next,
+ * maxMsgSize) with limitSize.  groups[i] takes n_sizes[i] sizes (at most
+ * HB_SIZE_WINDOW - 1): the entries (last_index - n_sizes[i], last_index], in
+ * index order, concatenated over i in `sizes` (host arrays).  hb_load_groups
+ * leaves a group with none (only a follower at Next = last_index + 1 can be
+ * served); a send that needs an older entry faults HB_FAULT_SIZE_WINDOW. */
+int  hb_load_entry_sizes(hb_handle* h, uint32_t count, const uint32_t* groups,
+                         const uint32_t* n_sizes, const uint32_t* sizes);
 /* Inflight window of (group, slot): buffer[(start + i) % max_inflight] = vals[i]. */
 int  hb_set_inflights(hb_handle* h, uint32_t group, uint32_t slot,
                       uint32_t start, uint32_t count, const uint64_t* vals);

@@ -52,7 +52,7 @@ class orc_msg(C.Structure):
     _fields_ = [("Type", C.c_int), ("To", C.c_uint64), ("From", C.c_uint64), ("Term", C.c_uint64),
                 ("LogTerm", C.c_uint64), ("Index", C.c_uint64), ("Commit", C.c_uint64),
                 ("Reject", C.c_int), ("RejectHint", C.c_uint64), ("nents", C.c_uint64),
-                ("ent_lo", C.c_uint64), ("snap_index", C.c_uint64)]
+                ("ent_lo", C.c_uint64), ("snap_index", C.c_uint64), ("edesc", C.c_void_p)]
 
     def __repr__(self):
         return (f"Msg(type={self.Type}, to={self.To}, from={self.From}, term={self.Term}, "
@@ -105,6 +105,8 @@ class orc_raft(C.Structure):
         ("msgs", C.POINTER(orc_msg)), ("nmsgs", C.c_int), ("msgs_cap", C.c_int),
         ("ev", C.c_void_p), ("nev", C.c_uint64), ("ev_cap", C.c_uint64), ("group", C.c_uint32),
         ("arrival", C.c_uint64), ("fault", C.c_int), ("n_won", C.c_uint64), ("n_lost", C.c_uint64),
+        ("szc", C.c_void_p), ("szc_base", C.c_uint64), ("szc_n", C.c_uint64), ("szc_cap", C.c_uint64),
+        ("sz_lo", C.c_uint64),
     ]
 
 
@@ -179,6 +181,9 @@ def lib():
                                          P(C.c_uint64), P(C.c_uint64)]),
             "orc_groups_load_timers": (None, [R, C.c_uint32, C.c_void_p]),
             "orc_groups_export_timers": (None, [R, C.c_uint32, C.c_void_p]),
+            "orc_entry_size": (C.c_uint64, [C.c_uint32, C.c_uint64, C.c_uint64]),
+            "orc_limit_size": (C.c_uint64, [P(C.c_uint64), C.c_uint64, C.c_uint64]),
+            "orc_raft_load_sizes": (C.c_int, [R, C.c_uint32, P(C.c_uint32)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -291,6 +296,12 @@ class Raft:
         if hard and any(hard):
             L.orc_raft_load_state(C.byref(self.r), *hard)
         self.r.election_timeout, self.r.heartbeat_timeout = election, heartbeat
+
+    def load_sizes(self, sizes):
+        """Entry.Size() of the last len(sizes) entries (finite max_msg_size, hb_load_entry_sizes)."""
+        a = (C.c_uint32 * max(1, len(sizes)))(*sizes)
+        if lib().orc_raft_load_sizes(C.byref(self.r), len(sizes), a) != 0:
+            raise ValueError("orc_raft_load_sizes failed")
 
     def __del__(self):
         try:
@@ -463,7 +474,8 @@ class OracleGroups:
         n = len(batch_arrays["group"])
         keep = {}
         for k, dt in (("group", np.uint32), ("info", np.uint32), ("term", np.uint64),
-                      ("index", np.uint64), ("hint", np.uint64), ("props", np.uint32)):
+                      ("index", np.uint64), ("hint", np.uint64), ("props", np.uint32),
+                      ("edesc", np.uint32), ("eoff", np.uint64), ("peoff", np.uint64)):
             a = batch_arrays.get(k)
             if a is None:
                 setattr(b, k, None)
@@ -472,6 +484,7 @@ class OracleGroups:
             keep[k] = a
             setattr(b, k, a.ctypes.data)
         b.n = n
+        b.n_edesc = len(keep["edesc"]) if "edesc" in keep else 0
         if ev_cap is None:
             ev_cap = (n + self.G) * (abi.HB_MAX_REPLICAS + 6) + 64
         if getattr(self, "_ev", None) is None or len(self._ev) < ev_cap:
@@ -513,6 +526,15 @@ class OracleGroups:
         out = np.zeros(self.G, dtype=abi.GROUP_DTYPE)
         lib().orc_groups_export(self.ptr, self.G, out.ctypes.data)
         return out
+
+    def load_sizes(self, sizes):
+        """Finite max_msg_size: {group: Entry.Size() of its last n entries} (hb_load_entry_sizes)."""
+        L = lib()
+        for g, z in sizes.items():
+            a = np.ascontiguousarray(z, dtype=np.uint32)
+            rc = L.orc_raft_load_sizes(L.orc_groups_at(self.ptr, g), len(a), a.ctypes.data_as(C.POINTER(C.c_uint32)))
+            if rc != 0:
+                raise ValueError(f"orc_raft_load_sizes(group {g}) failed")
 
     def inflights(self, g, slot):
         L = lib()

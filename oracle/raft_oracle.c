@@ -263,6 +263,8 @@ void orc_raft_free(orc_raft* r) {
   orc_log_free(&r->log);
   free(r->msgs);
   r->msgs = NULL;
+  free(r->szc);
+  r->szc = NULL;
   r->n = 0;
 }
 
@@ -330,6 +332,94 @@ void orc_raft_commit_to(orc_raft* r, uint64_t tocommit) { /* commitTo raft/log.g
   }
 }
 
+/* ---- entry sizes (finite MaxSizePerMsg) ---- */
+static uint64_t sov_raft(uint64_t x) {                    /* sovRaft raft/raftpb/raft.pb.go */
+  uint64_t n = 0;
+  for (;;) {
+    n++;
+    x >>= 7;
+    if (x == 0) break;
+  }
+  return n;
+}
+
+uint64_t orc_entry_size(uint32_t desc, uint64_t term, uint64_t index) {  /* Entry.Size() :1030-1043 */
+  uint64_t n = 0;
+  n += 1 + sov_raft((desc >> 30) & 1u);                   /* Type */
+  n += 1 + sov_raft(term);
+  n += 1 + sov_raft(index);
+  if (desc >> 31) {                                       /* Data != nil */
+    uint64_t l = desc & HB_ENT_MAX_DATA;
+    n += 1 + l + sov_raft(l);
+  }
+  return n;
+}
+
+uint64_t orc_limit_size(const uint64_t* sizes, uint64_t n, uint64_t max_size) {  /* limitSize raft/util.go:97-110 */
+  if (n == 0) return 0;
+  uint64_t size = sizes[0];
+  uint64_t limit;
+  for (limit = 1; limit < n; limit++) {
+    size += sizes[limit];
+    if (size > max_size) break;
+  }
+  return limit;
+}
+
+static int sized(const orc_raft* r) { return r->max_msg_size != 0 && r->max_msg_size != HB_NO_LIMIT; }
+
+static void szc_push(orc_raft* r, uint64_t v) {
+  if (r->szc_n == r->szc_cap) {
+    r->szc_cap = r->szc_cap ? 2 * r->szc_cap : 16;
+    r->szc = (uint64_t*)realloc(r->szc, sizeof(uint64_t) * (size_t)r->szc_cap);
+  }
+  r->szc[r->szc_n++] = v;
+}
+
+static void szc_reset(orc_raft* r, uint64_t base) {      /* no entry size known: szc = {base: 0} */
+  r->szc_n = 0;
+  r->szc_base = base;
+  r->sz_lo = base;
+  szc_push(r, 0);
+}
+
+int orc_raft_load_sizes(orc_raft* r, uint32_t n, const uint32_t* sizes) {
+  if (!sized(r) || n >= HB_SIZE_WINDOW || n > r->log.last_index) return -1;
+  szc_reset(r, r->log.last_index - n);
+  uint64_t acc = 0;
+  for (uint32_t j = 0; j < n; j++) szc_push(r, acc += sizes[j]);
+  return 0;
+}
+
+/* entries (last0, last0 + k] appended at the current Term (appendEntry) */
+static void szc_append(orc_raft* r, uint64_t last0, uint64_t k, const uint32_t* desc) {
+  if (!sized(r)) return;
+  if (r->szc_n == 0) szc_reset(r, last0);                 /* a raft built by orc_raft_init */
+  uint64_t acc = r->szc[last0 - r->szc_base];
+  for (uint64_t j = 1; j <= k; j++) szc_push(r, acc += orc_entry_size(desc ? desc[j - 1] : 0u, r->term, last0 + j));
+  uint64_t last = last0 + k;
+  if (last >= HB_SIZE_WINDOW && r->sz_lo < last - (HB_SIZE_WINDOW - 1)) r->sz_lo = last - (HB_SIZE_WINDOW - 1);
+}
+
+/* the last index of entries(next, maxMsgSize) (raft/log.go:219-224 + limitSize);
+ * -1 when the engine would not hold the sizes it needs */
+static int64_t entries_last(orc_raft* r, uint64_t next) {
+  uint64_t last = r->log.last_index;
+  if (r->max_msg_size == HB_NO_LIMIT) return (int64_t)last;
+  if (r->max_msg_size == 0) return (int64_t)next;
+  if (r->szc_n == 0) szc_reset(r, last);                  /* a raft built by orc_raft_init */
+  if (next - 1 < r->sz_lo) return -1;
+  uint64_t n = last - next + 1;
+  uint64_t* sz = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)n);
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t idx = next + i;
+    sz[i] = r->szc[idx - r->szc_base] - r->szc[idx - 1 - r->szc_base];
+  }
+  uint64_t k = orc_limit_size(sz, n, r->max_msg_size);
+  free(sz);
+  return (int64_t)(next + k - 1);
+}
+
 void orc_raft_send_append(orc_raft* r, uint64_t to) {     /* sendAppend raft/raft.go:239-282 */
   orc_progress* pr = orc_raft_pr(r, to);
   if (!pr) { fault(r, HB_FAULT_NIL_PROGRESS); return; }
@@ -347,10 +437,11 @@ void orc_raft_send_append(orc_raft* r, uint64_t to) {     /* sendAppend raft/raf
     m.index = pr->next - 1;
     m.log_term = orc_log_term(&r->log, pr->next - 1);
     /* entries(Next, maxMsgSize) raft/log.go:219-224 + limitSize raft/util.go:97-110:
-     * noLimit -> through lastIndex; 0 -> exactly one entry. */
+     * noLimit -> through lastIndex; 0 -> exactly one entry; finite -> limitSize */
     if (pr->next <= r->log.last_index) {
-      uint64_t last = r->max_msg_size == 0 ? pr->next : r->log.last_index;
-      m.nents = last - pr->next + 1;
+      int64_t last = entries_last(r, pr->next);
+      if (last < 0) { fault(r, HB_FAULT_SIZE_WINDOW); return; }
+      m.nents = (uint64_t)last - pr->next + 1;
       m.ent_lo = pr->next;
     }
     m.commit = r->log.committed;
@@ -434,8 +525,9 @@ void orc_raft_reset(orc_raft* r, uint64_t term) {         /* reset raft/raft.go:
   r->pending_conf = 0;
 }
 
-void orc_raft_append_entry(orc_raft* r, uint64_t k, int noop) {  /* appendEntry raft/raft.go:351-360 */
+static void append_entries(orc_raft* r, uint64_t k, int noop, const uint32_t* desc) {  /* appendEntry raft/raft.go:351-360 */
   /* entries get Term = r.Term, Index = li+1..; raftLog.append (raft/log.go:90-99) */
+  szc_append(r, r->log.last_index, k, noop ? NULL : desc);
   orc_log_push(&r->log, r->term, k);
   emit(r, HB_EV_LAST, 0, r->log.last_index, noop);
   orc_progress* self = orc_raft_pr(r, r->id);
@@ -443,6 +535,8 @@ void orc_raft_append_entry(orc_raft* r, uint64_t k, int noop) {  /* appendEntry 
   orc_pr_maybe_update(self, r->log.last_index);
   orc_raft_maybe_commit(r);
 }
+
+void orc_raft_append_entry(orc_raft* r, uint64_t k, int noop) { append_entries(r, k, noop, NULL); }
 
 static void emit_state_if_changed(orc_raft* r, uint64_t before) {
   uint64_t now = soft_pack(r);
@@ -523,7 +617,7 @@ static void step_leader(orc_raft* r, const orc_msg* m) {  /* stepLeader raft/raf
       if (m->nents == 0) { fault(r, HB_FAULT_EMPTY_PROP); return; }
       /* EntryConfChange / pendingConf rewriting (:504-511) acts on entry
        * payloads, which stay on the host. */
-      orc_raft_append_entry(r, m->nents, 0);
+      append_entries(r, m->nents, 0, m->edesc);
       if (r->fault) return;
       orc_raft_bcast_append(r);
       break;
@@ -717,6 +811,7 @@ int orc_raft_from_group(orc_raft* r, const hb_group* g, const orc_run* runs, int
     r->nvotes++;
   }
   r->fault = (int)g->fault;
+  if (sized(r)) szc_reset(r, r->log.last_index);            /* hb_load_groups: no entry size yet */
   return 0;
 }
 
@@ -858,6 +953,7 @@ int orc_step_batch(orc_raft* groups, uint32_t ngroups, const hb_batch* b,
       m.type = HB_MSG_PROP;
       m.from = r->id;                                     /* raft/multinode.go:229 */
       m.nents = b->props[g];
+      m.edesc = (b->edesc && b->peoff) ? b->edesc + b->peoff[g] : NULL;
       orc_raft_step(r, &m);
       UNBIND(r);
     }
@@ -891,7 +987,11 @@ int orc_step_batch(orc_raft* groups, uint32_t ngroups, const hb_batch* b,
     m.index = b->index[i];
     m.reject = reject;
     m.reject_hint = (reject && b->hint) ? b->hint[i] : 0;
-    if (type == HB_MSG_PROP) { m.nents = b->index[i]; m.index = 0; }
+    if (type == HB_MSG_PROP) {
+      m.nents = b->index[i];
+      m.index = 0;
+      m.edesc = (b->edesc && b->eoff) ? b->edesc + b->eoff[i] : NULL;
+    }
     orc_raft_step(r, &m);
     account(r, type, stats);
     UNBIND(r);

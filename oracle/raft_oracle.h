@@ -82,6 +82,7 @@ typedef struct orc_msg {
   uint64_t nents;       /* len(m.Entries) */
   uint64_t ent_lo;      /* index of first entry (MsgApp) */
   uint64_t snap_index;  /* MsgSnap snapshot metadata index */
+  const uint32_t* edesc;  /* MsgProp: descriptors of its nents entries (HB_ENT_DESC), or NULL */
 } orc_msg;
 
 typedef struct orc_raft {
@@ -114,6 +115,12 @@ typedef struct orc_raft {
   uint64_t arrival;               /* arrival index of the message being stepped */
   int fault;                      /* HB_FAULT_* once a reference panic happened */
   uint64_t n_won, n_lost;         /* elections won (-> leader) / lost by poll (-> follower) */
+  /* Entry.Size() of the log's entries, as cumulative sums (finite
+   * max_msg_size): szc[i - szc_base] = sum of sizes of (szc_base, i].  sz_lo
+   * = the oldest index the engine keeps a size for (its HB_SIZE_WINDOW
+   * bound, mirrored so the engine-defined HB_FAULT_SIZE_WINDOW is checked). */
+  uint64_t* szc;
+  uint64_t szc_base, szc_n, szc_cap, sz_lo;
 } orc_raft;
 
 /* ---- inflights (raft/progress.go:183-237) ---- */
@@ -164,6 +171,13 @@ void orc_raft_bcast_append(orc_raft* r);
 void orc_raft_bcast_heartbeat(orc_raft* r);
 int  orc_raft_maybe_commit(orc_raft* r);
 void orc_raft_append_entry(orc_raft* r, uint64_t k, int noop);
+/* entry sizes (finite MaxSizePerMsg): gogo Entry.Size() (raft/raftpb/raft.pb.go:
+ * 1030-1043) of a descriptor's entry, limitSize (raft/util.go:97-110) over
+ * entry sizes (how many entries it keeps), and the sizes of a loaded group's
+ * last n entries (hb_load_entry_sizes' contract) */
+uint64_t orc_entry_size(uint32_t desc, uint64_t term, uint64_t index);
+uint64_t orc_limit_size(const uint64_t* sizes, uint64_t n, uint64_t max_size);
+int  orc_raft_load_sizes(orc_raft* r, uint32_t n, const uint32_t* sizes);
 void orc_raft_become_follower(orc_raft* r, uint64_t term, uint64_t lead);
 void orc_raft_become_candidate(orc_raft* r);
 void orc_raft_become_leader(orc_raft* r);

@@ -60,7 +60,8 @@ def assert_inflights_equal(eng, og, groups_now, ctx=""):
 class Pair:
     """An engine and an oracle loaded with the same groups."""
 
-    def __init__(self, groups, runs, nmax, W, ins=None, max_msg_size=abi.HB_NO_LIMIT, max_batch=1 << 16):
+    def __init__(self, groups, runs, nmax, W, ins=None, max_msg_size=abi.HB_NO_LIMIT, max_batch=1 << 16,
+                 sizes=None):
         from etcd_amd.hipbatch import Engine
         self.og = OracleGroups(groups, runs, W, max_msg_size, ins)
         init = self.og.groups()  # canonical record (term run derived from the log)
@@ -69,6 +70,9 @@ class Pair:
         self.eng.load_groups(init)
         for (g, s), vals in (ins or {}).items():
             self.eng.set_inflights(g, s, int(init[g]["pr"][s]["ins_start"]), vals)
+        if sizes:  # finite max_msg_size: the latest entries' sizes on both sides
+            self.og.load_sizes(sizes)
+            self.eng.load_entry_sizes(sizes)
         assert_groups_equal(self.eng.get_groups(), init, "load")
 
     def set_timers(self, timers, draws):

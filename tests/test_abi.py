@@ -102,8 +102,8 @@ def test_library_rejects_bad_arguments_without_device_work():
     assert L.hb_create(0, 0, 3, 256, abi.HB_NO_LIMIT, 10, C.byref(h)) == abi.HB_EINVAL
     assert L.hb_create(0, 10, 8, 256, abi.HB_NO_LIMIT, 10, C.byref(h)) == abi.HB_EINVAL
     assert L.hb_create(0, 10, 3, 2048, abi.HB_NO_LIMIT, 10, C.byref(h)) == abi.HB_EINVAL
-    assert L.hb_create(0, 10, 3, 256, 1 << 20, 10, C.byref(h)) == abi.HB_EINVAL  # finite MaxSizePerMsg
     assert L.hb_step(None, None, 0) == abi.HB_EINVAL
+    assert L.hb_load_entry_sizes(None, 0, None, None, None) == abi.HB_EINVAL
 
 
 def test_oracle_exports():

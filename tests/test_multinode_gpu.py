@@ -420,3 +420,59 @@ def test_compaction_after_send_keeps_the_sent_entries():
     rd = cycle()
     assert [(m.Type, m.To, m.Snapshot.Index) for m in rd.Messages] == [(abi.HB_MSG_SNAP, 3, 8)]
     mn.Stop()
+
+
+def test_max_size_per_msg_cuts_msgapp_entries():
+    """MaxSizePerMsg finite (etcdserver runs with 1 MiB, etcdserver/raft.go:229):
+    sendAppend sends entries(pr.Next, maxMsgSize) cut by limitSize
+    (raft/raft.go:265, raft/util.go:97-110) — the device decides how far the
+    follower's Next moves, the host sends exactly those entries."""
+    from etcd_amd.multinode import entry_size
+    s = MemoryStorage()
+    mn = StartMultiNode(1, max_msg_size=60)
+    mn.CreateGroup(1, Config(10, 1), s, peers=[1, 2])
+
+    def cycle():
+        rds = mn.Ready()
+        if 1 in rds:
+            s.Append(rds[1].Entries)
+            mn.Advance(rds)
+        return rds.get(1)
+    cycle()
+    mn.Campaign(1)
+    cycle()
+    mn.Step(1, Message(Type=abi.HB_MSG_VOTE_RESP, From=2, To=1, Term=2))
+    rd = cycle()  # leader; noop 3; MsgApp(2, [3]) to 2 (Probe: paused)
+    assert [(m.Type, m.Index, len(m.Entries)) for m in rd.Messages] == [(abi.HB_MSG_APP, 2, 1)]
+    payloads = [b"a" * 10, b"b" * 20, b"c" * 30, None, b"e" * 40, b"f" * 3]
+    for p in payloads:
+        mn.Propose(1, p)
+        assert cycle().Messages == []  # follower 2 is paused in Probe
+    log = [Entry(Term=2, Index=3)] + [Entry(Term=2, Index=4 + i, Data=p) for i, p in enumerate(payloads)]
+    # the ack of the noop: Probe -> Replicate, Next = 4; commit 3 -> bcastAppend
+    mn.Step(1, Message(Type=abi.HB_MSG_APP_RESP, From=2, To=1, Term=2, Index=3))
+    sent = []
+    nxt = 4
+    for _ in range(6):
+        rd = cycle()
+        apps = [m for m in rd.Messages if m.Type == abi.HB_MSG_APP] if rd else []
+        if not apps:
+            break
+        m = apps[0]
+        assert m.Index == nxt - 1
+        ents = log[nxt - 3:]
+        if not ents:  # the commit's bcastAppend past the last entry: an empty MsgApp
+            assert m.Entries == []
+            break
+        size, k = entry_size(ents[0]), 1
+        while k < len(ents) and size + entry_size(ents[k]) <= 60:
+            size += entry_size(ents[k])
+            k += 1
+        assert [(e.Index, e.Data) for e in m.Entries] == [(e.Index, e.Data) for e in ents[:k]]
+        sent.append(k)
+        nxt += k
+        mn.Step(1, Message(Type=abi.HB_MSG_APP_RESP, From=2, To=1, Term=2, Index=nxt - 1))
+    assert sum(sent) == len(payloads) and len(sent) > 1
+    st = mn.Status(1)
+    assert st.Progress[2].match == 3 + len(payloads)
+    mn.Stop()

@@ -606,3 +606,85 @@ def test_multinode_start_campaign_single():  # raft/multinode_test.go:246-300 (r
     assert (r.state, r.lead, r.Term, r.Vote, r.committed, r.lastIndex) == (L, 1, 2, 1, 2, 2)
     r.Step(Msg(abi.HB_MSG_PROP, From=1, Entries=1))
     assert (r.committed, r.lastIndex) == (3, 3)
+
+
+# ---------------------------------------------------------------- MaxSizePerMsg (limitSize)
+def test_limit_size():  # raft/util_test.go:49-75
+    import ctypes as C
+    from oracle.pyoracle import lib
+    ents = [(4, 4), (5, 5), (6, 6)]  # pb.Entry{Index, Term}: Type 0, Data nil
+    sz = [int(lib().orc_entry_size(abi.hb_ent_desc(0, 0, False), t, i)) for i, t in ents]
+    assert sz == [6, 6, 6]
+    tests = [
+        (2 ** 64 - 1, 3),
+        (0, 1),  # even if maxsize is zero, the first entry should be returned
+        (sz[0] + sz[1], 2),  # limit to 2
+        (sz[0] + sz[1] + sz[2] // 2, 2),  # limit to 2
+        (sz[0] + sz[1] + sz[2] - 1, 2),
+        (sz[0] + sz[1] + sz[2], 3),  # all
+    ]
+    arr = (C.c_uint64 * 3)(*sz)
+    for maxsize, want in tests:
+        assert lib().orc_limit_size(arr, 3, maxsize) == want, maxsize
+    assert lib().orc_limit_size(arr, 0, 0) == 0
+
+
+@pytest.mark.parametrize("term,index,data_len,etype,has_data", [
+    (0, 0, 0, 0, False), (1, 1, 3, 0, True), (4, 4, 0, 0, True), (127, 128, 127, 0, True),
+    (300, 70000, 200, 1, True), (2 ** 40, 2 ** 62, 1 << 20, 0, True), (2 ** 64 - 1, 2 ** 63, 0, 1, False)])
+def test_entry_size_matches_gogo(term, index, data_len, etype, has_data):
+    """Entry.Size() (raft/raftpb/raft.pb.go:1030-1043): 1 + sov(Type) + 1 + sov(Term)
+    + 1 + sov(Index) + (Data != nil ? 1 + len + sov(len) : 0), from the oracle, the
+    Python mirror and the host library (hbn_entry_size) alike."""
+    from oracle.pyoracle import lib
+    from etcd_amd.multinode import Entry, entry_size
+
+    def sov(x):
+        n = 1
+        while x >= 0x80:
+            x >>= 7
+            n += 1
+        return n
+    want = 1 + sov(etype) + 1 + sov(term) + 1 + sov(index) + ((1 + data_len + sov(data_len)) if has_data else 0)
+    d = abi.hb_ent_desc(data_len, etype, has_data)
+    assert lib().orc_entry_size(d, term, index) == want
+    assert abi.entry_size(d, term, index) == want
+    assert entry_size(Entry(Term=term, Index=index, Type=etype, Data=(b"x" * data_len) if has_data else None)) == want
+
+
+def test_send_append_cut_by_max_size_per_msg():
+    """sendAppend's entries(pr.Next, r.maxMsgSize) (raft/raft.go:265) with a finite
+    MaxSizePerMsg: limitSize keeps the first entry and then every entry while the
+    running Entry.Size() sum stays <= maxSize; Replicate then records the last
+    entry sent (optimisticUpdate + inflights.add, :271-273)."""
+    for max_size, want in ((13, 2), (12, 2), (11, 1), (18, 3), (0, 1), (abi.HB_NO_LIMIT, 5)):
+        r = Raft(1, [1, 2], ents=[(1, 1), (2, 1), (3, 1), (4, 1)], max_msg_size=max_size)
+        if max_size not in (0, abi.HB_NO_LIMIT):
+            r.load_sizes([6, 6, 6, 6])  # Entry{Term 1, Index i}.Size() = 6
+        r.becomeCandidate()
+        r.becomeLeader()  # noop at 5 (Term 2): Size 6
+        r.readMessages()
+        r.setProgress(2, 0, 1)
+        r.pr(2).State = abi.HB_PR_REPLICATE  # becomeReplicate with Match 0: Next = 1
+        r.sendAppend(2)
+        ms = r.readMessages()
+        assert len(ms) == 1 and ms[0].Type == abi.HB_MSG_APP and ms[0].Index == 0
+        assert ms[0].nents == want, (max_size, ms[0].nents)
+        assert r.pr(2).Next == want + 1 and r.fault == 0
+
+
+def test_send_append_beyond_size_window_faults():
+    """Engine-defined bound (not a reference panic): with a finite MaxSizePerMsg
+    the engine keeps the sizes of the latest HB_SIZE_WINDOW - 1 entries; a send
+    that starts before them faults HB_FAULT_SIZE_WINDOW (oracle and engine alike)."""
+    r = Raft(1, [1, 2], ents=[(1, 1), (2, 1), (3, 1), (4, 1)], max_msg_size=100)
+    r.load_sizes([6, 6])  # only entries 3 and 4 are known: next - 1 >= 2 can be served
+    r.becomeCandidate()
+    r.becomeLeader()
+    r.readMessages()
+    r.setProgress(2, 0, 3)
+    r.sendAppend(2)
+    assert r.fault == 0 and r.readMessages()[0].nents == 3
+    r.setProgress(2, 0, 2)
+    r.sendAppend(2)
+    assert r.fault == abi.HB_FAULT_SIZE_WINDOW

@@ -279,3 +279,39 @@ def test_general_kernel_slot_boundary(nmax):
         grp = rng.permutation(np.repeat(np.arange(G, dtype=np.uint32), counts))
         pair.step(synth.random_batch(g, 0, seed=500 + 10 * nmax + k, grp=grp),
                   ctx=f"slot boundary n={nmax}/{k}")
+
+
+@pytest.mark.parametrize("seed,nmax,W,max_size", [(61, 3, 8, 40), (62, 5, 16, 150), (63, 7, 8, 1000),
+                                                  (64, 5, 256, 1)])
+def test_fuzz_finite_max_msg_size(seed, nmax, W, max_size):
+    """A finite MaxSizePerMsg (raft/raft.go:265 + limitSize raft/util.go:97-110):
+    fuzzed states and messages, MsgProps and dense proposals carrying entries of
+    random payload sizes; every MsgApp's last entry (optimisticUpdate /
+    inflights.add) follows limitSize over the entries' gogo sizes.  Groups whose
+    size window does not reach a follower's Next fault HB_FAULT_SIZE_WINDOW on
+    both sides."""
+    g, runs, ins = synth.random_groups(1200, nmax, seed=seed, W=W)
+    sizes = synth.window_sizes(g, runs, seed=seed + 1)
+    pair = Pair(g, runs, nmax, W, ins=ins, max_msg_size=max_size, sizes=sizes, max_batch=1 << 14)
+    for k in range(3):
+        b = synth.attach_entry_descs(synth.random_batch(g, 5000, seed=seed + 10 * k), len(g), seed=seed + 7 * k)
+        pair.step(b, ctx=f"finite max size {max_size} step {k}")
+
+
+def test_cfg2_finite_max_msg_size():
+    """cfg2 shape (the fast kernel's proposal and accept path) under a finite
+    MaxSizePerMsg: every proposal carries 1-3 entries of 0-300 bytes."""
+    G, n = 4000, 3
+    g, runs = synth.steady_groups(G, n, seed=65, last_hi=1 << 12)
+    sizes = synth.window_sizes(g, runs, seed=66, frac_full=1.0)
+    pair = Pair(g, runs, n, 256, max_msg_size=256, sizes=sizes, max_batch=4 * G)
+    rng = np.random.default_rng(67)
+    last = g["last_index"].copy()
+    for step in range(3):
+        b = synth.cfg2_batch(g, step, seed=68 + step)
+        b["props"] = rng.integers(1, 4, G).astype(np.uint32)
+        last = last + b["props"]
+        b["index"] = last[b["group"]].astype(np.uint64)
+        b = synth.attach_entry_descs(b, G, seed=69 + step, max_len=300)
+        _, st, _ = pair.step(b, ctx=f"cfg2 finite step {step}")
+        assert st[abi.HB_STAT_FAULTS] == 0
