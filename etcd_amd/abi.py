@@ -21,6 +21,8 @@ HB_MAX_INFLIGHT = 1024
 HB_NO_LIMIT = (1 << 64) - 1
 HB_NO_INDEX = (1 << 64) - 1
 HB_SIZE_WINDOW = 1024
+HB_TERM_RUNS = 8
+HB_INFO_VOTED = 0x200
 HB_ENT_MAX_DATA = 0x3FFFFFFF
 
 # StateType raft/raft.go:35-39
@@ -66,6 +68,8 @@ HB_FAULT_NO_SELF = 7
 HB_FAULT_FOLLOWER_LEADER = 8
 HB_FAULT_RAND_EXHAUSTED = 9
 HB_FAULT_SIZE_WINDOW = 10
+HB_FAULT_TERM_WINDOW = 11
+HB_FAULT_CONFLICT_COMMITTED = 12
 
 HB_EV_TERM = 1
 HB_EV_STATE = 2
@@ -78,6 +82,17 @@ HB_EV_VOTE = 8
 HB_EV_PROP_FWD = 9
 HB_EV_PROP_DROP = 10
 HB_EV_FAULT = 11
+HB_STATE_OTH_LEAD = 1
+HB_STATE_OTH_VOTE = 2
+HB_EV_RESP = 13
+HB_EV_FOLLOW = 14
+HB_RESP_APP = 0
+HB_RESP_HEARTBEAT = 1
+HB_RESP_VOTE = 2
+HB_RESP_REJECT = 8
+HB_FOLLOW_STEP = 0
+HB_FOLLOW_APPEND = 1
+HB_FOLLOW_RESTORE = 2
 HB_EVW_BCAST = 12  # device event word: HB_EV_APP to every slot of a mask
 HB_EVW_CONT = 15  # device event word: continuation (x bits 40..63)
 
@@ -203,6 +218,8 @@ class hb_batch(C.Structure):
         ("edesc", C.c_void_p),
         ("eoff", C.c_void_p),
         ("peoff", C.c_void_p),
+        ("commit", C.c_void_p),
+        ("eterm", C.c_void_p),
     ]
 
 

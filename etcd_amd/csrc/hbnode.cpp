@@ -228,7 +228,7 @@ struct Log {
   hbn_storage* st = nullptr;
   std::vector<Ent> unstable;  // unstable.entries, position i + offset
   uint64_t offset = 0;
-  bool has_usnap = false;     // unstable.snapshot (only set by follower-side restore: not on this path)
+  bool has_usnap = false;     // unstable.snapshot (set by the follower side's restore)
   Snap usnap;
   uint64_t committed = 0, applied = 0;
 
@@ -393,6 +393,20 @@ struct Log {
   void stable_snap_to(uint64_t i) {
     if (has_usnap && usnap.index == i) has_usnap = false;
   }
+  // restore raft/log.go:294-298 + unstable.restore raft/log_unstable.go:94-98
+  void restore(const Snap& s) {
+    committed = s.index;
+    offset = s.index + 1;
+    unstable.clear();
+    has_usnap = true;
+    usnap = s;
+  }
+  // findConflict raft/log.go:112-123 over the entries index+1, index+2, ...
+  uint64_t find_conflict(uint64_t index, const uint64_t* terms, uint64_t n) const {
+    for (uint64_t k = 0; k < n; ++k)
+      if (term(index + 1 + k) != terms[k]) return index + 1 + k;
+    return 0;
+  }
 };
 
 // ---------------------------------------------------------------- messages
@@ -444,6 +458,10 @@ struct Group {
   std::deque<Msg> props;  // MsgProp in flight through the device batch, arrival order
   std::vector<Msg> msgs;  // r.msgs since the last Ready
   uint32_t election = 10, heartbeat = 1;
+  // follower side: m.From of the message the device is stepping (HB_EV_FOLLOW)
+  uint64_t cur_from = 0;
+  std::vector<uint64_t> reload_nodes;  // a restored snapshot's ConfState, when it differs from peers
+  bool reload = false;
   // Ready bookkeeping flags (membership of the node's lists)
   bool touched = false, stepped = false, content = false, delivered = false;
   bool bounds = false;  // storage changed: device firstIndex / snapshot index to refresh (hbn_node::bounds)
@@ -471,11 +489,21 @@ struct hbn_node {
   // pending device batch (host SoA, HB_STEP_HOST_PTRS)
   std::vector<uint32_t> b_group, b_info;
   std::vector<uint64_t> b_term, b_index, b_hint;
-  // finite MaxSizePerMsg: entry descriptors of the batched proposals (hb_batch edesc / eoff)
+  // entries of the batch (hb_batch eoff / eterm / edesc): a MsgProp's (descriptors,
+  // finite MaxSizePerMsg) and a MsgApp's (terms; payloads kept here for the replay)
   bool sized = false;
   std::vector<uint32_t> b_edesc;
-  std::vector<uint64_t> b_eoff;
+  std::vector<uint64_t> b_eoff, b_eterm;
+  std::vector<Ent> b_ents;           // by entry position (MsgProp positions hold placeholders)
+  uint64_t b_nent = 0;
+  // follower side (hb_batch commit; the sender ids and snapshots stay here)
+  std::vector<uint64_t> b_commit, b_from;
+  std::vector<uint32_t> b_snapi;     // per message: index into b_snaps, or NO_SLOT
+  std::vector<Snap> b_snaps;
+  bool b_app = false, b_follow = false;
+  std::vector<Group*> reload;        // groups whose restored ConfState differs from their peers
   std::vector<Group*> pend_sz;  // groups (re)loaded on the device whose entry sizes are still to push
+  std::vector<Group*> pend_tr;  // ... and whose older log term runs are still to push
   std::vector<Group*> stepped;  // groups whose raft.Step runs in the pending batch
   std::vector<hb_event> evbuf;
   // CreateGroup loads, coalesced into one hb_load_groups / hb_load_timers per slot run
@@ -593,6 +621,58 @@ Msg base_msg(const hbn_node* n, const Group& g, uint32_t type, uint64_t to) {
   return m;
 }
 
+// ---- follower side (raft/raft.go:616-707): the device decided, the host log follows
+uint64_t batch_ent_end(const hbn_node* n, uint64_t x) {
+  return x + 1 < n->b_eoff.size() ? n->b_eoff[x + 1] : n->b_nent;
+}
+
+// HB_FOLLOW_APPEND: raftLog.maybeAppend of batch message x appended its entries
+// from the first conflict (raft/log.go:72-88 -> append :89-98).
+void follower_append(hbn_node* n, Group& g, uint64_t x) {
+  if (x >= n->b_eoff.size()) panicf("device appended for a message outside the batch");
+  const uint64_t e0 = n->b_eoff[x], e1 = batch_ent_end(n, x), index = n->b_index[x];
+  const uint64_t ci = g.log.find_conflict(index, n->b_eterm.data() + e0, e1 - e0);
+  if (ci == 0) panicf("device appended entries the host log already holds");
+  materialize(g);  // pending MsgApps of this group read entries the append may cut
+  std::vector<Ent> ents(n->b_ents.begin() + (e0 + (ci - index - 1)), n->b_ents.begin() + e1);
+  g.log.append(ents);
+}
+
+// HB_FOLLOW_RESTORE: restore of batch message x's snapshot (raft/raft.go:684-707)
+void follower_restore(hbn_node* n, Group& g, uint64_t x) {
+  if (x >= n->b_snapi.size() || n->b_snapi[x] == NO_SLOT) panicf("device restored a snapshot the host does not hold");
+  const Snap& s = n->b_snaps[n->b_snapi[x]];
+  materialize(g);
+  g.log.restore(s);
+  // r.prs from the ConfState (every Progress reset, the device did that for the
+  // current slots); a different peer set is reloaded after the batch
+  std::vector<uint64_t> a = s.nodes, b = g.peers;
+  std::sort(a.begin(), a.end());
+  std::sort(b.begin(), b.end());
+  if (a != b) {
+    g.reload_nodes = s.nodes;
+    if (!g.reload) {
+      g.reload = true;
+      n->reload.push_back(&g);
+    }
+  }
+}
+
+// HB_EV_RESP: the follower side's r.send of a response (raft/raft.go:227-236)
+void follower_resp(hbn_node* n, Group& g, const hb_event& e) {
+  const uint32_t kind = e.aux & 7u;
+  const uint64_t to = e.to < g.peers.size() ? g.peers[e.to] : g.cur_from;  // HB_REF_OTHER: the sender
+  const uint32_t type = kind == HB_RESP_APP ? HB_MSG_APP_RESP
+                                            : (kind == HB_RESP_HEARTBEAT ? HB_MSG_HEARTBEAT_RESP : HB_MSG_VOTE_RESP);
+  Msg m = base_msg(n, g, type, to);
+  m.reject = (e.aux & HB_RESP_REJECT) ? 1 : 0;
+  if (kind == HB_RESP_APP) {
+    m.index = e.x;
+    if (m.reject) m.reject_hint = g.log.last_index();  // handleAppendEntries :661-663
+  }
+  g.msgs.push_back(std::move(m));
+}
+
 void on_event(hbn_node* n, Group& g, const hb_event& e) {
   if (g.fault) return;
   switch (e.type) {
@@ -607,8 +687,8 @@ void on_event(hbn_node* n, Group& g, const hb_event& e) {
       const uint32_t st = (uint32_t)(e.x & 0xFF), lref = (uint32_t)((e.x >> 8) & 0xFF),
                      vref = (uint32_t)((e.x >> 16) & 0xFF);
       g.state = st;
-      g.lead = id_of_ref(g, n->id, lref, g.lead);
-      g.vote = id_of_ref(g, n->id, vref, g.vote);
+      g.lead = (e.aux & HB_STATE_OTH_LEAD) ? g.cur_from : id_of_ref(g, n->id, lref, g.lead);
+      g.vote = (e.aux & HB_STATE_OTH_VOTE) ? g.cur_from : id_of_ref(g, n->id, vref, g.vote);
       g.pending_conf = false;  // every become* runs reset
       if (st == HB_STATE_LEADER) {
         // becomeLeader's scan of the uncommitted tail (raft/raft.go:415-424)
@@ -703,6 +783,19 @@ void on_event(hbn_node* n, Group& g, const hb_event& e) {
       g.fault = e.aux;
       g.props.clear();
       break;
+    case HB_EV_FOLLOW:
+      if (e.aux == HB_FOLLOW_STEP) {
+        if (e.x >= n->b_from.size()) panicf("device stepped a message outside the batch");
+        g.cur_from = n->b_from[e.x];
+      } else if (e.aux == HB_FOLLOW_APPEND) {
+        follower_append(n, g, e.x);
+      } else if (e.aux == HB_FOLLOW_RESTORE) {
+        follower_restore(n, g, e.x);
+      }
+      break;
+    case HB_EV_RESP:
+      follower_resp(n, g, e);
+      break;
     default:
       panicf("unknown device event type " + std::to_string(e.type));
   }
@@ -762,10 +855,49 @@ void push_sizes(hbn_node* n) {
     check(hb_load_entry_sizes(n->h, (uint32_t)slots.size(), slots.data(), cnt.data(), sizes.data()));
 }
 
+// The follower side's raftLog.term() lookups below a (re)loaded group's
+// current-term run: its newest HB_TERM_RUNS older runs (hb_load_term_runs),
+// found by binary search (log terms never decrease).
+void push_term_runs(hbn_node* n) {
+  if (n->pend_tr.empty()) return;
+  std::vector<uint32_t> slots, cnt;
+  std::vector<uint64_t> runs;
+  for (Group* g : n->pend_tr) {
+    if (g->slot == NO_SLOT) continue;
+    uint64_t tf, tl;
+    term_run(*g, &tf, &tl);
+    const uint64_t lo = g->log.first_index() - 1;
+    uint64_t hi = tf == HB_NO_INDEX ? g->log.last_index() : tf - 1;
+    std::vector<std::pair<uint64_t, uint64_t>> rr;  // newest first
+    while (tf != lo && hi + 1 > lo && rr.size() < HB_TERM_RUNS) {
+      const uint64_t t = g->log.term(hi);
+      uint64_t a = lo, b = hi;  // smallest i in [lo, hi] with term(i) == t
+      while (a < b) {
+        const uint64_t mid = a + (b - a) / 2;
+        if (g->log.term(mid) == t) b = mid;
+        else a = mid + 1;
+      }
+      rr.emplace_back(a, t);
+      if (a == lo) break;
+      hi = a - 1;
+    }
+    slots.push_back(g->slot);
+    cnt.push_back((uint32_t)rr.size());
+    for (auto it = rr.rbegin(); it != rr.rend(); ++it) {
+      runs.push_back(it->first);
+      runs.push_back(it->second);
+    }
+  }
+  n->pend_tr.clear();
+  if (!slots.empty())
+    check(hb_load_term_runs(n->h, (uint32_t)slots.size(), slots.data(), cnt.data(), runs.data()));
+}
+
 void sync_loads(hbn_node* n) {
   load_runs(n->pend_rec, [&](uint32_t f, uint32_t c, const hb_group* r) { return hb_load_groups(n->h, f, c, r); });
   load_runs(n->pend_tm, [&](uint32_t f, uint32_t c, const hb_timer* t) { return hb_load_timers(n->h, f, c, t); });
   push_sizes(n);
+  push_term_runs(n);
   if (!n->bounds.empty()) {  // storage compactions / snapshots since the last step, one call
     std::vector<uint32_t> slots;
     std::vector<uint64_t> first, snap;
@@ -782,6 +914,9 @@ void sync_loads(hbn_node* n) {
   }
 }
 
+void reload_prs(hbn_node* n, Group& g, const std::vector<uint64_t>& new_peers,
+                const std::vector<std::pair<uint64_t, uint64_t>>& fresh, bool restored);
+
 void flush(hbn_node* n) {
   sync_loads(n);
   if (n->b_group.empty()) return;
@@ -793,11 +928,13 @@ void flush(hbn_node* n) {
   b.index = n->b_index.data();
   b.hint = n->b_hint.data();
   b.props = nullptr;
-  if (n->sized) {
-    b.n_edesc = n->b_edesc.size();
-    b.edesc = n->b_edesc.data();
+  if (n->sized || n->b_app) {
+    b.n_edesc = n->b_nent;
     b.eoff = n->b_eoff.data();
+    if (n->sized) b.edesc = n->b_edesc.data();
+    if (n->b_app) b.eterm = n->b_eterm.data();
   }
+  if (n->b_follow) b.commit = n->b_commit.data();
   check(hb_step(n->h, &b, HB_STEP_HOST_PTRS));
   consume_events(n);
   for (Group* g : n->stepped) {
@@ -812,6 +949,25 @@ void flush(hbn_node* n) {
   n->b_hint.clear();
   n->b_edesc.clear();
   n->b_eoff.clear();
+  n->b_eterm.clear();
+  n->b_ents.clear();
+  n->b_nent = 0;
+  n->b_commit.clear();
+  n->b_from.clear();
+  n->b_snapi.clear();
+  n->b_snaps.clear();
+  n->b_app = n->b_follow = false;
+  // restored snapshots whose ConfState differs from the peers: r.prs = the
+  // ConfState's nodes, every Progress as setProgress made it (raft/raft.go:700-705)
+  for (Group* g : n->reload) {
+    g->reload = false;
+    if (g->fault) continue;
+    std::vector<std::pair<uint64_t, uint64_t>> fresh;
+    for (uint64_t id : g->reload_nodes) fresh.emplace_back(id, g->log.last_index() + 1);
+    reload_prs(n, *g, g->reload_nodes, fresh, true);
+    g->reload_nodes.clear();
+  }
+  n->reload.clear();
 }
 
 bool is_response(uint32_t t) {  // IsResponseMsg raft/util.go:53-55
@@ -820,7 +976,7 @@ bool is_response(uint32_t t) {  // IsResponseMsg raft/util.go:53-55
 
 // One message of the Ready cycle into the device batch (raft/multinode.go:224-237).
 void push(hbn_node* n, Group& g, uint32_t type, uint64_t from, bool reject, uint64_t term, uint64_t index,
-          uint64_t hint) {
+          uint64_t hint, uint64_t commit = 0, bool voted = false) {
   const int s = g.slot_of(from);
   const uint32_t fs = s >= 0 ? (uint32_t)s : HB_SLOT_NONE;
   touch(n, g);
@@ -832,11 +988,14 @@ void push(hbn_node* n, Group& g, uint32_t type, uint64_t from, bool reject, uint
   }
   if (n->b_group.size() >= n->max_batch) flush(n);
   n->b_group.push_back(g.slot);
-  n->b_info.push_back(HB_INFO(type, fs, reject));
+  n->b_info.push_back(HB_INFO(type, fs, reject) | (voted ? HB_INFO_VOTED : 0u));
   n->b_term.push_back(term);
   n->b_index.push_back(index);
   n->b_hint.push_back(hint);
-  if (n->sized) n->b_eoff.push_back(n->b_edesc.size());  // a MsgProp's descriptors follow (propose)
+  n->b_eoff.push_back(n->b_nent);  // a MsgProp's / MsgApp's entries follow (push_entry)
+  n->b_commit.push_back(commit);
+  n->b_from.push_back(from);
+  n->b_snapi.push_back(NO_SLOT);
   if ((s >= 0 || !is_response(type)) && !g.stepped) {
     g.stepped = true;
     n->stepped.push_back(&g);
@@ -849,14 +1008,63 @@ Group& group_of(hbn_node* n, uint64_t id) {
   return *it->second;
 }
 
+// One entry of the last pushed message (its descriptor for the device's
+// limitSize, its term for the follower side; `keep`: the payload for the replay).
+void push_entry(hbn_node* n, const Ent& x, bool keep) {
+  if (n->sized) n->b_edesc.push_back(ent_desc(x));
+  n->b_eterm.push_back(x.term);
+  if (keep) n->b_ents.push_back(x);
+  else n->b_ents.emplace_back();
+  n->b_nent++;
+}
+
 void propose(hbn_node* n, Group& g, Msg m) {
   if (g.fault) throw Fail{HBN_EPANIC};
   m.from = n->id;  // raft/multinode.go:228
   const uint64_t k = m.entries.size(), term = m.term;
   if (g.slot != NO_SLOT) g.props.push_back(std::move(m));
   push(n, g, HB_MSG_PROP, n->id, false, term, k, 0);
-  if (n->sized && g.slot != NO_SLOT)
-    for (const Ent& x : g.props.back().entries) n->b_edesc.push_back(ent_desc(x));
+  if (g.slot != NO_SLOT)
+    for (const Ent& x : g.props.back().entries) push_entry(n, x, false);
+}
+
+// The follower side of Step (MsgApp / MsgHeartbeat / MsgSnap / MsgVote,
+// raft/raft.go:585-707): the device steps it; the payloads stay here.
+void step_follower(hbn_node* n, Group& g, const hbn_message* m) {
+  const uint32_t t = m->type;
+  if (g.fault) throw Fail{HBN_EPANIC};
+  if (g.slot == NO_SLOT) throw Fail{HBN_EUNSUPPORTED};  // a raft with no prs at all
+  for (uint64_t k = 0; k < m->n_entries; ++k)  // the device numbers a MsgApp's entries Index+1, +2, ...
+    if (m->entries[k].index != m->index + 1 + k) throw Fail{HB_EINVAL};
+  bool voted = false;
+  if (t == HB_MSG_VOTE && g.slot_of(m->from) < 0) {
+    // r.Vote == m.From for a sender outside prs: only the host knows ids outside
+    // prs, so the group's earlier messages of this batch are stepped first
+    if (g.stepped) flush(n);
+    voted = g.vote != 0 && g.vote == m->from;
+  }
+  uint64_t index = m->index, hint = m->log_term;
+  if (t == HB_MSG_SNAP) {
+    index = m->snapshot.index;
+    hint = m->snapshot.term;
+  }
+  push(n, g, t, m->from, m->reject != 0, m->term, index, hint,
+       (t == HB_MSG_APP || t == HB_MSG_HEARTBEAT) ? m->commit : 0, voted);
+  n->b_follow = true;
+  if (t == HB_MSG_APP && m->n_entries) {
+    n->b_app = true;
+    for (uint64_t k = 0; k < m->n_entries; ++k) push_entry(n, ent_from(m->entries[k]), true);
+  }
+  if (t == HB_MSG_SNAP) {
+    n->b_snapi.back() = (uint32_t)n->b_snaps.size();
+    n->b_snaps.push_back(snap_from(m->snapshot));
+    // a restore to another peer set reloads the group's prs after its batch: the
+    // group's later messages must see the new prs, so the batch ends here
+    std::vector<uint64_t> a = n->b_snaps.back().nodes, b = g.peers;
+    std::sort(a.begin(), a.end());
+    std::sort(b.begin(), b.end());
+    if (a != b) flush(n);
+  }
 }
 
 // ---------------------------------------------------------------- Ready
@@ -910,9 +1118,11 @@ void refresh_content(hbn_node* n, Group& g) {
   g.content = c;
 }
 
-// Rebuild the device record of g after prs changed (ApplyConfChange).
+// Rebuild the device record of g after prs changed (ApplyConfChange; with
+// `restored`, a snapshot restore's setProgress of every ConfState node).
 void reload_prs(hbn_node* n, Group& g, const std::vector<uint64_t>& new_peers,
-                const std::vector<std::pair<uint64_t, uint64_t>>& fresh /* id -> (match 0, next) */) {
+                const std::vector<std::pair<uint64_t, uint64_t>>& fresh /* id -> (match 0, next) */,
+                bool restored) {
   hb_group old;
   std::memset(&old, 0, sizeof(old));
   hb_timer tm;
@@ -950,8 +1160,12 @@ void reload_prs(hbn_node* n, Group& g, const std::vector<uint64_t>& new_peers,
   for (size_t s = 0; s < new_peers.size(); ++s) {
     std::memset(&prs[s], 0, sizeof(hb_progress));
     for (size_t o = 0; o < old_peers.size(); ++o)
-      if (old_peers[o] == new_peers[s] && g.slot != NO_SLOT) from_old[s] = (int)o;
-    if (from_old[s] >= 0) {
+      if (old_peers[o] == new_peers[s] && g.slot != NO_SLOT && !restored) from_old[s] = (int)o;
+    if (restored) {  // raft/raft.go:700-705
+      prs[s].next = g.log.last_index() + 1;
+      prs[s].match = new_peers[s] == n->id ? g.log.last_index() : 0;
+      prs[s].state = HB_PR_PROBE;
+    } else if (from_old[s] >= 0) {
       prs[s] = old.pr[from_old[s]];
     } else {
       for (const auto& f : fresh)
@@ -990,6 +1204,8 @@ void reload_prs(hbn_node* n, Group& g, const std::vector<uint64_t>& new_peers,
     n->pend_sz.push_back(&g);
     push_sizes(n);
   }
+  n->pend_tr.push_back(&g);
+  push_term_runs(n);
   hb_timer t2 = tm;
   t2.election_tick = (uint16_t)g.election;
   t2.heartbeat_tick = (uint16_t)g.heartbeat;
@@ -1338,6 +1554,7 @@ int hbn_create_group(hbn_node* n, uint64_t group, const hbn_config* cfg, hbn_sto
       n->pend_tm.emplace_back(g.slot, t);
       n->by_slot[g.slot] = &g;
       if (n->sized) n->pend_sz.push_back(&g);
+      n->pend_tr.push_back(&g);
     }
     // the initial hard and soft states (:213-215)
     g.prev_soft = g.soft();
@@ -1361,7 +1578,8 @@ int hbn_remove_group(hbn_node* n, uint64_t group) {
       n->free_slots.push_back(g.slot);
     }
     if (g.log.st) drop_user(g.log.st, n, group);
-    for (auto* v : {&n->touched, &n->content, &n->delivered, &n->stepped, &n->bounds, &n->pend_sz})
+    for (auto* v : {&n->touched, &n->content, &n->delivered, &n->stepped, &n->bounds, &n->pend_sz, &n->pend_tr,
+                    &n->reload})
       v->erase(std::remove(v->begin(), v->end(), &g), v->end());
     n->groups.erase(it);
   });
@@ -1450,6 +1668,10 @@ int hbn_step(hbn_node* n, uint64_t group, const hbn_message* m) {
       propose(n, g, std::move(p));
       return;
     }
+    if (t == HB_MSG_APP || t == HB_MSG_HEARTBEAT || t == HB_MSG_SNAP || t == HB_MSG_VOTE) {
+      step_follower(n, g, m);
+      return;
+    }
     if (t != HB_MSG_APP_RESP && t != HB_MSG_VOTE_RESP && t != HB_MSG_HEARTBEAT_RESP) throw Fail{HBN_EUNSUPPORTED};
     if (g.fault) throw Fail{HBN_EPANIC};
     push(n, g, t, m->from, m->reject != 0, m->term, m->index, m->reject_hint);
@@ -1488,13 +1710,13 @@ int hbn_apply_conf_change(hbn_node* n, uint64_t group, uint32_t cc_type, uint64_
         case HBN_CC_ADD_NODE:  // addNode raft/raft.go:729-738
           if (g.slot_of(node_id) < 0) {
             np.push_back(node_id);
-            reload_prs(n, g, np, {{node_id, g.log.last_index() + 1}});
+            reload_prs(n, g, np, {{node_id, g.log.last_index() + 1}}, false);
             g.pending_conf = false;
           }
           break;
         case HBN_CC_REMOVE_NODE:  // removeNode :740-743
           np.erase(std::remove(np.begin(), np.end(), node_id), np.end());
-          if (np.size() != g.peers.size()) reload_prs(n, g, np, {});
+          if (np.size() != g.peers.size()) reload_prs(n, g, np, {}, false);
           g.pending_conf = false;
           break;
         case HBN_CC_UPDATE_NODE:

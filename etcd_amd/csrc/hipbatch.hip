@@ -368,7 +368,9 @@ struct ApplyArgs {
   uint32_t* ev_counts;      // [NB] records in each chunk
   uint64_t* ev_off;         // [NB] chunk offsets (records)
   uint64_t* stats_shard;    // [8][16] step statistics, one shard per XCD slot (atomic adds)
-  uint32_t* pflag;          // [NB][PART/32] groups handed from k_apply_fast to k_apply
+  uint32_t* pflag;          // [NB][PART/32] groups handed from k_apply_fast to k_apply (and on to k_follow)
+  uint32_t* fl_cnt;         // k_follow's work list: partitions k_apply flagged
+  uint32_t* fl_list;        // [NB]
   uint32_t* resume;         // [G] messages consumed by k_apply_fast | not loaded << 30 | prop pending << 31
   uint64_t* commit0;        // [G] committed at batch start (for HB_STAT_COMMITS)
   // k_route -> k_apply_fast / k_apply: each group's first kmax messages, lane-major
@@ -884,50 +886,63 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
 }
 
 // ---------------------------------------------------------------------------
-// k_apply: the general state machine (Lane::step) for the groups k_apply_fast
-// handed over, from their resume point.  Partitions without such groups exit
-// after reading their flag words.  A group whose messages all sit in its
-// k_route slots (count <= route_kmax) steps them from there, in arrival order;
-// the bucket is walked (LDS rounds) only when some group of the partition has
-// more messages than slots.
+// k_apply / k_follow: the general state machine (Lane::step) for the groups
+// the previous kernel handed over, from their resume point.  k_apply takes
+// k_apply_fast's hand-overs and steps every leader / candidate message type;
+// at a group's first follower-side message (MsgApp / MsgHeartbeat / MsgSnap /
+// MsgVote) it hands the group on to k_follow, which steps everything with the
+// follower-capable lane (its code and registers stay out of k_apply, the hot
+// general kernel of cfg3 / cfg4).  k_follow runs over a work list of the
+// partitions k_apply flagged: an empty list costs one small launch.
+// Partitions without handed-over groups exit after reading their flag words.
+// A group whose messages all sit in its k_route slots (count <= route_kmax)
+// steps them from there, in arrival order; the bucket is walked (LDS rounds)
+// only when some group of the partition has more messages than slots.
 // ---------------------------------------------------------------------------
 #ifndef HB_GEN_WAVES
 #define HB_GEN_WAVES 2
 #endif
-template <int NMAX>
-__global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
-  __shared__ Stage<CHUNK> sl;
-  __shared__ uint32_t l_fill;
-  __shared__ uint32_t l_flag[FLAG_WORDS];
-  __shared__ uint64_t l_stats[ST_N + 1];
+constexpr uint32_t FOLLOW_GRID = 256;  // k_follow workgroups (persistent over the work list)
 
-  const uint32_t part = block_part();
-  if (part >= a.NB) return;  // uniform: grid padding
+struct GenShared {
+  Stage<CHUNK> sl;
+  uint32_t l_fill;
+  uint32_t l_flag[FLAG_WORDS];
+  uint32_t l_next[FLAG_WORDS];  // groups handed on to k_follow
+  uint64_t l_stats[ST_N + 1];
+};
+
+template <int NMAX, bool FOLLOW>
+__device__ __forceinline__ void apply_part(const ApplyArgs& a, uint32_t part, GenShared& sh) {
   const uint32_t tid = threadIdx.x;
   const uint32_t bk = part >> SIS_LOG, sub = part & (SIS - 1);
   const uint32_t g = part * PART + tid;
-  if (tid < FLAG_WORDS) l_flag[tid] = a.pflag[(size_t)part * FLAG_WORDS + tid];
+  if (tid < FLAG_WORDS) {
+    sh.l_flag[tid] = a.pflag[(size_t)part * FLAG_WORDS + tid];
+    sh.l_next[tid] = 0;
+  }
   __syncthreads();
   uint32_t any = 0;
 #pragma unroll
-  for (uint32_t w = 0; w < FLAG_WORDS; ++w) any |= l_flag[w];
+  for (uint32_t w = 0; w < FLAG_WORDS; ++w) any |= sh.l_flag[w];
   if (!any) return;  // uniform
-  const bool flagged = (l_flag[tid >> 5] >> (tid & 31)) & 1u;
+  const bool flagged = (sh.l_flag[tid >> 5] >> (tid & 31)) & 1u;
 
   const uint32_t fill0 = a.ev_counts[2 * part + 1];
-  if (tid == 0) l_fill = fill0;  // append to the M chunk after the fast kernel's events
-  if (tid <= ST_N) l_stats[tid] = 0;
+  if (tid == 0) sh.l_fill = fill0;  // append to the M chunk after the previous kernels' events
+  if (tid <= ST_N) sh.l_stats[tid] = 0;
 
-  Lane<NMAX> L;
+  Lane<NMAX, FOLLOW> L;
   L.S = a.S;
   L.E.chunk = a.ev + a.ev_off[2 * part + 1];
-  L.E.fill = &l_fill;
+  L.E.fill = &sh.l_fill;
   L.g = g;
   L.won = 0;
   L.lost = 0;
   L.nev = 0;
   L.dirty = 0;
   L.prog = false;
+  L.voted = false;
   L.meta = 0;
   L.last = 0;
   L.committed = 0;
@@ -943,6 +958,8 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
   uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
   const uint32_t skip = resume & 0x3FFFFFFFu;
   uint32_t j = 0;
+  bool handed = false;  // (k_apply) a follower-side message: the group goes on to k_follow
+  uint32_t hand_at = 0;
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
 
   constexpr uint32_t KS = route_kmax(NMAX);
@@ -950,6 +967,29 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
   const bool by_slot = flagged && cnt <= KS;
   const bool by_walk = flagged && !by_slot;
   __syncthreads();  // l_fill
+  // one message through the lane; false: handed on (k_apply only)
+  auto step_one = [&](uint32_t inf, uint32_t morig, uint64_t mterm, uint64_t mindex, uint32_t ordinal) -> bool {
+    const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
+    const bool reject = (inf >> 8) & 1u;
+    if (!FOLLOW && is_follower_type(type)) {
+      handed = true;
+      hand_at = ordinal;
+      return false;
+    }
+    if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
+      st_drop++;
+      return true;
+    }
+    L.arrival = morig;
+    L.voted = (inf & HB_INFO_VOTED) != 0;
+    // RejectHint of a rejected MsgAppResp; m.LogTerm / the snapshot term of the follower side
+    const bool wants_hint = (reject && type == HB_MSG_APP_RESP) || (FOLLOW && is_follower_type(type));
+    L.step(type, from, mterm, mindex, reject, (wants_hint && a.hint) ? a.hint[morig] : 0ull);
+    st_msgs++;
+    st_app += type == HB_MSG_APP_RESP;
+    st_vote += type == HB_MSG_VOTE_RESP;
+    return true;
+  };
   if (by_slot) {
     if (resume >> 31) {
       L.arrival = 0xFFFFFFFFu;
@@ -1000,17 +1040,7 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
         term_n = a.slot_term[o];
         index_n = a.slot_index[o];
       }
-      const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
-      const bool reject = (inf >> 8) & 1u;
-      if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
-        st_drop++;
-        continue;
-      }
-      L.arrival = morig;
-      L.step(type, from, mterm, mindex, reject, (reject && a.hint) ? a.hint[morig] : 0ull);
-      st_msgs++;
-      st_app += type == HB_MSG_APP_RESP;
-      st_vote += type == HB_MSG_VOTE_RESP;
+      if (!step_one(inf, morig, mterm, mindex, x)) break;
     }
   }
 
@@ -1023,43 +1053,64 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
   };
   auto round = [&](uint32_t fill) {
     uint32_t my_start, my_cnt;
-    gather_round(sl, a, lo, fill, &my_start, &my_cnt, []() {});
+    gather_round(sh.sl, a, lo, fill, &my_start, &my_cnt, []() {});
     if (by_walk) {
       for (uint32_t x = 0; x < my_cnt; ++x, ++j) {
-        if (j < skip) continue;
-        const uint32_t i = sl.perm[my_start + x];
-        const uint32_t inf = sl.info(i);
-        const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
-        const bool reject = (inf >> 8) & 1u;
+        if (j < skip || handed) continue;
         if (L.faulted()) break;
-        if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
-          st_drop++;
-          continue;
-        }
-        L.arrival = sl.orig(i);
-        L.step(type, from, sl.term(i), sl.index(i), reject, (reject && a.hint) ? a.hint[sl.orig(i)] : 0ull);
-        st_msgs++;
-        st_app += type == HB_MSG_APP_RESP;
-        st_vote += type == HB_MSG_VOTE_RESP;
+        const uint32_t i = sh.sl.perm[my_start + x];
+        (void)step_one(sh.sl.info(i), sh.sl.orig(i), sh.sl.term(i), sh.sl.index(i), j);
       }
     }
     __syncthreads();
   };
-  if (__syncthreads_or(by_walk)) walk_partition(sl, a, lo, hi, sub, nullptr, on_total, round);
+  if (__syncthreads_or(by_walk)) walk_partition(sh.sl, a, lo, hi, sub, nullptr, on_total, round);
 
   if (flagged) L.store();
+  if (handed) {  // k_follow resumes the group at its follower-side message
+    atomicOr(&sh.l_next[tid >> 5], 1u << (tid & 31));
+    a.resume[g] = hand_at;
+    a.commit0[g] = commit0;
+  }
+  const bool done = flagged && !handed;  // the group's batch ends in this kernel
   const uint64_t vals[ST_N + 1] = {st_msgs,
                                    st_app,
                                    st_vote,
                                    st_drop,
-                                   (uint64_t)(flagged && L.committed != commit0),
+                                   (uint64_t)(done && L.committed != commit0),
                                    L.won,
                                    L.lost,
-                                   (uint64_t)(flagged && L.faulted() != 0),
+                                   (uint64_t)(done && L.faulted() != 0),
                                    L.last - last0,
                                    L.nev};
-  reduce_stats(a, l_stats, vals);
-  if (tid == 0) a.ev_counts[2 * part + 1] = l_fill;
+  reduce_stats(a, sh.l_stats, vals);
+  if (tid == 0) a.ev_counts[2 * part + 1] = sh.l_fill;
+  if constexpr (!FOLLOW) {  // the flags k_follow reads; the partition joins its work list
+    __syncthreads();
+    if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = sh.l_next[tid];
+    uint32_t nx = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < FLAG_WORDS; ++w) nx |= sh.l_next[w];
+    if (tid == 0 && nx) a.fl_list[atomicAdd(a.fl_cnt, 1u)] = part;
+  }
+}
+
+template <int NMAX>
+__global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
+  __shared__ GenShared sh;
+  const uint32_t part = block_part();
+  if (part >= a.NB) return;  // uniform: grid padding
+  apply_part<NMAX, false>(a, part, sh);
+}
+
+template <int NMAX>
+__global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_follow(ApplyArgs a) {
+  __shared__ GenShared sh;
+  const uint32_t nl = *reinterpret_cast<volatile const uint32_t*>(a.fl_cnt);  // written by k_apply
+  for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+    apply_part<NMAX, true>(a, a.fl_list[i], sh);
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1323,7 +1374,7 @@ __global__ void __launch_bounds__(DEC_THREADS) k_decode_general(DecodeArgs a, co
 // ============================================================================
 // Phase 3: finish
 // ============================================================================
-__global__ void __launch_bounds__(64) k_finish(uint64_t* shard, uint64_t* stats, uint64_t* accum) {
+__global__ void __launch_bounds__(64) k_finish(uint64_t* shard, uint64_t* stats, uint64_t* accum, uint32_t* fl_cnt) {
   const int map[ST_N + 1] = {HB_STAT_MSGS,  HB_STAT_APPRESP, HB_STAT_VOTERESP, HB_STAT_DROPPED, HB_STAT_COMMITS,
                              HB_STAT_WON,   HB_STAT_LOST,    HB_STAT_FAULTS,   HB_STAT_ENTRIES, HB_STAT_EVENTS};
   const uint32_t k = threadIdx.x;
@@ -1337,6 +1388,7 @@ __global__ void __launch_bounds__(64) k_finish(uint64_t* shard, uint64_t* stats,
     stats[map[k]] = v;
     if (accum) accum[map[k]] += v;
   }
+  if (k == 0 && fl_cnt) *fl_cnt = 0;  // k_follow's work list, for the next step
 }
 
 // ============================================================================
@@ -1419,6 +1471,19 @@ __global__ void k_set_bounds(DevState S, uint32_t count, const uint32_t* groups,
   const uint32_t g = groups[i];
   S.first[g] = first[i];
   S.snap[g] = snap[i];
+}
+
+// hb_load_term_runs: group groups[i] takes runs (start, term) off[i] .. + n_i
+__global__ void k_load_runs(DevState S, uint32_t count, const uint32_t* groups, const uint32_t* n_runs,
+                            const uint64_t* off, const uint64_t* runs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint32_t g = groups[i], k = n_runs[i];
+  for (uint32_t j = 0; j < k; ++j) {
+    S.trs[(size_t)j * S.G + g] = runs[2 * (off[i] + j)];
+    S.trt[(size_t)j * S.G + g] = runs[2 * (off[i] + j) + 1];
+  }
+  S.meta[g] = (S.meta[g] & ~(0x7Full << 40)) | ((uint64_t)k << 40);  // count k, head 0
 }
 
 // hb_load_entry_sizes: group groups[i] takes the sizes of its entries
@@ -1588,10 +1653,13 @@ struct hb_handle {
   uint64_t* s_term = nullptr;
   uint64_t* s_index = nullptr;
   uint64_t* s_hint = nullptr;
-  uint64_t* s_eoff = nullptr;     // [max_batch] (finite max_msg_size)
-  uint64_t* s_peoff = nullptr;    // [G]
+  uint64_t* s_eoff = nullptr;     // [max_batch]
+  uint64_t* s_commit = nullptr;   // [max_batch]
+  uint64_t* s_peoff = nullptr;    // [G] (finite max_msg_size)
   uint32_t* s_edesc = nullptr;    // grown on demand
   uint64_t s_edesc_cap = 0;
+  uint64_t* s_eterm = nullptr;    // grown on demand
+  uint64_t s_eterm_cap = 0;
   // events
   uint64_t* ev = nullptr;   // compact event words
   uint64_t ev_region = 0;  // records
@@ -1601,6 +1669,8 @@ struct hb_handle {
   uint64_t* stats = nullptr;
   // fast -> general hand-over
   uint32_t* pflag = nullptr;      // [NB][PART/32]
+  uint32_t* fl_cnt = nullptr;     // k_follow work list (count, reset by k_finish)
+  uint32_t* fl_list = nullptr;    // [NB]
   uint32_t* resume = nullptr;     // [G]
   uint64_t* commit0 = nullptr;    // [G]
   uint64_t* peer = nullptr;       // [G][HB_PEER_ROW] node ids (hb_load_peers), allocated on first use
@@ -1669,6 +1739,7 @@ void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
   hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
   if (ev) (void)hipEventRecord(ev[3], h->stream);
   hipLaunchKernelGGL(k_apply<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
+  hipLaunchKernelGGL(k_follow<NMAX>, dim3(std::min(FOLLOW_GRID, h->NB)), dim3(PART), 0, h->stream, a);
   if (ev && full) (void)hipEventRecord(ev[4], h->stream);
 }
 
@@ -1730,6 +1801,8 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(s.elapsed, G);
   ALLOC(s.rpos, G);
   ALLOC(s.tcfg, G);
+  ALLOC(s.trs, (size_t)HB_TERM_RUNS * G);  // follower side: older term runs
+  ALLOC(s.trt, (size_t)HB_TERM_RUNS * G);
   if (sz_on(max_msg_size)) {  // limitSize needs the latest entries' sizes
     ALLOC(s.szp, (size_t)HB_SIZE_WINDOW * G);
     ALLOC(s.szlo, G);
@@ -1771,10 +1844,9 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->s_index, mb);
   ALLOC(h->s_hint, mb);
   ALLOC(h->s_props, G);
-  if (sz_on(max_msg_size)) {
-    ALLOC(h->s_eoff, mb);
-    ALLOC(h->s_peoff, G);
-  }
+  ALLOC(h->s_eoff, mb);
+  ALLOC(h->s_commit, mb);
+  if (sz_on(max_msg_size)) ALLOC(h->s_peoff, G);
   // events: (batch + one proposal slot per group) x EV_MAX (exact bound)
   h->ev_per_msg = EVC_WORDS_MAX * (h->nmax + 4);  // events per message <= nmax + 4, <= 2 words each
   // P chunks (one per partition, dense proposals) then the bucket regions of M chunks
@@ -1782,6 +1854,8 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->ev, h->ev_region);
   ALLOC(h->stats_shard, 8 * 16);
   ALLOC(h->pflag, (size_t)h->NB * FLAG_WORDS);
+  ALLOC(h->fl_cnt, 4);
+  ALLOC(h->fl_list, h->NB);
   ALLOC(h->resume, G);
   ALLOC(h->commit0, G);
   ALLOC(h->stats, HB_STAT_COUNT);
@@ -1810,6 +1884,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
       hipMemset(s.elapsed, 0, G * 4) != hipSuccess || hipMemset(s.rpos, 0, G * 4) != hipSuccess ||
       hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(s.tcfg), 10u | (1u << 16), G) != hipSuccess ||
       hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess || hipMemset(h->stats_shard, 0, 8 * 16 * 8) != hipSuccess ||
+      hipMemset(h->fl_cnt, 0, 4) != hipSuccess ||
       hipMemset(h->set[0].ev_counts, 0, h->NB * 8ull) != hipSuccess ||
       hipMemset(h->set[0].ev_off, 0, h->NB * 16ull) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
@@ -1835,6 +1910,7 @@ int hb_destroy(hb_handle* h) {
   if (h->rnd) (void)hipFree(h->rnd);
   if (h->evx) (void)hipFree(h->evx);
   if (h->s_edesc) (void)hipFree(h->s_edesc);
+  if (h->s_eterm) (void)hipFree(h->s_eterm);
   if (h->peer) (void)hipFree(h->peer);
   if (h->dec_q) (void)hipFree(h->dec_q);
   if (h->dec_qn) (void)hipFree(h->dec_qn);
@@ -1936,6 +2012,39 @@ int hb_set_log_bounds(hb_handle* h, uint32_t count, const uint32_t* groups, cons
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_set_bounds, dim3((count + 255) / 256), dim3(256), 0, h->stream, h->st, count,
                        (const uint32_t*)dgroup, (const uint64_t*)dfirst, (const uint64_t*)dsnap);
+    e = hipStreamSynchronize(h->stream);
+  }
+  (void)hipFree(d);
+  return e == hipSuccess ? HB_OK : HB_EDEVICE;
+}
+
+int hb_load_term_runs(hb_handle* h, uint32_t count, const uint32_t* groups, const uint32_t* n_runs,
+                      const uint64_t* runs) {
+  if (!h || (count && (!groups || !n_runs))) return HB_EINVAL;
+  if (count == 0) return HB_OK;
+  std::vector<uint64_t> off(count);
+  uint64_t tot = 0;
+  for (uint32_t i = 0; i < count; ++i) {
+    if (groups[i] >= h->G || n_runs[i] > HB_TERM_RUNS) return HB_EINVAL;
+    off[i] = tot;
+    tot += n_runs[i];
+  }
+  if (tot && !runs) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  char* d = nullptr;
+  const size_t bytes = count * (8ull + 4 + 4) + tot * 16 + 16;
+  HB_CHECK(hipMalloc(&d, bytes));
+  uint64_t* doff = reinterpret_cast<uint64_t*>(d);
+  uint64_t* druns = doff + count;
+  uint32_t* dgrp = reinterpret_cast<uint32_t*>(druns + 2 * tot);
+  uint32_t* dn = dgrp + count;
+  hipError_t e = hipMemcpyAsync(doff, off.data(), count * 8ull, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess && tot) e = hipMemcpyAsync(druns, runs, tot * 16ull, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dgrp, groups, count * 4ull, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dn, n_runs, count * 4ull, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_load_runs, dim3((count + 255) / 256), dim3(256), 0, h->stream, h->st, count,
+                       (const uint32_t*)dgrp, (const uint32_t*)dn, (const uint64_t*)doff, (const uint64_t*)druns);
     e = hipStreamSynchronize(h->stream);
   }
   (void)hipFree(d);
@@ -2149,7 +2258,7 @@ int hb_tick(hb_handle* h, uint32_t flags) {
     case 5: hipLaunchKernelGGL(k_tick<5>, dim3(grid), dim3(PART), 0, st, aa); break;
     default: hipLaunchKernelGGL(k_tick<7>, dim3(grid), dim3(PART), 0, st, aa); break;
   }
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, h->stats_shard, h->stats, h->stats_accum);
+  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, h->stats_shard, h->stats, h->stats_accum, h->fl_cnt);
   if (two) HB_CHECK(hipEventRecord(ps.applied, st));  // a later prep reusing this set waits for it
   HB_CHECK(hipGetLastError());
   ps.used = true;
@@ -2205,6 +2314,8 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   const uint32_t* bd_edesc = b->edesc;
   const uint64_t* bd_eoff = b->eoff;
   const uint64_t* bd_peoff = b->peoff;
+  const uint64_t* bd_commit = b->commit;
+  const uint64_t* bd_eterm = b->eterm;
   if (two) {
     HB_CHECK(hipEventRecord(h->in_ready, h->in_stream));
     HB_CHECK(hipStreamWaitEvent(ps_st, h->in_ready, 0));
@@ -2228,22 +2339,33 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     bd.index = h->s_index;
     bd.hint = b->hint ? h->s_hint : nullptr;
     bd.props = b->props ? h->s_props : nullptr;
-    if (sized) {  // entry descriptors are read by apply: apply stream
-      if (b->n_edesc > h->s_edesc_cap) {
-        HB_CHECK(hipStreamSynchronize(st));  // the old staging may still be read
-        if (h->s_edesc) (void)hipFree(h->s_edesc);
-        h->s_edesc = nullptr;
-        h->s_edesc_cap = 0;
-        HB_CHECK(hipMalloc(&h->s_edesc, b->n_edesc * 4));
-        h->s_edesc_cap = b->n_edesc;
-      }
-      if (b->n_edesc) HB_CHECK(hipMemcpyAsync(h->s_edesc, b->edesc, b->n_edesc * 4, hipMemcpyHostToDevice, st));
-      if (n) HB_CHECK(hipMemcpyAsync(h->s_eoff, b->eoff, n * 8, hipMemcpyHostToDevice, st));
-      if (b->props) HB_CHECK(hipMemcpyAsync(h->s_peoff, b->peoff, (size_t)h->G * 8, hipMemcpyHostToDevice, st));
-      bd_edesc = h->s_edesc;
-      bd_eoff = h->s_eoff;
-      bd_peoff = b->props ? h->s_peoff : nullptr;
+    // entry descriptors / terms, m.Commit: read by apply, so on the apply stream
+    auto grow = [&](auto** p, uint64_t* cap, uint64_t need, size_t elem) -> int {
+      if (need <= *cap) return HB_OK;
+      HB_CHECK(hipStreamSynchronize(st));  // the old staging may still be read
+      if (*p) (void)hipFree(*p);
+      *p = nullptr;
+      *cap = 0;
+      HB_CHECK(hipMalloc(reinterpret_cast<void**>(p), need * elem));
+      *cap = need;
+      return HB_OK;
+    };
+    if (sized && b->edesc && b->n_edesc) {
+      if (grow(&h->s_edesc, &h->s_edesc_cap, b->n_edesc, 4) != HB_OK) return HB_EDEVICE;
+      HB_CHECK(hipMemcpyAsync(h->s_edesc, b->edesc, b->n_edesc * 4, hipMemcpyHostToDevice, st));
     }
+    if (b->eterm && b->n_edesc) {
+      if (grow(&h->s_eterm, &h->s_eterm_cap, b->n_edesc, 8) != HB_OK) return HB_EDEVICE;
+      HB_CHECK(hipMemcpyAsync(h->s_eterm, b->eterm, b->n_edesc * 8, hipMemcpyHostToDevice, st));
+    }
+    if (b->eoff && n) HB_CHECK(hipMemcpyAsync(h->s_eoff, b->eoff, n * 8, hipMemcpyHostToDevice, st));
+    if (b->commit && n) HB_CHECK(hipMemcpyAsync(h->s_commit, b->commit, n * 8, hipMemcpyHostToDevice, st));
+    if (sized && b->props) HB_CHECK(hipMemcpyAsync(h->s_peoff, b->peoff, (size_t)h->G * 8, hipMemcpyHostToDevice, st));
+    bd_edesc = (sized && b->edesc) ? h->s_edesc : nullptr;
+    bd_eterm = b->eterm ? h->s_eterm : nullptr;
+    bd_eoff = b->eoff ? h->s_eoff : nullptr;
+    bd_commit = b->commit ? h->s_commit : nullptr;
+    bd_peoff = (sized && b->props) ? h->s_peoff : nullptr;
   }
   if (prof) HB_CHECK(hipEventRecord(ev[0], ps_st));
 
@@ -2282,6 +2404,12 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.S.edesc = bd_edesc;
   aa.S.eoff = bd_eoff;
   aa.S.peoff = bd_peoff;
+  aa.S.bcommit = bd_commit;
+  aa.S.eterm = bd_eterm;
+  aa.S.n_ent = b->n_edesc;
+  aa.S.bn = b->n;
+  aa.fl_cnt = h->fl_cnt;
+  aa.fl_list = h->fl_list;
   aa.rec = ps.rec;
   aa.key = ps.key;
   aa.bk_off = ps.bk_off;
@@ -2321,7 +2449,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     case 5: launch_apply<5>(h, aa, prof_apply ? ev : nullptr, prof); break;
     default: launch_apply<7>(h, aa, prof_apply ? ev : nullptr, prof); break;
   }
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, h->stats_shard, h->stats, h->stats_accum);
+  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, h->stats_shard, h->stats, h->stats_accum, h->fl_cnt);
   if (prof) HB_CHECK(hipEventRecord(ev[5], st));
   if (two) HB_CHECK(hipEventRecord(ps.applied, st));
   HB_CHECK(hipGetLastError());

@@ -32,6 +32,7 @@ constexpr uint32_t CHUNK = 4 * PART;         // messages staged in LDS per round
 // ---- packed group meta (u64) ------------------------------------------------
 //  [0:2) state  [2:5) n  [5:9) self slot  [9:13) lead ref  [13:17) vote ref
 //  [17:21) fault  [21] M_TL  [22] M_SM  [24:32) votes responded  [32:40) votes granted
+//  [40:44) older term runs kept  [44:47) their ring head (follower side)
 //  M_TL: tlast == last — the tlast array is then not kept (a leader's current-
 //  term run always ends at its last entry).  M_SM: the self slot's Match ==
 //  last and Next == last + 1 — its match / next arrays are then not kept (a
@@ -54,6 +55,9 @@ __host__ __device__ inline uint32_t m_vote(uint64_t m) { return (uint32_t)((m >>
 __host__ __device__ inline uint32_t m_fault(uint64_t m) { return (uint32_t)((m >> 17) & 0xF); }
 __host__ __device__ inline uint32_t m_resp(uint64_t m) { return (uint32_t)((m >> 24) & 0xFF); }
 __host__ __device__ inline uint32_t m_grant(uint64_t m) { return (uint32_t)((m >> 32) & 0xFF); }
+__host__ __device__ inline uint32_t m_trn(uint64_t m) { return (uint32_t)((m >> 40) & 0xF); }
+__host__ __device__ inline uint32_t m_trh(uint64_t m) { return (uint32_t)((m >> 44) & 0x7); }
+static_assert(HB_TERM_RUNS == 8, "term-run ring head is 3 bits");
 
 // ---- packed progress meta (u32) ----------------------------------------------
 //  [0:2) ProgressState  [2] Paused  [3:13) inflights.start  [13:24) inflights.count
@@ -97,6 +101,13 @@ struct DevState {
   const uint32_t* edesc;      // this step's entry descriptors (hb_batch.edesc / eoff / peoff)
   const uint64_t* eoff;
   const uint64_t* peoff;
+  // follower side
+  uint64_t* trs;              // [HB_TERM_RUNS][G] older term runs of the log: start index
+  uint64_t* trt;              // [HB_TERM_RUNS][G] ... and term (ring, meta holds count / head)
+  const uint64_t* bcommit;    // this step's hb_batch.commit (m.Commit of MsgApp / MsgHeartbeat)
+  const uint64_t* eterm;      // hb_batch.eterm (MsgApp entry terms)
+  uint64_t n_ent;             // hb_batch.n_edesc
+  uint64_t bn;                // hb_batch.n
 };
 
 // ---- entry sizes (finite MaxSizePerMsg) -----------------------------------------
@@ -227,6 +238,7 @@ constexpr uint32_t D_COMMIT = 1u << 2;
 constexpr uint32_t D_LAST = 1u << 3;
 constexpr uint32_t D_TRUN = 1u << 4;
 constexpr uint32_t D_ELAPSED = 1u << 5;  // reset zeroed r.elapsed
+constexpr uint32_t D_FIRST = 1u << 6;    // a restored snapshot moved firstIndex (and the snapshot index)
 constexpr uint32_t D_SLOT0 = 8;  // bit D_SLOT0 + s: slot s (match, next, pm)
 
 struct Pr {
@@ -254,7 +266,14 @@ template <> struct SlotVec<7> {
 
 // One lane = one raft group.  All state of the group is held in registers
 // between load() and store().
-template <int NMAX>
+__device__ __forceinline__ bool is_follower_type(uint32_t t) {  // the follower side of Step
+  return t == HB_MSG_APP || t == HB_MSG_HEARTBEAT || t == HB_MSG_SNAP || t == HB_MSG_VOTE;
+}
+
+// FOLLOW: the variant that also steps the follower side (MsgApp / MsgHeartbeat
+// / MsgSnap / MsgVote, raft/raft.go:585-707); the other one never sees those
+// types (its kernels hand such a group over to k_follow).
+template <int NMAX, bool FOLLOW = false>
 struct Lane {
   DevState S;
   EvSink E;
@@ -269,6 +288,7 @@ struct Lane {
   uint32_t won, lost;
   uint32_t nev;  // events emitted
   bool prog;     // match / next / pm / head hold the group's progress (loaded or reset)
+  bool voted;    // the message's HB_INFO_VOTED bit (follower side)
 
   // ---------------------------------------------------------------- meta
   __device__ __forceinline__ uint32_t n() const { return m_n(meta); }
@@ -373,6 +393,7 @@ struct Lane {
   }
 
   __device__ __forceinline__ void store() {
+    if (dirty & D_FIRST) S.first[g] = first;  // a restored snapshot
     {  // re-derive M_TL / M_SM; an array that was stale and no longer may be is written
       const uint32_t sf = self(), nn = n();
       const bool tl = tlast == last;
@@ -564,10 +585,37 @@ struct Lane {
     ev(HB_EV_APP, s, 0, x);
   }
 
+  // ---------------------------------------------------------------- term runs
+  // The log's terms as the device keeps them: the current-term run [tfirst,
+  // last] (tfirst = HB_NO_INDEX: none) plus up to HB_TERM_RUNS older runs
+  // (start, term) in a ring [slot][G], count / head in meta.
+  __device__ __forceinline__ uint64_t* trs_at(uint32_t k) const { return S.trs + (size_t)k * S.G + g; }
+  __device__ __forceinline__ uint64_t* trt_at(uint32_t k) const { return S.trt + (size_t)k * S.G + g; }
+  __device__ __forceinline__ uint32_t tr_slot(uint32_t k) const { return (m_trh(meta) + k) & (HB_TERM_RUNS - 1); }
+  __device__ __forceinline__ void set_tr(uint32_t n, uint32_t h) {
+    meta = (meta & ~(0x7Full << 40)) | ((uint64_t)(n & 0xF) << 40) | ((uint64_t)(h & 7) << 44);
+    dirty |= D_META;
+  }
+  __device__ __forceinline__ void tr_push(uint64_t start, uint64_t t) {
+    uint32_t n = m_trn(meta), h = m_trh(meta);
+    if (n > 0 && *trt_at(tr_slot(n - 1)) == t) return;  // the run goes on
+    if (n == HB_TERM_RUNS) {  // the oldest run leaves the window
+      h = (h + 1) & (HB_TERM_RUNS - 1);
+      --n;
+    }
+    const uint32_t k = (h + n) & (HB_TERM_RUNS - 1);
+    *trs_at(k) = start;
+    *trt_at(k) = t;
+    set_tr(n + 1, h);
+  }
+
   // ---------------------------------------------------------------- transitions
   // reset raft/raft.go:334-349
   __device__ __forceinline__ void reset(uint64_t t) {
     if (term != t) {
+#ifndef HB_X_NOPUSH
+      if (tfirst != HB_NO_INDEX) tr_push(tfirst, term);  // the old current-term run becomes an older run
+#endif
       term = t;
       set_vote(HB_REF_NONE);
       tfirst = HB_NO_INDEX;  // no entry carries a term newer than the old Term
@@ -592,7 +640,8 @@ struct Lane {
   }
   // becomeFollower :384-391 / becomeCandidate :393-404 / becomeLeader :406-427.
   // Returns true when the transition happened (false on a reference panic).
-  __device__ __forceinline__ bool transition(uint32_t kind, uint64_t t, uint32_t ld) {
+  // oth: HB_STATE_OTH_LEAD when ld is the stepped message's sender outside prs.
+  __device__ __forceinline__ bool transition(uint32_t kind, uint64_t t, uint32_t ld, uint32_t oth = 0) {
     if (kind == HB_STATE_CANDIDATE && state() == HB_STATE_LEADER) {
       fault(HB_FAULT_LEADER_CAMPAIGN);
       return false;
@@ -606,7 +655,7 @@ struct Lane {
     set_lead(kind == HB_STATE_LEADER ? self_ref() : (kind == HB_STATE_FOLLOWER ? ld : (uint32_t)HB_REF_NONE));
     if (kind == HB_STATE_CANDIDATE) set_vote(self_ref());
     set_state(kind);
-    if (soft() != before) ev(HB_EV_STATE, 0, 0, soft());
+    if (soft() != before || oth) ev(HB_EV_STATE, 0, oth, soft());
     return true;
   }
   // poll raft/raft.go:445-460 (votes map as responded/granted bitmasks)
@@ -618,6 +667,218 @@ struct Lane {
       set_votes(resp, grant);
     }
     return (uint32_t)__popc(grant);
+  }
+
+  // ---------------------------------------------------------------- follower side
+  // raftLog.term(i) from what the device keeps: 0 outside [first-1, last]
+  // (raft/log.go:198-203), Term in the current-term run, else the newest older
+  // run starting at or before i; *ok = false when the runs do not reach back.
+  __device__ __forceinline__ uint64_t fterm(uint64_t i, bool* ok) const {
+    if (i + 1 < first || i > last) return 0;
+    if (tfirst != HB_NO_INDEX && i >= tfirst) return term;
+    for (int k = (int)m_trn(meta) - 1; k >= 0; --k)
+      if (*trs_at(tr_slot((uint32_t)k)) <= i) return *trt_at(tr_slot((uint32_t)k));
+    *ok = false;
+    return 0;
+  }
+  __device__ __forceinline__ void resp(uint32_t to, uint32_t kind, uint64_t x) { ev(HB_EV_RESP, to, kind, x); }
+
+  // raftLog.append of the MsgApp's entries from the first conflict ci
+  // (maybeAppend raft/log.go:80-85 -> unstable.truncateAndAppend): the log is
+  // cut at ci - 1 and takes entries ci .. index + ne (terms eterm[e0 ..]).
+  __device__ __forceinline__ void follower_append(uint64_t ci, uint64_t index, uint64_t e0, uint64_t ne) {
+    if (!prog) load_progress();  // M_SM derives the self Match from last: pin it before last moves
+    uint32_t nr = m_trn(meta);
+    const uint32_t h = m_trh(meta);
+    while (nr > 0 && *trs_at(tr_slot(nr - 1)) >= ci) --nr;
+    set_tr(nr, h);
+    if (tfirst != HB_NO_INDEX && tfirst >= ci) tfirst = HB_NO_INDEX;
+    const bool sized = sz_on(S.max_msg_size);
+    uint64_t acc = 0;
+    if (sized) {
+      if (ci - 1 < S.szlo[g]) {
+        S.szlo[g] = ci - 1;
+        *szp_at(S, g, ci - 1) = 0;
+      }
+      acc = *szp_at(S, g, ci - 1);
+    }
+    const uint64_t lastnewi = index + ne;
+#pragma nounroll
+    for (uint64_t j = ci; j <= lastnewi; ++j) {
+      const uint64_t k = e0 + (j - index - 1);
+      const uint64_t t = S.eterm[k];
+      if (t == term) {
+        if (tfirst == HB_NO_INDEX) tfirst = j;
+      } else {
+        if (tfirst != HB_NO_INDEX) {  // a lower term after Term entries
+          tr_push(tfirst, term);
+          tfirst = HB_NO_INDEX;
+        }
+        tr_push(j, t);
+      }
+      if (sized) {
+        acc += ent_size(S.edesc ? S.edesc[k] : 0u, t, j);
+        *szp_at(S, g, j) = acc;
+      }
+    }
+    last = lastnewi;
+    tlast = tfirst != HB_NO_INDEX ? last : 0;
+    dirty |= D_LAST | D_TRUN;
+    if (sized && last >= HB_SIZE_WINDOW && S.szlo[g] < last - (HB_SIZE_WINDOW - 1))
+      S.szlo[g] = last - (HB_SIZE_WINDOW - 1);
+    ev(HB_EV_FOLLOW, 0, HB_FOLLOW_APPEND, arrival_x());
+  }
+
+  // handleAppendEntries raft/raft.go:651-665 + maybeAppend raft/log.go:72-88
+  __device__ __forceinline__ void handle_append(uint64_t index, uint64_t lterm, uint32_t fref) {
+    const uint64_t mcommit = S.bcommit ? S.bcommit[arrival] : 0;
+    uint64_t e0 = 0, ne = 0;
+    if (S.eoff && S.eterm) {
+      e0 = S.eoff[arrival];
+      ne = (arrival + 1 < S.bn ? S.eoff[arrival + 1] : S.n_ent) - e0;
+    }
+    if (index < committed) {  // r.Commit (== committed at a Step boundary)
+      resp(fref, HB_RESP_APP, committed);
+      return;
+    }
+    const uint64_t lastnewi = index + ne;
+    bool ok = true;
+    const uint64_t t = fterm(index, &ok);
+    if (!ok) {
+      fault(HB_FAULT_TERM_WINDOW);
+      return;
+    }
+    if (t != lterm) {  // reject; RejectHint = lastIndex (the host reads it from its log)
+      resp(fref, HB_RESP_APP | HB_RESP_REJECT, index);
+      return;
+    }
+    uint64_t ci = 0;  // findConflict raft/log.go:112-123
+#pragma nounroll
+    for (uint64_t k = 0; k < ne; ++k) {
+      const uint64_t et = fterm(index + 1 + k, &ok);
+      if (!ok) {
+        fault(HB_FAULT_TERM_WINDOW);
+        return;
+      }
+      if (et != S.eterm[e0 + k]) {
+        ci = index + 1 + k;
+        break;
+      }
+    }
+    if (ci) {
+      if (ci <= committed) {  // "entry %d conflict with committed entry" raft/log.go:79
+        fault(HB_FAULT_CONFLICT_COMMITTED);
+        return;
+      }
+      follower_append(ci, index, e0, ne);
+    }
+    commit_to(umin64(mcommit, lastnewi));
+    if (faulted()) return;
+    resp(fref, HB_RESP_APP, lastnewi);
+  }
+
+  // restore raft/raft.go:684-707 + handleSnapshot :671-682
+  __device__ __forceinline__ void handle_snapshot(uint64_t sidx, uint64_t sterm, uint32_t fref) {
+    bool restored = false;
+    if (sidx > committed) {
+      bool ok = true;
+      const uint64_t t = fterm(sidx, &ok);
+      if (!ok) {
+        fault(HB_FAULT_TERM_WINDOW);
+        return;
+      }
+      if (t == sterm) {  // matchTerm: fast-forward the commit
+        commit_to(sidx);
+        if (faulted()) return;
+      } else {  // raftLog.restore: committed = index, the log = the snapshot
+        restored = true;
+        first = sidx + 1;
+        last = sidx;
+        committed = sidx;
+        S.snap[g] = sidx;
+        dirty |= D_FIRST | D_LAST | D_COMMIT | D_TRUN;
+        set_tr(0, 0);
+        tfirst = HB_NO_INDEX;
+        tlast = 0;
+        if (sterm == term) {
+          tfirst = sidx;
+          tlast = sidx;
+        } else {
+          tr_push(sidx, sterm);
+        }
+        const uint32_t nn = n(), sf = self();
+#pragma unroll
+        for (int s = 0; s < NMAX; ++s) {  // setProgress for every peer of the ConfState
+          if ((uint32_t)s < nn) {
+            match[s] = ((uint32_t)s == sf) ? last : 0;
+            next[s] = last + 1;
+            pm[s] = pm_make(HB_PR_PROBE, 0, 0, 0);
+            dirty |= 1u << (D_SLOT0 + s);
+          }
+        }
+        prog = true;
+        if (sz_on(S.max_msg_size)) {
+          S.szlo[g] = sidx;
+          *szp_at(S, g, sidx) = 0;
+        }
+        ev(HB_EV_FOLLOW, 0, HB_FOLLOW_RESTORE, arrival_x());
+      }
+    }
+    resp(fref, HB_RESP_APP, restored ? last : committed);
+  }
+
+  // The follower-side message types after the term gate: stepLeader /
+  // stepCandidate / stepFollower (raft/raft.go:494-649); lterm = m.LogTerm
+  // (MsgApp / MsgVote) or the snapshot's term (MsgSnap).
+  __device__ __forceinline__ void follow(uint32_t type, uint32_t from, uint64_t mterm, uint64_t index,
+                                         uint64_t lterm) {
+    const uint32_t fref = from < n() ? from : (uint32_t)HB_REF_OTHER;
+    const uint32_t oth = fref == HB_REF_OTHER ? (uint32_t)HB_STATE_OTH_LEAD : 0u;
+    const uint32_t st = state();
+    if (st == HB_STATE_LEADER || (st == HB_STATE_CANDIDATE && type == HB_MSG_VOTE)) {
+      if (type == HB_MSG_VOTE) resp(fref, HB_RESP_VOTE | HB_RESP_REJECT, 0);  // :555-558, :600-602
+      return;
+    }
+    if (st == HB_STATE_CANDIDATE) {  // :591-599: becomeFollower, then handle
+      if (!transition(HB_STATE_FOLLOWER, type == HB_MSG_SNAP ? mterm : term, fref, oth)) return;
+    } else if (type == HB_MSG_VOTE) {  // stepFollower :636-648
+      const bool can = vote() == HB_REF_NONE || (from < n() ? vote() == from : voted);
+      bool grant = false;
+      if (can) {
+        bool ok = true;
+        const uint64_t lt = fterm(last, &ok);  // isUpToDate raft/log.go:235-237
+        if (!ok) {
+          fault(HB_FAULT_TERM_WINDOW);
+          return;
+        }
+        grant = lterm > lt || (lterm == lt && index >= last);
+      }
+      if (grant) {
+        dirty |= D_ELAPSED;
+        const uint64_t before = soft();
+        set_vote(fref);
+        if (soft() != before || oth) ev(HB_EV_STATE, 0, oth ? (uint32_t)HB_STATE_OTH_VOTE : 0u, soft());
+        resp(fref, HB_RESP_VOTE, 0);
+      } else {
+        resp(fref, HB_RESP_VOTE | HB_RESP_REJECT, 0);
+      }
+      return;
+    } else {  // stepFollower :625-635: r.elapsed = 0; lead = m.From (not for MsgSnap)
+      dirty |= D_ELAPSED;
+      if (type != HB_MSG_SNAP) {
+        const uint64_t before = soft();
+        set_lead(fref);
+        if (soft() != before || oth) ev(HB_EV_STATE, 0, oth, soft());
+      }
+    }
+    if (type == HB_MSG_APP) {
+      handle_append(index, lterm, fref);
+    } else if (type == HB_MSG_HEARTBEAT) {  // handleHeartbeat :666-669
+      commit_to(S.bcommit ? S.bcommit[arrival] : 0);
+      if (!faulted()) resp(fref, HB_RESP_HEARTBEAT, 0);
+    } else {
+      handle_snapshot(index, lterm, fref);
+    }
   }
 
   // ---------------------------------------------------------------- step
@@ -641,12 +902,23 @@ struct Lane {
       if (mterm > term) {
         t1 = HB_STATE_FOLLOWER;
         tt1 = mterm;
-        if (from < n()) ld1 = from;
+        if (type == HB_MSG_VOTE) ld1 = HB_REF_NONE;             // lead = None for MsgVote (:476-478)
+        else if (from < n()) ld1 = from;
         else if (type == HB_MSG_BEAT || type == HB_MSG_PROP) ld1 = self_ref();
         else ld1 = HB_REF_OTHER;
       }
     }
-    if (t1 != 0xFF) transition(t1, tt1, ld1);
+    if constexpr (FOLLOW) {  // the events up to the next marker belong to this message
+      if (is_follower_type(type)) ev(HB_EV_FOLLOW, 0, HB_FOLLOW_STEP, arrival_x());
+    }
+    if (t1 != 0xFF) transition(t1, tt1, ld1, ld1 == HB_REF_OTHER ? (uint32_t)HB_STATE_OTH_LEAD : 0u);
+    if constexpr (FOLLOW) {
+      if (is_follower_type(type)) {
+        if (!faulted()) follow(type, from, mterm, index, lasthint);
+        if (faulted()) ev(HB_EV_FAULT, 0, faulted(), arrival_x());
+        return;
+      }
+    }
     // Only a leader reads its progress without resetting it first: a candidate
     // or follower polls, and becomeCandidate / becomeLeader / becomeFollower
     // reset every Progress before a send or an append touches one.

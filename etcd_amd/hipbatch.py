@@ -54,6 +54,7 @@ def lib():
         "hb_set_inflights": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
         "hb_set_log_bounds": (C.c_int, [H, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
         "hb_load_entry_sizes": (C.c_int, [H, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
+        "hb_load_term_runs": (C.c_int, [H, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
         "hb_get_inflights": (C.c_int, [H, C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32), C.c_void_p]),
         "hb_step": (C.c_int, [H, P(abi.hb_batch), C.c_uint32]),
         "hb_load_timers": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
@@ -179,6 +180,14 @@ class Engine:
         _check("hb_load_entry_sizes", lib().hb_load_entry_sizes(self.h, len(gs), gs.ctypes.data, ns.ctypes.data,
                                                                 flat.ctypes.data))
 
+    def load_term_runs(self, runs):
+        """Follower side: {group slot: [(start index, term), ...] older term runs, oldest first}."""
+        gs = np.ascontiguousarray(sorted(runs), dtype=np.uint32)
+        ns = np.ascontiguousarray([len(runs[int(g)]) for g in gs], dtype=np.uint32)
+        flat = np.ascontiguousarray([x for g in gs for r in runs[int(g)] for x in r] or [0], dtype=np.uint64)
+        _check("hb_load_term_runs", lib().hb_load_term_runs(self.h, len(gs), gs.ctypes.data, ns.ctypes.data,
+                                                            flat.ctypes.data))
+
     def get_inflights(self, group, slot):
         out = np.zeros(self.max_inflight, dtype=np.uint64)
         s, c = C.c_uint32(), C.c_uint32()
@@ -188,7 +197,7 @@ class Engine:
 
     # ---- hot path --------------------------------------------------------------
     def step(self, group, info, term, index, hint=None, props=None, host=None, profile=False, edesc=None,
-             eoff=None, peoff=None):
+             eoff=None, peoff=None, commit=None, eterm=None):
         """Step one batch.  Arrays are numpy (host) or torch tensors (host or cuda).
         profile: False, True (every phase) or "apply" (only HB_PHASE_APPLY).
         edesc / eoff / peoff: entry descriptors (finite max_msg_size, include/hipbatch.h)."""
@@ -196,13 +205,14 @@ class Engine:
         b.n = len(group)
         b.group, b.info, b.term, b.index = _ptr(group), _ptr(info), _ptr(term), _ptr(index)
         b.hint, b.props = _ptr(hint), _ptr(props)
-        b.n_edesc = 0 if edesc is None else len(edesc)
+        b.n_edesc = len(edesc) if edesc is not None else (len(eterm) if eterm is not None else 0)
         b.edesc, b.eoff, b.peoff = _ptr(edesc), _ptr(eoff), _ptr(peoff)
+        b.commit, b.eterm = _ptr(commit), _ptr(eterm)
         if host is None:
             host = not (hasattr(group, "is_cuda") and group.is_cuda)
         prof = {True: abi.HB_STEP_PROFILE, "apply": abi.HB_STEP_PROFILE_APPLY}.get(profile, 0)
         flags = (abi.HB_STEP_HOST_PTRS if host else 0) | prof
-        self._keep = (group, info, term, index, hint, props, edesc, eoff, peoff)
+        self._keep = (group, info, term, index, hint, props, edesc, eoff, peoff, commit, eterm)
         _check("hb_step", lib().hb_step(self.h, C.byref(b), flags))
 
     # ---- timers (MultiNode.Tick) ----------------------------------------------
@@ -245,7 +255,7 @@ class Engine:
     def step_batch(self, batch, **kw):
         return self.step(batch["group"], batch["info"], batch["term"], batch["index"],
                          batch.get("hint"), batch.get("props"), edesc=batch.get("edesc"), eoff=batch.get("eoff"),
-                         peoff=batch.get("peoff"), **kw)
+                         peoff=batch.get("peoff"), commit=batch.get("commit"), eterm=batch.get("eterm"), **kw)
 
     def events(self):
         """Dense events of the last step (host copy, synchronizes)."""

@@ -244,6 +244,18 @@ def _snap_out(s):
                     Data=_bytes(s.data, s.data_len) if s.has_data else None)
 
 
+def _snap_in(snap):
+    """pb.Snapshot in C layout; returns (struct, buffers to keep alive)."""
+    nodes = (C.c_uint64 * max(1, len(snap.Nodes)))(*snap.Nodes)
+    s = hbn_snapshot(snap.Index, snap.Term, C.cast(nodes, C.POINTER(C.c_uint64)), len(snap.Nodes),
+                     snap.Data is not None, None, 0)
+    buf = None
+    if snap.Data:
+        buf = C.create_string_buffer(bytes(snap.Data), len(snap.Data))
+        s.data, s.data_len = C.cast(buf, C.c_void_p), len(snap.Data)
+    return s, (nodes, buf)
+
+
 class _EntryArray:
     """Entries in C layout (payload buffers kept alive with the array)."""
 
@@ -332,13 +344,7 @@ class MemoryStorage:
         return _snap_out(s)
 
     def ApplySnapshot(self, snap):
-        nodes = (C.c_uint64 * max(1, len(snap.Nodes)))(*snap.Nodes)
-        s = hbn_snapshot(snap.Index, snap.Term, C.cast(nodes, C.POINTER(C.c_uint64)), len(snap.Nodes),
-                         snap.Data is not None, None, 0)
-        buf = None
-        if snap.Data:
-            buf = C.create_string_buffer(bytes(snap.Data), len(snap.Data))
-            s.data, s.data_len = C.cast(buf, C.c_void_p), len(snap.Data)
+        s, keep = _snap_in(snap)
         _check("hbn_storage_apply_snapshot", lib().hbn_storage_apply_snapshot(self.p, C.byref(s)))
 
     def CreateSnapshot(self, i, nodes, data):
@@ -430,6 +436,7 @@ class MultiNode:
         cm.type, cm.reject, cm.to, cm.from_ = m.Type, int(m.Reject), m.To, m.From
         cm.term, cm.log_term, cm.index, cm.commit, cm.reject_hint = m.Term, m.LogTerm, m.Index, m.Commit, m.RejectHint
         cm.entries, cm.n_entries = ents.arr, ents.n
+        cm.snapshot, keep = _snap_in(m.Snapshot)
         _check("hbn_step", lib().hbn_step(self.p, group, C.byref(cm)))
 
     def ReportUnreachable(self, id, group):

@@ -280,6 +280,109 @@ def window_sizes(groups, runs, seed=4, max_len=64, frac_full=0.7):
     return out
 
 
+def older_runs(groups, runs, keep=A.HB_TERM_RUNS):
+    """The log term runs below each group's current-term run (term_first), the
+    newest `keep` of them: what hb_load_term_runs takes (follower side)."""
+    out = {}
+    for g in range(len(groups)):
+        tf = int(groups["term_first"][g])
+        rr = [(int(i), int(t)) for i, t in runs[g] if tf == A.HB_NO_INDEX or int(i) < tf]
+        out[g] = rr[-keep:]
+    return out
+
+
+def follower_messages(now, term_of, nmsg, seed=5, nonmember=0.05, max_ents=4):
+    """Random follower-side messages (MsgApp with entries / MsgHeartbeat /
+    MsgSnap / MsgVote) against the groups' current state `now`; term_of(g, i)
+    gives a group's log term (the oracle's).  Mostly well-formed (matching
+    LogTerms, entries continuing the log at the message's term), with stale,
+    conflicting, rejected and out-of-range cases mixed in; every entry and
+    snapshot term is one a leader could send (non-decreasing, <= the group's
+    term after the gate), so the log keeps the reference's term order.  Returns the batch
+    arrays plus commit / eterm / eoff."""
+    rng = np.random.default_rng(seed)
+    G = len(now)
+    grp, info, term, index, hint, commit, eoff, eterm = [], [], [], [], [], [], [], []
+    types = [A.HB_MSG_APP, A.HB_MSG_HEARTBEAT, A.HB_MSG_SNAP, A.HB_MSG_VOTE]
+    for _ in range(nmsg):
+        g = int(rng.integers(0, G))
+        r = now[g]
+        n = int(r["n"])
+        t = types[int(rng.choice(4, p=[0.55, 0.2, 0.05, 0.2]))]
+        slot = int(rng.integers(0, n)) if rng.random() > nonmember else A.HB_SLOT_NONE
+        voted = int(slot == A.HB_SLOT_NONE and rng.random() < 0.5)
+        gt, last, com = int(r["term"]), int(r["last_index"]), int(r["committed"])
+        u = rng.random()
+        mt = gt if u < 0.7 else (gt + 1 if u < 0.85 else (0 if u < 0.92 else max(gt - 1, 0)))
+        # the term the group has after the gate; a leader of that term never sends
+        # an entry or a snapshot of a later term, and its log's terms never decrease
+        if t == A.HB_MSG_SNAP and mt == 0:  # a candidate takes a MsgSnap's Term as its own (raft/raft.go:596-598)
+            mt = gt
+        mte = max(mt, gt, 1)
+        x = h = c = 0
+        ents = []
+        if t == A.HB_MSG_APP:
+            x = max(0, last + int(rng.integers(-3, 2)))
+            h = term_of(g, x) if rng.random() < 0.8 else int(rng.integers(0, gt + 2))
+            if x > 0 and h == 0:  # LogTerm 0 names index 0 only: a leader holds the entry it sends after
+                h = int(rng.integers(1, gt + 2))
+            k = int(rng.integers(0, max_ents + 1))
+            et = min(max(h, 1), mte)
+            for _j in range(k):
+                if rng.random() < 0.3:
+                    et = min(et + 1, mte)
+                ents.append(et)
+            c = max(0, com + int(rng.integers(-2, 6)))
+        elif t == A.HB_MSG_HEARTBEAT:
+            c = max(0, com + int(rng.integers(-1, 3)))
+        elif t == A.HB_MSG_SNAP:
+            x = max(0, com + int(rng.integers(-2, 20)))
+            h = term_of(g, x) if rng.random() < 0.3 else int(rng.integers(1, mte + 1))
+        else:
+            x = max(0, last + int(rng.integers(-2, 3)))
+            h = max(0, term_of(g, last) + int(rng.integers(-1, 2)))
+        grp.append(g)
+        info.append(t | (slot << 4) | (voted << 9))
+        term.append(mt)
+        index.append(x)
+        hint.append(h)
+        commit.append(c)
+        eoff.append(len(eterm))
+        eterm.extend(ents)
+    return dict(group=np.array(grp, np.uint32), info=np.array(info, np.uint32), term=np.array(term, np.uint64),
+                index=np.array(index, np.uint64), hint=np.array(hint, np.uint64), commit=np.array(commit, np.uint64),
+                eoff=np.array(eoff, np.uint64), eterm=np.array(eterm or [0], np.uint64)[:len(eterm)], props=None)
+
+
+def merge_batches(a, b, seed=6):
+    """Interleave two batches (arrival order within each kept), re-basing b's
+    entry offsets; a must carry no entries of its own."""
+    rng = np.random.default_rng(seed)
+    na, nb = len(a["group"]), len(b["group"])
+    pick = np.zeros(na + nb, bool)
+    pick[rng.choice(na + nb, nb, replace=False)] = True  # True: from b
+    out = {}
+    for k in ("group", "info", "term", "index"):
+        v = np.empty(na + nb, a[k].dtype)
+        v[~pick], v[pick] = a[k], b[k]
+        out[k] = v
+    for k, dt in (("hint", np.uint64), ("commit", np.uint64)):
+        v = np.zeros(na + nb, dt)
+        if a.get(k) is not None:
+            v[~pick] = a[k]
+        if b.get(k) is not None:
+            v[pick] = b[k]
+        out[k] = v
+    # message i's entries: eoff[i] .. eoff[i+1]; a's messages carry none
+    cnt_b = np.diff(np.append(b["eoff"], len(b["eterm"]))).astype(np.uint64)
+    cnt = np.zeros(na + nb, np.uint64)
+    cnt[pick] = cnt_b
+    out["eoff"] = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint64)
+    out["eterm"] = b["eterm"]
+    out["props"] = a.get("props")
+    return out
+
+
 def random_timers(G, seed=1, et_hi=12, ht_hi=4, pos_hi=50):
     """Per-group timers for tick parity: ElectionTick 1..et_hi, HeartbeatTick
     1..ht_hi, elapsed anywhere in [0, 2 ElectionTick], rand positions spread."""

@@ -41,9 +41,8 @@ extern "C" {
 #define HBN_EEXIST         -11  /* CreateGroup for an id that exists                        */
 #define HBN_EAGAIN         -12  /* Ready: nothing to report, or the last Ready is not
                                    advanced yet (the reference's readyc is nil then)        */
-#define HBN_EUNSUPPORTED   -13  /* follower-side receipt (MsgApp / MsgHeartbeat / MsgVote /
-                                   MsgSnap), SURVEY.md 8(f) rank 4, or a group whose prs is
-                                   empty receiving a message the device would have to step  */
+#define HBN_EUNSUPPORTED   -13  /* a group whose prs is empty receiving a message the device
+                                   would have to step (MsgHup, MsgProp, MsgApp, MsgVote ...) */
 #define HBN_EPANIC         -14  /* the reference panics here; see hbn_last_error()          */
 /* MemoryStorage errors (raft/storage.go:25-31) */
 #define HBN_ECOMPACTED     -20  /* ErrCompacted */
@@ -185,7 +184,10 @@ int hbn_propose(hbn_node* n, uint64_t group, const uint8_t* data, uint64_t len);
 int hbn_propose_conf_change(hbn_node* n, uint64_t group, uint64_t cc_id, uint32_t cc_type, uint64_t node_id,
                             const uint8_t* cc_context, uint64_t context_len);
 /* Step (:431-439): local types are ignored, MsgProp goes the Propose way,
- * responses and reports go to the device batch. */
+ * responses, reports and the follower side (MsgApp with its entries, whose
+ * Index must run m.index+1, +2, ...; MsgHeartbeat; MsgSnap with its snapshot;
+ * MsgVote) go to the device batch.  A MsgSnap whose ConfState differs from the
+ * group's peers ends the batch (the restore reloads the group's prs). */
 int hbn_step(hbn_node* n, uint64_t group, const hbn_message* m);
 int hbn_report_unreachable(hbn_node* n, uint64_t id, uint64_t group);           /* :461-469 */
 int hbn_report_snapshot(hbn_node* n, uint64_t id, uint64_t group, int failure); /* :471-481 */

@@ -49,6 +49,7 @@ extern "C" {
 #define HB_NO_LIMIT       UINT64_MAX  /* raft noLimit (raft/raft.go:30)                */
 #define HB_NO_INDEX       UINT64_MAX
 #define HB_SIZE_WINDOW    1024   /* entries whose sizes the device keeps per group (finite MaxSizePerMsg) */
+#define HB_TERM_RUNS      8      /* older log term runs the device keeps per group (follower side) */
 
 /* ---- raft enums (values equal the reference's) --------------------------- */
 /* StateType raft/raft.go:35-39 */
@@ -87,15 +88,26 @@ extern "C" {
  * them on recvc/propc.  Only the relative order of messages of the same group
  * is significant (groups are independent, raft/multinode.go:125-131).
  *
- * info[i] = type | from_slot << 4 | reject << 8
+ * info[i] = type | from_slot << 4 | reject << 8 | voted << 9
  *   type      : HB_MSG_* of m.Type.  Device types: HUP, BEAT, PROP, APP_RESP,
- *               VOTE_RESP, HEARTBEAT_RESP, UNREACHABLE, SNAP_STATUS.
+ *               VOTE_RESP, HEARTBEAT_RESP, UNREACHABLE, SNAP_STATUS and the
+ *               follower side: APP, HEARTBEAT, SNAP, VOTE.
  *   from_slot : slot of m.From in the group's prs, HB_SLOT_NONE if absent.
  *   reject    : m.Reject.
+ *   voted     : only for from_slot == HB_SLOT_NONE: m.From is the node the
+ *               group voted for (its Vote is HB_REF_OTHER), read by MsgVote's
+ *               `r.Vote == m.From` (raft/raft.go:641).
  * term[i]  = m.Term (0 = local message, no term gate, raft/raft.go:471-472)
- * index[i] = m.Index; for HB_MSG_PROP the number of entries (>0).
- * hint[i]  = m.RejectHint; read only for rejected MsgAppResp (may be NULL when
- *            the batch holds none).
+ * index[i] = m.Index; for HB_MSG_PROP the number of entries (>0); for
+ *            HB_MSG_SNAP the snapshot's Metadata.Index.
+ * hint[i]  = m.RejectHint of a rejected MsgAppResp; m.LogTerm of MsgApp /
+ *            MsgVote; the snapshot's Metadata.Term of MsgSnap (may be NULL
+ *            when the batch holds none of these).
+ * commit[i]= m.Commit of MsgApp / MsgHeartbeat (may be NULL when it holds none).
+ * MsgApp entries: message i's entries are k = eoff[i]..eoff[i+1] (the last
+ *            message's run ends at n_edesc); eterm[k] = their terms (Index =
+ *            m.Index + 1 + position), edesc[k] their descriptors (finite
+ *            max_msg_size).
  * props    = optional dense [capacity] entry counts: group g first steps one
  *            MsgProp carrying props[g] entries (if > 0), before its messages
  *            in this batch.  NULL = none.
@@ -113,6 +125,7 @@ extern "C" {
  */
 #define HB_INFO(type, from_slot, reject) \
   ((uint32_t)(type) | ((uint32_t)(from_slot) << 4) | ((uint32_t)((reject) ? 1 : 0) << 8))
+#define HB_INFO_VOTED     0x200u
 #define HB_ENT_MAX_DATA   0x3FFFFFFF
 #define HB_ENT_DESC(data_len, type, has_data) \
   ((uint32_t)(data_len) | ((uint32_t)(type) << 30) | ((uint32_t)((has_data) ? 1 : 0) << 31))
@@ -125,10 +138,12 @@ typedef struct hb_batch {
   const uint64_t* index;
   const uint64_t* hint;
   const uint32_t* props;
-  uint64_t        n_edesc;
+  uint64_t        n_edesc;   /* entries described by edesc / eterm */
   const uint32_t* edesc;
   const uint64_t* eoff;
   const uint64_t* peoff;
+  const uint64_t* commit;
+  const uint64_t* eterm;
 } hb_batch;
 
 /* hb_step flags */
@@ -197,6 +212,10 @@ typedef struct hb_group {
 #define HB_FAULT_SIZE_WINDOW    10  /* engine-defined, no reference panic: with a finite
                                        max_msg_size, sendAppend needed the size of an entry
                                        older than the device's HB_SIZE_WINDOW - 1 latest */
+#define HB_FAULT_TERM_WINDOW    11  /* engine-defined, no reference panic: the follower side
+                                       needed the term of an entry older than the device's
+                                       HB_TERM_RUNS older term runs (hb_load_term_runs) */
+#define HB_FAULT_CONFLICT_COMMITTED 12  /* "entry %d conflict with committed entry" raft/log.go:79 */
 
 /* ---- events (the sparse delta list) ---------------------------------------
  * One ordered stream of 16-byte records per group describes everything the
@@ -207,7 +226,13 @@ typedef struct hb_group {
  * point the reference changes the value.
  *
  *   HB_EV_TERM      x = new Term                   (raft.reset, raft/raft.go:334-338)
- *   HB_EV_STATE     x = state | lead<<8 | vote<<16 (becomeFollower/Candidate/Leader)
+ *   HB_EV_STATE     x = state | lead<<8 | vote<<16 (becomeFollower/Candidate/Leader,
+ *                   and the follower side's r.lead / r.Vote = m.From); aux =
+ *                   HB_STATE_OTH_LEAD / _VOTE when that lead / vote was just
+ *                   set to the sender of the message being stepped and the
+ *                   sender is outside prs (ref HB_REF_OTHER: its id is that
+ *                   message's m.From); such an event is emitted even when the
+ *                   packed refs did not change
  *   HB_EV_COMMIT    x = new committed              (raftLog.commitTo, raft/log.go:172-180)
  *   HB_EV_LAST      x = new lastIndex, aux = 1 for the becomeLeader noop entry,
  *                   0 for proposal entries        (raft.appendEntry, raft/raft.go:351-360)
@@ -225,10 +250,28 @@ typedef struct hb_group {
  *   HB_EV_PROP_DROP x = arrival index (HB_NO_INDEX for props[]): proposal dropped
  *                   (raft/raft.go:587-589, 619-621)
  *   HB_EV_FAULT     aux = HB_FAULT_*, x = arrival index of the message
+ *   HB_EV_RESP      a response the follower side sends to `to` (m.From of the
+ *                   message being stepped: slot, or HB_REF_OTHER for a sender
+ *                   outside prs): aux = HB_RESP_APP (MsgAppResp, x = m.Index),
+ *                   HB_RESP_HEARTBEAT (MsgHeartbeatResp), HB_RESP_VOTE
+ *                   (MsgVoteResp), | HB_RESP_REJECT; a rejecting MsgAppResp's
+ *                   RejectHint is lastIndex at that point (raft/raft.go:651-682)
+ *   HB_EV_FOLLOW    aux = HB_FOLLOW_STEP: the follower-side message at arrival
+ *                   x (MsgApp / MsgHeartbeat / MsgSnap / MsgVote) is stepped
+ *                   (it is not of a lower term; emitted before the term gate's
+ *                   becomeFollower): the events up to the next one belong to it.
+ *                   aux = HB_FOLLOW_APPEND: raftLog.maybeAppend appended that
+ *                   MsgApp's entries from its first conflict (raft/log.go:72-88).
+ *                   aux = HB_FOLLOW_RESTORE: that MsgSnap's snapshot was
+ *                   restored (raft/raft.go:684-707): log = the snapshot, every
+ *                   peer slot's Progress reset; a caller whose snapshot
+ *                   ConfState differs from the group's peers reloads the group.
  */
 #define HB_EV_TERM      1
 #define HB_EV_STATE     2
 #define HB_EV_COMMIT    3
+#define HB_STATE_OTH_LEAD  1
+#define HB_STATE_OTH_VOTE  2
 #define HB_EV_LAST      4
 #define HB_EV_APP       5
 #define HB_EV_SNAP      6
@@ -237,6 +280,15 @@ typedef struct hb_group {
 #define HB_EV_PROP_FWD  9
 #define HB_EV_PROP_DROP 10
 #define HB_EV_FAULT     11
+#define HB_EV_RESP      13
+#define HB_EV_FOLLOW    14
+#define HB_RESP_APP        0
+#define HB_RESP_HEARTBEAT  1
+#define HB_RESP_VOTE       2
+#define HB_RESP_REJECT     8
+#define HB_FOLLOW_STEP     0
+#define HB_FOLLOW_APPEND   1
+#define HB_FOLLOW_RESTORE  2
 
 typedef struct hb_event {
   uint64_t x;
@@ -325,6 +377,16 @@ int  hb_set_log_bounds(hb_handle* h, uint32_t count, const uint32_t* groups,
  * served); a send that needs an older entry faults HB_FAULT_SIZE_WINDOW. */
 int  hb_load_entry_sizes(hb_handle* h, uint32_t count, const uint32_t* groups,
                          const uint32_t* n_sizes, const uint32_t* sizes);
+/* Follower side: the terms of a loaded group's log below its current-term run
+ * (term_first), which raftLog.term() lookups of MsgApp / MsgVote / MsgSnap
+ * need (matchTerm, findConflict, isUpToDate; raft/log.go:72-123, 249-251).
+ * groups[i] takes n_runs[i] <= HB_TERM_RUNS runs (start index, term), oldest
+ * first, the pairs of all groups concatenated in `runs` (host arrays): run k
+ * covers [start_k, start_k+1) and the last one reaches term_first - 1 (or
+ * last_index when term_first = HB_NO_INDEX).  hb_load_groups leaves a group
+ * with none: a lookup below term_first then faults HB_FAULT_TERM_WINDOW. */
+int  hb_load_term_runs(hb_handle* h, uint32_t count, const uint32_t* groups,
+                       const uint32_t* n_runs, const uint64_t* runs);
 /* Inflight window of (group, slot): buffer[(start + i) % max_inflight] = vals[i]. */
 int  hb_set_inflights(hb_handle* h, uint32_t group, uint32_t slot,
                       uint32_t start, uint32_t count, const uint64_t* vals);

@@ -52,7 +52,8 @@ class orc_msg(C.Structure):
     _fields_ = [("Type", C.c_int), ("To", C.c_uint64), ("From", C.c_uint64), ("Term", C.c_uint64),
                 ("LogTerm", C.c_uint64), ("Index", C.c_uint64), ("Commit", C.c_uint64),
                 ("Reject", C.c_int), ("RejectHint", C.c_uint64), ("nents", C.c_uint64),
-                ("ent_lo", C.c_uint64), ("snap_index", C.c_uint64), ("edesc", C.c_void_p)]
+                ("ent_lo", C.c_uint64), ("snap_index", C.c_uint64), ("edesc", C.c_void_p), ("eterm", C.c_void_p),
+                ("snap_term", C.c_uint64), ("outsider", C.c_int), ("voted", C.c_int)]
 
     def __repr__(self):
         return (f"Msg(type={self.Type}, to={self.To}, from={self.From}, term={self.Term}, "
@@ -107,6 +108,8 @@ class orc_raft(C.Structure):
         ("arrival", C.c_uint64), ("fault", C.c_int), ("n_won", C.c_uint64), ("n_lost", C.c_uint64),
         ("szc", C.c_void_p), ("szc_base", C.c_uint64), ("szc_n", C.c_uint64), ("szc_cap", C.c_uint64),
         ("sz_lo", C.c_uint64),
+        ("tw_start", C.c_uint64 * abi.HB_TERM_RUNS), ("tw_term", C.c_uint64 * abi.HB_TERM_RUNS), ("tw_n", C.c_int),
+        ("tw_tfirst", C.c_uint64),
     ]
 
 
@@ -184,6 +187,14 @@ def lib():
             "orc_entry_size": (C.c_uint64, [C.c_uint32, C.c_uint64, C.c_uint64]),
             "orc_limit_size": (C.c_uint64, [P(C.c_uint64), C.c_uint64, C.c_uint64]),
             "orc_raft_load_sizes": (C.c_int, [R, C.c_uint32, P(C.c_uint32)]),
+            "orc_raft_load_term_runs": (C.c_int, [R, C.c_uint32, P(C.c_uint64)]),
+            "orc_log_find_conflict": (C.c_uint64, [P(orc_log), C.c_uint64, P(C.c_uint64), C.c_uint64]),
+            "orc_log_is_up_to_date": (C.c_int, [P(orc_log), C.c_uint64, C.c_uint64]),
+            "orc_log_truncate": (None, [P(orc_log), C.c_uint64]),
+            "orc_log_maybe_append": (C.c_int, [P(orc_log), C.c_uint64, C.c_uint64, C.c_uint64, P(C.c_uint64),
+                                               C.c_uint64, P(C.c_uint64)]),
+            "orc_raft_handle_append_entries": (None, [R, P(orc_msg)]),
+            "orc_raft_handle_heartbeat": (None, [R, P(orc_msg)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -263,10 +274,23 @@ class Progress:
         return bool(lib().orc_pr_is_paused(C.byref(self.p)))
 
 
-def Msg(Type, From=0, To=0, Term=0, Index=0, LogTerm=0, Commit=0, Reject=False, RejectHint=0, Entries=0):
+def Msg(Type, From=0, To=0, Term=0, Index=0, LogTerm=0, Commit=0, Reject=False, RejectHint=0, Entries=0,
+        Snapshot=None):
+    """pb.Message for the oracle.  Entries: a count (MsgProp) or a list of
+    (index, term) pairs (MsgApp; indices must follow Index); Snapshot: (index, term)."""
     m = orc_msg()
     m.Type, m.From, m.To, m.Term, m.Index = Type, From, To, Term, Index
-    m.LogTerm, m.Commit, m.Reject, m.RejectHint, m.nents = LogTerm, Commit, int(Reject), RejectHint, Entries
+    m.LogTerm, m.Commit, m.Reject, m.RejectHint = LogTerm, Commit, int(Reject), RejectHint
+    if isinstance(Entries, (list, tuple)):
+        for k, (i, _) in enumerate(Entries):
+            assert i == Index + 1 + k, "entries must follow Index"
+        m._terms = (C.c_uint64 * max(1, len(Entries)))(*[t for _, t in Entries])  # kept alive with m
+        m.eterm = C.cast(m._terms, C.c_void_p)
+        m.nents = len(Entries)
+    else:
+        m.nents = Entries
+    if Snapshot is not None:
+        m.snap_index, m.snap_term = Snapshot
     return m
 
 
@@ -363,6 +387,17 @@ class Raft:
         return lib().orc_log_term(C.byref(self.r.log), i)
 
     # -- methods -----------------------------------------------------------
+    def handleAppendEntries(self, m):
+        lib().orc_raft_handle_append_entries(C.byref(self.r), C.byref(m))
+
+    def handleHeartbeat(self, m):
+        lib().orc_raft_handle_heartbeat(C.byref(self.r), C.byref(m))
+
+    def entries(self):
+        """(index, term) of every entry in [firstIndex, lastIndex] (allEntries)."""
+        lo = self.r.log.first_index
+        return [(i, self.term(i)) for i in range(lo, self.r.log.last_index + 1)]
+
     def Step(self, m):
         lib().orc_raft_step(C.byref(self.r), C.byref(m))
 
@@ -475,7 +510,8 @@ class OracleGroups:
         keep = {}
         for k, dt in (("group", np.uint32), ("info", np.uint32), ("term", np.uint64),
                       ("index", np.uint64), ("hint", np.uint64), ("props", np.uint32),
-                      ("edesc", np.uint32), ("eoff", np.uint64), ("peoff", np.uint64)):
+                      ("edesc", np.uint32), ("eoff", np.uint64), ("peoff", np.uint64), ("commit", np.uint64),
+                      ("eterm", np.uint64)):
             a = batch_arrays.get(k)
             if a is None:
                 setattr(b, k, None)
@@ -484,7 +520,7 @@ class OracleGroups:
             keep[k] = a
             setattr(b, k, a.ctypes.data)
         b.n = n
-        b.n_edesc = len(keep["edesc"]) if "edesc" in keep else 0
+        b.n_edesc = len(keep["edesc"]) if "edesc" in keep else (len(keep["eterm"]) if "eterm" in keep else 0)
         if ev_cap is None:
             ev_cap = (n + self.G) * (abi.HB_MAX_REPLICAS + 6) + 64
         if getattr(self, "_ev", None) is None or len(self._ev) < ev_cap:
@@ -535,6 +571,19 @@ class OracleGroups:
             rc = L.orc_raft_load_sizes(L.orc_groups_at(self.ptr, g), len(a), a.ctypes.data_as(C.POINTER(C.c_uint32)))
             if rc != 0:
                 raise ValueError(f"orc_raft_load_sizes(group {g}) failed")
+
+    def load_term_runs(self, runs):
+        """Follower side: {group: [(start, term), ...] older term runs} (hb_load_term_runs)."""
+        L = lib()
+        for g, rr in runs.items():
+            a = (C.c_uint64 * max(1, 2 * len(rr)))(*[x for r in rr for x in r])
+            if L.orc_raft_load_term_runs(L.orc_groups_at(self.ptr, g), len(rr), a) != 0:
+                raise ValueError(f"orc_raft_load_term_runs(group {g}) failed")
+
+    def term(self, g, i):
+        """raftLog.term(i) of group g (the oracle's whole log)."""
+        L = lib()
+        return L.orc_log_term(C.byref(L.orc_groups_at(self.ptr, g).contents.log), i)
 
     def inflights(self, g, slot):
         L = lib()

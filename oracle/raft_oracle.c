@@ -183,10 +183,28 @@ uint64_t orc_log_last_term(const orc_log* l) {            /* lastTerm raft/log.g
   return orc_log_term(l, l->last_index);
 }
 
+void orc_log_truncate(orc_log* l, uint64_t after) {      /* unstable.truncateAndAppend's cut */
+  while (l->nruns > 1 && l->runs[l->nruns - 1].index > after) l->nruns--;
+  l->last_index = after;
+}
+
+uint64_t orc_log_find_conflict(const orc_log* l, uint64_t from, const uint64_t* terms, uint64_t n) {
+  /* findConflict raft/log.go:112-123: first entry whose term does not match */
+  for (uint64_t k = 0; k < n; k++)
+    if (orc_log_term(l, from + k) != terms[k]) return from + k;
+  return 0;
+}
+
+int orc_log_is_up_to_date(const orc_log* l, uint64_t lasti, uint64_t term) {  /* :235-237 */
+  uint64_t lt = orc_log_last_term(l);
+  return term > lt || (term == lt && lasti >= l->last_index);
+}
+
 /* ========================================================================
  * raft — raft/raft.go
  * ======================================================================== */
 static void fault(orc_raft* r, int code);
+static void tw_push(orc_raft* r, uint64_t start, uint64_t term);
 
 static void emit(orc_raft* r, int type, int to, uint64_t x, int aux) {
   if (r->ev) {
@@ -255,6 +273,8 @@ void orc_raft_init(orc_raft* r, uint64_t id, const uint64_t* peers, int npeers,
     r->n++;
   }
   r->state = HB_STATE_FOLLOWER;
+  r->tw_tfirst = HB_NO_INDEX;                             /* KAT rafts: the engine would know every run */
+  for (int k = 0; k < r->log.nruns; k++) tw_push(r, r->log.runs[k].index, r->log.runs[k].term);
   orc_raft_become_follower(r, r->term, ORC_NONE);         /* :199 */
 }
 
@@ -309,7 +329,10 @@ static void send(orc_raft* r, orc_msg m) {                /* send raft/raft.go:2
     case HB_MSG_HEARTBEAT: emit(r, HB_EV_HEARTBEAT, to, m.commit, 0); break;
     case HB_MSG_VOTE: emit(r, HB_EV_VOTE, to, m.index, 0); break;
     case HB_MSG_PROP: emit(r, HB_EV_PROP_FWD, to, r->arrival, 0); break;
-    default: break;  /* MsgVoteResp etc.: off the engine's path */
+    case HB_MSG_APP_RESP: emit(r, HB_EV_RESP, to, m.index, HB_RESP_APP | (m.reject ? HB_RESP_REJECT : 0)); break;
+    case HB_MSG_HEARTBEAT_RESP: emit(r, HB_EV_RESP, to, 0, HB_RESP_HEARTBEAT); break;
+    case HB_MSG_VOTE_RESP: emit(r, HB_EV_RESP, to, 0, HB_RESP_VOTE | (m.reject ? HB_RESP_REJECT : 0)); break;
+    default: break;
   }
 }
 
@@ -330,6 +353,59 @@ void orc_raft_commit_to(orc_raft* r, uint64_t tocommit) { /* commitTo raft/log.g
     r->log.committed = tocommit;
     emit(r, HB_EV_COMMIT, 0, tocommit, 0);
   }
+}
+
+/* ---- the engine's term window (follower side) ---- */
+static void tw_push(orc_raft* r, uint64_t start, uint64_t term) {
+  if (r->tw_n > 0 && r->tw_term[r->tw_n - 1] == term) return;  /* the run goes on */
+  if (r->tw_n == HB_TERM_RUNS) {                          /* the oldest run leaves the window */
+    for (int k = 1; k < HB_TERM_RUNS; k++) {
+      r->tw_start[k - 1] = r->tw_start[k];
+      r->tw_term[k - 1] = r->tw_term[k];
+    }
+    r->tw_n--;
+  }
+  r->tw_start[r->tw_n] = start;
+  r->tw_term[r->tw_n] = term;
+  r->tw_n++;
+}
+
+static void tw_term_change(orc_raft* r, uint64_t old_term) {  /* reset to a new Term */
+  if (r->tw_tfirst != HB_NO_INDEX) tw_push(r, r->tw_tfirst, old_term);
+  r->tw_tfirst = HB_NO_INDEX;
+}
+
+static void tw_leader_append(orc_raft* r, uint64_t first_new) {  /* entries at Term */
+  if (r->tw_tfirst == HB_NO_INDEX) r->tw_tfirst = first_new;
+}
+
+/* the engine knows term(i) for every i >= this in [first-1, last] */
+static uint64_t tw_known_lo(const orc_raft* r) {
+  if (r->tw_n > 0) return r->tw_start[0];
+  if (r->tw_tfirst != HB_NO_INDEX) return r->tw_tfirst;
+  return r->log.last_index + 1;
+}
+
+/* raftLog.term(i) on the follower side; sets the engine-defined fault when
+ * the engine could not answer (returns 0 then) */
+static uint64_t f_term(orc_raft* r, uint64_t i) {
+  if (i + 1 < r->log.first_index || i > r->log.last_index) return 0;
+  if (i < tw_known_lo(r)) {
+    fault(r, HB_FAULT_TERM_WINDOW);
+    return 0;
+  }
+  return orc_log_term(&r->log, i);
+}
+
+int orc_raft_load_term_runs(orc_raft* r, uint32_t n, const uint64_t* runs) {
+  if (n > HB_TERM_RUNS) return -1;
+  r->tw_n = 0;
+  for (uint32_t k = 0; k < n; k++) {
+    r->tw_start[r->tw_n] = runs[2 * k];
+    r->tw_term[r->tw_n] = runs[2 * k + 1];
+    r->tw_n++;
+  }
+  return 0;
 }
 
 /* ---- entry sizes (finite MaxSizePerMsg) ---- */
@@ -507,6 +583,7 @@ int orc_raft_maybe_commit(orc_raft* r) {                  /* maybeCommit raft/ra
 
 void orc_raft_reset(orc_raft* r, uint64_t term) {         /* reset raft/raft.go:334-349 */
   if (r->term != term) {
+    tw_term_change(r, r->term);
     r->term = term;
     r->vote = ORC_NONE;
     emit(r, HB_EV_TERM, 0, term, 0);
@@ -528,6 +605,7 @@ void orc_raft_reset(orc_raft* r, uint64_t term) {         /* reset raft/raft.go:
 static void append_entries(orc_raft* r, uint64_t k, int noop, const uint32_t* desc) {  /* appendEntry raft/raft.go:351-360 */
   /* entries get Term = r.Term, Index = li+1..; raftLog.append (raft/log.go:90-99) */
   szc_append(r, r->log.last_index, k, noop ? NULL : desc);
+  if (k) tw_leader_append(r, r->log.last_index + 1);
   orc_log_push(&r->log, r->term, k);
   emit(r, HB_EV_LAST, 0, r->log.last_index, noop);
   orc_progress* self = orc_raft_pr(r, r->id);
@@ -538,17 +616,20 @@ static void append_entries(orc_raft* r, uint64_t k, int noop, const uint32_t* de
 
 void orc_raft_append_entry(orc_raft* r, uint64_t k, int noop) { append_entries(r, k, noop, NULL); }
 
-static void emit_state_if_changed(orc_raft* r, uint64_t before) {
+/* oth: HB_STATE_OTH_* of the fields just set to a batch sender outside prs
+ * (the event names the assignment even when the packed refs did not change) */
+static void emit_state_oth(orc_raft* r, uint64_t before, uint32_t oth) {
   uint64_t now = soft_pack(r);
-  if (now != before) emit(r, HB_EV_STATE, 0, now, 0);
+  if (now != before || oth) emit(r, HB_EV_STATE, 0, now, oth);
 }
+static void emit_state_if_changed(orc_raft* r, uint64_t before) { emit_state_oth(r, before, 0); }
 
 void orc_raft_become_follower(orc_raft* r, uint64_t term, uint64_t lead) {  /* :384-391 */
   uint64_t before = soft_pack(r);
   orc_raft_reset(r, term);
   r->lead = lead;
   r->state = HB_STATE_FOLLOWER;
-  emit_state_if_changed(r, before);
+  emit_state_oth(r, before, lead == ORC_OUTSIDER ? HB_STATE_OTH_LEAD : 0);
 }
 
 void orc_raft_become_candidate(orc_raft* r) {             /* :393-404 */
@@ -605,6 +686,174 @@ void orc_raft_campaign(orc_raft* r) {                     /* campaign raft/raft.
     m.log_term = orc_log_last_term(&r->log);
     send(r, m);
   }
+}
+
+/* ======================================================================
+ * follower side — raft/raft.go:616-707, raft/log.go:72-123
+ * ====================================================================== */
+
+/* maybeAppend's raftLog.append of ents[ci-offset:] (raft/log.go:80-85, 90-98) */
+static void follower_append(orc_raft* r, const orc_msg* m, uint64_t ci) {
+  const uint64_t off = m->index + 1;
+  orc_log_truncate(&r->log, ci - 1);                      /* unstable.truncateAndAppend */
+  /* the engine's term window: runs from ci on are gone */
+  while (r->tw_n > 0 && r->tw_start[r->tw_n - 1] >= ci) r->tw_n--;
+  if (r->tw_tfirst != HB_NO_INDEX && r->tw_tfirst >= ci) r->tw_tfirst = HB_NO_INDEX;
+  if (sized(r)) {                                         /* and its entry sizes */
+    if (r->szc_n == 0 || ci - 1 < r->sz_lo) szc_reset(r, ci - 1);
+    else r->szc_n = ci - r->szc_base;
+  }
+  for (uint64_t j = ci; j < off + m->nents; j++) {
+    const uint64_t t = m->eterm[j - off];
+    if (t == r->term) {
+      if (r->tw_tfirst == HB_NO_INDEX) r->tw_tfirst = j;
+    } else {
+      if (r->tw_tfirst != HB_NO_INDEX) {                  /* a lower term after Term entries */
+        tw_push(r, r->tw_tfirst, r->term);
+        r->tw_tfirst = HB_NO_INDEX;
+      }
+      tw_push(r, j, t);
+    }
+    if (sized(r)) {
+      const uint64_t acc = r->szc[r->szc_n - 1];
+      szc_push(r, acc + orc_entry_size(m->edesc ? m->edesc[j - off] : 0u, t, j));
+    }
+    orc_log_push(&r->log, t, 1);
+  }
+  if (sized(r)) {
+    const uint64_t last = r->log.last_index;
+    if (last >= HB_SIZE_WINDOW && r->sz_lo < last - (HB_SIZE_WINDOW - 1)) r->sz_lo = last - (HB_SIZE_WINDOW - 1);
+  }
+  emit(r, HB_EV_FOLLOW, 0, r->arrival, HB_FOLLOW_APPEND);
+}
+
+static void handle_append_entries(orc_raft* r, const orc_msg* m) {  /* raft/raft.go:651-665 */
+  orc_msg resp;
+  memset(&resp, 0, sizeof(resp));
+  resp.to = m->from;
+  resp.type = HB_MSG_APP_RESP;
+  if (m->index < r->commit) {
+    resp.index = r->commit;
+    send(r, resp);
+    return;
+  }
+  /* maybeAppend raft/log.go:72-88 */
+  const uint64_t lastnewi = m->index + m->nents;
+  const uint64_t t = f_term(r, m->index);                 /* matchTerm(index, logTerm) */
+  if (r->fault) return;
+  if (t == m->log_term) {
+    uint64_t ci = 0;                                      /* findConflict :112-123 */
+    for (uint64_t k = 0; k < m->nents; k++) {
+      const uint64_t et = f_term(r, m->index + 1 + k);
+      if (r->fault) return;
+      if (et != m->eterm[k]) {
+        ci = m->index + 1 + k;
+        break;
+      }
+    }
+    if (ci != 0) {
+      if (ci <= r->log.committed) {                       /* "entry %d conflict with committed entry" */
+        fault(r, HB_FAULT_CONFLICT_COMMITTED);
+        return;
+      }
+      follower_append(r, m, ci);
+    }
+    orc_raft_commit_to(r, lastnewi < m->commit ? lastnewi : m->commit);
+    if (r->fault) return;
+    resp.index = lastnewi;
+  } else {
+    resp.index = m->index;
+    resp.reject = 1;
+    resp.reject_hint = r->log.last_index;
+  }
+  send(r, resp);
+}
+
+static void handle_heartbeat(orc_raft* r, const orc_msg* m) {  /* raft/raft.go:666-669 */
+  orc_raft_commit_to(r, m->commit);
+  if (r->fault) return;
+  orc_msg resp;
+  memset(&resp, 0, sizeof(resp));
+  resp.to = m->from;
+  resp.type = HB_MSG_HEARTBEAT_RESP;
+  send(r, resp);
+}
+
+static int restore(orc_raft* r, uint64_t sindex, uint64_t sterm) {  /* raft/raft.go:684-707 */
+  if (sindex <= r->log.committed) return 0;
+  const uint64_t t = f_term(r, sindex);                   /* matchTerm */
+  if (r->fault) return 0;
+  if (t == sterm) {
+    orc_raft_commit_to(r, sindex);
+    return 0;
+  }
+  /* raftLog.restore (raft/log.go:249-253): committed = index, unstable = the snapshot */
+  const uint64_t applied = r->log.applied;
+  orc_log_free(&r->log);
+  orc_log_init(&r->log, sindex + 1, sterm);
+  r->log.applied = applied;
+  r->log.snap_index = sindex;
+  /* prs from the snapshot's ConfState: the engine resets the group's peers */
+  const uint64_t last = r->log.last_index;
+  for (int i = 0; i < r->n; i++) {
+    orc_progress* pr = &r->prs[i];
+    orc_ins_free(&pr->ins);
+    memset(pr, 0, sizeof(*pr));
+    pr->next = last + 1;
+    pr->match = r->ids[i] == r->id ? last : 0;
+    orc_ins_init(&pr->ins, r->max_inflight);
+  }
+  r->tw_n = 0;
+  r->tw_tfirst = HB_NO_INDEX;
+  if (sterm == r->term) r->tw_tfirst = sindex;
+  else tw_push(r, sindex, sterm);
+  if (sized(r)) szc_reset(r, sindex);
+  emit(r, HB_EV_FOLLOW, 0, r->arrival, HB_FOLLOW_RESTORE);
+  return 1;
+}
+
+static void handle_snapshot(orc_raft* r, const orc_msg* m) {  /* raft/raft.go:671-682 */
+  const int ok = restore(r, m->snap_index, m->snap_term);
+  if (r->fault) return;
+  orc_msg resp;
+  memset(&resp, 0, sizeof(resp));
+  resp.to = m->from;
+  resp.type = HB_MSG_APP_RESP;
+  resp.index = ok ? r->log.last_index : r->log.committed;
+  send(r, resp);
+}
+
+void orc_raft_handle_append_entries(orc_raft* r, const orc_msg* m) { handle_append_entries(r, m); }
+void orc_raft_handle_heartbeat(orc_raft* r, const orc_msg* m) { handle_heartbeat(r, m); }
+
+int orc_log_maybe_append(orc_log* l, uint64_t index, uint64_t log_term, uint64_t committed,
+                         const uint64_t* terms, uint64_t n, uint64_t* lastnewi) {
+  *lastnewi = index + n;
+  if (orc_log_term(l, index) != log_term) {              /* matchTerm */
+    *lastnewi = 0;
+    return 0;
+  }
+  const uint64_t ci = orc_log_find_conflict(l, index + 1, terms, n);
+  if (ci != 0 && ci <= l->committed) return -1;           /* Panicf: conflict with committed entry */
+  if (ci != 0) {
+    orc_log_truncate(l, ci - 1);
+    for (uint64_t j = ci; j <= index + n; j++) orc_log_push(l, terms[j - index - 1], 1);
+  }
+  const uint64_t to = committed < *lastnewi ? committed : *lastnewi;
+  if (l->committed < to) {                                /* commitTo */
+    if (l->last_index < to) return -1;
+    l->committed = to;
+  }
+  return 1;
+}
+
+static void reject_vote(orc_raft* r, const orc_msg* m) {
+  orc_msg resp;
+  memset(&resp, 0, sizeof(resp));
+  resp.to = m->from;
+  resp.type = HB_MSG_VOTE_RESP;
+  resp.reject = 1;
+  send(r, resp);
 }
 
 static void step_leader(orc_raft* r, const orc_msg* m) {  /* stepLeader raft/raft.go:494-583 */
@@ -694,6 +943,18 @@ static void step_candidate(orc_raft* r, const orc_msg* m) {  /* stepCandidate ra
       send(r, resp);
       break;
     }
+    case HB_MSG_APP:                                      /* :591-593 */
+      orc_raft_become_follower(r, r->term, m->from);
+      if (!r->fault) handle_append_entries(r, m);
+      break;
+    case HB_MSG_HEARTBEAT:                                /* :594-596 */
+      orc_raft_become_follower(r, r->term, m->from);
+      if (!r->fault) handle_heartbeat(r, m);
+      break;
+    case HB_MSG_SNAP:                                     /* :597-599 */
+      orc_raft_become_follower(r, m->term, m->from);
+      if (!r->fault) handle_snapshot(r, m);
+      break;
     case HB_MSG_VOTE_RESP: {
       int gr = orc_raft_poll(r, m->from, !m->reject);
       int q = orc_raft_q(r);
@@ -708,7 +969,7 @@ static void step_candidate(orc_raft* r, const orc_msg* m) {  /* stepCandidate ra
       break;
     }
     default:
-      break;  /* MsgApp/MsgHeartbeat/MsgSnap: follower side, off the engine's path */
+      break;
   }
 }
 
@@ -724,8 +985,52 @@ static void step_follower(orc_raft* r, const orc_msg* m) {   /* stepFollower raf
         send(r, fwd);
       }
       break;
+    case HB_MSG_APP: {                                    /* :625-628 */
+      uint64_t before = soft_pack(r);
+      r->elapsed = 0;
+      r->lead = m->from;
+      emit_state_oth(r, before, m->from == ORC_OUTSIDER ? HB_STATE_OTH_LEAD : 0);
+      handle_append_entries(r, m);
+      break;
+    }
+    case HB_MSG_HEARTBEAT: {                              /* :629-632 */
+      uint64_t before = soft_pack(r);
+      r->elapsed = 0;
+      r->lead = m->from;
+      emit_state_oth(r, before, m->from == ORC_OUTSIDER ? HB_STATE_OTH_LEAD : 0);
+      handle_heartbeat(r, m);
+      break;
+    }
+    case HB_MSG_SNAP:                                     /* :633-635 */
+      r->elapsed = 0;
+      handle_snapshot(r, m);
+      break;
+    case HB_MSG_VOTE: {                                   /* :636-648 */
+      int grant = 0;
+      /* r.Vote == m.From: for a batch sender outside prs the host says (HB_INFO_VOTED) */
+      const int same = m->outsider ? m->voted : r->vote == m->from;
+      if (r->vote == ORC_NONE || same) {
+        const uint64_t lt = f_term(r, r->log.last_index); /* isUpToDate (raft/log.go:235-237) */
+        if (r->fault) return;
+        grant = m->log_term > lt || (m->log_term == lt && m->index >= r->log.last_index);
+      }
+      if (grant) {
+        uint64_t before = soft_pack(r);
+        r->elapsed = 0;
+        r->vote = m->from;
+        emit_state_oth(r, before, m->from == ORC_OUTSIDER ? HB_STATE_OTH_VOTE : 0);
+        orc_msg resp;
+        memset(&resp, 0, sizeof(resp));
+        resp.to = m->from;
+        resp.type = HB_MSG_VOTE_RESP;
+        send(r, resp);
+      } else {
+        reject_vote(r, m);
+      }
+      break;
+    }
     default:
-      break;  /* MsgApp/MsgHeartbeat/MsgSnap/MsgVote: follower side, off the engine's path */
+      break;
   }
 }
 
@@ -736,14 +1041,13 @@ void orc_raft_step(orc_raft* r, const orc_msg* m) {       /* Step raft/raft.go:4
     r->commit = r->log.committed;
     return;
   }
-  if (m->term == 0) {
-    /* local message */
-  } else if (m->term > r->term) {
+  if (m->term != 0 && m->term < r->term) return;          /* ignore */
+  if (m->type == HB_MSG_APP || m->type == HB_MSG_HEARTBEAT || m->type == HB_MSG_SNAP || m->type == HB_MSG_VOTE)
+    emit(r, HB_EV_FOLLOW, 0, r->arrival, HB_FOLLOW_STEP);  /* the events that follow belong to it */
+  if (m->term > r->term) {                                /* (m.Term == 0: local message, no gate) */
     uint64_t lead = m->from;
     if (m->type == HB_MSG_VOTE) lead = ORC_NONE;
     orc_raft_become_follower(r, m->term, lead);
-  } else if (m->term < r->term) {
-    return;                                               /* ignore */
   }
   if (r->fault) return;
   switch (r->state) {
@@ -812,6 +1116,14 @@ int orc_raft_from_group(orc_raft* r, const hb_group* g, const orc_run* runs, int
   }
   r->fault = (int)g->fault;
   if (sized(r)) szc_reset(r, r->log.last_index);            /* hb_load_groups: no entry size yet */
+  r->tw_n = 0;                                              /* hb_load_groups: no older term run yet */
+  r->tw_tfirst = HB_NO_INDEX;
+  for (int k = 0; k < r->log.nruns; k++)                    /* the current-term run (term_first) */
+    if (r->log.runs[k].term == r->term) {
+      r->tw_tfirst = r->log.runs[k].index;
+      break;
+    }
+  if (r->tw_tfirst != HB_NO_INDEX && r->tw_tfirst > r->log.last_index) r->tw_tfirst = HB_NO_INDEX;
   return 0;
 }
 
@@ -976,6 +1288,8 @@ int orc_step_batch(orc_raft* groups, uint32_t ngroups, const hb_batch* b,
     }
     if (from_slot >= (uint32_t)r->n && (type == HB_MSG_HUP || type == HB_MSG_BEAT || type == HB_MSG_PROP))
       from = r->id;
+    else if (from_slot >= (uint32_t)r->n)                 /* a sender outside prs (its id is the host's) */
+      from = ORC_OUTSIDER;
     BIND(r);
     r->arrival = i;
     orc_msg m;
@@ -986,7 +1300,23 @@ int orc_step_batch(orc_raft* groups, uint32_t ngroups, const hb_batch* b,
     m.term = b->term[i];
     m.index = b->index[i];
     m.reject = reject;
-    m.reject_hint = (reject && b->hint) ? b->hint[i] : 0;
+    m.outsider = from_slot >= (uint32_t)r->n;
+    m.voted = (info & HB_INFO_VOTED) != 0;
+    m.reject_hint = (reject && type == HB_MSG_APP_RESP && b->hint) ? b->hint[i] : 0;
+    if (type == HB_MSG_APP || type == HB_MSG_VOTE) m.log_term = b->hint ? b->hint[i] : 0;
+    if (type == HB_MSG_APP || type == HB_MSG_HEARTBEAT) m.commit = b->commit ? b->commit[i] : 0;
+    if (type == HB_MSG_SNAP) {
+      m.snap_index = b->index[i];
+      m.snap_term = b->hint ? b->hint[i] : 0;
+      m.index = 0;
+    }
+    if (type == HB_MSG_APP && b->eoff) {                  /* entries eoff[i] .. eoff[i+1] */
+      const uint64_t e0 = b->eoff[i], e1 = i + 1 < b->n ? b->eoff[i + 1] : b->n_edesc;
+      m.nents = e1 - e0;
+      m.eterm = b->eterm ? b->eterm + e0 : NULL;
+      m.edesc = b->edesc ? b->edesc + e0 : NULL;
+      if (!m.eterm) m.nents = 0;
+    }
     if (type == HB_MSG_PROP) {
       m.nents = b->index[i];
       m.index = 0;

@@ -82,8 +82,14 @@ typedef struct orc_msg {
   uint64_t nents;       /* len(m.Entries) */
   uint64_t ent_lo;      /* index of first entry (MsgApp) */
   uint64_t snap_index;  /* MsgSnap snapshot metadata index */
-  const uint32_t* edesc;  /* MsgProp: descriptors of its nents entries (HB_ENT_DESC), or NULL */
+  const uint32_t* edesc;  /* MsgProp / MsgApp: descriptors of its nents entries (HB_ENT_DESC), or NULL */
+  const uint64_t* eterm;  /* MsgApp: terms of its nents entries (Index = index + 1 + k) */
+  uint64_t snap_term;     /* MsgSnap snapshot metadata term */
+  int outsider;           /* batch path: the sender is outside prs (from = ORC_OUTSIDER) ... */
+  int voted;              /* ... and HB_INFO_VOTED says it is the node this group voted for */
 } orc_msg;
+
+#define ORC_OUTSIDER 0xFFFFFFFFFFFFFFF0ull  /* id of a batch message's sender outside prs */
 
 typedef struct orc_raft {
   /* pb.HardState + id, raft/raft.go:125-155 */
@@ -121,6 +127,13 @@ typedef struct orc_raft {
    * bound, mirrored so the engine-defined HB_FAULT_SIZE_WINDOW is checked). */
   uint64_t* szc;
   uint64_t szc_base, szc_n, szc_cap, sz_lo;
+  /* The engine's view of the log terms on the follower side (mirrored so the
+   * engine-defined HB_FAULT_TERM_WINDOW is checked; the terms themselves come
+   * from `log`): at most HB_TERM_RUNS older runs (start, term) plus the
+   * current-term run [tw_tfirst, last_index] (HB_NO_INDEX: none). */
+  uint64_t tw_start[HB_TERM_RUNS], tw_term[HB_TERM_RUNS];
+  int tw_n;
+  uint64_t tw_tfirst;
 } orc_raft;
 
 /* ---- inflights (raft/progress.go:183-237) ---- */
@@ -178,6 +191,18 @@ void orc_raft_append_entry(orc_raft* r, uint64_t k, int noop);
 uint64_t orc_entry_size(uint32_t desc, uint64_t term, uint64_t index);
 uint64_t orc_limit_size(const uint64_t* sizes, uint64_t n, uint64_t max_size);
 int  orc_raft_load_sizes(orc_raft* r, uint32_t n, const uint32_t* sizes);
+/* follower side (raft/raft.go:616-707, raft/log.go:72-123, 235-239) */
+void orc_log_truncate(orc_log* l, uint64_t after);       /* keep entries <= after */
+uint64_t orc_log_find_conflict(const orc_log* l, uint64_t from, const uint64_t* terms, uint64_t n);
+int  orc_log_is_up_to_date(const orc_log* l, uint64_t lasti, uint64_t term);
+/* the engine's older term runs of a loaded group (hb_load_term_runs' contract) */
+int  orc_raft_load_term_runs(orc_raft* r, uint32_t n, const uint64_t* runs);
+/* raftLog.maybeAppend (raft/log.go:72-88) on a bare log: 1 appended (*lastnewi
+ * set), 0 no match, -1 the reference's "conflict with committed entry" panic */
+int  orc_log_maybe_append(orc_log* l, uint64_t index, uint64_t log_term, uint64_t committed,
+                          const uint64_t* terms, uint64_t n, uint64_t* lastnewi);
+void orc_raft_handle_append_entries(orc_raft* r, const orc_msg* m);  /* raft/raft.go:651-665 */
+void orc_raft_handle_heartbeat(orc_raft* r, const orc_msg* m);       /* raft/raft.go:666-669 */
 void orc_raft_become_follower(orc_raft* r, uint64_t term, uint64_t lead);
 void orc_raft_become_candidate(orc_raft* r);
 void orc_raft_become_leader(orc_raft* r);

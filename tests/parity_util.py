@@ -61,7 +61,7 @@ class Pair:
     """An engine and an oracle loaded with the same groups."""
 
     def __init__(self, groups, runs, nmax, W, ins=None, max_msg_size=abi.HB_NO_LIMIT, max_batch=1 << 16,
-                 sizes=None):
+                 sizes=None, term_runs=None):
         from etcd_amd.hipbatch import Engine
         self.og = OracleGroups(groups, runs, W, max_msg_size, ins)
         init = self.og.groups()  # canonical record (term run derived from the log)
@@ -73,6 +73,12 @@ class Pair:
         if sizes:  # finite max_msg_size: the latest entries' sizes on both sides
             self.og.load_sizes(sizes)
             self.eng.load_entry_sizes(sizes)
+        if term_runs:  # follower side: the older term runs on both sides (True: all the log's, newest first)
+            if term_runs is True:
+                from etcd_amd import synth
+                term_runs = synth.older_runs(init, runs)
+            self.og.load_term_runs(term_runs)
+            self.eng.load_term_runs(term_runs)
         assert_groups_equal(self.eng.get_groups(), init, "load")
 
     def set_timers(self, timers, draws):

@@ -688,3 +688,215 @@ def test_send_append_beyond_size_window_faults():
     r.setProgress(2, 0, 2)
     r.sendAppend(2)
     assert r.fault == abi.HB_FAULT_SIZE_WINDOW
+
+
+# ---------------------------------------------------------------- follower side
+APP, APPRESP, HB, HBRESP = abi.HB_MSG_APP, abi.HB_MSG_APP_RESP, abi.HB_MSG_HEARTBEAT, abi.HB_MSG_HEARTBEAT_RESP
+VOTE, VOTERESP, SNAP = abi.HB_MSG_VOTE, abi.HB_MSG_VOTE_RESP, abi.HB_MSG_SNAP
+
+
+def _log_with(ents):
+    import ctypes as C
+    from oracle.pyoracle import lib, orc_log
+    lg = orc_log()
+    lib().orc_log_init(C.byref(lg), 1, 0)
+    for i, t in ents:
+        assert i == lg.last_index + 1
+        lib().orc_log_push(C.byref(lg), t, 1)
+    return lg
+
+
+@pytest.mark.parametrize("ents,wconflict", [  # raft/log_test.go:24-57 TestFindConflict
+    ([], 0), ([], 0),
+    ([(1, 1), (2, 2), (3, 3)], 0), ([(2, 2), (3, 3)], 0), ([(3, 3)], 0),
+    ([(1, 1), (2, 2), (3, 3), (4, 4), (5, 4)], 4), ([(2, 2), (3, 3), (4, 4), (5, 4)], 4),
+    ([(3, 3), (4, 4), (5, 4)], 4), ([(4, 4), (5, 4)], 4),
+    ([(1, 4), (2, 4)], 1), ([(2, 1), (3, 4), (4, 4)], 2), ([(3, 1), (4, 2), (5, 4), (6, 4)], 3)])
+def test_find_conflict(ents, wconflict):
+    import ctypes as C
+    from oracle.pyoracle import lib
+    lg = _log_with([(1, 1), (2, 2), (3, 3)])
+    terms = (C.c_uint64 * max(1, len(ents)))(*[t for _, t in ents])
+    frm = ents[0][0] if ents else 1
+    assert lib().orc_log_find_conflict(C.byref(lg), frm, terms, len(ents)) == wconflict
+
+
+@pytest.mark.parametrize("lasti,term,want", [  # raft/log_test.go:59-88 TestIsUpToDate
+    (2, 4, True), (3, 4, True), (4, 4, True), (2, 2, False), (3, 2, False), (4, 2, False),
+    (2, 3, False), (3, 3, True), (4, 3, True)])
+def test_is_up_to_date(lasti, term, want):
+    import ctypes as C
+    from oracle.pyoracle import lib
+    lg = _log_with([(1, 1), (2, 2), (3, 3)])
+    assert bool(lib().orc_log_is_up_to_date(C.byref(lg), lasti, term)) == want
+
+
+LI, LT, CM = 3, 3, 1
+
+
+@pytest.mark.parametrize("log_term,index,committed,ents,wlasti,wappend,wcommit,wpanic", [  # log_test.go:152-240
+    (LT - 1, LI, LI, [(LI + 1, 4)], 0, False, CM, False),
+    (LT, LI + 1, LI, [(LI + 2, 4)], 0, False, CM, False),
+    (LT, LI, LI, [], LI, True, LI, False),
+    (LT, LI, LI + 1, [], LI, True, LI, False),
+    (LT, LI, LI - 1, [], LI, True, LI - 1, False),
+    (LT, LI, 0, [], LI, True, CM, False),
+    (0, 0, LI, [], 0, True, CM, False),
+    (LT, LI, LI, [(LI + 1, 4)], LI + 1, True, LI, False),
+    (LT, LI, LI + 1, [(LI + 1, 4)], LI + 1, True, LI + 1, False),
+    (LT, LI, LI + 2, [(LI + 1, 4)], LI + 1, True, LI + 1, False),
+    (LT, LI, LI + 2, [(LI + 1, 4), (LI + 2, 4)], LI + 2, True, LI + 2, False),
+    (LT - 1, LI - 1, LI, [(LI, 4)], LI, True, LI, False),
+    (LT - 2, LI - 2, LI, [(LI - 1, 4)], LI - 1, True, LI - 1, False),
+    (LT - 3, LI - 3, LI, [(LI - 2, 4)], LI - 2, True, LI - 2, True),
+    (LT - 2, LI - 2, LI, [(LI - 1, 4), (LI, 4)], LI, True, LI, False)])
+def test_log_maybe_append(log_term, index, committed, ents, wlasti, wappend, wcommit, wpanic):
+    import ctypes as C
+    from oracle.pyoracle import lib
+    lg = _log_with([(1, 1), (2, 2), (3, 3)])
+    lg.committed = CM
+    terms = (C.c_uint64 * max(1, len(ents)))(*[t for _, t in ents])
+    lasti = C.c_uint64()
+    rc = lib().orc_log_maybe_append(C.byref(lg), index, log_term, committed, terms, len(ents), C.byref(lasti))
+    if wpanic:
+        assert rc == -1
+        return
+    assert (rc == 1) == wappend and lasti.value == wlasti and lg.committed == wcommit
+    if wappend and ents:
+        assert [lib().orc_log_term(C.byref(lg), i) for i, _ in ents] == [t for _, t in ents]
+
+
+@pytest.mark.parametrize("m,windex,wcommit,wreject", [  # raft/raft_test.go:803-850 TestHandleMsgApp
+    (dict(Term=2, LogTerm=3, Index=2, Commit=3), 2, 0, True),
+    (dict(Term=2, LogTerm=3, Index=3, Commit=3), 2, 0, True),
+    (dict(Term=2, LogTerm=1, Index=1, Commit=1), 2, 1, False),
+    (dict(Term=2, LogTerm=0, Index=0, Commit=1, Entries=[(1, 2)]), 1, 1, False),
+    (dict(Term=2, LogTerm=2, Index=2, Commit=3, Entries=[(3, 2), (4, 2)]), 4, 3, False),
+    (dict(Term=2, LogTerm=2, Index=2, Commit=4, Entries=[(3, 2)]), 3, 3, False),
+    (dict(Term=2, LogTerm=1, Index=1, Commit=4, Entries=[(2, 2)]), 2, 2, False),
+    (dict(Term=1, LogTerm=1, Index=1, Commit=3), 2, 1, False),
+    (dict(Term=1, LogTerm=1, Index=1, Commit=3, Entries=[(2, 2)]), 2, 2, False),
+    (dict(Term=2, LogTerm=2, Index=2, Commit=3), 2, 2, False),
+    (dict(Term=2, LogTerm=2, Index=2, Commit=4), 2, 2, False)])
+def test_handle_msg_app(m, windex, wcommit, wreject):
+    sm = Raft(1, [1], ents=[(1, 1), (2, 2)])
+    sm.becomeFollower(2, None_)
+    sm.handleAppendEntries(Msg(APP, **m))
+    assert sm.lastIndex == windex and sm.committed == wcommit
+    ms = sm.readMessages()
+    assert len(ms) == 1 and bool(ms[0].Reject) == wreject
+
+
+@pytest.mark.parametrize("mcommit,wcommit", [(3, 3), (1, 2)])  # raft/raft_test.go:852-882 TestHandleHeartbeat
+def test_handle_heartbeat(mcommit, wcommit):
+    sm = Raft(1, [1, 2], ents=[(1, 1), (2, 2), (3, 3)], election=5)
+    sm.becomeFollower(2, 2)
+    sm.commitTo(2)
+    sm.handleHeartbeat(Msg(APP, From=2, To=1, Term=2, Commit=mcommit))
+    assert sm.committed == wcommit
+    ms = sm.readMessages()
+    assert len(ms) == 1 and ms[0].Type == HBRESP
+
+
+@pytest.mark.parametrize("state,i,term,vote_for,wreject", [  # raft/raft_test.go:1004-1066 TestRecvMsgVote
+    (F, 0, 0, None_, True), (F, 0, 1, None_, True), (F, 0, 2, None_, True), (F, 0, 3, None_, False),
+    (F, 1, 0, None_, True), (F, 1, 1, None_, True), (F, 1, 2, None_, True), (F, 1, 3, None_, False),
+    (F, 2, 0, None_, True), (F, 2, 1, None_, True), (F, 2, 2, None_, False), (F, 2, 3, None_, False),
+    (F, 3, 0, None_, True), (F, 3, 1, None_, True), (F, 3, 2, None_, False), (F, 3, 3, None_, False),
+    (F, 3, 2, 2, False), (F, 3, 2, 1, True),
+    (L, 3, 3, 1, True), (Cd, 3, 3, 1, True)])
+def test_recv_msg_vote(state, i, term, vote_for, wreject):
+    sm = Raft(1, [1], ents=[(1, 2), (2, 2)])  # storage ents {}, 1/2, 2/2; unstable offset 3
+    sm.r.state = state
+    sm.r.Vote = vote_for
+    sm.Step(Msg(VOTE, From=2, Index=i, LogTerm=term))
+    ms = sm.readMessages()
+    assert len(ms) == 1 and ms[0].Type == VOTERESP and bool(ms[0].Reject) == wreject
+
+
+@pytest.mark.parametrize("ents,commit", [  # raft/raft_paper_test.go:547-590 TestFollowerCommitEntry
+    ([(1, 1)], 1), ([(1, 1), (2, 1)], 2), ([(1, 1), (2, 1)], 2), ([(1, 1), (2, 1)], 1)])
+def test_follower_commit_entry(ents, commit):
+    r = Raft(1, [1, 2, 3])
+    r.becomeFollower(1, 2)
+    r.Step(Msg(APP, From=2, To=1, Term=1, Entries=ents, Commit=commit))
+    assert r.committed == commit
+    # nextEnts = (applied, committed]
+    assert list(range(r.r.log.applied + 1, r.committed + 1)) == [i for i, _ in ents[:commit]]
+
+
+@pytest.mark.parametrize("term,index,windex,wreject,whint", [  # raft_paper_test.go:597-631 TestFollowerCheckMsgApp
+    (0, 0, 1, False, 0), (1, 1, 1, False, 0), (2, 2, 2, False, 0), (1, 2, 2, True, 2), (3, 3, 3, True, 2)])
+def test_follower_check_msg_app(term, index, windex, wreject, whint):
+    r = Raft(1, [1, 2, 3], ents=[(1, 1), (2, 2)], hard=(0, 0, 1))
+    r.becomeFollower(2, 2)
+    r.Step(Msg(APP, From=2, To=1, Term=2, LogTerm=term, Index=index))
+    ms = r.readMessages()
+    assert len(ms) == 1
+    m = ms[0]
+    assert (m.From, m.To, m.Type, m.Term, m.Index, bool(m.Reject), m.RejectHint) == (1, 2, APPRESP, 2, windex,
+                                                                                     wreject, whint)
+
+
+@pytest.mark.parametrize("index,term,ents,wents", [  # raft_paper_test.go:638-681 TestFollowerAppendEntries
+    (2, 2, [(3, 3)], [(1, 1), (2, 2), (3, 3)]),
+    (1, 1, [(2, 3), (3, 4)], [(1, 1), (2, 3), (3, 4)]),
+    (0, 0, [(1, 1)], [(1, 1), (2, 2)]),
+    (0, 0, [(1, 3)], [(1, 3)])])
+def test_follower_append_entries(index, term, ents, wents):
+    # the unstable/stable split (wunstable) is host-side raftLog state: the engine's
+    # host half (hbnode) keeps it; the oracle pins the resulting log
+    r = Raft(1, [1, 2, 3], ents=[(1, 1), (2, 2)])
+    r.becomeFollower(2, 2)
+    r.Step(Msg(APP, From=2, To=1, Term=2, LogTerm=term, Index=index, Entries=ents))
+    assert r.entries() == wents
+
+
+@pytest.mark.parametrize("ents,logterm,index,wreject", [  # raft_paper_test.go:821-861 TestVoter
+    ([(1, 1)], 1, 1, False), ([(1, 1)], 1, 2, False), ([(1, 1), (2, 1)], 1, 1, True),
+    ([(1, 1)], 2, 1, False), ([(1, 1)], 2, 2, False), ([(1, 1), (2, 1)], 2, 1, False),
+    ([(1, 2)], 1, 1, True), ([(1, 2)], 1, 2, True), ([(1, 2), (2, 1)], 1, 1, True)])
+def test_voter(ents, logterm, index, wreject):
+    r = Raft(1, [1, 2], ents=ents)
+    r.Step(Msg(VOTE, From=2, To=1, Term=3, LogTerm=logterm, Index=index))
+    ms = r.readMessages()
+    assert len(ms) == 1 and ms[0].Type == VOTERESP and bool(ms[0].Reject) == wreject
+
+
+def test_restore_snapshot_via_msg_snap():
+    """handleSnapshot + restore (raft/raft.go:671-707, cf. raft/raft_test.go
+    TestRestore / TestProvideSnap): a follower behind the snapshot restores it
+    (log = the snapshot, Progress reset) and answers MsgAppResp{lastIndex};
+    one that already holds the entry fast-forwards its commit; one whose commit
+    is past it ignores it and answers MsgAppResp{committed}."""
+    r = Raft(1, [1, 2, 3], ents=[(1, 1), (2, 1)])
+    r.becomeFollower(2, 2)
+    r.Step(Msg(SNAP, From=2, To=1, Term=2, Snapshot=(11, 2)))
+    assert (r.lastIndex, r.committed, r.r.log.first_index, r.term(11)) == (11, 11, 12, 2)
+    ms = r.readMessages()
+    assert [(m.Type, m.To, m.Index, bool(m.Reject)) for m in ms] == [(APPRESP, 2, 11, False)]
+    assert r.pr(1).Match == 11 and r.pr(2).Match == 0 and r.pr(2).Next == 12
+    # the snapshot's entry is already in the log: commit fast-forwards, no restore
+    r2 = Raft(1, [1, 2], ents=[(1, 1), (2, 1), (3, 2)])
+    r2.becomeFollower(2, 2)
+    r2.Step(Msg(SNAP, From=2, To=1, Term=2, Snapshot=(2, 1)))
+    assert (r2.lastIndex, r2.committed, r2.r.log.first_index) == (3, 2, 1)
+    assert [(m.Type, m.Index) for m in r2.readMessages()] == [(APPRESP, 2)]
+    # commit is past the snapshot: ignored
+    r2.Step(Msg(SNAP, From=2, To=1, Term=2, Snapshot=(1, 1)))
+    assert [(m.Type, m.Index) for m in r2.readMessages()] == [(APPRESP, 2)]
+
+
+def test_follower_term_window_fault():
+    """Engine-defined bound: the engine keeps HB_TERM_RUNS older term runs; a
+    follower-side lookup below them faults HB_FAULT_TERM_WINDOW."""
+    ents = [(i + 1, i + 1) for i in range(abi.HB_TERM_RUNS + 2)]  # one run per entry
+    r = Raft(1, [1, 2], ents=ents)
+    r.becomeFollower(20, 2)
+    r.Step(Msg(APP, From=2, To=1, Term=20, LogTerm=2, Index=2))  # term(2): dropped from the window
+    assert r.fault == abi.HB_FAULT_TERM_WINDOW
+    r2 = Raft(1, [1, 2], ents=ents)
+    r2.becomeFollower(20, 2)
+    last = len(ents)
+    r2.Step(Msg(APP, From=2, To=1, Term=20, LogTerm=last, Index=last, Commit=0))
+    assert r2.fault == 0 and [m.Index for m in r2.readMessages()] == [last]

@@ -315,3 +315,53 @@ def test_cfg2_finite_max_msg_size():
         b = synth.attach_entry_descs(b, G, seed=69 + step, max_len=300)
         _, st, _ = pair.step(b, ctx=f"cfg2 finite step {step}")
         assert st[abi.HB_STAT_FAULTS] == 0
+
+
+# ---------------------------------------------------------------- follower side
+@pytest.mark.parametrize("seed,nmax,W", [(71, 3, 8), (72, 5, 16), (73, 7, 8), (74, 3, 256)])
+def test_fuzz_follower_side(seed, nmax, W):
+    """MsgApp (entries, conflicts, rejections), MsgHeartbeat, MsgSnap (restore /
+    fast-forward / ignore) and MsgVote (grant / reject, senders outside prs)
+    interleaved with every leader-side message type: k_apply hands a group over
+    at its first follower-side message and k_follow steps the rest; events
+    (responses, appends, restores), statistics, records, inflights and timers
+    (the follower side zeroes r.elapsed) equal the oracle's."""
+    g, runs, ins = synth.random_groups(1500, nmax, seed=seed, W=W)
+    pair = Pair(g, runs, nmax, W, ins=ins, max_batch=1 << 15, term_runs=True)
+    pair.set_timers(synth.random_timers(len(g), seed=seed), DRAWS)
+    now = pair.og.groups()
+    for k in range(4):
+        f = synth.follower_messages(now, pair.og.term, 3000, seed=seed + 13 * k)
+        b = synth.merge_batches(synth.random_batch(g, 3000, seed=seed + 7 * k), f, seed=seed + k)
+        _, st, now = pair.step(b, ctx=f"follower fuzz {seed} step {k}")
+
+
+def test_follower_replication_stream():
+    """Steady follower-side replication: 20k follower groups, each step one
+    MsgApp per group from its leader carrying 1-3 new entries at the leader's
+    term (Index / LogTerm = the follower's last entry) and the leader's commit,
+    plus heartbeats: every group appends, commits and answers."""
+    G, n = 20_000, 3
+    g, runs = synth.steady_groups(G, n, seed=91, last_hi=1 << 12)
+    g["state"] = abi.HB_STATE_FOLLOWER
+    g["lead"] = 1
+    g["vote"] = 1
+    for s in range(n):
+        g["pr"][:, s]["state"] = abi.HB_PR_PROBE
+    pair = Pair(g, runs, n, 256, max_batch=4 * G, term_runs=True)
+    rng = np.random.default_rng(92)
+    last = g["last_index"].astype(np.uint64).copy()
+    term = g["term"].astype(np.uint64)
+    for step in range(3):
+        k = rng.integers(1, 4, G).astype(np.uint64)
+        order = rng.permutation(G)
+        eoff = np.concatenate([[0], np.cumsum(k[order])[:-1]]).astype(np.uint64)
+        b = dict(group=order.astype(np.uint32),
+                 info=np.full(G, abi.HB_MSG_APP | (1 << 4), np.uint32),
+                 term=term[order], index=last[order], hint=term[order],
+                 commit=(last[order] + k[order]), eoff=eoff,
+                 eterm=np.repeat(term[order], k[order].astype(np.int64)).astype(np.uint64), props=None)
+        _, st, now = pair.step(b, ctx=f"follower stream step {step}", check_inflights=False)
+        last = last + k
+        assert np.array_equal(now["last_index"], last)
+        assert st[abi.HB_STAT_COMMITS] == G and st[abi.HB_STAT_FAULTS] == 0
