@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-HB_ABI_VERSION = 2
+HB_ABI_VERSION = 3
 
 HB_OK = 0
 HB_EINVAL = -1

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define HB_ABI_VERSION 2
+#define HB_ABI_VERSION 3
 
 /* ---- error codes -------------------------------------------------------- */
 #define HB_OK          0
