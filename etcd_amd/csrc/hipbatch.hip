@@ -368,9 +368,15 @@ struct ApplyArgs {
   uint32_t* ev_counts;      // [NB] records in each chunk
   uint64_t* ev_off;         // [NB] chunk offsets (records)
   uint64_t* stats_shard;    // [8][16] step statistics, one shard per XCD slot (atomic adds)
-  uint32_t* pflag;          // [NB][PART/32] groups handed from k_apply_fast to k_apply (and on to k_follow)
-  uint32_t* fl_cnt;         // k_follow's work list: partitions k_apply flagged
+  uint32_t* pflag;          // [NB][PART/32] groups handed from k_apply_fast to k_apply
+  uint32_t* ap_cnt;         // [8] k_apply's work lists: partitions k_apply_fast flagged, one list per
+  uint32_t* ap_list;        // [8][NB]  XCD slot (blockIdx % 8) of the flagging workgroup
+  uint32_t* fl_cnt;         // k_follow's work list: partitions with groups k_apply handed on
   uint32_t* fl_list;        // [NB]
+  uint32_t grid;            // apply_grid: virtual workgroups of the partition mapping (part_of)
+  uint32_t* done;           // k_apply workgroups finished (the last one runs the finish)
+  uint64_t* stats;          // [HB_STAT_COUNT] this step's statistics (finish)
+  uint64_t* accum;          // caller accumulator or null (finish)
   uint32_t* resume;         // [G] messages consumed by k_apply_fast | not loaded << 30 | prop pending << 31
   uint64_t* commit0;        // [G] committed at batch start (for HB_STAT_COMMITS)
   // k_route -> k_apply_fast / k_apply: each group's first kmax messages, lane-major
@@ -425,10 +431,11 @@ constexpr uint32_t SEG = PART * KPL;        // positions per key-scan segment
 // blockIdx -> partition.  The SIS sister partitions of a bucket get block ids
 // with equal blockIdx % 8, i.e. one XCD under the round-robin placement, so
 // the bucket's keys and records are fetched into one L2 (speed only).
-__device__ __forceinline__ uint32_t block_part() {
-  const uint32_t x = blockIdx.x, r = x & 7, q = x >> 3;
+__device__ __forceinline__ uint32_t part_of(uint32_t x) {
+  const uint32_t r = x & 7, q = x >> 3;
   return ((((q >> SIS_LOG) << 3) | r) << SIS_LOG) | (q & (SIS - 1));
 }
+__device__ __forceinline__ uint32_t block_part() { return part_of(blockIdx.x); }
 
 // LDS staging of one round (<= CH messages) of a partition's messages.
 // w[j][i] = word j of the round's i-th MsgRec (info, orig, term lo/hi, index lo/hi).
@@ -882,53 +889,59 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   if (tid == 0) {
     a.ev_counts[2 * part] = l_pfill;
     a.ev_counts[2 * part + 1] = l_fill;
+    uint32_t any = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < FLAG_WORDS; ++w) any |= l_flag[w];
+    if (any) {  // the partition joins k_apply's list of its XCD slot
+      const uint32_t xs = blockIdx.x & 7;
+      a.ap_list[(size_t)xs * a.NB + atomicAdd(&a.ap_cnt[xs], 1u)] = part;
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
-// k_apply / k_follow: the general state machine (Lane::step) for the groups
-// the previous kernel handed over, from their resume point.  k_apply takes
-// k_apply_fast's hand-overs and steps every leader / candidate message type;
-// at a group's first follower-side message (MsgApp / MsgHeartbeat / MsgSnap /
-// MsgVote) it hands the group on to k_follow, which steps everything with the
-// follower-capable lane (its code and registers stay out of k_apply, the hot
-// general kernel of cfg3 / cfg4).  k_follow runs over a work list of the
-// partitions k_apply flagged: an empty list costs one small launch.
-// Partitions without handed-over groups exit after reading their flag words.
-// A group whose messages all sit in its k_route slots (count <= route_kmax)
-// steps them from there, in arrival order; the bucket is walked (LDS rounds)
-// only when some group of the partition has more messages than slots.
+// k_apply: the general state machine (Lane::step) for the groups
+// k_apply_fast handed over, from their resume point: every leader / candidate
+// message type; at a group's first follower-side message (MsgApp /
+// MsgHeartbeat / MsgSnap / MsgVote) the group is handed on to a second pass
+// over the same partition with the follower-capable lane (Lane<NMAX, true>).
+// Only partitions k_apply_fast put on a work list are visited.  A group whose
+// messages all sit in its k_route slots (count <= route_kmax) steps them from
+// there, in arrival order; the bucket is walked (LDS rounds) only when some
+// group of the partition has more messages than slots.
 // ---------------------------------------------------------------------------
 #ifndef HB_GEN_WAVES
 #define HB_GEN_WAVES 2
 #endif
-constexpr uint32_t FOLLOW_GRID = 256;  // k_follow workgroups (persistent over the work list)
-
 struct GenShared {
   Stage<CHUNK> sl;
   uint32_t l_fill;
   uint32_t l_flag[FLAG_WORDS];
-  uint32_t l_next[FLAG_WORDS];  // groups handed on to k_follow
+  uint32_t l_next[FLAG_WORDS];  // groups handed on to the follower-side pass
   uint64_t l_stats[ST_N + 1];
 };
 
+// One partition through the general lane.  FOLLOW = false: the groups
+// k_apply_fast flagged (pflag); returns whether any was handed on at a
+// follower-side message (sh.l_next).  FOLLOW = true, chained: those groups,
+// right after, in the same workgroup (flags and the chunk fill from LDS).
 template <int NMAX, bool FOLLOW>
-__device__ __forceinline__ void apply_part(const ApplyArgs& a, uint32_t part, GenShared& sh) {
+__device__ __forceinline__ bool apply_part(const ApplyArgs& a, uint32_t part, GenShared& sh, bool chained) {
   const uint32_t tid = threadIdx.x;
   const uint32_t bk = part >> SIS_LOG, sub = part & (SIS - 1);
   const uint32_t g = part * PART + tid;
+  const uint32_t fill0 = chained ? sh.l_fill : a.ev_counts[2 * part + 1];
   if (tid < FLAG_WORDS) {
-    sh.l_flag[tid] = a.pflag[(size_t)part * FLAG_WORDS + tid];
+    sh.l_flag[tid] = chained ? sh.l_next[tid] : a.pflag[(size_t)part * FLAG_WORDS + tid];
     sh.l_next[tid] = 0;
   }
   __syncthreads();
   uint32_t any = 0;
 #pragma unroll
   for (uint32_t w = 0; w < FLAG_WORDS; ++w) any |= sh.l_flag[w];
-  if (!any) return;  // uniform
+  if (!any) return false;  // uniform
   const bool flagged = (sh.l_flag[tid >> 5] >> (tid & 31)) & 1u;
 
-  const uint32_t fill0 = a.ev_counts[2 * part + 1];
   if (tid == 0) sh.l_fill = fill0;  // append to the M chunk after the previous kernels' events
   if (tid <= ST_N) sh.l_stats[tid] = 0;
 
@@ -958,7 +971,7 @@ __device__ __forceinline__ void apply_part(const ApplyArgs& a, uint32_t part, Ge
   uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
   const uint32_t skip = resume & 0x3FFFFFFFu;
   uint32_t j = 0;
-  bool handed = false;  // (k_apply) a follower-side message: the group goes on to k_follow
+  bool handed = false;  // (!FOLLOW) a follower-side message: the group goes on to the follower pass
   uint32_t hand_at = 0;
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
 
@@ -1067,7 +1080,7 @@ __device__ __forceinline__ void apply_part(const ApplyArgs& a, uint32_t part, Ge
   if (__syncthreads_or(by_walk)) walk_partition(sh.sl, a, lo, hi, sub, nullptr, on_total, round);
 
   if (flagged) L.store();
-  if (handed) {  // k_follow resumes the group at its follower-side message
+  if (handed) {  // the follower-side pass resumes the group at its follower-side message
     atomicOr(&sh.l_next[tid >> 5], 1u << (tid & 31));
     a.resume[g] = hand_at;
     a.commit0[g] = commit0;
@@ -1083,34 +1096,84 @@ __device__ __forceinline__ void apply_part(const ApplyArgs& a, uint32_t part, Ge
                                    (uint64_t)(done && L.faulted() != 0),
                                    L.last - last0,
                                    L.nev};
-  reduce_stats(a, sh.l_stats, vals);
+  reduce_stats(a, sh.l_stats, vals);  // (ends with a barrier: l_next and l_fill are final)
   if (tid == 0) a.ev_counts[2 * part + 1] = sh.l_fill;
-  if constexpr (!FOLLOW) {  // the flags k_follow reads; the partition joins its work list
-    __syncthreads();
-    if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = sh.l_next[tid];
-    uint32_t nx = 0;
+  uint32_t nx = 0;
+  if constexpr (!FOLLOW) {
 #pragma unroll
     for (uint32_t w = 0; w < FLAG_WORDS; ++w) nx |= sh.l_next[w];
-    if (tid == 0 && nx) a.fl_list[atomicAdd(a.fl_cnt, 1u)] = part;
+  }
+  return nx != 0;
+}
+
+// k_apply runs over k_apply_fast's work lists, on the apply grid: workgroup w
+// takes entry w / 8 of the list of XCD slot w % 8 (the slot of the workgroup
+// that flagged the partition, so a bucket's sisters stay on one XCD; a list
+// holds at most grid / 8 entries).  Partitions it hands on at a follower-side
+// message (MsgApp / MsgHeartbeat / MsgSnap / MsgVote) go to k_follow's list.
+#ifndef HB_FOLLOW_GRID
+#define HB_FOLLOW_GRID 128
+#endif
+constexpr uint32_t FOLLOW_GRID = HB_FOLLOW_GRID;
+
+// The step's finish (as k_finish), run by the last k_follow workgroup: the
+// statistics shards (agent-scope atomics of every apply kernel) summed into
+// stats (+ accum), the shards and the work lists cleared for the next step.
+__device__ __forceinline__ void finish_step(const ApplyArgs& a) {
+  const int map[ST_N + 1] = {HB_STAT_MSGS,  HB_STAT_APPRESP, HB_STAT_VOTERESP, HB_STAT_DROPPED, HB_STAT_COMMITS,
+                             HB_STAT_WON,   HB_STAT_LOST,    HB_STAT_FAULTS,   HB_STAT_ENTRIES, HB_STAT_EVENTS};
+  const uint32_t k = threadIdx.x;
+  if (k <= ST_N) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      v += __hip_atomic_load(&a.stats_shard[x * 16 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.stats_shard[x * 16 + k], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    a.stats[map[k]] = v;
+    if (a.accum) a.accum[map[k]] += v;
+  }
+  if (k < 8) __hip_atomic_store(&a.ap_cnt[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (k == 0) {
+    __hip_atomic_store(a.fl_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 template <int NMAX>
 __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
   __shared__ GenShared sh;
-  const uint32_t part = block_part();
-  if (part >= a.NB) return;  // uniform: grid padding
-  apply_part<NMAX, false>(a, part, sh);
+  const uint32_t xs = blockIdx.x & 7, i = blockIdx.x >> 3;
+  if (i >= __hip_atomic_load(&a.ap_cnt[xs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // uniform
+  const uint32_t part = a.ap_list[(size_t)xs * a.NB + i];
+  if (apply_part<NMAX, false>(a, part, sh, false)) {  // uniform: the partition goes on to k_follow
+    if (threadIdx.x < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + threadIdx.x] = sh.l_next[threadIdx.x];
+    if (threadIdx.x == 0) a.fl_list[atomicAdd(a.fl_cnt, 1u)] = part;
+  }
 }
 
+// k_follow: the follower-capable lane (Lane<NMAX, true>) for the groups
+// k_apply handed on at a follower-side message, over k_apply's work list (its
+// registers and code stay out of k_apply, the hot general kernel of cfg3 /
+// cfg4).  Its last workgroup out runs the step's finish: the statistics are
+// agent-scope atomics, performed at the memory side, so each workgroup waits
+// for its own (vmcnt(0)) before taking a ticket, and the last reads the shards
+// with agent-scope loads.
 template <int NMAX>
 __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_follow(ApplyArgs a) {
   __shared__ GenShared sh;
-  const uint32_t nl = *reinterpret_cast<volatile const uint32_t*>(a.fl_cnt);  // written by k_apply
+  __shared__ uint32_t l_last;
+  const uint32_t nl = __hip_atomic_load(a.fl_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
-    apply_part<NMAX, true>(a, a.fl_list[i], sh);
+    (void)apply_part<NMAX, true>(a, a.fl_list[i], sh, false);
     __syncthreads();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's stats atomics are performed
+  __syncthreads();
+  if (threadIdx.x == 0)
+    l_last = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (l_last) finish_step(a);  // uniform
 }
 
 // ---------------------------------------------------------------------------
@@ -1374,7 +1437,7 @@ __global__ void __launch_bounds__(DEC_THREADS) k_decode_general(DecodeArgs a, co
 // ============================================================================
 // Phase 3: finish
 // ============================================================================
-__global__ void __launch_bounds__(64) k_finish(uint64_t* shard, uint64_t* stats, uint64_t* accum, uint32_t* fl_cnt) {
+__global__ void __launch_bounds__(64) k_finish(uint64_t* shard, uint64_t* stats, uint64_t* accum) {
   const int map[ST_N + 1] = {HB_STAT_MSGS,  HB_STAT_APPRESP, HB_STAT_VOTERESP, HB_STAT_DROPPED, HB_STAT_COMMITS,
                              HB_STAT_WON,   HB_STAT_LOST,    HB_STAT_FAULTS,   HB_STAT_ENTRIES, HB_STAT_EVENTS};
   const uint32_t k = threadIdx.x;
@@ -1388,7 +1451,6 @@ __global__ void __launch_bounds__(64) k_finish(uint64_t* shard, uint64_t* stats,
     stats[map[k]] = v;
     if (accum) accum[map[k]] += v;
   }
-  if (k == 0 && fl_cnt) *fl_cnt = 0;  // k_follow's work list, for the next step
 }
 
 // ============================================================================
@@ -1669,8 +1731,11 @@ struct hb_handle {
   uint64_t* stats = nullptr;
   // fast -> general hand-over
   uint32_t* pflag = nullptr;      // [NB][PART/32]
-  uint32_t* fl_cnt = nullptr;     // k_follow work list (count, reset by k_finish)
+  uint32_t* ap_cnt = nullptr;     // [8] k_apply work lists (counts, reset by the step's finish)
+  uint32_t* ap_list = nullptr;    // [8][NB]
+  uint32_t* fl_cnt = nullptr;     // k_follow work list
   uint32_t* fl_list = nullptr;    // [NB]
+  uint32_t* done = nullptr;       // k_apply workgroups finished this step
   uint32_t* resume = nullptr;     // [G]
   uint64_t* commit0 = nullptr;    // [G]
   uint64_t* peer = nullptr;       // [G][HB_PEER_ROW] node ids (hb_load_peers), allocated on first use
@@ -1739,7 +1804,8 @@ void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
   hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
   if (ev) (void)hipEventRecord(ev[3], h->stream);
   hipLaunchKernelGGL(k_apply<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
-  hipLaunchKernelGGL(k_follow<NMAX>, dim3(std::min(FOLLOW_GRID, h->NB)), dim3(PART), 0, h->stream, a);
+  // k_follow's last workgroup also runs the step's finish (k_finish)
+  hipLaunchKernelGGL(k_follow<NMAX>, dim3(FOLLOW_GRID), dim3(PART), 0, h->stream, a);
   if (ev && full) (void)hipEventRecord(ev[4], h->stream);
 }
 
@@ -1854,8 +1920,11 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->ev, h->ev_region);
   ALLOC(h->stats_shard, 8 * 16);
   ALLOC(h->pflag, (size_t)h->NB * FLAG_WORDS);
+  ALLOC(h->ap_cnt, 8);
+  ALLOC(h->ap_list, 8ull * h->NB);
   ALLOC(h->fl_cnt, 4);
   ALLOC(h->fl_list, h->NB);
+  ALLOC(h->done, 4);
   ALLOC(h->resume, G);
   ALLOC(h->commit0, G);
   ALLOC(h->stats, HB_STAT_COUNT);
@@ -1884,6 +1953,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
       hipMemset(s.elapsed, 0, G * 4) != hipSuccess || hipMemset(s.rpos, 0, G * 4) != hipSuccess ||
       hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(s.tcfg), 10u | (1u << 16), G) != hipSuccess ||
       hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess || hipMemset(h->stats_shard, 0, 8 * 16 * 8) != hipSuccess ||
+      hipMemset(h->ap_cnt, 0, 32) != hipSuccess || hipMemset(h->done, 0, 4) != hipSuccess ||
       hipMemset(h->fl_cnt, 0, 4) != hipSuccess ||
       hipMemset(h->set[0].ev_counts, 0, h->NB * 8ull) != hipSuccess ||
       hipMemset(h->set[0].ev_off, 0, h->NB * 16ull) != hipSuccess ||
@@ -2258,7 +2328,7 @@ int hb_tick(hb_handle* h, uint32_t flags) {
     case 5: hipLaunchKernelGGL(k_tick<5>, dim3(grid), dim3(PART), 0, st, aa); break;
     default: hipLaunchKernelGGL(k_tick<7>, dim3(grid), dim3(PART), 0, st, aa); break;
   }
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, h->stats_shard, h->stats, h->stats_accum, h->fl_cnt);
+  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, h->stats_shard, h->stats, h->stats_accum);
   if (two) HB_CHECK(hipEventRecord(ps.applied, st));  // a later prep reusing this set waits for it
   HB_CHECK(hipGetLastError());
   ps.used = true;
@@ -2408,8 +2478,14 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.S.eterm = bd_eterm;
   aa.S.n_ent = b->n_edesc;
   aa.S.bn = b->n;
+  aa.ap_cnt = h->ap_cnt;
+  aa.ap_list = h->ap_list;
   aa.fl_cnt = h->fl_cnt;
   aa.fl_list = h->fl_list;
+  aa.grid = apply_grid(h);
+  aa.done = h->done;
+  aa.stats = h->stats;
+  aa.accum = h->stats_accum;
   aa.rec = ps.rec;
   aa.key = ps.key;
   aa.bk_off = ps.bk_off;
@@ -2449,8 +2525,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     case 5: launch_apply<5>(h, aa, prof_apply ? ev : nullptr, prof); break;
     default: launch_apply<7>(h, aa, prof_apply ? ev : nullptr, prof); break;
   }
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, h->stats_shard, h->stats, h->stats_accum, h->fl_cnt);
-  if (prof) HB_CHECK(hipEventRecord(ev[5], st));
+  if (prof) HB_CHECK(hipEventRecord(ev[5], st));  // (the finish runs inside k_follow)
   if (two) HB_CHECK(hipEventRecord(ps.applied, st));
   HB_CHECK(hipGetLastError());
   ps.used = true;
