@@ -854,6 +854,11 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     elif args.workload == "tick":
         metric, unit, val = "group ticks/sec (MultiNode.Tick over 1M groups x 3)", "group-ticks/s", \
             world * G * args.steps / sec
+        # per group: meta 8 + tcfg 4 + elapsed 4 R + 4 W; a due MsgBeat / MsgHup steps the
+        # group (state ~100 B, SURVEY.md 8(d) per-group figures) and its events (8 B words)
+        alg = (G * 20 * args.steps + int(st[abi.HB_STAT_MSGS]) * 100 + int(st[abi.HB_STAT_EVENTS]) * 8) / world
+        alg_note = ("per tick: 20 B per group (meta, tcfg, elapsed r/w) + 100 B per stepped MsgBeat / MsgHup "
+                    "+ 8 B per event word")
         extra = {"msgs_stepped_per_s": int(st[abi.HB_STAT_MSGS]) / sec, "events_per_s": int(st[abi.HB_STAT_EVENTS]) / sec,
                  "campaigns": int(st[abi.HB_STAT_MSGS]) - world * (G // 2 + G % 2) * args.steps}
         ok = int(st[abi.HB_STAT_FAULTS]) == 0
@@ -862,6 +867,14 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     elif args.workload == "cfg4":
         metric, unit, val = "MsgVoteResp tallied/sec + elections decided/sec (cfg4 election storm)", "MsgVoteResp/s", \
             int(st[abi.HB_STAT_VOTERESP]) / sec
+        # 37 B per MsgVoteResp (message 24, vote masks 2R + 2W, state 1, Term 8);
+        # 24 B per other message; every transition (each group steps down and campaigns, and a
+        # decided election is a third) writes state/lead/Term/Vote ~26 B + n Progress resets x 30 B
+        nvr = int(st[abi.HB_STAT_VOTERESP])
+        trans = 2 * world * G * args.steps + int(st[abi.HB_STAT_WON]) + int(st[abi.HB_STAT_LOST])
+        alg = (nvr * 37 + (int(st[abi.HB_STAT_MSGS]) - nvr) * 24 + trans * (26 + 30 * n)) / world
+        alg_note = ("37 B per MsgVoteResp + 24 B per other message + (26 + 30 n) B per transition "
+                    "(2 per group + 1 per decided election)")
         extra = {"elections_decided_per_s": (int(st[abi.HB_STAT_WON]) + int(st[abi.HB_STAT_LOST])) / sec,
                  "elections_won": int(st[abi.HB_STAT_WON]), "elections_lost": int(st[abi.HB_STAT_LOST])}
         ok = int(st[abi.HB_STAT_VOTERESP]) == world * G * (n - 1) * args.steps and int(st[abi.HB_STAT_FAULTS]) == 0
@@ -870,10 +883,23 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     else:
         metric, unit, val = "MsgAppResp applied/sec (cfg3 lagging followers)", "MsgAppResp/s", \
             int(st[abi.HB_STAT_APPRESP]) / sec
+        # SURVEY.md 8(d) cfg2 figures applied to cfg3: 66 B per stepped message (message 24,
+        # Match/Next/state/inflights), 80 B per group per batch, 21 B per follower per appended entry
+        alg = (int(st[abi.HB_STAT_MSGS]) * 66 + world * G * args.steps * 80 +
+               int(st[abi.HB_STAT_ENTRIES]) * (n - 1) * 21) / world
+        alg_note = "66 B per stepped message + 80 B per group + 21 B per follower per appended entry"
+
         extra = {"msgs_per_s": int(st[abi.HB_STAT_MSGS]) / sec, "commits_per_s": int(st[abi.HB_STAT_COMMITS]) / sec}
         ok = int(st[abi.HB_STAT_FAULTS]) == 0
         wl = f"cfg3: {G} raft groups x {n} per GPU, lagging followers (W={W})"
         data = "synthetic (seeded open-loop cfg3 stream generated from the engine state each step)"
+    if args.workload in ("cfg3", "cfg4", "tick"):
+        # whole-step roofline (several kernels share the step; per-kernel times: profiles/*kernel_stats.csv)
+        ach = alg / (ms / args.steps * 1e-3) / args.steps / 1e9 if ms > 0 else 0.0
+        extra["roofline"] = {"bound": "hbm", "kernel": "hb_step (whole step)" if args.workload != "tick" else
+                             "hb_tick (k_tick + finish)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                             "alg_bytes_per_step": round(alg / args.steps), "alg_bytes_note": alg_note}
     out = {"metric": metric, "value": val, "unit": unit, "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": ms / args.steps, "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "u64", "data": data,

@@ -24,6 +24,7 @@
 
 #include "hipbatch_kernels.h"
 #include "hipbatch_fast.h"
+#include "hipbatch_elect.h"
 #include "hipbatch_wire.h"
 
 using namespace hb;
@@ -373,6 +374,9 @@ struct ApplyArgs {
   uint32_t* ap_list;        // [8][NB]  XCD slot (blockIdx % 8) of the flagging workgroup
   uint32_t* fl_cnt;         // k_follow's work list: partitions with groups k_apply handed on
   uint32_t* fl_list;        // [NB]
+  uint32_t* eflag;          // [NB][PART/32] (n >= 5) handed-over groups k_elect should try: not a
+  uint32_t* el_cnt;         // [8]   leader, or a leader with a higher-term message in its slots;
+  uint32_t* el_list;        // [8][NB]  k_elect's work lists (per XCD slot, as ap_list)
   uint32_t grid;            // apply_grid: virtual workgroups of the partition mapping (part_of)
   uint32_t* done;           // k_apply workgroups finished (the last one runs the finish)
   uint64_t* stats;          // [HB_STAT_COUNT] this step's statistics (finish)
@@ -749,6 +753,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   constexpr uint32_t KMAX = NMAX - 1;  // one MsgAppResp per follower per batch
   __shared__ uint32_t l_fill, l_pfill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
+  __shared__ uint32_t l_eflag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
 
   const uint32_t part = block_part();
@@ -758,7 +763,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   const bool gvalid = g < a.S.G;
   if (tid == 0) l_fill = l_pfill = 0;
   if (tid <= ST_N) l_stats[tid] = 0;
-  if (tid < FLAG_WORDS) l_flag[tid] = 0;
+  if (tid < FLAG_WORDS) l_flag[tid] = l_eflag[tid] = 0;
 
   // ---- every load of the lane, one round trip
   FastLane<NMAX> L;
@@ -869,6 +874,12 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   }
 
   if (lead) L.store();
+  if constexpr (NMAX >= 5) {  // k_elect's candidates: an election (or a step-down) is likely
+    bool higher = false;
+#pragma unroll
+    for (uint32_t k = 0; k < KMAX; ++k) higher |= k < cnt && s_term[k] > L.term;
+    if (flagged && (!lead || higher)) atomicOr(&l_eflag[tid >> 5], 1u << (tid & 31));
+  }
   if (flagged) {
     atomicOr(&l_flag[tid >> 5], 1u << (tid & 31));
     a.resume[g] = resume | (lead ? 0u : 1u << 30);
@@ -886,16 +897,23 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
                                    L.nev};
   reduce_stats(a, l_stats, vals);
   if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
+  if constexpr (NMAX >= 5) {
+    if (tid < FLAG_WORDS) a.eflag[(size_t)part * FLAG_WORDS + tid] = l_eflag[tid];
+  }
   if (tid == 0) {
     a.ev_counts[2 * part] = l_pfill;
     a.ev_counts[2 * part + 1] = l_fill;
-    uint32_t any = 0;
+    uint32_t any = 0, eany = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < FLAG_WORDS; ++w) any |= l_flag[w];
-    if (any) {  // the partition joins k_apply's list of its XCD slot
-      const uint32_t xs = blockIdx.x & 7;
-      a.ap_list[(size_t)xs * a.NB + atomicAdd(&a.ap_cnt[xs], 1u)] = part;
+    for (uint32_t w = 0; w < FLAG_WORDS; ++w) {
+      any |= l_flag[w];
+      eany |= l_eflag[w];
     }
+    const uint32_t xs = blockIdx.x & 7;
+    if (any)  // the partition joins k_apply's list of its XCD slot
+      a.ap_list[(size_t)xs * a.NB + atomicAdd(&a.ap_cnt[xs], 1u)] = part;
+    if (eany)  // ... and k_elect's
+      a.el_list[(size_t)xs * a.NB + atomicAdd(&a.el_cnt[xs], 1u)] = part;
   }
 }
 
@@ -1115,6 +1133,15 @@ __device__ __forceinline__ bool apply_part(const ApplyArgs& a, uint32_t part, Ge
 #define HB_FOLLOW_GRID 128
 #endif
 constexpr uint32_t FOLLOW_GRID = HB_FOLLOW_GRID;
+// k_apply's grid: 0 = one workgroup per partition (each takes at most one list
+// entry); else a persistent grid of that many (a multiple of 8).  Measured on
+// MI355X: 512 saves ~1.5 us on an empty cfg2 step but costs 5-7 % on cfg3 /
+// cfg4, where every partition is on the lists.
+#ifndef HB_GEN_GRID
+#define HB_GEN_GRID 0
+#endif
+constexpr uint32_t GEN_GRID = HB_GEN_GRID;
+static_assert(GEN_GRID % 8 == 0, "k_apply strides its XCD-slot lists by gridDim.x / 8");
 
 // The step's finish (as k_finish), run by the last k_follow workgroup: the
 // statistics shards (agent-scope atomics of every apply kernel) summed into
@@ -1133,7 +1160,10 @@ __device__ __forceinline__ void finish_step(const ApplyArgs& a) {
     a.stats[map[k]] = v;
     if (a.accum) a.accum[map[k]] += v;
   }
-  if (k < 8) __hip_atomic_store(&a.ap_cnt[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (k < 8) {
+    __hip_atomic_store(&a.ap_cnt[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.el_cnt) __hip_atomic_store(&a.el_cnt[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (k == 0) {
     __hip_atomic_store(a.fl_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1143,12 +1173,149 @@ __device__ __forceinline__ void finish_step(const ApplyArgs& a) {
 template <int NMAX>
 __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
   __shared__ GenShared sh;
-  const uint32_t xs = blockIdx.x & 7, i = blockIdx.x >> 3;
-  if (i >= __hip_atomic_load(&a.ap_cnt[xs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // uniform
-  const uint32_t part = a.ap_list[(size_t)xs * a.NB + i];
-  if (apply_part<NMAX, false>(a, part, sh, false)) {  // uniform: the partition goes on to k_follow
-    if (threadIdx.x < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + threadIdx.x] = sh.l_next[threadIdx.x];
-    if (threadIdx.x == 0) a.fl_list[atomicAdd(a.fl_cnt, 1u)] = part;
+  // persistent over the list of its XCD slot: a grid of (resident) workgroups
+  // instead of one per partition, so an empty step costs one wave of exits
+  const uint32_t xs = blockIdx.x & 7, stride = gridDim.x >> 3;
+  const uint32_t nl = __hip_atomic_load(&a.ap_cnt[xs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t i = blockIdx.x >> 3; i < nl; i += stride) {  // uniform
+    const uint32_t part = a.ap_list[(size_t)xs * a.NB + i];
+    if (apply_part<NMAX, false>(a, part, sh, false)) {  // uniform: the partition goes on to k_follow
+      if (threadIdx.x < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + threadIdx.x] = sh.l_next[threadIdx.x];
+      if (threadIdx.x == 0) a.fl_list[atomicAdd(a.fl_cnt, 1u)] = part;
+    }
+    __syncthreads();  // sh is reused by the next partition
+  }
+}
+
+// k_elect: the election lane (hipbatch_elect.h) over k_apply_fast's work
+// lists, before k_apply (n >= 5, unsized logs): a handed-over group whose
+// messages all sit in its route slots is stepped by ElectLane as far as it
+// takes them; a group it finishes leaves the partition's flags, a group it
+// hands over resumes in k_apply at the first message it did not take.
+#ifndef HB_ELECT_WAVES
+#define HB_ELECT_WAVES 4
+#endif
+#ifndef HB_ELECT_GRID
+#define HB_ELECT_GRID 0  // as HB_GEN_GRID
+#endif
+constexpr uint32_t ELECT_GRID = HB_ELECT_GRID;
+static_assert(ELECT_GRID % 8 == 0, "k_elect strides its XCD-slot lists by gridDim.x / 8");
+
+template <int NMAX>
+__global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
+  constexpr uint32_t KS = route_kmax(NMAX);
+  __shared__ uint32_t l_fill;
+  __shared__ uint32_t l_flag[FLAG_WORDS];
+  __shared__ uint32_t l_eflag[FLAG_WORDS];
+  __shared__ uint64_t l_stats[ST_N + 1];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t xs = blockIdx.x & 7, stride = gridDim.x >> 3;
+  const uint32_t nl = __hip_atomic_load(&a.el_cnt[xs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t i = blockIdx.x >> 3; i < nl; i += stride) {  // uniform
+    const uint32_t part = a.el_list[(size_t)xs * a.NB + i];
+    const uint32_t g = part * PART + tid;
+    if (tid < FLAG_WORDS) {
+      l_flag[tid] = a.pflag[(size_t)part * FLAG_WORDS + tid];
+      l_eflag[tid] = a.eflag[(size_t)part * FLAG_WORDS + tid];
+    }
+    if (tid == 0) l_fill = a.ev_counts[2 * part + 1];  // after k_apply_fast's events
+    if (tid <= ST_N) l_stats[tid] = 0;
+    __syncthreads();
+    const bool flagged = (l_eflag[tid >> 5] >> (tid & 31)) & 1u;  // (a subset of the k_apply flags)
+    ElectLane<NMAX> L;
+    L.S = a.S;
+    L.E.chunk = a.ev + a.ev_off[2 * part + 1];
+    L.E.fill = &l_fill;
+    L.g = g;
+    L.meta = flagged ? a.S.meta[g] : 0ull;
+    const uint32_t cnt = flagged ? a.cnt[g] : 0u;
+    const uint32_t resume = flagged ? a.resume[g] : 0u;
+    // (flagged groups are live and not faulted; a pending dense proposal goes to k_apply)
+    const bool mine = flagged && cnt <= KS && (resume >> 31) == 0 && L.self() < L.n();
+    uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
+    bool done = false;
+    uint64_t last0 = 0, commit0 = 0;
+    L.won = L.lost = L.nev = 0;
+    L.committed = L.last = 0;
+    if (mine) {
+      L.load();
+      last0 = L.last;
+      commit0 = ((resume >> 30) & 1u) ? L.committed : a.commit0[g];
+      // arrival order of the slots (odd-even transposition, slot numbers as nibbles)
+      uint32_t key[KS];
+      uint32_t perm = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < KS; ++k) {
+        key[k] = k < cnt ? a.slot_orig[(size_t)k * a.S.G + g] : 0xFFFFFFFFu;
+        perm |= k << (4 * k);
+      }
+#pragma unroll
+      for (uint32_t r = 0; r < KS; ++r) {
+#pragma unroll
+        for (uint32_t k = (r & 1); k + 1 < KS; k += 2) {
+          const uint32_t k0 = key[k], k1 = key[k + 1];
+          const bool sw = k1 < k0;
+          key[k] = sw ? k1 : k0;
+          key[k + 1] = sw ? k0 : k1;
+          const uint32_t p0 = (perm >> (4 * k)) & 0xF, p1 = (perm >> (4 * (k + 1))) & 0xF;
+          const uint32_t swp = (perm & ~(0xFFu << (4 * k))) | (p1 << (4 * k)) | (p0 << (4 * (k + 1)));
+          perm = sw ? swp : perm;
+        }
+      }
+      const uint32_t skip = resume & 0x3FFFFFFFu;
+      uint32_t x = skip;
+      uint32_t inf_n = 0;
+      uint64_t term_n = 0;
+      if (x < cnt) {
+        const size_t o = (size_t)((perm >> (4 * x)) & 0xF) * a.S.G + g;
+        inf_n = a.slot_info[o];
+        term_n = a.slot_term[o];
+      }
+#pragma nounroll
+      for (; x < cnt; ++x) {
+        const uint32_t inf = inf_n;
+        const uint64_t mterm = term_n;
+        if (x + 1 < cnt) {  // the next message's loads before this one is stepped
+          const size_t o = (size_t)((perm >> (4 * (x + 1))) & 0xF) * a.S.G + g;
+          inf_n = a.slot_info[o];
+          term_n = a.slot_term[o];
+        }
+        const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
+        if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
+          st_drop++;
+          continue;
+        }
+        if (!L.takes(type, from, mterm)) break;
+        L.step(type, from, mterm, (inf >> 8) & 1u);
+        st_msgs++;
+        st_app += type == HB_MSG_APP_RESP;
+        st_vote += type == HB_MSG_VOTE_RESP;
+      }
+      if (x > skip) {
+        L.store();
+        if (x == cnt) {
+          done = true;  // the group's batch ends here
+          atomicAnd(&l_flag[tid >> 5], ~(1u << (tid & 31)));
+        } else {  // k_apply resumes at message x, loading what was stored
+          a.resume[g] = x;
+          a.commit0[g] = commit0;
+        }
+      }
+    }
+    const uint64_t vals[ST_N + 1] = {st_msgs,
+                                     st_app,
+                                     st_vote,
+                                     st_drop,
+                                     (uint64_t)(done && L.committed != commit0),
+                                     L.won,
+                                     L.lost,
+                                     0,
+                                     mine ? L.last - last0 : 0ull,
+                                     L.nev};
+    reduce_stats(a, l_stats, vals);  // (ends with a barrier: l_flag and l_fill are final)
+    if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
+    if (tid == 0) a.ev_counts[2 * part + 1] = l_fill;
+    __syncthreads();  // the next partition reuses the LDS
   }
 }
 
@@ -1735,6 +1902,9 @@ struct hb_handle {
   uint32_t* ap_list = nullptr;    // [8][NB]
   uint32_t* fl_cnt = nullptr;     // k_follow work list
   uint32_t* fl_list = nullptr;    // [NB]
+  uint32_t* eflag = nullptr;      // [NB][PART/32] k_elect's groups (n >= 5)
+  uint32_t* el_cnt = nullptr;     // [8] k_elect work lists (counts, reset by the step's finish)
+  uint32_t* el_list = nullptr;    // [8][NB]
   uint32_t* done = nullptr;       // k_apply workgroups finished this step
   uint32_t* resume = nullptr;     // [G]
   uint64_t* commit0 = nullptr;    // [G]
@@ -1803,7 +1973,16 @@ void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
   if (ev) (void)hipEventRecord(ev[2], h->stream);
   hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
   if (ev) (void)hipEventRecord(ev[3], h->stream);
-  hipLaunchKernelGGL(k_apply<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
+  if constexpr (NMAX >= 5) {  // the general kernel spills at n >= 5: elections go first
+#ifndef HB_X_NO_ELECT
+    if (!sz_on(h->max_msg_size))
+#else
+    if (false)
+#endif
+      hipLaunchKernelGGL(k_elect<NMAX>, dim3(ELECT_GRID ? std::min(grid, ELECT_GRID) : grid), dim3(PART), 0,
+                         h->stream, a);
+  }
+  hipLaunchKernelGGL(k_apply<NMAX>, dim3(GEN_GRID ? std::min(grid, GEN_GRID) : grid), dim3(PART), 0, h->stream, a);
   // k_follow's last workgroup also runs the step's finish (k_finish)
   hipLaunchKernelGGL(k_follow<NMAX>, dim3(FOLLOW_GRID), dim3(PART), 0, h->stream, a);
   if (ev && full) (void)hipEventRecord(ev[4], h->stream);
@@ -1924,6 +2103,11 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->ap_list, 8ull * h->NB);
   ALLOC(h->fl_cnt, 4);
   ALLOC(h->fl_list, h->NB);
+  if (h->nmax >= 5) {
+    ALLOC(h->eflag, (size_t)h->NB * FLAG_WORDS);
+    ALLOC(h->el_cnt, 8);
+    ALLOC(h->el_list, 8ull * h->NB);
+  }
   ALLOC(h->done, 4);
   ALLOC(h->resume, G);
   ALLOC(h->commit0, G);
@@ -1954,7 +2138,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
       hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(s.tcfg), 10u | (1u << 16), G) != hipSuccess ||
       hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess || hipMemset(h->stats_shard, 0, 8 * 16 * 8) != hipSuccess ||
       hipMemset(h->ap_cnt, 0, 32) != hipSuccess || hipMemset(h->done, 0, 4) != hipSuccess ||
-      hipMemset(h->fl_cnt, 0, 4) != hipSuccess ||
+      hipMemset(h->fl_cnt, 0, 4) != hipSuccess || (h->el_cnt && hipMemset(h->el_cnt, 0, 32) != hipSuccess) ||
       hipMemset(h->set[0].ev_counts, 0, h->NB * 8ull) != hipSuccess ||
       hipMemset(h->set[0].ev_off, 0, h->NB * 16ull) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
@@ -2482,6 +2666,9 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.ap_list = h->ap_list;
   aa.fl_cnt = h->fl_cnt;
   aa.fl_list = h->fl_list;
+  aa.eflag = h->eflag;
+  aa.el_cnt = h->el_cnt;
+  aa.el_list = h->el_list;
   aa.grid = apply_grid(h);
   aa.done = h->done;
   aa.stats = h->stats;
