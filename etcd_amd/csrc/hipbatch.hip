@@ -784,13 +784,18 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   if (lead) L.load();
   uint32_t s_info[KMAX], s_orig[KMAX];
   uint64_t s_term[KMAX], s_index[KMAX];
+  // a leader's used slots, in the state loads' round trip (both wait for meta
+  // and the count); a group the fast path cannot finish reads none
+  const bool slots = lead && cnt <= KMAX;
 #pragma unroll
-  for (uint32_t k = 0; k < KMAX; ++k) {  // independent of cnt: one round trip (unused slots are ignored)
+  for (uint32_t k = 0; k < KMAX; ++k) {
     const size_t o = (size_t)k * a.S.G + g;
-    s_info[k] = gvalid ? a.slot_info[o] : 0u;
-    s_orig[k] = gvalid ? a.slot_orig[o] : 0u;
-    s_term[k] = gvalid ? a.slot_term[o] : 0ull;
-    s_index[k] = gvalid ? a.slot_index[o] : 0ull;
+    const bool u = slots && k < cnt;
+    s_info[k] = u ? a.slot_info[o] : 0u;
+    s_orig[k] = u ? a.slot_orig[o] : 0u;
+    // (n >= 5: a busier leader's terms too, for k_elect's step-down test below)
+    s_term[k] = (NMAX >= 5 ? lead && k < cnt : u) ? a.slot_term[o] : 0ull;
+    s_index[k] = u ? a.slot_index[o] : 0ull;
   }
   const uint64_t moff = a.ev_off[2 * part + 1];
   const uint64_t last0 = L.last, commit0 = L.committed;
