@@ -72,10 +72,11 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh16, 
 // ============================================================================
 // Phase 1: partition the batch into buckets
 //
-// A bucket is BK = 4096 consecutive group slots (the groups of SIS = 16 apply
-// partitions).  The batch is sorted by bucket id with a stable LSD radix sort,
-// 8-bit digits: one pass up to 256 buckets (1M groups), two passes up to 64K
-// buckets.  A 512-lane workgroup ranks a 2048-message tile stably (ballot
+// A bucket is 2^sis_log consecutive apply partitions (sis_log <= 4: up to
+// 4096 groups; hb_create picks the smallest that needs no extra pass, down to
+// one k_route workgroup per bucket).  The batch is sorted by bucket id with a
+// stable LSD radix sort, 8-bit digits: one pass up to 256 buckets, two up to
+// 64K.  A 512-lane workgroup ranks a 2048-message tile stably (ballot
 // matching inside a wave, per-wave counters across waves), stages it in LDS
 // in digit order and writes each digit's run contiguously, so the global
 // stores are coalesced runs (~8 records per digit per tile) instead of
@@ -84,10 +85,8 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh16, 
 //
 // The final pass writes the apply input: one 24-byte MsgRec per message
 // (info with the group's lane in bits 16-23, arrival index, term, index) and
-// one key byte = the message's partition within its bucket.  Each apply
-// workgroup scans its bucket's key bytes to pick its own messages (the 16
-// sisters of a bucket run on one XCD and share the bucket through its L2),
-// which replaces a second full pass over the batch.
+// one key byte = the message's partition within its bucket (k_route reads the
+// records; the general kernel's bucket walk scans the key bytes).
 // ============================================================================
 struct BatchDev {
   const uint32_t* group;
@@ -99,9 +98,10 @@ struct BatchDev {
   uint64_t n;
 };
 
-constexpr uint32_t SIS_LOG = 4;
-constexpr uint32_t SIS = 1u << SIS_LOG;           // apply partitions per bucket
-constexpr uint32_t BK_LOG = PART_LOG + SIS_LOG;   // groups per bucket = 4096
+// A bucket is 2^sis_log apply partitions (hb_handle::sis_log, chosen at
+// hb_create: at most SIS_MAX, fewer when that costs no extra radix pass, so
+// that one k_route workgroup owns a whole bucket and reads it once).
+constexpr uint32_t SIS_LOG_MAX = 4;
 constexpr uint32_t RDX_BITS = 8;
 constexpr uint32_t RDX_BINS = 1u << RDX_BITS;
 constexpr uint32_t RDX_THREADS = 512;
@@ -140,12 +140,12 @@ struct FinalDst {  // final pass output = apply input
   uint32_t* bucket;  // bucket id per message (multi-pass only, for k_bucket_bounds)
   uint32_t* bk_off;  // [NBK + 1] written by the one-pass scatter
   uint32_t NBK;
+  uint32_t sis_log;  // partitions per bucket (log2)
 };
 
 __device__ __forceinline__ uint32_t src_n(const RadixSrc& s) { return s.n_dev ? *s.n_dev : s.n; }
-__device__ __forceinline__ uint32_t rdx_digit(uint32_t g, uint32_t shift) {
-  return ((g >> BK_LOG) >> shift) & (RDX_BINS - 1);
-}
+// shift = the bucket's log2 size + the pass's digit offset
+__device__ __forceinline__ uint32_t rdx_digit(uint32_t g, uint32_t shift) { return (g >> shift) & (RDX_BINS - 1); }
 
 // Exclusive scan over the first 256 threads of the block (all threads call it).
 __device__ __forceinline__ uint32_t excl_scan256(uint32_t v, uint32_t* sh4, uint32_t* total) {
@@ -323,8 +323,8 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
         m.term = st_term[p];
         m.index = st_index[p];
         f.rec[o] = m;
-        f.key[o] = (uint8_t)((g >> PART_LOG) & (SIS - 1));
-        if (f.bucket) f.bucket[o] = g >> BK_LOG;
+        f.key[o] = (uint8_t)((g >> PART_LOG) & ((1u << f.sis_log) - 1));
+        if (f.bucket) f.bucket[o] = g >> (PART_LOG + f.sis_log);
       } else {
         d.group[o] = g;
         d.info[o] = st_info[p];
@@ -378,6 +378,7 @@ struct ApplyArgs {
   uint32_t* el_cnt;         // [8]   leader, or a leader with a higher-term message in its slots;
   uint32_t* el_list;        // [8][NB]  k_elect's work lists (per XCD slot, as ap_list)
   uint32_t grid;            // apply_grid: virtual workgroups of the partition mapping (part_of)
+  uint32_t sis_log;         // partitions per bucket (log2)
   uint32_t* done;           // k_apply workgroups finished (the last one runs the finish)
   uint64_t* stats;          // [HB_STAT_COUNT] this step's statistics (finish)
   uint64_t* accum;          // caller accumulator or null (finish)
@@ -410,11 +411,11 @@ enum { ST_MSGS, ST_APPRESP, ST_VOTERESP, ST_DROPPED, ST_COMMITS, ST_WON, ST_LOST
 __device__ uint64_t g_stamps[1 << 20];
 #define XSTAMP(k)                                                                          \
   do {                                                                                     \
-    if (threadIdx.x == 0) g_stamps[(size_t)block_part() * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0) g_stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #define XSTAMP_RT(k)                                                                       \
   do {                                                                                     \
-    if (threadIdx.x == 0) g_stamps[(size_t)block_part() * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (threadIdx.x == 0) g_stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define XSTAMP(k) \
@@ -432,14 +433,14 @@ constexpr uint32_t FLAG_WORDS = PART / 32;  // per-partition bitmask of groups h
 constexpr uint32_t KPL = 64;                // bucket key bytes scanned per lane per segment
 constexpr uint32_t SEG = PART * KPL;        // positions per key-scan segment
 
-// blockIdx -> partition.  The SIS sister partitions of a bucket get block ids
+// blockIdx -> partition.  The sister partitions of a bucket get block ids
 // with equal blockIdx % 8, i.e. one XCD under the round-robin placement, so
 // the bucket's keys and records are fetched into one L2 (speed only).
-__device__ __forceinline__ uint32_t part_of(uint32_t x) {
+__device__ __forceinline__ uint32_t part_of(uint32_t x, uint32_t sl) {
   const uint32_t r = x & 7, q = x >> 3;
-  return ((((q >> SIS_LOG) << 3) | r) << SIS_LOG) | (q & (SIS - 1));
+  return ((((q >> sl) << 3) | r) << sl) | (q & ((1u << sl) - 1));
 }
-__device__ __forceinline__ uint32_t block_part() { return part_of(blockIdx.x); }
+__device__ __forceinline__ uint32_t block_part(uint32_t sl) { return part_of(blockIdx.x, sl); }
 
 // LDS staging of one round (<= CH messages) of a partition's messages.
 // w[j][i] = word j of the round's i-th MsgRec (info, orig, term lo/hi, index lo/hi).
@@ -653,16 +654,18 @@ constexpr uint32_t ROUTE_THREADS = 1024;
 #define HB_ROUTE_UNROLL 4
 #endif
 constexpr uint32_t ROUTE_UNROLL = HB_ROUTE_UNROLL;  // records in flight per lane
+constexpr uint32_t route_rg_log(uint32_t kmax) { return kmax <= 2 ? 11 : (kmax <= 4 ? 10 : 9); }
 template <int KMAX> struct RouteGeom {
-  static constexpr uint32_t RG_LOG = KMAX <= 2 ? 11 : (KMAX <= 4 ? 10 : 9);
+  static constexpr uint32_t RG_LOG = route_rg_log(KMAX);
   static constexpr uint32_t RG = 1u << RG_LOG;     // groups per workgroup
-  static constexpr uint32_t W = (1u << BK_LOG) / RG;  // workgroups per bucket
+  // workgroups per bucket: 2^(PART_LOG + sis_log - RG_LOG) (sis_log >= RG_LOG - PART_LOG)
 };
 
 template <int KMAX>
 __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   using RGm = RouteGeom<KMAX>;
-  constexpr uint32_t RG = RGm::RG, W = RGm::W, NP = RG / PART;
+  constexpr uint32_t RG = RGm::RG, NP = RG / PART;
+  const uint32_t sl = a.sis_log, W = 1u << (PART_LOG + sl - RGm::RG_LOG);
   __shared__ uint32_t l_cnt[RG];
   __shared__ uint32_t l_info[KMAX][RG];
   __shared__ uint32_t l_orig[KMAX][RG];
@@ -707,7 +710,7 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
     }
   }
   __syncthreads();
-  const uint32_t gbase = (bk << BK_LOG) + lg0;
+  const uint32_t gbase = (bk << (PART_LOG + sl)) + lg0;
   for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) {
     const uint32_t c = l_cnt[i], g = gbase + i;
     if (g < G) {
@@ -730,11 +733,11 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   }
   __syncthreads();
   if (tid < NP) {
-    const uint32_t part = (bk << SIS_LOG) + w * NP + tid;
+    const uint32_t part = (bk << sl) + w * NP + tid;
     if (part < a.NB) {
       const uint32_t r = atomicAdd(&a.bk_fill[bk], a.ev_per_msg * (l_ptot[tid] + PART * a.props_on));
       a.ev_off[2 * part + 1] =
-          (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + lo + (uint64_t)bk * (PART * SIS) * a.props_on) + r;
+          (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + lo + ((uint64_t)bk * PART << sl) * a.props_on) + r;
     }
   }
 }
@@ -756,7 +759,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   __shared__ uint32_t l_eflag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
 
-  const uint32_t part = block_part();
+  const uint32_t part = block_part(a.sis_log);
   if (part >= a.NB) return;  // uniform: grid padding
   const uint32_t tid = threadIdx.x;
   const uint32_t g = part * PART + tid;
@@ -951,7 +954,7 @@ struct GenShared {
 template <int NMAX, bool FOLLOW>
 __device__ __forceinline__ bool apply_part(const ApplyArgs& a, uint32_t part, GenShared& sh, bool chained) {
   const uint32_t tid = threadIdx.x;
-  const uint32_t bk = part >> SIS_LOG, sub = part & (SIS - 1);
+  const uint32_t bk = part >> a.sis_log, sub = part & ((1u << a.sis_log) - 1);
   const uint32_t g = part * PART + tid;
   const uint32_t fill0 = chained ? sh.l_fill : a.ev_counts[2 * part + 1];
   if (tid < FLAG_WORDS) {
@@ -1360,7 +1363,7 @@ template <int NMAX>
 __global__ void __launch_bounds__(PART, 2) k_tick(ApplyArgs a) {
   __shared__ uint32_t l_fill;
   __shared__ uint64_t l_stats[ST_N + 1];
-  const uint32_t part = block_part();
+  const uint32_t part = block_part(a.sis_log);
   if (part >= a.NB) return;  // uniform: grid padding
   const uint32_t tid = threadIdx.x;
   const uint32_t g = part * PART + tid;
@@ -1879,6 +1882,7 @@ struct hb_handle {
   PrepSet set[2];
   uint32_t next_set = 0, cur = 0;  // set of the next / the last step
   uint32_t NBK = 0;               // buckets
+  uint32_t sis_log = SIS_LOG_MAX;  // partitions per bucket (log2)
   uint32_t passes = 1;
   // host-pointer staging
   uint32_t* s_group = nullptr;
@@ -1964,12 +1968,12 @@ uint32_t ceil_log2(uint32_t x) {
 
 template <int KMAX>
 void launch_route(hb_handle* h, const ApplyArgs& a, hipStream_t st) {
-  const uint32_t grid = ((h->NBK + 7) & ~7u) * RouteGeom<KMAX>::W;
+  const uint32_t grid = ((h->NBK + 7) & ~7u) << (PART_LOG + h->sis_log - RouteGeom<KMAX>::RG_LOG);
   hipLaunchKernelGGL(k_route<KMAX>, dim3(grid), dim3(ROUTE_THREADS), 0, st, a);
 }
 
-// XCD-aware grid (see block_part()): whole groups of 8 buckets x SIS partitions.
-uint32_t apply_grid(const hb_handle* h) { return ((h->NBK + 7) & ~7u) * SIS; }
+// XCD-aware grid (see block_part()): whole groups of 8 buckets x 2^sis_log partitions.
+uint32_t apply_grid(const hb_handle* h) { return ((h->NBK + 7) & ~7u) << h->sis_log; }
 
 // The apply kernels; ev = this step's phase events (HB_STEP_PROFILE) or null.
 template <int NMAX>
@@ -2059,9 +2063,19 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   }
   // partition scratch
   const size_t mb = max_batch ? max_batch : 1;
-  h->NBK = (capacity + (1u << BK_LOG) - 1) >> BK_LOG;
-  const uint32_t pbits = std::max<uint32_t>(ceil_log2(h->NBK), 1);
-  h->passes = (pbits + RDX_BITS - 1) / RDX_BITS;
+  // buckets: SIS_MAX partitions each, or fewer — down to one k_route
+  // workgroup per bucket — while that needs no extra radix pass
+  auto nbk_for = [&](uint32_t sl) { return (capacity + (PART << sl) - 1) / (PART << sl); };
+  auto passes_for = [&](uint32_t sl) {
+    return (std::max<uint32_t>(ceil_log2(nbk_for(sl)), 1) + RDX_BITS - 1) / RDX_BITS;
+  };
+  h->sis_log = SIS_LOG_MAX;
+#ifndef HB_FIXED_SIS
+  const uint32_t sl_min = route_rg_log(route_kmax(h->nmax)) - PART_LOG;
+  while (h->sis_log > sl_min && passes_for(h->sis_log - 1) == passes_for(SIS_LOG_MAX)) --h->sis_log;
+#endif
+  h->NBK = nbk_for(h->sis_log);
+  h->passes = passes_for(h->sis_log);
   const size_t tiles_max = (mb + RDX_TILE - 1) / RDX_TILE;
   ALLOC(h->hist, (size_t)RDX_BINS * tiles_max);
   ALLOC(h->n_valid, 4);
@@ -2100,7 +2114,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   // events: (batch + one proposal slot per group) x EV_MAX (exact bound)
   h->ev_per_msg = EVC_WORDS_MAX * (h->nmax + 4);  // events per message <= nmax + 4, <= 2 words each
   // P chunks (one per partition, dense proposals) then the bucket regions of M chunks
-  h->ev_region = ((uint64_t)h->NB * PART + mb + (uint64_t)h->NBK * (PART * SIS)) * h->ev_per_msg;
+  h->ev_region = ((uint64_t)h->NB * PART + mb + ((uint64_t)h->NBK * PART << h->sis_log)) * h->ev_per_msg;
   ALLOC(h->ev, h->ev_region);
   ALLOC(h->stats_shard, 8 * 16);
   ALLOC(h->pflag, (size_t)h->NB * FLAG_WORDS);
@@ -2508,6 +2522,7 @@ int hb_tick(hb_handle* h, uint32_t flags) {
   aa.ev_per_msg = h->ev_per_msg;
   aa.NB = h->NB;
   aa.NBK = h->NBK;
+  aa.sis_log = h->sis_log;
   aa.ev_counts = ps.ev_counts;
   aa.ev_off = ps.ev_off;
   aa.stats_shard = h->stats_shard;
@@ -2636,11 +2651,11 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   } else {
     const uint32_t ntiles = (uint32_t)((b->n + RDX_TILE - 1) / RDX_TILE);
     RadixSrc src{bd.group, bd.info, nullptr, bd.term, bd.index, nullptr, (uint32_t)b->n};
-    const FinalDst fin{ps.rec, ps.key, ps.bucket, h->passes == 1 ? ps.bk_off : nullptr, h->NBK};
+    const FinalDst fin{ps.rec, ps.key, ps.bucket, h->passes == 1 ? ps.bk_off : nullptr, h->NBK, h->sis_log};
     for (uint32_t p = 0; p < h->passes; ++p) {
       const bool last_pass = p + 1 == h->passes;
       const RadixDst& dst = h->tmp[p & 1];
-      const uint32_t shift = p * RDX_BITS;
+      const uint32_t shift = PART_LOG + h->sis_log + p * RDX_BITS;
       hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, h->G, shift, ntiles, h->hist);
       hipLaunchKernelGGL(k_scan_rows, dim3(RDX_BINS), dim3(1024), 0, ps_st, h->hist, ntiles, h->totals, h->bk_fill,
                          h->NBK);
@@ -2675,6 +2690,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.el_cnt = h->el_cnt;
   aa.el_list = h->el_list;
   aa.grid = apply_grid(h);
+  aa.sis_log = h->sis_log;
   aa.done = h->done;
   aa.stats = h->stats;
   aa.accum = h->stats_accum;
