@@ -621,7 +621,8 @@ __device__ __forceinline__ bool is_response(uint32_t type) {  // raft/util.go:53
 // it reserved) to this XCD slot's shard of the step statistics: one no-return
 // atomic per value per workgroup, spread over 8 shards; k_finish sums them.
 // vals[ST_N] = the lane's events (public count).
-__device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_stats, const uint64_t (&vals)[ST_N + 1]) {
+template <class T>
+__device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_stats, const T (&vals)[ST_N + 1]) {
   const uint32_t tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k <= ST_N; ++k) {
@@ -751,6 +752,144 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
 // the lane's bit is set in pflag[part] and resume[g] = messages already
 // consumed | prop-pending bit.
 // ---------------------------------------------------------------------------
+// The fast lane's work on one group once its loads are in: the dense proposal into the
+// partition's P chunk, then the slot messages in arrival order into its M
+// chunk, as far as FastLane takes them.  Sets the group's hand-over bit in
+// l_flag (and, n >= 5, its k_elect bit in l_eflag), resume / commit0, and
+// returns the statistics of the lane.
+template <int NMAX>
+__device__ __forceinline__ bool fast_step(const ApplyArgs& a, FastLane<NMAX>& L, uint32_t part, uint32_t lane,
+                                          bool live, bool lead, uint32_t prop_raw, uint32_t cnt,
+                                          uint32_t (&s_info)[NMAX - 1], uint32_t (&s_orig)[NMAX - 1],
+                                          uint64_t (&s_term)[NMAX - 1], uint64_t (&s_index)[NMAX - 1],
+                                          uint64_t moff, uint32_t* l_pfill, uint32_t* l_fill, uint32_t* l_flag,
+                                          uint32_t* l_eflag, uint32_t (&vals)[ST_N + 1]) {
+  constexpr uint32_t KMAX = NMAX - 1;
+  const uint32_t g = part * PART + lane;
+  const uint64_t last0 = L.last, commit0 = L.committed;
+
+  bool flagged = false;
+  uint32_t resume = 0;
+  uint32_t st_msgs = 0, st_drop = 0;
+
+  // ---- the dense proposal: its events go to the partition's P chunk (fixed
+  // slot of ev_per_msg x PART words), before any message event of the group.
+  const uint64_t poff = (uint64_t)part * PART * a.ev_per_msg;
+  if (lane == 0) a.ev_off[2 * part] = poff;
+  L.E.chunk = a.ev + poff;
+  L.E.fill = l_pfill;
+  const uint32_t prop_k = live ? prop_raw : 0u;
+  if (prop_k) {
+    if (L.prop_ok(prop_k)) {
+      L.arrival = 0xFFFFFFFFu;
+      L.prop(prop_k);
+    } else {
+      flagged = true;
+      resume = 1u << 31;  // the proposal itself is pending (stepped by k_apply into the M chunk)
+    }
+  }
+
+  // ---- the lane's messages, arrival order (M chunk reserved by k_route).  The
+  // slots arrive in k_route's counter order: sort them by arrival index
+  // (odd-even transposition over KMAX registers; unused slots sort last).
+#pragma unroll
+  for (uint32_t k = 0; k < KMAX; ++k) s_orig[k] = k < cnt ? s_orig[k] : 0xFFFFFFFFu;
+#pragma unroll
+  for (uint32_t r = 0; r < KMAX; ++r) {
+#pragma unroll
+    for (uint32_t k = (r & 1); k + 1 < KMAX; k += 2) {
+      const bool sw = s_orig[k + 1] < s_orig[k];
+      const uint32_t i0 = s_info[k], o0 = s_orig[k];
+      const uint64_t t0 = s_term[k], x0 = s_index[k];
+      s_info[k] = sw ? s_info[k + 1] : i0;
+      s_orig[k] = sw ? s_orig[k + 1] : o0;
+      s_term[k] = sw ? s_term[k + 1] : t0;
+      s_index[k] = sw ? s_index[k + 1] : x0;
+      s_info[k + 1] = sw ? i0 : s_info[k + 1];
+      s_orig[k + 1] = sw ? o0 : s_orig[k + 1];
+      s_term[k + 1] = sw ? t0 : s_term[k + 1];
+      s_index[k + 1] = sw ? x0 : s_index[k + 1];
+    }
+  }
+  L.E.chunk = a.ev + moff;
+  L.E.fill = l_fill;
+  uint32_t j = 0;  // messages consumed
+  if (live && !lead && cnt > 0 && !flagged) {
+    flagged = true;
+    resume = 0;
+  }
+  if (live && cnt > KMAX && !flagged && !L.faulted()) {  // the slots hold an arbitrary KMAX: all to k_apply
+    flagged = true;
+    resume = 0;
+  }
+  if (lead) {
+#pragma unroll
+    for (uint32_t k = 0; k < KMAX; ++k) {
+      if (k >= cnt || flagged || L.faulted()) break;
+      const uint32_t inf = s_info[k];
+      const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
+      const bool reject = (inf >> 8) & 1u;
+      if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
+        st_drop++;
+        j++;
+        continue;
+      }
+      if (!L.accept_ok(type, from, s_term[k], reject)) {
+        flagged = true;
+        resume = j;
+        break;
+      }
+      L.arrival = s_orig[k];
+      L.accept(from, s_index[k]);
+      st_msgs++;
+      j++;
+    }
+  }
+
+  if (lead) L.store();
+  if constexpr (NMAX >= 5) {  // k_elect's candidates: an election (or a step-down) is likely
+    bool higher = false;
+#pragma unroll
+    for (uint32_t k = 0; k < KMAX; ++k) higher |= k < cnt && s_term[k] > L.term;
+    if (flagged && (!lead || higher)) atomicOr(&l_eflag[lane >> 5], 1u << (lane & 31));
+  }
+  if (flagged) {
+    atomicOr(&l_flag[lane >> 5], 1u << (lane & 31));
+    a.resume[g] = resume | (lead ? 0u : 1u << 30);
+    if (lead) a.commit0[g] = commit0;
+  }
+  vals[ST_MSGS] = st_msgs;
+  vals[ST_APPRESP] = st_msgs;  // every fast message is a MsgAppResp
+  vals[ST_VOTERESP] = 0;
+  vals[ST_DROPPED] = st_drop;
+  vals[ST_COMMITS] = (uint32_t)(!flagged && L.committed != commit0);  // commitTo only raises
+  vals[ST_WON] = 0;
+  vals[ST_LOST] = 0;
+  vals[ST_FAULTS] = (uint32_t)(L.faulted() != 0 && live);
+  vals[ST_ENTRIES] = (uint32_t)(L.last - last0);  // (entries appended to one group in one step)
+  vals[ST_N] = L.nev;
+  return flagged;
+}
+
+// The partition's bookkeeping after its lanes (one lane: `lane == 0`'s thread):
+// event fills, and the k_apply / k_elect work lists of this XCD slot.
+__device__ __forceinline__ void fast_close(const ApplyArgs& a, uint32_t part, const uint32_t* l_flag,
+                                           const uint32_t* l_eflag, uint32_t pfill, uint32_t fill) {
+  a.ev_counts[2 * part] = pfill;
+  a.ev_counts[2 * part + 1] = fill;
+  uint32_t any = 0, eany = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < FLAG_WORDS; ++w) {
+    any |= l_flag[w];
+    eany |= l_eflag ? l_eflag[w] : 0u;
+  }
+  const uint32_t xs = blockIdx.x & 7;
+  if (any)  // the partition joins k_apply's list of its XCD slot
+    a.ap_list[(size_t)xs * a.NB + atomicAdd(&a.ap_cnt[xs], 1u)] = part;
+  if (eany)  // ... and k_elect's
+    a.el_list[(size_t)xs * a.NB + atomicAdd(&a.el_cnt[xs], 1u)] = part;
+}
+
 template <int NMAX>
 __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply_fast(ApplyArgs a) {
   constexpr uint32_t KMAX = NMAX - 1;  // one MsgAppResp per follower per batch
@@ -800,129 +939,15 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
     s_term[k] = (NMAX >= 5 ? lead && k < cnt : u) ? a.slot_term[o] : 0ull;
     s_index[k] = u ? a.slot_index[o] : 0ull;
   }
-  const uint64_t moff = a.ev_off[2 * part + 1];
-  const uint64_t last0 = L.last, commit0 = L.committed;
-
-  bool flagged = false;
-  uint32_t resume = 0;
-  uint32_t st_msgs = 0, st_drop = 0;
-
-  // ---- the dense proposal: its events go to the partition's P chunk (fixed
-  // slot of ev_per_msg x PART words), before any message event of the group.
-  const uint64_t poff = (uint64_t)part * PART * a.ev_per_msg;
-  if (tid == 0) a.ev_off[2 * part] = poff;
-  L.E.chunk = a.ev + poff;
-  L.E.fill = &l_pfill;
-  const uint32_t prop_k = live ? prop_raw : 0u;
-  if (prop_k) {
-    if (L.prop_ok(prop_k)) {
-      L.arrival = 0xFFFFFFFFu;
-      L.prop(prop_k);
-    } else {
-      flagged = true;
-      resume = 1u << 31;  // the proposal itself is pending (stepped by k_apply into the M chunk)
-    }
-  }
-
-  // ---- the lane's messages, arrival order (M chunk reserved by k_route).  The
-  // slots arrive in k_route's counter order: sort them by arrival index
-  // (odd-even transposition over KMAX registers; unused slots sort last).
-#pragma unroll
-  for (uint32_t k = 0; k < KMAX; ++k) s_orig[k] = k < cnt ? s_orig[k] : 0xFFFFFFFFu;
-#pragma unroll
-  for (uint32_t r = 0; r < KMAX; ++r) {
-#pragma unroll
-    for (uint32_t k = (r & 1); k + 1 < KMAX; k += 2) {
-      const bool sw = s_orig[k + 1] < s_orig[k];
-      const uint32_t i0 = s_info[k], o0 = s_orig[k];
-      const uint64_t t0 = s_term[k], x0 = s_index[k];
-      s_info[k] = sw ? s_info[k + 1] : i0;
-      s_orig[k] = sw ? s_orig[k + 1] : o0;
-      s_term[k] = sw ? s_term[k + 1] : t0;
-      s_index[k] = sw ? s_index[k + 1] : x0;
-      s_info[k + 1] = sw ? i0 : s_info[k + 1];
-      s_orig[k + 1] = sw ? o0 : s_orig[k + 1];
-      s_term[k + 1] = sw ? t0 : s_term[k + 1];
-      s_index[k + 1] = sw ? x0 : s_index[k + 1];
-    }
-  }
-  L.E.chunk = a.ev + moff;
-  L.E.fill = &l_fill;
-  uint32_t j = 0;  // messages consumed
-  if (live && !lead && cnt > 0 && !flagged) {
-    flagged = true;
-    resume = 0;
-  }
-  if (live && cnt > KMAX && !flagged && !L.faulted()) {  // the slots hold an arbitrary KMAX: all to k_apply
-    flagged = true;
-    resume = 0;
-  }
-  if (lead) {
-#pragma unroll
-    for (uint32_t k = 0; k < KMAX; ++k) {
-      if (k >= cnt || flagged || L.faulted()) break;
-      const uint32_t inf = s_info[k];
-      const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
-      const bool reject = (inf >> 8) & 1u;
-      if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
-        st_drop++;
-        j++;
-        continue;
-      }
-      if (!L.accept_ok(type, from, s_term[k], reject)) {
-        flagged = true;
-        resume = j;
-        break;
-      }
-      L.arrival = s_orig[k];
-      L.accept(from, s_index[k]);
-      st_msgs++;
-      j++;
-    }
-  }
-
-  if (lead) L.store();
-  if constexpr (NMAX >= 5) {  // k_elect's candidates: an election (or a step-down) is likely
-    bool higher = false;
-#pragma unroll
-    for (uint32_t k = 0; k < KMAX; ++k) higher |= k < cnt && s_term[k] > L.term;
-    if (flagged && (!lead || higher)) atomicOr(&l_eflag[tid >> 5], 1u << (tid & 31));
-  }
-  if (flagged) {
-    atomicOr(&l_flag[tid >> 5], 1u << (tid & 31));
-    a.resume[g] = resume | (lead ? 0u : 1u << 30);
-    if (lead) a.commit0[g] = commit0;
-  }
-  const uint64_t vals[ST_N + 1] = {st_msgs,
-                                   st_msgs,  // every fast message is a MsgAppResp
-                                   0,
-                                   st_drop,
-                                   (uint64_t)(!flagged && L.committed != commit0),  // commitTo only raises
-                                   0,
-                                   0,
-                                   (uint64_t)(L.faulted() != 0 && live),
-                                   L.last - last0,
-                                   L.nev};
+  uint32_t vals[ST_N + 1];
+  (void)fast_step<NMAX>(a, L, part, tid, live, lead, prop_raw, cnt, s_info, s_orig, s_term, s_index,
+                        a.ev_off[2 * part + 1], &l_pfill, &l_fill, l_flag, l_eflag, vals);
   reduce_stats(a, l_stats, vals);
   if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
   if constexpr (NMAX >= 5) {
     if (tid < FLAG_WORDS) a.eflag[(size_t)part * FLAG_WORDS + tid] = l_eflag[tid];
   }
-  if (tid == 0) {
-    a.ev_counts[2 * part] = l_pfill;
-    a.ev_counts[2 * part + 1] = l_fill;
-    uint32_t any = 0, eany = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < FLAG_WORDS; ++w) {
-      any |= l_flag[w];
-      eany |= l_eflag[w];
-    }
-    const uint32_t xs = blockIdx.x & 7;
-    if (any)  // the partition joins k_apply's list of its XCD slot
-      a.ap_list[(size_t)xs * a.NB + atomicAdd(&a.ap_cnt[xs], 1u)] = part;
-    if (eany)  // ... and k_elect's
-      a.el_list[(size_t)xs * a.NB + atomicAdd(&a.el_cnt[xs], 1u)] = part;
-  }
+  if (tid == 0) fast_close(a, part, l_flag, NMAX >= 5 ? l_eflag : nullptr, l_pfill, l_fill);
 }
 
 // ---------------------------------------------------------------------------
@@ -1850,6 +1875,7 @@ struct PrepSet {
   uint8_t* key = nullptr;         // partition-in-bucket per record (+ SEG bytes of padding)
   uint32_t* bucket = nullptr;     // bucket id per record (multi-pass only)
   uint32_t* bk_off = nullptr;     // [NBK + 1]
+  uint32_t* bk_fill = nullptr;    // [NBK] event words reserved in each bucket's region (k_route)
   uint8_t* cnt = nullptr;         // [G]
   uint32_t* slot_info = nullptr;  // [nmax-1][G]
   uint32_t* slot_orig = nullptr;
@@ -1878,7 +1904,6 @@ struct hb_handle {
   uint32_t* n_valid = nullptr;    // messages kept after pass 1 (device)
   uint32_t* totals = nullptr;     // [RDX_BINS] digit totals of the current pass
   RadixDst tmp[2] = {};           // intermediate passes (ping-pong)
-  uint32_t* bk_fill = nullptr;    // [NBK]
   PrepSet set[2];
   uint32_t next_set = 0, cur = 0;  // set of the next / the last step
   uint32_t NBK = 0;               // buckets
@@ -1967,9 +1992,12 @@ uint32_t ceil_log2(uint32_t x) {
 }
 
 template <int KMAX>
+uint32_t route_grid(const hb_handle* h) {
+  return ((h->NBK + 7) & ~7u) << (PART_LOG + h->sis_log - RouteGeom<KMAX>::RG_LOG);
+}
+template <int KMAX>
 void launch_route(hb_handle* h, const ApplyArgs& a, hipStream_t st) {
-  const uint32_t grid = ((h->NBK + 7) & ~7u) << (PART_LOG + h->sis_log - RouteGeom<KMAX>::RG_LOG);
-  hipLaunchKernelGGL(k_route<KMAX>, dim3(grid), dim3(ROUTE_THREADS), 0, st, a);
+  hipLaunchKernelGGL(k_route<KMAX>, dim3(route_grid<KMAX>(h)), dim3(ROUTE_THREADS), 0, st, a);
 }
 
 // XCD-aware grid (see block_part()): whole groups of 8 buckets x 2^sis_log partitions.
@@ -2080,7 +2108,6 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->hist, (size_t)RDX_BINS * tiles_max);
   ALLOC(h->n_valid, 4);
   ALLOC(h->totals, RDX_BINS);
-  ALLOC(h->bk_fill, h->NBK);
   for (uint32_t k = 0; k + 1 < h->passes && k < 2; ++k) {  // ping-pong buffers of intermediate passes
     RadixDst& d = h->tmp[k];
     ALLOC(d.group, mb);
@@ -2094,6 +2121,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
     ALLOC(ps.key, mb + SEG);
     if (h->passes > 1) ALLOC(ps.bucket, mb);
     ALLOC(ps.bk_off, h->NBK + 1);
+    ALLOC(ps.bk_fill, h->NBK);
     ALLOC(ps.cnt, G);
     ALLOC(ps.slot_info, route_kmax(R) * G);
     ALLOC(ps.slot_orig, route_kmax(R) * G);
@@ -2647,7 +2675,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   const uint32_t NB = h->NB;
   if (b->n == 0) {
     HB_CHECK(hipMemsetAsync(ps.bk_off, 0, (h->NBK + 1) * 4ull, ps_st));
-    HB_CHECK(hipMemsetAsync(h->bk_fill, 0, h->NBK * 4ull, ps_st));
+    HB_CHECK(hipMemsetAsync(ps.bk_fill, 0, h->NBK * 4ull, ps_st));
   } else {
     const uint32_t ntiles = (uint32_t)((b->n + RDX_TILE - 1) / RDX_TILE);
     RadixSrc src{bd.group, bd.info, nullptr, bd.term, bd.index, nullptr, (uint32_t)b->n};
@@ -2657,7 +2685,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
       const RadixDst& dst = h->tmp[p & 1];
       const uint32_t shift = PART_LOG + h->sis_log + p * RDX_BITS;
       hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, h->G, shift, ntiles, h->hist);
-      hipLaunchKernelGGL(k_scan_rows, dim3(RDX_BINS), dim3(1024), 0, ps_st, h->hist, ntiles, h->totals, h->bk_fill,
+      hipLaunchKernelGGL(k_scan_rows, dim3(RDX_BINS), dim3(1024), 0, ps_st, h->hist, ntiles, h->totals, ps.bk_fill,
                          h->NBK);
       if (last_pass)
         hipLaunchKernelGGL(k_radix_scatter<true>, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
@@ -2697,7 +2725,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.rec = ps.rec;
   aa.key = ps.key;
   aa.bk_off = ps.bk_off;
-  aa.bk_fill = h->bk_fill;
+  aa.bk_fill = ps.bk_fill;
   aa.hint = bd.hint;
   aa.props = bd.props;
   aa.ev = h->ev;
