@@ -102,6 +102,8 @@ struct BatchDev {
 // hb_create: at most SIS_MAX, fewer when that costs no extra radix pass, so
 // that one k_route workgroup owns a whole bucket and reads it once).
 constexpr uint32_t SIS_LOG_MAX = 4;
+// a prep set's counters: k_apply's 8 work-list lengths, k_elect's 8, k_follow's, the finish ticket
+enum : uint32_t { CTR_AP = 0, CTR_EL = 8, CTR_FL = 16, CTR_DONE = 17, CTR_WORDS = 32 };
 constexpr uint32_t RDX_BITS = 8;
 constexpr uint32_t RDX_BINS = 1u << RDX_BITS;
 constexpr uint32_t RDX_THREADS = 512;
@@ -188,11 +190,12 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t
 // into one L2 once.  It also clears the per-bucket event-chunk cursors for
 // the coming apply.
 __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t ntiles, uint32_t* totals,
-                                                    uint32_t* bk_fill, uint32_t NBK) {
+                                                    uint32_t* bk_fill, uint32_t NBK, uint32_t* ctr) {
   __shared__ uint32_t sh16[16];
   const uint32_t d = (blockIdx.x & 7) * (RDX_BINS / 8) + (blockIdx.x >> 3);
   uint32_t* col = hist + d;
   for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < NBK; i += gridDim.x * 1024) bk_fill[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < CTR_WORDS) ctr[threadIdx.x] = 0;
   uint32_t carry = 0;
   for (uint32_t base = 0; base < ntiles; base += 4096) {
     const uint32_t i0 = base + threadIdx.x * 4;
@@ -1174,6 +1177,10 @@ constexpr uint32_t FOLLOW_GRID = HB_FOLLOW_GRID;
 #define HB_GEN_GRID 0
 #endif
 constexpr uint32_t GEN_GRID = HB_GEN_GRID;
+#ifndef HB_GEN_GRID3
+#define HB_GEN_GRID3 512  // n = 3 (cfg2 / cfg5: few partitions handed over): persistent, 2 per CU
+#endif
+constexpr uint32_t GEN_GRID3 = HB_GEN_GRID3;
 static_assert(GEN_GRID % 8 == 0, "k_apply strides its XCD-slot lists by gridDim.x / 8");
 
 // The step's finish (as k_finish), run by the last k_follow workgroup: the
@@ -1193,31 +1200,64 @@ __device__ __forceinline__ void finish_step(const ApplyArgs& a) {
     a.stats[map[k]] = v;
     if (a.accum) a.accum[map[k]] += v;
   }
-  if (k < 8) {
-    __hip_atomic_store(&a.ap_cnt[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.el_cnt) __hip_atomic_store(&a.el_cnt[k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (k == 0) {
-    __hip_atomic_store(a.fl_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
+// The workgroups that finish the step take tickets; the step's finish runs
+// in the last.  Only workgroups that had work take one (`working` of them, a
+// count every workgroup derives from the work-list lengths): a ticket per
+// workgroup of the grid serialises hundreds of atomics on one word (~11 ns
+// each).  With no work anywhere, workgroup 0 finishes at once.  (The
+// work-list counters and the ticket word belong to the prep set and are
+// cleared by the next prep that reuses it, never by a workgroup still
+// reading them.)
+__device__ __forceinline__ void finish_by_ticket(const ApplyArgs& a, bool worked, uint32_t working,
+                                                 uint32_t* l_last) {
+  if (working == 0) {
+    if (blockIdx.x == 0) finish_step(a);  // uniform
+    return;
+  }
+  if (!worked) return;  // uniform
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's stats atomics are performed
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *l_last = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == working - 1;
+  __syncthreads();
+  if (*l_last) finish_step(a);  // uniform
+}
+
+// CHAIN (n = 3): the follower-side pass runs chained in the same workgroup
+// and k_apply's last workgroup runs the step's finish — no k_follow launch
+// (n = 3's general kernel does not spill either way; at n >= 5 the follower
+// lane's registers stay out of the hot general kernel).
 template <int NMAX>
 __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
+  constexpr bool CHAIN = NMAX <= 3;
   __shared__ GenShared sh;
-  // persistent over the list of its XCD slot: a grid of (resident) workgroups
-  // instead of one per partition, so an empty step costs one wave of exits
+  __shared__ uint32_t l_last;
+  // persistent over the list of its XCD slot when the grid is smaller than
+  // the partitions (HB_GEN_GRID)
   const uint32_t xs = blockIdx.x & 7, stride = gridDim.x >> 3;
-  const uint32_t nl = __hip_atomic_load(&a.ap_cnt[xs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t nl = 0, working = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) {
+    const uint32_t c = __hip_atomic_load(&a.ap_cnt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    nl = k == xs ? c : nl;
+    working += c < stride ? c : stride;  // workgroups of slot k with at least one entry
+  }
   for (uint32_t i = blockIdx.x >> 3; i < nl; i += stride) {  // uniform
     const uint32_t part = a.ap_list[(size_t)xs * a.NB + i];
-    if (apply_part<NMAX, false>(a, part, sh, false)) {  // uniform: the partition goes on to k_follow
-      if (threadIdx.x < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + threadIdx.x] = sh.l_next[threadIdx.x];
-      if (threadIdx.x == 0) a.fl_list[atomicAdd(a.fl_cnt, 1u)] = part;
+    if (apply_part<NMAX, false>(a, part, sh, false)) {  // uniform: the partition goes on to the follower pass
+      if constexpr (CHAIN) {
+        __syncthreads();
+        (void)apply_part<NMAX, true>(a, part, sh, true);
+      } else {
+        if (threadIdx.x < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + threadIdx.x] = sh.l_next[threadIdx.x];
+        if (threadIdx.x == 0) a.fl_list[atomicAdd(a.fl_cnt, 1u)] = part;
+      }
     }
     __syncthreads();  // sh is reused by the next partition
   }
+  if constexpr (CHAIN) finish_by_ticket(a, (blockIdx.x >> 3) < nl, working, &l_last);
 }
 
 // k_elect: the election lane (hipbatch_elect.h) over k_apply_fast's work
@@ -1368,12 +1408,7 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_follow(ApplyArgs a) {
     (void)apply_part<NMAX, true>(a, a.fl_list[i], sh, false);
     __syncthreads();
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's stats atomics are performed
-  __syncthreads();
-  if (threadIdx.x == 0)
-    l_last = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-  __syncthreads();
-  if (l_last) finish_step(a);  // uniform
+  finish_by_ticket(a, blockIdx.x < nl, nl < gridDim.x ? nl : gridDim.x, &l_last);
 }
 
 // ---------------------------------------------------------------------------
@@ -1876,6 +1911,7 @@ struct PrepSet {
   uint32_t* bucket = nullptr;     // bucket id per record (multi-pass only)
   uint32_t* bk_off = nullptr;     // [NBK + 1]
   uint32_t* bk_fill = nullptr;    // [NBK] event words reserved in each bucket's region (k_route)
+  uint32_t* ctr = nullptr;        // [CTR_WORDS] work-list counters + finish ticket (cleared by this set's prep)
   uint8_t* cnt = nullptr;         // [G]
   uint32_t* slot_info = nullptr;  // [nmax-1][G]
   uint32_t* slot_orig = nullptr;
@@ -1932,12 +1968,9 @@ struct hb_handle {
   uint64_t* stats = nullptr;
   // fast -> general hand-over
   uint32_t* pflag = nullptr;      // [NB][PART/32]
-  uint32_t* ap_cnt = nullptr;     // [8] k_apply work lists (counts, reset by the step's finish)
   uint32_t* ap_list = nullptr;    // [8][NB]
-  uint32_t* fl_cnt = nullptr;     // k_follow work list
   uint32_t* fl_list = nullptr;    // [NB]
   uint32_t* eflag = nullptr;      // [NB][PART/32] k_elect's groups (n >= 5)
-  uint32_t* el_cnt = nullptr;     // [8] k_elect work lists (counts, reset by the step's finish)
   uint32_t* el_list = nullptr;    // [8][NB]
   uint32_t* done = nullptr;       // k_apply workgroups finished this step
   uint32_t* resume = nullptr;     // [G]
@@ -2019,9 +2052,14 @@ void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
       hipLaunchKernelGGL(k_elect<NMAX>, dim3(ELECT_GRID ? std::min(grid, ELECT_GRID) : grid), dim3(PART), 0,
                          h->stream, a);
   }
-  hipLaunchKernelGGL(k_apply<NMAX>, dim3(GEN_GRID ? std::min(grid, GEN_GRID) : grid), dim3(PART), 0, h->stream, a);
-  // k_follow's last workgroup also runs the step's finish (k_finish)
-  hipLaunchKernelGGL(k_follow<NMAX>, dim3(FOLLOW_GRID), dim3(PART), 0, h->stream, a);
+  if constexpr (NMAX <= 3) {  // chained follower pass; the last workgroup runs the finish
+    const uint32_t gg = GEN_GRID3 ? std::min(grid, GEN_GRID3) : grid;
+    hipLaunchKernelGGL(k_apply<NMAX>, dim3(gg), dim3(PART), 0, h->stream, a);
+  } else {
+    hipLaunchKernelGGL(k_apply<NMAX>, dim3(GEN_GRID ? std::min(grid, GEN_GRID) : grid), dim3(PART), 0, h->stream, a);
+    // k_follow's last workgroup also runs the step's finish (k_finish)
+    hipLaunchKernelGGL(k_follow<NMAX>, dim3(FOLLOW_GRID), dim3(PART), 0, h->stream, a);
+  }
   if (ev && full) (void)hipEventRecord(ev[4], h->stream);
 }
 
@@ -2122,6 +2160,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
     if (h->passes > 1) ALLOC(ps.bucket, mb);
     ALLOC(ps.bk_off, h->NBK + 1);
     ALLOC(ps.bk_fill, h->NBK);
+    ALLOC(ps.ctr, CTR_WORDS);
     ALLOC(ps.cnt, G);
     ALLOC(ps.slot_info, route_kmax(R) * G);
     ALLOC(ps.slot_orig, route_kmax(R) * G);
@@ -2146,16 +2185,12 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->ev, h->ev_region);
   ALLOC(h->stats_shard, 8 * 16);
   ALLOC(h->pflag, (size_t)h->NB * FLAG_WORDS);
-  ALLOC(h->ap_cnt, 8);
   ALLOC(h->ap_list, 8ull * h->NB);
-  ALLOC(h->fl_cnt, 4);
   ALLOC(h->fl_list, h->NB);
   if (h->nmax >= 5) {
     ALLOC(h->eflag, (size_t)h->NB * FLAG_WORDS);
-    ALLOC(h->el_cnt, 8);
     ALLOC(h->el_list, 8ull * h->NB);
   }
-  ALLOC(h->done, 4);
   ALLOC(h->resume, G);
   ALLOC(h->commit0, G);
   ALLOC(h->stats, HB_STAT_COUNT);
@@ -2184,8 +2219,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
       hipMemset(s.elapsed, 0, G * 4) != hipSuccess || hipMemset(s.rpos, 0, G * 4) != hipSuccess ||
       hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(s.tcfg), 10u | (1u << 16), G) != hipSuccess ||
       hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess || hipMemset(h->stats_shard, 0, 8 * 16 * 8) != hipSuccess ||
-      hipMemset(h->ap_cnt, 0, 32) != hipSuccess || hipMemset(h->done, 0, 4) != hipSuccess ||
-      hipMemset(h->fl_cnt, 0, 4) != hipSuccess || (h->el_cnt && hipMemset(h->el_cnt, 0, 32) != hipSuccess) ||
+      hipMemset(h->set[0].ctr, 0, CTR_WORDS * 4) != hipSuccess || hipMemset(h->set[1].ctr, 0, CTR_WORDS * 4) != hipSuccess ||
       hipMemset(h->set[0].ev_counts, 0, h->NB * 8ull) != hipSuccess ||
       hipMemset(h->set[0].ev_off, 0, h->NB * 16ull) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
@@ -2676,6 +2710,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   if (b->n == 0) {
     HB_CHECK(hipMemsetAsync(ps.bk_off, 0, (h->NBK + 1) * 4ull, ps_st));
     HB_CHECK(hipMemsetAsync(ps.bk_fill, 0, h->NBK * 4ull, ps_st));
+    HB_CHECK(hipMemsetAsync(ps.ctr, 0, CTR_WORDS * 4ull, ps_st));
   } else {
     const uint32_t ntiles = (uint32_t)((b->n + RDX_TILE - 1) / RDX_TILE);
     RadixSrc src{bd.group, bd.info, nullptr, bd.term, bd.index, nullptr, (uint32_t)b->n};
@@ -2686,7 +2721,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
       const uint32_t shift = PART_LOG + h->sis_log + p * RDX_BITS;
       hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, h->G, shift, ntiles, h->hist);
       hipLaunchKernelGGL(k_scan_rows, dim3(RDX_BINS), dim3(1024), 0, ps_st, h->hist, ntiles, h->totals, ps.bk_fill,
-                         h->NBK);
+                         h->NBK, ps.ctr);
       if (last_pass)
         hipLaunchKernelGGL(k_radix_scatter<true>, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
                            shift, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
@@ -2710,16 +2745,16 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.S.eterm = bd_eterm;
   aa.S.n_ent = b->n_edesc;
   aa.S.bn = b->n;
-  aa.ap_cnt = h->ap_cnt;
+  aa.ap_cnt = ps.ctr + CTR_AP;
   aa.ap_list = h->ap_list;
-  aa.fl_cnt = h->fl_cnt;
+  aa.fl_cnt = ps.ctr + CTR_FL;
   aa.fl_list = h->fl_list;
   aa.eflag = h->eflag;
-  aa.el_cnt = h->el_cnt;
+  aa.el_cnt = ps.ctr + CTR_EL;
   aa.el_list = h->el_list;
   aa.grid = apply_grid(h);
   aa.sis_log = h->sis_log;
-  aa.done = h->done;
+  aa.done = ps.ctr + CTR_DONE;
   aa.stats = h->stats;
   aa.accum = h->stats_accum;
   aa.rec = ps.rec;
