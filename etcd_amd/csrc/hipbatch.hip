@@ -102,8 +102,14 @@ struct BatchDev {
 // hb_create: at most SIS_MAX, fewer when that costs no extra radix pass, so
 // that one k_route workgroup owns a whole bucket and reads it once).
 constexpr uint32_t SIS_LOG_MAX = 4;
-// a prep set's counters: k_apply's 8 work-list lengths, k_elect's 8, k_follow's, the finish ticket
-enum : uint32_t { CTR_AP = 0, CTR_EL = 8, CTR_FL = 16, CTR_DONE = 17, CTR_WORDS = 32 };
+// a prep set's counters: k_apply's 8 work-list lengths, k_elect's 8, k_follow's, the finish ticket —
+// each on a 128-byte line of its own (CTR_STRIDE words): the returning atomics of every partition
+// on one line serialise at the memory side (~7 ns each; 16K partitions put 16K on a list)
+enum : uint32_t { CTR_STRIDE = 32, CTR_AP = 0, CTR_EL = 8 * CTR_STRIDE, CTR_FL = 16 * CTR_STRIDE,
+                  CTR_DONE = 17 * CTR_STRIDE, CTR_WORDS = 18 * CTR_STRIDE };
+// step statistics: NSH shards per value, each (value, shard) on a 128-byte line of its own
+constexpr uint32_t NSH = 8;  // (a shard per XCD slot; a finish lane per (value, shard))
+__host__ __device__ constexpr uint32_t shard_at(uint32_t k, uint32_t sh) { return (k * NSH + sh) * 16; }
 constexpr uint32_t RDX_BITS = 8;
 constexpr uint32_t RDX_BINS = 1u << RDX_BITS;
 constexpr uint32_t RDX_THREADS = 512;
@@ -195,7 +201,8 @@ __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t nti
   const uint32_t d = (blockIdx.x & 7) * (RDX_BINS / 8) + (blockIdx.x >> 3);
   uint32_t* col = hist + d;
   for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < NBK; i += gridDim.x * 1024) bk_fill[i] = 0;
-  if (blockIdx.x == 0 && threadIdx.x < CTR_WORDS) ctr[threadIdx.x] = 0;
+  if (blockIdx.x == 0)
+    for (uint32_t i = threadIdx.x; i < CTR_WORDS; i += blockDim.x) ctr[i] = 0;
   uint32_t carry = 0;
   for (uint32_t base = 0; base < ntiles; base += 4096) {
     const uint32_t i0 = base + threadIdx.x * 4;
@@ -371,7 +378,7 @@ struct ApplyArgs {
   uint32_t NBK;             // buckets
   uint32_t* ev_counts;      // [NB] records in each chunk
   uint64_t* ev_off;         // [NB] chunk offsets (records)
-  uint64_t* stats_shard;    // [8][16] step statistics, one shard per XCD slot (atomic adds)
+  uint64_t* stats_shard;    // step statistics, NSH shards per value (shard_at; atomic adds)
   uint32_t* pflag;          // [NB][PART/32] groups handed from k_apply_fast to k_apply
   uint32_t* ap_cnt;         // [8] k_apply's work lists: partitions k_apply_fast flagged, one list per
   uint32_t* ap_list;        // [8][NB]  XCD slot (blockIdx % 8) of the flagging workgroup
@@ -636,7 +643,8 @@ __device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_sta
   }
   __syncthreads();
   const uint64_t v = tid <= ST_N ? l_stats[tid] : 0ull;
-  if (tid <= ST_N && v) atomicAdd((unsigned long long*)&a.stats_shard[(blockIdx.x & 7) * 16 + tid], (unsigned long long)v);
+  if (tid <= ST_N && v)
+    atomicAdd((unsigned long long*)&a.stats_shard[shard_at(tid, blockIdx.x & (NSH - 1))], (unsigned long long)v);
 }
 
 // ---------------------------------------------------------------------------
@@ -888,9 +896,9 @@ __device__ __forceinline__ void fast_close(const ApplyArgs& a, uint32_t part, co
   }
   const uint32_t xs = blockIdx.x & 7;
   if (any)  // the partition joins k_apply's list of its XCD slot
-    a.ap_list[(size_t)xs * a.NB + atomicAdd(&a.ap_cnt[xs], 1u)] = part;
+    a.ap_list[(size_t)xs * a.NB + atomicAdd(&a.ap_cnt[xs * CTR_STRIDE], 1u)] = part;
   if (eany)  // ... and k_elect's
-    a.el_list[(size_t)xs * a.NB + atomicAdd(&a.el_cnt[xs], 1u)] = part;
+    a.el_list[(size_t)xs * a.NB + atomicAdd(&a.el_cnt[xs * CTR_STRIDE], 1u)] = part;
 }
 
 template <int NMAX>
@@ -1186,17 +1194,20 @@ static_assert(GEN_GRID % 8 == 0, "k_apply strides its XCD-slot lists by gridDim.
 // The step's finish (as k_finish), run by the last k_follow workgroup: the
 // statistics shards (agent-scope atomics of every apply kernel) summed into
 // stats (+ accum), the shards and the work lists cleared for the next step.
+static_assert((ST_N + 1) * NSH <= PART && (NSH & (NSH - 1)) == 0, "a finish lane per (value, shard)");
 __device__ __forceinline__ void finish_step(const ApplyArgs& a) {
   const int map[ST_N + 1] = {HB_STAT_MSGS,  HB_STAT_APPRESP, HB_STAT_VOTERESP, HB_STAT_DROPPED, HB_STAT_COMMITS,
                              HB_STAT_WON,   HB_STAT_LOST,    HB_STAT_FAULTS,   HB_STAT_ENTRIES, HB_STAT_EVENTS};
-  const uint32_t k = threadIdx.x;
+  // one lane per (value, shard): one round trip; the NSH lanes of a value are adjacent in a wave
+  const uint32_t t = threadIdx.x, k = t / NSH;
+  uint64_t v = 0;
   if (k <= ST_N) {
-    uint64_t v = 0;
+    v = __hip_atomic_load(&a.stats_shard[shard_at(k, t % NSH)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.stats_shard[shard_at(k, t % NSH)], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 #pragma unroll
-    for (int x = 0; x < 8; ++x) {
-      v += __hip_atomic_load(&a.stats_shard[x * 16 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&a.stats_shard[x * 16 + k], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+  for (uint32_t d = 1; d < NSH; d <<= 1) v += __shfl_xor(v, d);
+  if (k <= ST_N && t % NSH == 0) {
     a.stats[map[k]] = v;
     if (a.accum) a.accum[map[k]] += v;
   }
@@ -1240,7 +1251,7 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
   uint32_t nl = 0, working = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 8; ++k) {
-    const uint32_t c = __hip_atomic_load(&a.ap_cnt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t c = __hip_atomic_load(&a.ap_cnt[k * CTR_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     nl = k == xs ? c : nl;
     working += c < stride ? c : stride;  // workgroups of slot k with at least one entry
   }
@@ -1283,7 +1294,7 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
   __shared__ uint64_t l_stats[ST_N + 1];
   const uint32_t tid = threadIdx.x;
   const uint32_t xs = blockIdx.x & 7, stride = gridDim.x >> 3;
-  const uint32_t nl = __hip_atomic_load(&a.el_cnt[xs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nl = __hip_atomic_load(&a.el_cnt[xs * CTR_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (uint32_t i = blockIdx.x >> 3; i < nl; i += stride) {  // uniform
     const uint32_t part = a.el_list[(size_t)xs * a.NB + i];
     const uint32_t g = part * PART + tid;
@@ -1672,17 +1683,18 @@ __global__ void __launch_bounds__(DEC_THREADS) k_decode_general(DecodeArgs a, co
 // ============================================================================
 // Phase 3: finish
 // ============================================================================
-__global__ void __launch_bounds__(64) k_finish(uint64_t* shard, uint64_t* stats, uint64_t* accum) {
+__global__ void __launch_bounds__(128) k_finish(uint64_t* shard, uint64_t* stats, uint64_t* accum) {
   const int map[ST_N + 1] = {HB_STAT_MSGS,  HB_STAT_APPRESP, HB_STAT_VOTERESP, HB_STAT_DROPPED, HB_STAT_COMMITS,
                              HB_STAT_WON,   HB_STAT_LOST,    HB_STAT_FAULTS,   HB_STAT_ENTRIES, HB_STAT_EVENTS};
-  const uint32_t k = threadIdx.x;
+  const uint32_t t = threadIdx.x, k = t / NSH;
+  uint64_t v = 0;
   if (k <= ST_N) {
-    uint64_t v = 0;
+    v = shard[shard_at(k, t % NSH)];
+    shard[shard_at(k, t % NSH)] = 0;  // ready for the next step
+  }
 #pragma unroll
-    for (int x = 0; x < 8; ++x) {
-      v += shard[x * 16 + k];
-      shard[x * 16 + k] = 0;  // ready for the next step
-    }
+  for (uint32_t d = 1; d < NSH; d <<= 1) v += __shfl_xor(v, d);
+  if (k <= ST_N && t % NSH == 0) {
     stats[map[k]] = v;
     if (accum) accum[map[k]] += v;
   }
@@ -1963,7 +1975,7 @@ struct hb_handle {
   uint64_t* ev = nullptr;   // compact event words
   uint64_t ev_region = 0;  // records
   uint32_t ev_per_msg = 0;
-  uint64_t* stats_shard = nullptr;  // [8][16]
+  uint64_t* stats_shard = nullptr;  // shard_at(value, shard)
   uint64_t* stats_accum = nullptr;  // optional caller buffer (hb_set_stats_accum)
   uint64_t* stats = nullptr;
   // fast -> general hand-over
@@ -2183,7 +2195,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   // P chunks (one per partition, dense proposals) then the bucket regions of M chunks
   h->ev_region = ((uint64_t)h->NB * PART + mb + ((uint64_t)h->NBK * PART << h->sis_log)) * h->ev_per_msg;
   ALLOC(h->ev, h->ev_region);
-  ALLOC(h->stats_shard, 8 * 16);
+  ALLOC(h->stats_shard, shard_at(ST_N + 1, 0));
   ALLOC(h->pflag, (size_t)h->NB * FLAG_WORDS);
   ALLOC(h->ap_list, 8ull * h->NB);
   ALLOC(h->fl_list, h->NB);
@@ -2218,7 +2230,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   if (hipMemset(s.meta, 0, G * 8) != hipSuccess || hipMemset(s.pm, 0, R * G * 4) != hipSuccess ||
       hipMemset(s.elapsed, 0, G * 4) != hipSuccess || hipMemset(s.rpos, 0, G * 4) != hipSuccess ||
       hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(s.tcfg), 10u | (1u << 16), G) != hipSuccess ||
-      hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess || hipMemset(h->stats_shard, 0, 8 * 16 * 8) != hipSuccess ||
+      hipMemset(h->stats, 0, HB_STAT_COUNT * 8) != hipSuccess || hipMemset(h->stats_shard, 0, shard_at(ST_N + 1, 0) * 8ull) != hipSuccess ||
       hipMemset(h->set[0].ctr, 0, CTR_WORDS * 4) != hipSuccess || hipMemset(h->set[1].ctr, 0, CTR_WORDS * 4) != hipSuccess ||
       hipMemset(h->set[0].ev_counts, 0, h->NB * 8ull) != hipSuccess ||
       hipMemset(h->set[0].ev_off, 0, h->NB * 16ull) != hipSuccess ||
@@ -2594,7 +2606,7 @@ int hb_tick(hb_handle* h, uint32_t flags) {
     case 5: hipLaunchKernelGGL(k_tick<5>, dim3(grid), dim3(PART), 0, st, aa); break;
     default: hipLaunchKernelGGL(k_tick<7>, dim3(grid), dim3(PART), 0, st, aa); break;
   }
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, h->stats_shard, h->stats, h->stats_accum);
+  hipLaunchKernelGGL(k_finish, dim3(1), dim3(128), 0, st, h->stats_shard, h->stats, h->stats_accum);
   if (two) HB_CHECK(hipEventRecord(ps.applied, st));  // a later prep reusing this set waits for it
   HB_CHECK(hipGetLastError());
   ps.used = true;
