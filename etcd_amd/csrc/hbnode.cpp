@@ -505,7 +505,8 @@ struct hbn_node {
   std::vector<Group*> pend_sz;  // groups (re)loaded on the device whose entry sizes are still to push
   std::vector<Group*> pend_tr;  // ... and whose older log term runs are still to push
   std::vector<Group*> stepped;  // groups whose raft.Step runs in the pending batch
-  std::vector<hb_event> evbuf;
+  hb_event* evbuf = nullptr;  // pinned (hb_alloc_pinned): the event copy lands straight in it
+  uint64_t evcap = 0;
   // CreateGroup loads, coalesced into one hb_load_groups / hb_load_timers per slot run
   std::vector<std::pair<uint32_t, hb_group>> pend_rec;
   std::vector<std::pair<uint32_t, hb_timer>> pend_tm;
@@ -802,13 +803,22 @@ void on_event(hbn_node* n, Group& g, const hb_event& e) {
 }
 
 void consume_events(hbn_node* n) {
+  // one copy call per cycle: into the pinned buffer, grown (and the call
+  // repeated) only when the step produced more events than it holds
   uint64_t cnt = 0;
-  int rc = hb_copy_events(n->h, nullptr, 0, &cnt);
-  if (rc != HB_OK && rc != HB_EINVAL) throw Fail{rc};
-  if (cnt) {
-    if (n->evbuf.size() < cnt) n->evbuf.resize(cnt);
-    check(hb_copy_events(n->h, n->evbuf.data(), n->evbuf.size(), &cnt));
+  int rc = hb_copy_events(n->h, n->evbuf, n->evcap, &cnt);
+  if (rc == HB_EINVAL && cnt > n->evcap) {
+    if (n->evbuf) (void)hb_free_pinned(n->evbuf);
+    n->evbuf = nullptr;
+    n->evcap = 0;
+    const uint64_t cap = cnt + cnt / 4 + 1024;
+    void* p = nullptr;
+    check(hb_alloc_pinned(cap * sizeof(hb_event), &p));
+    n->evbuf = static_cast<hb_event*>(p);
+    n->evcap = cap;
+    rc = hb_copy_events(n->h, n->evbuf, n->evcap, &cnt);
   }
+  check(rc);
   for (uint64_t i = 0; i < cnt; ++i) {
     const hb_event& e = n->evbuf[i];
     if (e.group >= n->by_slot.size() || !n->by_slot[e.group]) continue;
@@ -1476,6 +1486,7 @@ int hbn_stop(hbn_node* n) {
   if (!n) return HB_EINVAL;
   for (auto& kv : n->groups)
     if (kv.second->log.st) drop_user(kv.second->log.st, n, kv.first);
+  if (n->evbuf) (void)hb_free_pinned(n->evbuf);
   const int rc = hb_destroy(n->h);
   delete n;
   return rc;

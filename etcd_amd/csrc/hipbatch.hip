@@ -108,7 +108,8 @@ constexpr uint32_t SIS_LOG_MAX = 4;
 enum : uint32_t { CTR_STRIDE = 32, CTR_AP = 0, CTR_EL = 8 * CTR_STRIDE, CTR_FL = 16 * CTR_STRIDE,
                   CTR_DONE = 17 * CTR_STRIDE, CTR_WORDS = 18 * CTR_STRIDE };
 // step statistics: NSH shards per value, each (value, shard) on a 128-byte line of its own
-constexpr uint32_t NSH = 8;  // (a shard per XCD slot; a finish lane per (value, shard))
+constexpr uint32_t NSH = 8;
+constexpr uint64_t STAGE_MAX = 8ull << 20;  // host-pointer batches packed into one pinned copy up to this size  // (a shard per XCD slot; a finish lane per (value, shard))
 __host__ __device__ constexpr uint32_t shard_at(uint32_t k, uint32_t sh) { return (k * NSH + sh) * 16; }
 constexpr uint32_t RDX_BITS = 8;
 constexpr uint32_t RDX_BINS = 1u << RDX_BITS;
@@ -126,20 +127,21 @@ struct MsgRec {      // apply input record (24 B)
 
 struct RadixSrc {
   const uint32_t* group;
-  const uint32_t* info;
-  const uint32_t* orig;   // null: arrival index = position
+  const uint32_t* info;   // the batch's fields (first pass) ...
   const uint64_t* term;
   const uint64_t* index;
+  const MsgRec* rec;      // ... or an intermediate pass's records (info without lane bits, arrival index)
   const uint32_t* n_dev;  // null: n
   uint32_t n;
 };
 
-struct RadixDst {  // intermediate pass output
+// Intermediate pass output: the group ids (what the next pass's histogram
+// reads) plus one 24-byte record per message, so that a digit's run of a tile
+// is one contiguous ~190-byte store instead of five runs of 32-64 bytes (the
+// SoA layout wrote 1.6x its bytes as partial lines on cfg4).
+struct RadixDst {
   uint32_t* group;
-  uint32_t* info;
-  uint32_t* orig;
-  uint64_t* term;
-  uint64_t* index;
+  MsgRec* rec;
 };
 
 struct FinalDst {  // final pass output = apply input
@@ -200,7 +202,7 @@ __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t nti
   __shared__ uint32_t sh16[16];
   const uint32_t d = (blockIdx.x & 7) * (RDX_BINS / 8) + (blockIdx.x >> 3);
   uint32_t* col = hist + d;
-  for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < NBK; i += gridDim.x * 1024) bk_fill[i] = 0;
+  for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < NBK; i += gridDim.x * 1024) bk_fill[i * CTR_STRIDE] = 0;
   if (blockIdx.x == 0)
     for (uint32_t i = threadIdx.x; i < CTR_WORDS; i += blockDim.x) ctr[i] = 0;
   uint32_t carry = 0;
@@ -267,10 +269,19 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
     vv[r] = i < n;
     vg[r] = vv[r] ? s.group[i] : 0u;
     vv[r] = vv[r] && vg[r] < G;
-    vi[r] = vv[r] ? s.info[i] : 0u;
-    vo[r] = vv[r] ? (s.orig ? s.orig[i] : i) : 0u;
-    vt[r] = vv[r] ? s.term[i] : 0ull;
-    vx[r] = vv[r] ? s.index[i] : 0ull;
+    if (s.rec) {
+      MsgRec m{};
+      if (vv[r]) m = s.rec[i];
+      vi[r] = m.info;
+      vo[r] = m.orig;
+      vt[r] = m.term;
+      vx[r] = m.index;
+    } else {
+      vi[r] = vv[r] ? s.info[i] : 0u;
+      vo[r] = vv[r] ? i : 0u;
+      vt[r] = vv[r] ? s.term[i] : 0ull;
+      vx[r] = vv[r] ? s.index[i] : 0ull;
+    }
     vd[r] = rdx_digit(vg[r], shift);
   }
   // stable rank inside the wave: rounds in order, lanes in order
@@ -337,10 +348,12 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
         if (f.bucket) f.bucket[o] = g >> (PART_LOG + f.sis_log);
       } else {
         d.group[o] = g;
-        d.info[o] = st_info[p];
-        d.orig[o] = st_orig[p];
-        d.term[o] = st_term[p];
-        d.index[o] = st_index[p];
+        MsgRec m;
+        m.info = st_info[p];
+        m.orig = st_orig[p];
+        m.term = st_term[p];
+        m.index = st_index[p];
+        d.rec[o] = m;
       }
     }
   }
@@ -368,7 +381,7 @@ struct ApplyArgs {
   const MsgRec* rec;        // sorted batch: bucket order, arrival order inside a bucket
   const uint8_t* key;       // partition-in-bucket of each record
   const uint32_t* bk_off;   // [NBK+1] bucket bounds in rec
-  uint32_t* bk_fill;        // [NBK] event records reserved by the bucket's partitions
+  uint32_t* bk_fill;        // [NBK x CTR_STRIDE] event records reserved by the bucket's partitions (a line each)
   const uint64_t* hint;     // original-order RejectHint
   const uint32_t* props;    // dense proposals or null
   uint64_t* ev;             // event region base (compact words, hipbatch_kernels.h)
@@ -747,7 +760,7 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   if (tid < NP) {
     const uint32_t part = (bk << sl) + w * NP + tid;
     if (part < a.NB) {
-      const uint32_t r = atomicAdd(&a.bk_fill[bk], a.ev_per_msg * (l_ptot[tid] + PART * a.props_on));
+      const uint32_t r = atomicAdd(&a.bk_fill[bk * CTR_STRIDE], a.ev_per_msg * (l_ptot[tid] + PART * a.props_on));
       a.ev_off[2 * part + 1] =
           (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + lo + ((uint64_t)bk * PART << sl) * a.props_on) + r;
     }
@@ -1925,6 +1938,8 @@ struct PrepSet {
   uint32_t* bk_fill = nullptr;    // [NBK] event words reserved in each bucket's region (k_route)
   uint32_t* ctr = nullptr;        // [CTR_WORDS] work-list counters + finish ticket (cleared by this set's prep)
   uint8_t* cnt = nullptr;         // [G]
+  uint8_t* dstage = nullptr;      // device copy of the packed host batch (grown on demand)
+  uint64_t dstage_cap = 0;
   uint32_t* slot_info = nullptr;  // [nmax-1][G]
   uint32_t* slot_orig = nullptr;
   uint64_t* slot_term = nullptr;
@@ -1977,6 +1992,11 @@ struct hb_handle {
   uint32_t ev_per_msg = 0;
   uint64_t* stats_shard = nullptr;  // shard_at(value, shard)
   uint64_t* stats_accum = nullptr;  // optional caller buffer (hb_set_stats_accum)
+  uint64_t* stats_pin = nullptr;    // [HB_STAT_COUNT] pinned readback (hb_copy_events' count)
+  // host-pointer batches up to STAGE_MAX bytes: packed into one pinned block, one H2D copy
+  uint8_t* hstage = nullptr;        // pinned host block
+  uint64_t hstage_cap = 0;
+  hipEvent_t hstage_done = nullptr; // the last copy out of hstage has completed
   uint64_t* stats = nullptr;
   // fast -> general hand-over
   uint32_t* pflag = nullptr;      // [NB][PART/32]
@@ -2161,17 +2181,14 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   for (uint32_t k = 0; k + 1 < h->passes && k < 2; ++k) {  // ping-pong buffers of intermediate passes
     RadixDst& d = h->tmp[k];
     ALLOC(d.group, mb);
-    ALLOC(d.info, mb);
-    ALLOC(d.orig, mb);
-    ALLOC(d.term, mb);
-    ALLOC(d.index, mb);
+    ALLOC(d.rec, mb);
   }
   for (PrepSet& ps : h->set) {
     ALLOC(ps.rec, mb);
     ALLOC(ps.key, mb + SEG);
     if (h->passes > 1) ALLOC(ps.bucket, mb);
     ALLOC(ps.bk_off, h->NBK + 1);
-    ALLOC(ps.bk_fill, h->NBK);
+    ALLOC(ps.bk_fill, (size_t)h->NBK * CTR_STRIDE);
     ALLOC(ps.ctr, CTR_WORDS);
     ALLOC(ps.cnt, G);
     ALLOC(ps.slot_info, route_kmax(R) * G);
@@ -2216,7 +2233,9 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   int prio_least = 0, prio_greatest = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
   bool ok = hipStreamCreateWithPriority(&h->prep, hipStreamNonBlocking, prio_least) == hipSuccess &&
-            hipEventCreateWithFlags(&h->in_ready, hipEventDisableTiming) == hipSuccess;
+            hipEventCreateWithFlags(&h->in_ready, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&h->hstage_done, hipEventDisableTiming) == hipSuccess &&
+            hipHostMalloc(reinterpret_cast<void**>(&h->stats_pin), HB_STAT_COUNT * 8, hipHostMallocDefault) == hipSuccess;
   for (PrepSet& ps : h->set)
     ok = ok && hipEventCreateWithFlags(&ps.prepped, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&ps.applied, hipEventDisableTiming) == hipSuccess;
@@ -2256,6 +2275,11 @@ int hb_destroy(hb_handle* h) {
   }
   if (h->rnd) (void)hipFree(h->rnd);
   if (h->evx) (void)hipFree(h->evx);
+  for (PrepSet& ps : h->set)
+    if (ps.dstage) (void)hipFree(ps.dstage);
+  if (h->hstage) (void)hipHostFree(h->hstage);
+  if (h->stats_pin) (void)hipHostFree(h->stats_pin);
+  if (h->hstage_done) (void)hipEventDestroy(h->hstage_done);
   if (h->s_edesc) (void)hipFree(h->s_edesc);
   if (h->s_eterm) (void)hipFree(h->s_eterm);
   if (h->peer) (void)hipFree(h->peer);
@@ -2669,7 +2693,71 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     HB_CHECK(hipStreamWaitEvent(ps_st, h->in_ready, 0));
     if (ps.used) HB_CHECK(hipStreamWaitEvent(ps_st, ps.applied, 0));
   }
+  // Host-pointer batches.  Small ones (the host MultiNode's Ready cycles) are
+  // packed into one pinned block and sent with ONE copy; larger ones go
+  // array by array into the handle's staging buffers.
+  bool packed = false;
   if (flags & HB_STEP_HOST_PTRS) {
+    const size_t n = b->n;
+    struct Part {
+      const void* src;
+      size_t bytes;
+      size_t off;
+    };
+    Part parts[11] = {{b->group, n * 4, 0},
+                      {b->info, n * 4, 0},
+                      {b->term, n * 8, 0},
+                      {b->index, n * 8, 0},
+                      {b->hint, b->hint ? n * 8 : 0, 0},
+                      {b->props, b->props ? (size_t)h->G * 4 : 0, 0},
+                      {b->edesc, (sized && b->edesc) ? b->n_edesc * 4 : 0, 0},
+                      {b->eterm, b->eterm ? b->n_edesc * 8 : 0, 0},
+                      {b->eoff, b->eoff ? n * 8 : 0, 0},
+                      {b->commit, b->commit ? n * 8 : 0, 0},
+                      {b->peoff, (sized && b->props) ? (size_t)h->G * 8 : 0, 0}};
+    size_t total = 0;
+    for (Part& q : parts) {
+      q.off = total;
+      total += (q.src && q.bytes) ? (q.bytes + 255) & ~(size_t)255 : 0;
+    }
+    if (total > 0 && total <= STAGE_MAX) {
+      packed = true;
+      if (total > h->hstage_cap) {
+        HB_CHECK(hipEventSynchronize(h->hstage_done));
+        if (h->hstage) (void)hipHostFree(h->hstage);
+        h->hstage = nullptr;
+        h->hstage_cap = 0;
+        HB_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h->hstage), STAGE_MAX, hipHostMallocDefault));
+        h->hstage_cap = STAGE_MAX;
+      }
+      if (total > ps.dstage_cap) {  // (this set's last reader is done: the prep stream waited for it)
+        HB_CHECK(hipStreamSynchronize(st));
+        if (ps.dstage) (void)hipFree(ps.dstage);
+        ps.dstage = nullptr;
+        ps.dstage_cap = 0;
+        HB_CHECK(hipMalloc(reinterpret_cast<void**>(&ps.dstage), STAGE_MAX));
+        ps.dstage_cap = STAGE_MAX;
+      }
+      HB_CHECK(hipEventSynchronize(h->hstage_done));  // the previous step's copy has left the block
+      for (const Part& q : parts)
+        if (q.src && q.bytes) std::memcpy(h->hstage + q.off, q.src, q.bytes);
+      HB_CHECK(hipMemcpyAsync(ps.dstage, h->hstage, total, hipMemcpyHostToDevice, ps_st));
+      HB_CHECK(hipEventRecord(h->hstage_done, ps_st));
+      auto at = [&](int k) { return parts[k].src && parts[k].bytes ? ps.dstage + parts[k].off : nullptr; };
+      bd.group = reinterpret_cast<const uint32_t*>(at(0));
+      bd.info = reinterpret_cast<const uint32_t*>(at(1));
+      bd.term = reinterpret_cast<const uint64_t*>(at(2));
+      bd.index = reinterpret_cast<const uint64_t*>(at(3));
+      bd.hint = reinterpret_cast<const uint64_t*>(at(4));
+      bd.props = reinterpret_cast<const uint32_t*>(at(5));
+      bd_edesc = reinterpret_cast<const uint32_t*>(at(6));
+      bd_eterm = reinterpret_cast<const uint64_t*>(at(7));
+      bd_eoff = reinterpret_cast<const uint64_t*>(at(8));
+      bd_commit = reinterpret_cast<const uint64_t*>(at(9));
+      bd_peoff = reinterpret_cast<const uint64_t*>(at(10));
+    }
+  }
+  if ((flags & HB_STEP_HOST_PTRS) && !packed) {
     // partition inputs on the prep stream (staging is reused in prep-stream
     // order); props / hint are read by apply, so they go on the apply stream.
     const size_t n = b->n;
@@ -2721,11 +2809,11 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   const uint32_t NB = h->NB;
   if (b->n == 0) {
     HB_CHECK(hipMemsetAsync(ps.bk_off, 0, (h->NBK + 1) * 4ull, ps_st));
-    HB_CHECK(hipMemsetAsync(ps.bk_fill, 0, h->NBK * 4ull, ps_st));
+    HB_CHECK(hipMemsetAsync(ps.bk_fill, 0, h->NBK * 4ull * CTR_STRIDE, ps_st));
     HB_CHECK(hipMemsetAsync(ps.ctr, 0, CTR_WORDS * 4ull, ps_st));
   } else {
     const uint32_t ntiles = (uint32_t)((b->n + RDX_TILE - 1) / RDX_TILE);
-    RadixSrc src{bd.group, bd.info, nullptr, bd.term, bd.index, nullptr, (uint32_t)b->n};
+    RadixSrc src{bd.group, bd.info, bd.term, bd.index, nullptr, nullptr, (uint32_t)b->n};
     const FinalDst fin{ps.rec, ps.key, ps.bucket, h->passes == 1 ? ps.bk_off : nullptr, h->NBK, h->sis_log};
     for (uint32_t p = 0; p < h->passes; ++p) {
       const bool last_pass = p + 1 == h->passes;
@@ -2740,7 +2828,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
       else
         hipLaunchKernelGGL(k_radix_scatter<false>, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
                            shift, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
-      src = RadixSrc{dst.group, dst.info, dst.orig, dst.term, dst.index, h->n_valid, (uint32_t)b->n};
+      src = RadixSrc{dst.group, nullptr, nullptr, nullptr, dst.rec, h->n_valid, (uint32_t)b->n};
     }
     if (h->passes > 1)
       hipLaunchKernelGGL(k_bucket_bounds, dim3((h->NBK + 1 + 255) / 256), dim3(256), 0, ps_st,
@@ -2835,10 +2923,9 @@ int hb_events_device(hb_handle* h, const uint64_t** base, const uint64_t** chunk
 int hb_copy_events(hb_handle* h, hb_event* out, uint64_t cap, uint64_t* n) {
   if (!h || !n) return HB_EINVAL;
   DeviceGuard guard(h->device);
-  uint64_t stats[HB_STAT_COUNT];
-  HB_CHECK(hipMemcpyAsync(stats, h->stats, sizeof(stats), hipMemcpyDeviceToHost, h->stream));
+  HB_CHECK(hipMemcpyAsync(h->stats_pin, h->stats, HB_STAT_COUNT * 8, hipMemcpyDeviceToHost, h->stream));
   HB_CHECK(hipStreamSynchronize(h->stream));
-  const uint64_t total = h->stepped ? stats[HB_STAT_EVENTS] : 0;
+  const uint64_t total = h->stepped ? h->stats_pin[HB_STAT_EVENTS] : 0;
   *n = total;
   if (total == 0) return HB_OK;
   if (!out || cap < total) return HB_EINVAL;

@@ -60,7 +60,7 @@ def main():
     if os.path.exists(bpath):
         lines = [ln for ln in open(bpath) if ln.startswith("{")]
         bench = json.loads(lines[-1]) if lines else None
-    nmsg = bench["config"]["msgappresp_per_step"] if bench else None
+    nmsg = bench["config"].get("msgappresp_per_step") if bench else None
 
     def traffic(k):
         f = fetch.get(k)
