@@ -84,9 +84,11 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh16, 
 // the first pass.  Arrival order is preserved within every bucket.
 //
 // The final pass writes the apply input: one 24-byte MsgRec per message
-// (info with the group's lane in bits 16-23, arrival index, term, index) and
-// one key byte = the message's partition within its bucket (k_route reads the
-// records; the general kernel's bucket walk scans the key bytes).
+// (info with the group's lane in bits 16-23 and its partition in the bucket
+// in bits 24-27, arrival index, term, index).  k_route reads the records and
+// writes the partition once more as a key byte per message, contiguous, for
+// the general kernel's bucket walk (a separate key array written here took
+// 8-byte runs per digit per tile: partial lines).
 // ============================================================================
 struct BatchDev {
   const uint32_t* group;
@@ -146,7 +148,6 @@ struct RadixDst {
 
 struct FinalDst {  // final pass output = apply input
   MsgRec* rec;
-  uint8_t* key;
   uint32_t* bucket;  // bucket id per message (multi-pass only, for k_bucket_bounds)
   uint32_t* bk_off;  // [NBK + 1] written by the one-pass scatter
   uint32_t NBK;
@@ -339,12 +340,11 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
       const uint32_t o = s_off[dg] + (p - s_dstart[dg]);
       if (FINAL) {
         MsgRec m;
-        m.info = (st_info[p] & 0xFFFFu) | ((g & (PART - 1)) << 16);
+        m.info = (st_info[p] & 0xFFFFu) | ((g & (PART - 1)) << 16) | (((g >> PART_LOG) & ((1u << f.sis_log) - 1)) << 24);
         m.orig = st_orig[p];
         m.term = st_term[p];
         m.index = st_index[p];
         f.rec[o] = m;
-        f.key[o] = (uint8_t)((g >> PART_LOG) & ((1u << f.sis_log) - 1));
         if (f.bucket) f.bucket[o] = g >> (PART_LOG + f.sis_log);
       } else {
         d.group[o] = g;
@@ -379,7 +379,7 @@ __global__ void k_bucket_bounds(const uint32_t* bucket, const uint32_t* n_dev, u
 struct ApplyArgs {
   DevState S;
   const MsgRec* rec;        // sorted batch: bucket order, arrival order inside a bucket
-  const uint8_t* key;       // partition-in-bucket of each record
+  uint8_t* key;             // partition-in-bucket of each record (k_route writes it for the walk)
   const uint32_t* bk_off;   // [NBK+1] bucket bounds in rec
   uint32_t* bk_fill;        // [NBK x CTR_STRIDE] event records reserved by the bucket's partitions (a line each)
   const uint64_t* hint;     // original-order RejectHint
@@ -715,8 +715,15 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
 #pragma unroll
     for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
       const uint32_t p = base + u * ROUTE_THREADS + tid;
-      sub[u] = p < hi ? a.key[p] : 0xFFu;
       if (p < hi) m[u] = a.rec[p];
+      sub[u] = p < hi ? (m[u].info >> 24) & 0xFu : 0xFFu;  // the partition in the bucket
+    }
+    if (w == 0) {  // the key bytes the general kernel's bucket walk scans (one coalesced store per lane)
+#pragma unroll
+      for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
+        const uint32_t p = base + u * ROUTE_THREADS + tid;
+        if (p < hi) a.key[p] = (uint8_t)sub[u];
+      }
     }
 #pragma unroll
     for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
@@ -2814,7 +2821,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   } else {
     const uint32_t ntiles = (uint32_t)((b->n + RDX_TILE - 1) / RDX_TILE);
     RadixSrc src{bd.group, bd.info, bd.term, bd.index, nullptr, nullptr, (uint32_t)b->n};
-    const FinalDst fin{ps.rec, ps.key, ps.bucket, h->passes == 1 ? ps.bk_off : nullptr, h->NBK, h->sis_log};
+    const FinalDst fin{ps.rec, ps.bucket, h->passes == 1 ? ps.bk_off : nullptr, h->NBK, h->sis_log};
     for (uint32_t p = 0; p < h->passes; ++p) {
       const bool last_pass = p + 1 == h->passes;
       const RadixDst& dst = h->tmp[p & 1];
