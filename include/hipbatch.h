@@ -147,7 +147,9 @@ typedef struct hb_batch {
 } hb_batch;
 
 /* hb_step flags */
-#define HB_STEP_HOST_PTRS 0x1u   /* batch arrays are host pointers (copied H2D) */
+#define HB_STEP_HOST_PTRS 0x1u   /* batch arrays are host pointers (copied H2D; up to 8 MiB in all
+                                    they are packed into one pinned block during the call and sent
+                                    with one copy, so the arrays may be reused once hb_step returns) */
 #define HB_STEP_PROFILE   0x2u   /* record per-phase HIP events (hb_phase_ms)   */
 #define HB_STEP_PROFILE_APPLY 0x4u  /* only the HB_PHASE_APPLY events (two, on the apply stream) */
 
