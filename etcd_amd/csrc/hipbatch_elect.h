@@ -231,10 +231,14 @@ struct ElectLane {
     }
     // bcastAppend (slot order): every peer is in Probe, not paused, Next =
     // rlast + 1 <= last: MsgApp{Index = rlast} and pause
-    if (bcast) {
-#pragma nounroll
-      for (uint32_t s = 0; s < nn; ++s)
-        if (s != sf) ev(HB_EV_APP, s, 0, rlast);
+    if (bcast) {  // one EVC_BCAST word for two or more sends (the same records once expanded)
+      const uint32_t mask = ((1u << nn) - 1) & ~(1u << sf);
+      if (mask & (mask - 1)) {
+        emit_ev(E, g & (PART - 1), EVC_BCAST, mask, 0, rlast);
+        nev += __popc(mask);
+      } else if (mask) {
+        ev(HB_EV_APP, __ffs(mask) - 1, 0, rlast);
+      }
       sent = true;
     }
   }
