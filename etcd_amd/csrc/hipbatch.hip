@@ -788,9 +788,12 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
 // chunk, as far as FastLane takes them.  Sets the group's hand-over bit in
 // l_flag (and, n >= 5, its k_elect bit in l_eflag), resume / commit0, and
 // returns the statistics of the lane.
+// lead: a leader whose state is loaded (the fast path may step it); leader:
+// the group is a leader (for k_elect's test) — a leader with more messages
+// than slots and no proposal is handed over with its state unloaded.
 template <int NMAX>
 __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FastLane<NMAX>& L, uint32_t part, uint32_t lane,
-                                          bool live, bool lead, uint32_t prop_raw, uint32_t cnt,
+                                          bool live, bool lead, bool leader, uint32_t prop_raw, uint32_t cnt,
                                           uint32_t (&s_info)[NMAX - 1], uint32_t (&s_orig)[NMAX - 1],
                                           uint64_t (&s_term)[NMAX - 1], uint64_t (&s_index)[NMAX - 1],
                                           uint64_t moff, uint32_t* l_pfill, uint32_t* l_fill, uint32_t* l_flag,
@@ -882,7 +885,7 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FastLane<NMAX>& L,
     bool higher = false;
 #pragma unroll
     for (uint32_t k = 0; k < KMAX; ++k) higher |= k < cnt && s_term[k] > L.term;
-    if (flagged && (!lead || higher)) atomicOr(&l_eflag[lane >> 5], 1u << (lane & 31));
+    if (flagged && (!leader || higher)) atomicOr(&l_eflag[lane >> 5], 1u << (lane & 31));
   }
   if (flagged) {
     atomicOr(&l_flag[lane >> 5], 1u << (lane & 31));
@@ -950,11 +953,18 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
   // Only a leader has fast-path work: any other live group is handed to
   // k_apply whole, without loading its state here (resume bit 30: commit0 =
   // its committed as k_apply loads it).
-  const bool lead = live && L.state() == HB_STATE_LEADER;
+  const bool leader = live && L.state() == HB_STATE_LEADER;
+  // a leader the fast path cannot finish (more messages than slots) and
+  // without a dense proposal is handed over whole, its state unloaded (cfg4:
+  // every group; k_elect / k_apply load it); n >= 5 reads its Term for
+  // k_elect's step-down test
+  const bool lead = leader && (cnt <= KMAX || prop_raw != 0);
   L.dirty = 0;
   L.nev = 0;
   L.last = L.committed = 0;
+  L.term = 0;
   if (lead) L.load();
+  else if (NMAX >= 5 && leader) L.term = a.S.term[g];
   uint32_t s_info[KMAX], s_orig[KMAX];
   uint64_t s_term[KMAX], s_index[KMAX];
   // a leader's used slots, in the state loads' round trip (both wait for meta
@@ -967,11 +977,11 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply
     s_info[k] = u ? a.slot_info[o] : 0u;
     s_orig[k] = u ? a.slot_orig[o] : 0u;
     // (n >= 5: a busier leader's terms too, for k_elect's step-down test below)
-    s_term[k] = (NMAX >= 5 ? lead && k < cnt : u) ? a.slot_term[o] : 0ull;
+    s_term[k] = (NMAX >= 5 ? leader && k < cnt : u) ? a.slot_term[o] : 0ull;
     s_index[k] = u ? a.slot_index[o] : 0ull;
   }
   uint32_t vals[ST_N + 1];
-  (void)fast_step<NMAX>(a, L, part, tid, live, lead, prop_raw, cnt, s_info, s_orig, s_term, s_index,
+  (void)fast_step<NMAX>(a, L, part, tid, live, lead, leader, prop_raw, cnt, s_info, s_orig, s_term, s_index,
                         a.ev_off[2 * part + 1], &l_pfill, &l_fill, l_flag, l_eflag, vals);
   reduce_stats(a, l_stats, vals);
   if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
