@@ -452,6 +452,12 @@ __device__ uint64_t g_stamps[1 << 20];
 #ifndef HB_FAST_WAVES
 #define HB_FAST_WAVES 4
 #endif
+#ifndef HB_FAST5_WAVES  // k_apply_fast<5>
+#define HB_FAST5_WAVES 2
+#endif
+#ifndef HB_FAST7_WAVES  // k_apply_fast<7>
+#define HB_FAST7_WAVES 2
+#endif
 constexpr uint32_t FLAG_WORDS = PART / 32;  // per-partition bitmask of groups handed to k_apply
 constexpr uint32_t KPL = 64;                // bucket key bytes scanned per lane per segment
 constexpr uint32_t SEG = PART * KPL;        // positions per key-scan segment
@@ -925,7 +931,7 @@ __device__ __forceinline__ void fast_close(const ApplyArgs& a, uint32_t part, co
 }
 
 template <int NMAX>
-__global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : 2)) k_apply_fast(ApplyArgs a) {
+__global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 ? HB_FAST5_WAVES : HB_FAST7_WAVES))) k_apply_fast(ApplyArgs a) {
   constexpr uint32_t KMAX = NMAX - 1;  // one MsgAppResp per follower per batch
   __shared__ uint32_t l_fill, l_pfill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
