@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-HB_ABI_VERSION = 3
+HB_ABI_VERSION = 4
 
 HB_OK = 0
 HB_EINVAL = -1
@@ -20,8 +20,8 @@ HB_MAX_REPLICAS = 7
 HB_MAX_INFLIGHT = 1024
 HB_NO_LIMIT = (1 << 64) - 1
 HB_NO_INDEX = (1 << 64) - 1
-HB_SIZE_WINDOW = 1024
-HB_TERM_RUNS = 8
+HB_SIZE_RING_MIN = 16
+HB_TERM_RING_MIN = 8
 HB_INFO_VOTED = 0x200
 HB_ENT_MAX_DATA = 0x3FFFFFFF
 

@@ -466,6 +466,13 @@ struct Group {
   bool touched = false, stepped = false, content = false, delivered = false;
   bool bounds = false;  // storage changed: device firstIndex / snapshot index to refresh (hbn_node::bounds)
   Delivered dlv;  // what the last Ready delivered for this group (commitReady input)
+  // the device log index (hb_reserve_log): ring capacities reserved so far, an
+  // upper bound on the term runs the device must keep (every run of the log),
+  // and what the pending batch can add: entries and messages (each may start a
+  // run or append a noop), and the top of its MsgApps' entries
+  uint64_t lx_sz = 0, lx_tr = 0, lx_runs = 0;
+  uint64_t bx = 0, bx_top = 0;
+  bool in_bx = false;
 
   hbn_hard_state hard() const { return hbn_hard_state{term, vote, hs_commit}; }
   Soft soft() const { return Soft{lead, state}; }
@@ -505,6 +512,7 @@ struct hbn_node {
   std::vector<Group*> pend_sz;  // groups (re)loaded on the device whose entry sizes are still to push
   std::vector<Group*> pend_tr;  // ... and whose older log term runs are still to push
   std::vector<Group*> stepped;  // groups whose raft.Step runs in the pending batch
+  std::vector<Group*> bx;       // groups with messages in the pending batch (Group::bx)
   hb_event* evbuf = nullptr;  // pinned (hb_alloc_pinned): the event copy lands straight in it
   uint64_t evcap = 0;
   // CreateGroup loads, coalesced into one hb_load_groups / hb_load_timers per slot run
@@ -846,61 +854,133 @@ void load_runs(std::vector<std::pair<uint32_t, T>>& v, F&& load) {
   v.clear();
 }
 
-// Finite MaxSizePerMsg: the sizes of the latest entries of groups whose device
-// record was (re)loaded, so the device's limitSize can reach back
-// HB_SIZE_WINDOW - 1 entries.
+// ---- the device log index (include/hipbatch.h, hb_reserve_log) ----
+// The term runs of [lo, hi] of g's log, newest first (binary search per run:
+// log terms never decrease with the index).
+template <class F>
+void log_runs(const Group& g, uint64_t lo, uint64_t hi, F&& f) {
+  while (hi + 1 > lo) {
+    const uint64_t t = g.log.term(hi);
+    uint64_t a = lo, b = hi;  // smallest i in [lo, hi] with term(i) == t
+    while (a < b) {
+      const uint64_t mid = a + (b - a) / 2;
+      if (g.log.term(mid) == t) b = mid;
+      else a = mid + 1;
+    }
+    f(a, t);
+    if (a == lo) break;
+    hi = a - 1;
+  }
+}
+// every term run of [firstIndex - 1, lastIndex]: the device's runs plus its current-term run
+uint64_t count_runs(const Group& g) {
+  uint64_t k = 0;
+  log_runs(g, g.log.first_index() - 1, g.log.last_index(), [&](uint64_t, uint64_t) { ++k; });
+  return k;
+}
+uint64_t pow2_at_least(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// Capacity for g's rings before a step that can add up to g.bx entries / runs
+// (and MsgApp entries up to g.bx_top): sizes cover [firstIndex - 1, the new
+// lastIndex], runs every run of the log plus the new ones.  Requested with 2x
+// headroom (amortised); the exact run count is taken only when the bound grows
+// past the reserved capacity.
+void want_log(const hbn_node* n, Group& g, uint64_t extra, std::vector<uint32_t>& slots,
+              std::vector<uint64_t>& szc, std::vector<uint64_t>& trc) {
+  const uint64_t lo = g.log.first_index() - 1;
+  const uint64_t need_sz = n->sized ? std::max(g.log.last_index(), g.bx_top) + extra - lo + 1 : 0;
+  uint64_t need_tr = g.lx_runs + extra + 1;
+  if (need_tr > g.lx_tr) {
+    g.lx_runs = count_runs(g);
+    need_tr = g.lx_runs + extra + 1;
+  }
+  const bool gs = need_sz > g.lx_sz, gt = need_tr > g.lx_tr;
+  if (!gs && !gt) return;
+  if (gs) g.lx_sz = pow2_at_least(2 * need_sz);
+  if (gt) g.lx_tr = pow2_at_least(2 * need_tr);
+  slots.push_back(g.slot);
+  szc.push_back(gs ? g.lx_sz : 0);
+  trc.push_back(gt ? g.lx_tr : 0);
+}
+void reserve(hbn_node* n, const std::vector<uint32_t>& slots, const std::vector<uint64_t>& szc,
+             const std::vector<uint64_t>& trc) {
+  if (!slots.empty())
+    check(hb_reserve_log(n->h, (uint32_t)slots.size(), slots.data(), n->sized ? szc.data() : nullptr, trc.data()));
+}
+
+// Finite MaxSizePerMsg: the sizes of every entry of (re)loaded groups
+// (hb_load_entry_sizes: (firstIndex - 1, lastIndex]), so the device's limitSize
+// serves a follower at any Next in the log.
 void push_sizes(hbn_node* n) {
   if (n->pend_sz.empty()) return;
   std::vector<uint32_t> slots, cnt, sizes;
+  std::vector<uint32_t> rs;
+  std::vector<uint64_t> rz, rt;
   for (Group* g : n->pend_sz) {
     if (g->slot == NO_SLOT) continue;
     const uint64_t li = g->log.last_index(), fi = g->log.first_index();
-    const uint64_t k = std::min<uint64_t>(li + 1 - fi, HB_SIZE_WINDOW - 1);
+    const uint64_t k = li + 1 - fi;
     slots.push_back(g->slot);
     cnt.push_back((uint32_t)k);
-    g->log.visit(li + 1 - k, li + 1, [&](const Ent& x) { sizes.push_back((uint32_t)ent_size(x)); });
+    g->log.visit(fi, li + 1, [&](const Ent& x) { sizes.push_back((uint32_t)ent_size(x)); });
+    g->lx_sz = 0;  // a reload: reserve afresh
+    want_log(n, *g, 0, rs, rz, rt);
   }
   n->pend_sz.clear();
+  reserve(n, rs, rz, rt);
   if (!slots.empty())
     check(hb_load_entry_sizes(n->h, (uint32_t)slots.size(), slots.data(), cnt.data(), sizes.data()));
 }
 
 // The follower side's raftLog.term() lookups below a (re)loaded group's
-// current-term run: its newest HB_TERM_RUNS older runs (hb_load_term_runs),
-// found by binary search (log terms never decrease).
+// current-term run: every older run down to firstIndex - 1 (hb_load_term_runs).
 void push_term_runs(hbn_node* n) {
   if (n->pend_tr.empty()) return;
   std::vector<uint32_t> slots, cnt;
   std::vector<uint64_t> runs;
+  std::vector<uint32_t> rs;
+  std::vector<uint64_t> rz, rt;
   for (Group* g : n->pend_tr) {
     if (g->slot == NO_SLOT) continue;
     uint64_t tf, tl;
     term_run(*g, &tf, &tl);
     const uint64_t lo = g->log.first_index() - 1;
-    uint64_t hi = tf == HB_NO_INDEX ? g->log.last_index() : tf - 1;
     std::vector<std::pair<uint64_t, uint64_t>> rr;  // newest first
-    while (tf != lo && hi + 1 > lo && rr.size() < HB_TERM_RUNS) {
-      const uint64_t t = g->log.term(hi);
-      uint64_t a = lo, b = hi;  // smallest i in [lo, hi] with term(i) == t
-      while (a < b) {
-        const uint64_t mid = a + (b - a) / 2;
-        if (g->log.term(mid) == t) b = mid;
-        else a = mid + 1;
-      }
-      rr.emplace_back(a, t);
-      if (a == lo) break;
-      hi = a - 1;
-    }
+    if (tf != lo) log_runs(*g, lo, tf == HB_NO_INDEX ? g->log.last_index() : tf - 1,
+                           [&](uint64_t a, uint64_t t) { rr.emplace_back(a, t); });
     slots.push_back(g->slot);
     cnt.push_back((uint32_t)rr.size());
     for (auto it = rr.rbegin(); it != rr.rend(); ++it) {
       runs.push_back(it->first);
       runs.push_back(it->second);
     }
+    g->lx_tr = 0;  // a reload: reserve afresh, with the exact count
+    g->lx_runs = rr.size() + (tf != HB_NO_INDEX ? 1 : 0);
+    want_log(n, *g, 0, rs, rz, rt);
   }
   n->pend_tr.clear();
+  reserve(n, rs, rz, rt);
   if (!slots.empty())
     check(hb_load_term_runs(n->h, (uint32_t)slots.size(), slots.data(), cnt.data(), runs.data()));
+}
+
+// Before hb_step: room in every batch group's rings for what the batch can add.
+void reserve_batch(hbn_node* n) {
+  std::vector<uint32_t> rs;
+  std::vector<uint64_t> rz, rt;
+  for (Group* g : n->bx)
+    if (g->slot != NO_SLOT) want_log(n, *g, g->bx, rs, rz, rt);
+  reserve(n, rs, rz, rt);
+  for (Group* g : n->bx) {  // after the step: the bound on the log's runs grows by what it could add
+    g->lx_runs += g->bx;
+    g->bx = g->bx_top = 0;
+    g->in_bx = false;
+  }
+  n->bx.clear();
 }
 
 void sync_loads(hbn_node* n) {
@@ -945,6 +1025,7 @@ void flush(hbn_node* n) {
     if (n->b_app) b.eterm = n->b_eterm.data();
   }
   if (n->b_follow) b.commit = n->b_commit.data();
+  reserve_batch(n);
   check(hb_step(n->h, &b, HB_STEP_HOST_PTRS));
   consume_events(n);
   for (Group* g : n->stepped) {
@@ -1006,6 +1087,11 @@ void push(hbn_node* n, Group& g, uint32_t type, uint64_t from, bool reject, uint
   n->b_commit.push_back(commit);
   n->b_from.push_back(from);
   n->b_snapi.push_back(NO_SLOT);
+  g.bx++;  // a noop (becomeLeader) or a new term run at most
+  if (!g.in_bx) {
+    g.in_bx = true;
+    n->bx.push_back(&g);
+  }
   if ((s >= 0 || !is_response(type)) && !g.stepped) {
     g.stepped = true;
     n->stepped.push_back(&g);
@@ -1021,6 +1107,7 @@ Group& group_of(hbn_node* n, uint64_t id) {
 // One entry of the last pushed message (its descriptor for the device's
 // limitSize, its term for the follower side; `keep`: the payload for the replay).
 void push_entry(hbn_node* n, const Ent& x, bool keep) {
+  n->by_slot[n->b_group.back()]->bx++;  // one more entry (and possibly term run) the step can append
   if (n->sized) n->b_edesc.push_back(ent_desc(x));
   n->b_eterm.push_back(x.term);
   if (keep) n->b_ents.push_back(x);
@@ -1064,6 +1151,7 @@ void step_follower(hbn_node* n, Group& g, const hbn_message* m) {
   if (t == HB_MSG_APP && m->n_entries) {
     n->b_app = true;
     for (uint64_t k = 0; k < m->n_entries; ++k) push_entry(n, ent_from(m->entries[k]), true);
+    g.bx_top = std::max(g.bx_top, m->index + m->n_entries);  // a MsgApp can cut the log and append up to here
   }
   if (t == HB_MSG_SNAP) {
     n->b_snapi.back() = (uint32_t)n->b_snaps.size();
@@ -1590,7 +1678,7 @@ int hbn_remove_group(hbn_node* n, uint64_t group) {
     }
     if (g.log.st) drop_user(g.log.st, n, group);
     for (auto* v : {&n->touched, &n->content, &n->delivered, &n->stepped, &n->bounds, &n->pend_sz, &n->pend_tr,
-                    &n->reload})
+                    &n->reload, &n->bx})
       v->erase(std::remove(v->begin(), v->end(), &g), v->end());
     n->groups.erase(it);
   });
@@ -1607,6 +1695,16 @@ int hbn_tick(hbn_node* n) {
   if (!n) return HB_EINVAL;
   return guarded([&] {
     flush(n);  // (also pushes queued loads)
+    {  // a one-peer group's tick can win an election at once and append its noop
+      std::vector<uint32_t> rs;
+      std::vector<uint64_t> rz, rt;
+      for (Group* g : n->by_slot)
+        if (g && g->peers.size() == 1) {
+          want_log(n, *g, 1, rs, rz, rt);
+          g->lx_runs += 1;
+        }
+      reserve(n, rs, rz, rt);
+    }
     check(hb_tick(n->h, 0));
     consume_events(n);
     size_t k = 0;  // every group with pending content is a Ready candidate again; drop stale entries

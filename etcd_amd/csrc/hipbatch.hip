@@ -1758,10 +1758,11 @@ __global__ void k_load(DevState S, uint32_t first, uint32_t count, const hb_grou
   S.meta[g] = m;
   S.elapsed[g] = 0;  // newRaft: fresh r.rand, becomeFollower -> reset
   S.rpos[g] = 0;
-  if (S.szp) {  // finite max_msg_size: no entry sizes yet (hb_load_entry_sizes)
+  if (S.szx) {  // finite max_msg_size: no entry sizes yet (hb_load_entry_sizes)
     S.szlo[g] = r.last_index;
-    *szp_at(S, g, r.last_index) = 0;
+    *cum_at(S.szx[g], r.last_index) = 0;
   }
+  S.trc[g] = 0;  // no older term runs yet (hb_load_term_runs)
   for (uint32_t s = 0; s < S.nmax; ++s) {
     const bool on = s < r.n;
     const size_t o = (size_t)s * S.G + g;
@@ -1824,11 +1825,12 @@ __global__ void k_load_runs(DevState S, uint32_t count, const uint32_t* groups, 
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   const uint32_t g = groups[i], k = n_runs[i];
+  uint64_t* R = lx_base(S.trx[g]);  // the host reserved >= k runs
   for (uint32_t j = 0; j < k; ++j) {
-    S.trs[(size_t)j * S.G + g] = runs[2 * (off[i] + j)];
-    S.trt[(size_t)j * S.G + g] = runs[2 * (off[i] + j) + 1];
+    R[2 * j] = runs[2 * (off[i] + j)];
+    R[2 * j + 1] = runs[2 * (off[i] + j) + 1];
   }
-  S.meta[g] = (S.meta[g] & ~(0x7Full << 40)) | ((uint64_t)k << 40);  // count k, head 0
+  S.trc[g] = k;  // count k, head 0
 }
 
 // hb_load_entry_sizes: group groups[i] takes the sizes of its entries
@@ -1838,15 +1840,43 @@ __global__ void k_load_sizes(DevState S, uint32_t count, const uint32_t* groups,
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   const uint32_t g = groups[i], k = n_sizes[i];
-  const uint64_t last = S.last[g], lo = last - k;
+  const uint64_t last = S.last[g], lo = last - k, x = S.szx[g];  // the host reserved > k entries
   const uint32_t* z = sizes + off[i];
   uint64_t acc = 0;
-  *szp_at(S, g, lo) = 0;
+  *cum_at(x, lo) = 0;
   for (uint32_t j = 1; j <= k; ++j) {
     acc += z[j - 1];
-    *szp_at(S, g, lo + j) = acc;
+    *cum_at(x, lo + j) = acc;
   }
   S.szlo[g] = lo;
+}
+
+// hb_reserve_log: move job i's ring to a larger extent, keeping its content.
+// A job is 4 words: group | kind << 32 (0 sizes, 1 runs), old extent word, new extent word, unused.
+__global__ void k_regrow(DevState S, uint32_t count, const uint64_t* jobs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint64_t* j = jobs + 4 * (size_t)i;
+  const uint32_t g = (uint32_t)j[0], kind = (uint32_t)(j[0] >> 32);
+  const uint64_t ox = j[1], nx = j[2];
+  if (kind == 0) {  // cum(i) for i in [szlo, last]: same index, new mask
+    const uint64_t lo = S.szlo[g], last = S.last[g];
+    for (uint64_t k = lo; k <= last; ++k) *cum_at(nx, k) = *cum_at(ox, k);
+    S.szx[g] = nx;
+  } else {  // runs in ring order, to the front of the new ring (head 0)
+    const uint64_t c = S.trc[g];
+    const uint32_t n = (uint32_t)c, h = (uint32_t)(c >> 32);
+    const uint64_t om = lx_cap(ox) - 1;
+    const uint64_t* O = lx_base(ox);
+    uint64_t* N = lx_base(nx);
+    for (uint32_t k = 0; k < n; ++k) {
+      const uint64_t o = 2 * ((h + k) & om);
+      N[2 * k] = O[o];
+      N[2 * k + 1] = O[o + 1];
+    }
+    S.trx[g] = nx;
+    S.trc[g] = n;
+  }
 }
 
 __global__ void k_remove(DevState S, uint32_t first, uint32_t count) {
@@ -1948,6 +1978,38 @@ __global__ void __launch_bounds__(256) k_expand_events(const uint64_t* base, con
   }
 }
 
+// The compact delta to the host (hb_events_to_host): the words themselves,
+// densely in chunk order, plus the words per chunk and their total.  Host
+// destinations are pinned memory the kernels write through (posted PCIe writes,
+// one coalesced 512-byte run per wave), so the copy is sized on the device.
+__global__ void __launch_bounds__(1024) k_scan_words(const uint32_t* counts, uint32_t n, uint64_t* dst,
+                                                     uint32_t* h_counts, uint64_t* h_total) {
+  __shared__ uint32_t sh16[16];
+  const uint32_t per = (n + 1023) / 1024, b0 = threadIdx.x * per;
+  uint64_t sum = 0;
+  for (uint32_t i = b0; i < b0 + per && i < n; ++i) sum += counts[i];
+  uint32_t tot;
+  uint64_t run = block_excl_scan((uint32_t)sum, sh16, &tot);  // total words < 2^32
+  for (uint32_t i = b0; i < b0 + per && i < n; ++i) {
+    dst[i] = run;
+    run += counts[i];
+  }
+  for (uint32_t i = threadIdx.x; i < n; i += 1024) h_counts[i] = counts[i];
+  if (threadIdx.x == 0) {
+    dst[n] = tot;
+    *h_total = tot;
+  }
+}
+__global__ void __launch_bounds__(256) k_gather_words(const uint64_t* base, const uint32_t* counts,
+                                                      const uint64_t* offs, const uint64_t* dst, uint64_t* out,
+                                                      uint64_t cap) {
+  const uint32_t c = blockIdx.x, n = counts[c];
+  if (dst[gridDim.x] > cap) return;  // the caller's buffer is too small: counts and total only
+  const uint64_t* src = base + offs[c];
+  uint64_t* o = out + dst[c];
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) o[i] = src[i];
+}
+
 // ============================================================================
 // host side
 // ============================================================================
@@ -1974,6 +2036,54 @@ struct PrepSet {
   bool used = false;
 };
 
+// The log pool: extents of the per-group log index rings (DevState szx / trx),
+// power-of-two sizes carved from device slabs, recycled through per-size free
+// lists.  Only the host allocates (hb_reserve_log, hb_load_*): the device never
+// grows a ring, it relies on the capacity reserved before the step.
+struct LogPool {
+  std::vector<void*> slabs;
+  char* cur = nullptr;
+  size_t left = 0;
+  std::vector<uint64_t> free_[48];  // by log2(bytes)
+  uint64_t bytes_live = 0;
+  // an extent of 2^lb bytes (lb >= 7: 128-byte aligned, the extent word's tag bits stay free)
+  uint64_t get(uint32_t lb) {
+    if (!free_[lb].empty()) {
+      const uint64_t a = free_[lb].back();
+      free_[lb].pop_back();
+      bytes_live += 1ull << lb;
+      return a;
+    }
+    const size_t bytes = 1ull << lb;
+    const size_t align = bytes < 4096 ? bytes : 4096;
+    size_t pad = (align - (reinterpret_cast<uintptr_t>(cur) & (align - 1))) & (align - 1);
+    if (!cur || left < pad + bytes) {
+      const size_t slab = std::max<size_t>(bytes, 256ull << 20);
+      void* p = nullptr;
+      if (hipMalloc(&p, slab) != hipSuccess) return 0;
+      slabs.push_back(p);
+      cur = static_cast<char*>(p);
+      left = slab;
+      pad = 0;
+    }
+    const uint64_t a = reinterpret_cast<uint64_t>(cur + pad);
+    cur += pad + bytes;
+    left -= pad + bytes;
+    bytes_live += bytes;
+    return a;
+  }
+  void put(uint64_t a, uint32_t lb) {
+    free_[lb].push_back(a);
+    bytes_live -= 1ull << lb;
+  }
+  void release() {
+    for (void* p : slabs) (void)hipFree(p);
+    slabs.clear();
+  }
+};
+constexpr uint32_t SZ_LOG_MIN = 4;  // a size ring starts at 16 entries (128 B)
+constexpr uint32_t TR_LOG_MIN = 3;  // a run ring at 8 runs (128 B)
+
 struct hb_handle {
   int device = 0;
   hipStream_t stream = nullptr;   // apply stream (hb_set_stream)
@@ -1985,6 +2095,11 @@ struct hb_handle {
   uint64_t max_msg_size = 0, max_batch = 0;
   DevState st{};
   std::vector<void*> allocs;
+  // the log index (host mirror of DevState szx / trx: extent address | log2 capacity)
+  LogPool pool;
+  std::vector<uint64_t> h_szx, h_trx;
+  uint64_t* lx_jobs = nullptr;     // device scratch of hb_reserve_log's regrow jobs
+  uint64_t lx_jobs_cap = 0;
   // partition scratch
   uint32_t* hist = nullptr;       // [tiles][RDX_BINS]
   uint32_t* n_valid = nullptr;    // messages kept after pass 1 (device)
@@ -2036,6 +2151,8 @@ struct hb_handle {
   uint32_t* dec_qn = nullptr;     // [queue length, finished pass-2 workgroups]
   void* evx = nullptr;            // hb_copy_events expansion scratch, grown on demand
   uint64_t evx_cap = 0;
+  uint64_t* evw = nullptr;        // hb_events_to_host: per-chunk word offsets + total
+  uint64_t evw_cap = 0;
   uint64_t* rnd = nullptr;        // the r.rand stream (hb_set_rand), grown on demand
   uint64_t rnd_cap = 0;
   static constexpr uint32_t PROF_RING = 256;
@@ -2077,6 +2194,69 @@ uint32_t ceil_log2(uint32_t x) {
   uint32_t b = 0;
   while ((1u << b) < x) ++b;
   return b;
+}
+uint32_t ceil_log2_64(uint64_t x) {
+  uint32_t b = 0;
+  while (b < 63 && (1ull << b) < x) ++b;
+  return b;
+}
+
+// Grow the log-index rings of groups[i] to hold at least szcap[i] entry sizes
+// and trcap[i] term runs (null array or 0: unchanged); the content moves
+// along (k_regrow).  Never shrinks.
+int reserve_log(hb_handle* h, uint32_t count, const uint32_t* groups, const uint64_t* szcap, const uint64_t* trcap) {
+  struct Need {
+    uint32_t g;
+    uint64_t sz, tr;
+  };
+  std::vector<Need> need;
+  need.reserve(count);
+  for (uint32_t i = 0; i < count; ++i) {
+    if (groups[i] >= h->G) return HB_EINVAL;
+    const uint64_t sz = (szcap && h->st.szx) ? szcap[i] : 0, tr = trcap ? trcap[i] : 0;
+    const bool grow_sz = sz > (1ull << (h->h_szx.empty() ? 0 : (h->h_szx[groups[i]] & LX_TAG)));
+    const bool grow_tr = tr > (1ull << (h->h_trx[groups[i]] & LX_TAG));
+    if ((sz && grow_sz) || (tr && grow_tr)) need.push_back({groups[i], sz, tr});
+  }
+  if (need.empty()) return HB_OK;
+  // one job per (group, ring): duplicates of a group merge to their largest need
+  std::sort(need.begin(), need.end(), [](const Need& a, const Need& b) { return a.g < b.g; });
+  std::vector<uint64_t> jobs;
+  std::vector<std::pair<uint64_t, uint32_t>> old;  // extents to recycle once the copies ran
+  for (size_t i = 0; i < need.size();) {
+    Need m = need[i++];
+    while (i < need.size() && need[i].g == m.g) {
+      m.sz = std::max(m.sz, need[i].sz);
+      m.tr = std::max(m.tr, need[i].tr);
+      ++i;
+    }
+    for (uint32_t kind = 0; kind < 2; ++kind) {
+      const uint64_t want = kind ? m.tr : m.sz;
+      uint64_t& hx = kind ? h->h_trx[m.g] : h->h_szx[m.g];
+      const uint32_t lc = (uint32_t)(hx & LX_TAG);
+      if (!want || want <= (1ull << lc)) continue;
+      const uint32_t l = ceil_log2_64(want), rec = kind ? 4 : 3;  // 16-byte runs, 8-byte sizes
+      const uint64_t a = h->pool.get(l + rec);
+      if (!a) return HB_ENOMEM;
+      const uint64_t nx = lx_word(a, l);
+      jobs.insert(jobs.end(), {(uint64_t)m.g | ((uint64_t)kind << 32), hx, nx, 0});
+      old.emplace_back(hx & ~LX_TAG, lc + rec);
+      hx = nx;
+    }
+  }
+  const uint32_t nj = (uint32_t)(jobs.size() / 4);
+  if (h->lx_jobs_cap < jobs.size()) {
+    if (h->lx_jobs) (void)hipFree(h->lx_jobs);
+    h->lx_jobs = nullptr;
+    h->lx_jobs_cap = 0;
+    if (hipMalloc(&h->lx_jobs, jobs.size() * 8) != hipSuccess) return HB_ENOMEM;
+    h->lx_jobs_cap = jobs.size();
+  }
+  HB_CHECK(hipMemcpyAsync(h->lx_jobs, jobs.data(), jobs.size() * 8, hipMemcpyHostToDevice, h->stream));
+  hipLaunchKernelGGL(k_regrow, dim3((nj + 255) / 256), dim3(256), 0, h->stream, h->st, nj, (const uint64_t*)h->lx_jobs);
+  HB_CHECK(hipStreamSynchronize(h->stream));
+  for (auto& o : old) h->pool.put(o.first, o.second);
+  return HB_OK;
 }
 
 template <int KMAX>
@@ -2176,10 +2356,10 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(s.elapsed, G);
   ALLOC(s.rpos, G);
   ALLOC(s.tcfg, G);
-  ALLOC(s.trs, (size_t)HB_TERM_RUNS * G);  // follower side: older term runs
-  ALLOC(s.trt, (size_t)HB_TERM_RUNS * G);
-  if (sz_on(max_msg_size)) {  // limitSize needs the latest entries' sizes
-    ALLOC(s.szp, (size_t)HB_SIZE_WINDOW * G);
+  ALLOC(s.trx, G);  // the log index (DevState): older term runs (follower side) ...
+  ALLOC(s.trc, G);
+  if (sz_on(max_msg_size)) {  // ... and, for limitSize, the entries' cumulative sizes
+    ALLOC(s.szx, G);
     ALLOC(s.szlo, G);
   }
   // partition scratch
@@ -2276,9 +2456,24 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
       hipMemset(h->set[0].ctr, 0, CTR_WORDS * 4) != hipSuccess || hipMemset(h->set[1].ctr, 0, CTR_WORDS * 4) != hipSuccess ||
       hipMemset(h->set[0].ev_counts, 0, h->NB * 8ull) != hipSuccess ||
       hipMemset(h->set[0].ev_off, 0, h->NB * 16ull) != hipSuccess ||
-      hipDeviceSynchronize() != hipSuccess) {
+      hipMemset(s.trc, 0, G * 8) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     hb_destroy(h);
     return HB_EDEVICE;
+  }
+  // the log index: every group starts with a 128-byte extent per ring, carved
+  // from one slab each (hb_reserve_log moves a group to a larger one)
+  auto init_rings = [&](std::vector<uint64_t>& hx, uint64_t* dx, uint32_t log2cap) {
+    void* slab = nullptr;
+    if (hipMalloc(&slab, G * 128) != hipSuccess) return false;
+    h->pool.slabs.push_back(slab);
+    hx.resize(G);
+    const uint64_t base = reinterpret_cast<uint64_t>(slab);
+    for (size_t g = 0; g < G; ++g) hx[g] = lx_word(base + 128 * g, log2cap);
+    return hipMemcpy(dx, hx.data(), G * 8, hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!init_rings(h->h_trx, s.trx, TR_LOG_MIN) || (s.szx && !init_rings(h->h_szx, s.szx, SZ_LOG_MIN))) {
+    hb_destroy(h);
+    return HB_ENOMEM;
   }
   *out = h;
   return HB_OK;
@@ -2289,6 +2484,8 @@ int hb_destroy(hb_handle* h) {
   DeviceGuard guard(h->device);
   (void)hipDeviceSynchronize();
   for (void* p : h->allocs) (void)hipFree(p);
+  h->pool.release();
+  if (h->lx_jobs) (void)hipFree(h->lx_jobs);
   for (auto& row : h->ph)
     for (auto& e : row)
       if (e) (void)hipEventDestroy(e);
@@ -2298,6 +2495,7 @@ int hb_destroy(hb_handle* h) {
   }
   if (h->rnd) (void)hipFree(h->rnd);
   if (h->evx) (void)hipFree(h->evx);
+  if (h->evw) (void)hipFree(h->evw);
   for (PrepSet& ps : h->set)
     if (ps.dstage) (void)hipFree(ps.dstage);
   if (h->hstage) (void)hipHostFree(h->hstage);
@@ -2416,15 +2614,18 @@ int hb_load_term_runs(hb_handle* h, uint32_t count, const uint32_t* groups, cons
                       const uint64_t* runs) {
   if (!h || (count && (!groups || !n_runs))) return HB_EINVAL;
   if (count == 0) return HB_OK;
-  std::vector<uint64_t> off(count);
+  std::vector<uint64_t> off(count), cap(count);
   uint64_t tot = 0;
   for (uint32_t i = 0; i < count; ++i) {
-    if (groups[i] >= h->G || n_runs[i] > HB_TERM_RUNS) return HB_EINVAL;
+    if (groups[i] >= h->G) return HB_EINVAL;
     off[i] = tot;
     tot += n_runs[i];
+    cap[i] = (uint64_t)n_runs[i] + 1;  // room for the reset that pushes the current-term run
   }
   if (tot && !runs) return HB_EINVAL;
   DeviceGuard guard(h->device);
+  const int rc = reserve_log(h, count, groups, nullptr, cap.data());
+  if (rc != HB_OK) return rc;
   char* d = nullptr;
   const size_t bytes = count * (8ull + 4 + 4) + tot * 16 + 16;
   HB_CHECK(hipMalloc(&d, bytes));
@@ -2450,15 +2651,18 @@ int hb_load_entry_sizes(hb_handle* h, uint32_t count, const uint32_t* groups, co
   if (!h || (count && (!groups || !n_sizes))) return HB_EINVAL;
   if (!sz_on(h->max_msg_size)) return HB_EINVAL;
   if (count == 0) return HB_OK;
-  std::vector<uint64_t> off(count);
+  std::vector<uint64_t> off(count), cap(count);
   uint64_t tot = 0;
   for (uint32_t i = 0; i < count; ++i) {
-    if (groups[i] >= h->G || n_sizes[i] >= HB_SIZE_WINDOW) return HB_EINVAL;
+    if (groups[i] >= h->G) return HB_EINVAL;
     off[i] = tot;
     tot += n_sizes[i];
+    cap[i] = (uint64_t)n_sizes[i] + 1;  // the base entry plus n sizes
   }
   if (tot && !sizes) return HB_EINVAL;
   DeviceGuard guard(h->device);
+  const int rc = reserve_log(h, count, groups, cap.data(), nullptr);
+  if (rc != HB_OK) return rc;
   char* d = nullptr;
   const size_t bytes = count * (4ull + 4 + 8) + tot * 4 + 16;
   HB_CHECK(hipMalloc(&d, bytes));
@@ -2477,6 +2681,21 @@ int hb_load_entry_sizes(hb_handle* h, uint32_t count, const uint32_t* groups, co
   }
   (void)hipFree(d);
   return e == hipSuccess ? HB_OK : HB_EDEVICE;
+}
+
+int hb_reserve_log(hb_handle* h, uint32_t count, const uint32_t* groups, const uint64_t* size_cap,
+                   const uint64_t* run_cap) {
+  if (!h || (count && !groups)) return HB_EINVAL;
+  if (count == 0 || (!size_cap && !run_cap)) return HB_OK;
+  DeviceGuard guard(h->device);
+  return reserve_log(h, count, groups, size_cap, run_cap);
+}
+
+int hb_log_capacity(hb_handle* h, uint32_t group, uint64_t* size_cap, uint64_t* run_cap) {
+  if (!h || group >= h->G) return HB_EINVAL;
+  if (size_cap) *size_cap = h->h_szx.empty() ? 0 : 1ull << (h->h_szx[group] & LX_TAG);
+  if (run_cap) *run_cap = 1ull << (h->h_trx[group] & LX_TAG);
+  return HB_OK;
 }
 
 int hb_set_inflights(hb_handle* h, uint32_t group, uint32_t slot, uint32_t start, uint32_t count,
@@ -2691,6 +2910,16 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   if (b->n && (!b->group || !b->info || !b->term || !b->index)) return HB_EINVAL;
   const bool sized = sz_on(h->max_msg_size);  // appended entries carry descriptors
   if (sized && ((b->n && !b->eoff) || (b->props && !b->peoff) || (b->n_edesc && !b->edesc))) return HB_EINVAL;
+  // MsgApp entry terms need their per-message offsets, and described entries
+  // need terms or descriptors (else a MsgApp's entries would silently vanish)
+  if ((b->eterm && b->n && !b->eoff) || (b->n_edesc && !b->eterm && !b->edesc)) return HB_EINVAL;
+  if ((flags & HB_STEP_HOST_PTRS) && b->eoff) {  // offsets non-decreasing and within the entries
+    uint64_t prev = 0;
+    for (uint64_t i = 0; i < b->n; ++i) {
+      if (b->eoff[i] < prev || b->eoff[i] > b->n_edesc) return HB_EINVAL;
+      prev = b->eoff[i];
+    }
+  }
   DeviceGuard guard(h->device);
   hipStream_t st = h->stream;  // apply stream
   // prep stream (partition + route): the library's own stream when the caller
@@ -2973,6 +3202,73 @@ int hb_copy_events(hb_handle* h, hb_event* out, uint64_t cap, uint64_t* n) {
   hipError_t e = hipMemcpyAsync(out, d, total * sizeof(hb_event), hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   return e == hipSuccess ? HB_OK : HB_EDEVICE;
+}
+
+int hb_events_to_host(hb_handle* h, uint64_t* words, uint64_t cap, uint32_t* counts, uint64_t* total) {
+  if (!h || !counts || !total || (cap && !words)) return HB_EINVAL;
+  DeviceGuard guard(h->device);
+  void *dw = nullptr, *dc = nullptr, *dt = nullptr;
+  if (hipHostGetDevicePointer(&dc, counts, 0) != hipSuccess || hipHostGetDevicePointer(&dt, total, 0) != hipSuccess ||
+      (cap && hipHostGetDevicePointer(&dw, words, 0) != hipSuccess))
+    return HB_EINVAL;  // not memory from hb_alloc_pinned
+  const uint32_t nc = 2 * h->NB;
+  if (!h->stepped) {  // no step yet: no events
+    HB_CHECK(hipMemsetAsync(dc, 0, nc * 4ull, h->stream));
+    HB_CHECK(hipMemsetAsync(dt, 0, 8, h->stream));
+    return HB_OK;
+  }
+  if (h->evw_cap < nc + 1ull) {
+    if (h->evw) (void)hipFree(h->evw);
+    h->evw = nullptr;
+    h->evw_cap = 0;
+    HB_CHECK(hipMalloc(&h->evw, (nc + 1ull) * 8));
+    h->evw_cap = nc + 1ull;
+  }
+  const PrepSet& ps = h->set[h->cur];
+  hipLaunchKernelGGL(k_scan_words, dim3(1), dim3(1024), 0, h->stream, (const uint32_t*)ps.ev_counts, nc, h->evw,
+                     static_cast<uint32_t*>(dc), static_cast<uint64_t*>(dt));
+  hipLaunchKernelGGL(k_gather_words, dim3(nc), dim3(256), 0, h->stream, (const uint64_t*)h->ev,
+                     (const uint32_t*)ps.ev_counts, (const uint64_t*)ps.ev_off, (const uint64_t*)h->evw,
+                     static_cast<uint64_t*>(dw), cap);
+  return hipGetLastError() == hipSuccess ? HB_OK : HB_EDEVICE;
+}
+
+int hb_event_words_chunks(hb_handle* h, uint32_t* n_chunks, uint32_t* groups_per_chunk) {
+  if (!h || !n_chunks) return HB_EINVAL;
+  *n_chunks = 2 * h->NB;
+  if (groups_per_chunk) *groups_per_chunk = PART;
+  return HB_OK;
+}
+
+int hb_expand_event_words(const uint64_t* words, uint64_t n_words, const uint32_t* counts, uint32_t n_chunks,
+                          hb_event* out, uint64_t cap, uint64_t* n_out) {
+  if (!n_out || (n_words && (!words || !counts))) return HB_EINVAL;
+  uint64_t k = 0, w = 0;
+  for (uint32_t c = 0; c < n_chunks; ++c) {
+    const uint64_t end = w + counts[c];
+    if (end > n_words) return HB_EINVAL;
+    for (; w < end; ++w) {
+      const uint64_t x0 = words[w];
+      const uint32_t type = (uint32_t)x0 & 0xF;
+      if (type == EVC_CONT) continue;
+      const uint32_t to = (uint32_t)(x0 >> 4) & 0x7F, aux = (uint32_t)(x0 >> 12) & 0xF;
+      const uint32_t group = (c >> 1) * PART + ((uint32_t)(x0 >> 16) & 0xFF);
+      uint64_t x = x0 >> 24;
+      if (((x0 >> 11) & 1u) && w + 1 < end) x |= (words[w + 1] >> 4) << 40;
+      if (type == EVC_BCAST) {
+        for (uint32_t s = 0; s < 7; ++s)
+          if ((to >> s) & 1u) {
+            if (out && k < cap) out[k] = hb_event{x, group, (uint8_t)HB_EV_APP, (uint8_t)s, 0};
+            ++k;
+          }
+      } else {
+        if (out && k < cap) out[k] = hb_event{x, group, (uint8_t)type, (uint8_t)to, (uint16_t)aux};
+        ++k;
+      }
+    }
+  }
+  *n_out = k;
+  return (out && k > cap) ? HB_EINVAL : HB_OK;
 }
 
 int hb_stats_device(hb_handle* h, uint64_t** dev_stats) {

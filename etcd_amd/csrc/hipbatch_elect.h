@@ -113,26 +113,11 @@ struct ElectLane {
     }
   }
 
-  // Lane::tr_push / reset / transition / poll (raft/raft.go:334-404, :445-460)
-  __device__ __forceinline__ uint64_t* trs_at(uint32_t k) const { return S.trs + (size_t)k * S.G + g; }
-  __device__ __forceinline__ uint64_t* trt_at(uint32_t k) const { return S.trt + (size_t)k * S.G + g; }
-  __device__ __forceinline__ void tr_push(uint64_t start, uint64_t t) {
-    uint32_t nr = m_trn(meta), h = m_trh(meta);
-    if (nr > 0 && *trt_at((h + nr - 1) & (HB_TERM_RUNS - 1)) == t) return;  // the run goes on
-    if (nr == HB_TERM_RUNS) {
-      h = (h + 1) & (HB_TERM_RUNS - 1);
-      --nr;
-    }
-    const uint32_t k = (h + nr) & (HB_TERM_RUNS - 1);
-    *trs_at(k) = start;
-    *trt_at(k) = t;
-    meta = (meta & ~(0x7Full << 40)) | ((uint64_t)((nr + 1) & 0xF) << 40) | ((uint64_t)(h & 7) << 44);
-    dirty |= D_META;
-  }
+  // Lane::reset / transition / poll (raft/raft.go:334-404, :445-460)
   __device__ __forceinline__ void reset(uint64_t t) {
     if (term != t) {
 #ifndef HB_X_NOPUSH
-      if (tfirst != HB_NO_INDEX) tr_push(tfirst, term);
+      if (tfirst != HB_NO_INDEX) tr_push(S, g, tfirst, term);
 #endif
       term = t;
       set_vote(HB_REF_NONE);

@@ -32,7 +32,6 @@ constexpr uint32_t CHUNK = 4 * PART;         // messages staged in LDS per round
 // ---- packed group meta (u64) ------------------------------------------------
 //  [0:2) state  [2:5) n  [5:9) self slot  [9:13) lead ref  [13:17) vote ref
 //  [17:21) fault  [21] M_TL  [22] M_SM  [24:32) votes responded  [32:40) votes granted
-//  [40:44) older term runs kept  [44:47) their ring head (follower side)
 //  M_TL: tlast == last — the tlast array is then not kept (a leader's current-
 //  term run always ends at its last entry).  M_SM: the self slot's Match ==
 //  last and Next == last + 1 — its match / next arrays are then not kept (a
@@ -55,9 +54,6 @@ __host__ __device__ inline uint32_t m_vote(uint64_t m) { return (uint32_t)((m >>
 __host__ __device__ inline uint32_t m_fault(uint64_t m) { return (uint32_t)((m >> 17) & 0xF); }
 __host__ __device__ inline uint32_t m_resp(uint64_t m) { return (uint32_t)((m >> 24) & 0xFF); }
 __host__ __device__ inline uint32_t m_grant(uint64_t m) { return (uint32_t)((m >> 32) & 0xFF); }
-__host__ __device__ inline uint32_t m_trn(uint64_t m) { return (uint32_t)((m >> 40) & 0xF); }
-__host__ __device__ inline uint32_t m_trh(uint64_t m) { return (uint32_t)((m >> 44) & 0x7); }
-static_assert(HB_TERM_RUNS == 8, "term-run ring head is 3 bits");
 
 // ---- packed progress meta (u32) ----------------------------------------------
 //  [0:2) ProgressState  [2] Paused  [3:13) inflights.start  [13:24) inflights.count
@@ -95,24 +91,31 @@ struct DevState {
   uint32_t* tcfg;             // [G] ElectionTick | HeartbeatTick << 16
   const uint64_t* rnd;        // [nrnd] the node's r.rand.Int() stream (host supplied)
   uint64_t nrnd;
-  // finite max_msg_size only (sz_on): sizes of the latest entries, for limitSize
-  uint64_t* szp;              // [HB_SIZE_WINDOW][G] szp[i % R] = sum of Entry.Size() of (szlo, i]
-  uint64_t* szlo;             // [G] oldest index i whose szp(i) is kept (szp(szlo) = the base)
+  // The log index (§3.12 of DESIGN.md): per group, two rings in extents of the
+  // handle's log pool whose capacities the host reserves (hb_reserve_log).
+  // An extent word is the extent's address (128-byte aligned) | log2(capacity).
+  // finite max_msg_size only (sz_on): the cumulative Entry.Size() of the log, for limitSize
+  uint64_t* szx;              // [G] extent of u64 cum[i & (cap-1)] = sum of Entry.Size() of (szlo, i]
+  uint64_t* szlo;             // [G] oldest index i whose cum(i) is kept (cum(szlo) = the base)
   const uint32_t* edesc;      // this step's entry descriptors (hb_batch.edesc / eoff / peoff)
   const uint64_t* eoff;
   const uint64_t* peoff;
-  // follower side
-  uint64_t* trs;              // [HB_TERM_RUNS][G] older term runs of the log: start index
-  uint64_t* trt;              // [HB_TERM_RUNS][G] ... and term (ring, meta holds count / head)
+  // the log's term runs below the current-term run (follower side lookups)
+  uint64_t* trx;              // [G] extent of {start, term} u64 pairs (a ring, oldest at head)
+  uint64_t* trc;              // [G] runs kept | ring head << 32
   const uint64_t* bcommit;    // this step's hb_batch.commit (m.Commit of MsgApp / MsgHeartbeat)
   const uint64_t* eterm;      // hb_batch.eterm (MsgApp entry terms)
   uint64_t n_ent;             // hb_batch.n_edesc
   uint64_t bn;                // hb_batch.n
 };
 
+// ---- log-pool extents ------------------------------------------------------------
+constexpr uint64_t LX_TAG = 0x3F;  // low bits of an extent word: log2(capacity)
+__host__ __device__ inline uint64_t lx_word(uint64_t addr, uint32_t log2cap) { return addr | log2cap; }
+__device__ __forceinline__ uint64_t* lx_base(uint64_t x) { return reinterpret_cast<uint64_t*>(x & ~LX_TAG); }
+__device__ __forceinline__ uint64_t lx_cap(uint64_t x) { return 1ull << (x & LX_TAG); }
+
 // ---- entry sizes (finite MaxSizePerMsg) -----------------------------------------
-static_assert((HB_SIZE_WINDOW & (HB_SIZE_WINDOW - 1)) == 0, "size window is a power of two");
-constexpr uint64_t SZ_MASK = HB_SIZE_WINDOW - 1;
 __host__ __device__ inline bool sz_on(uint64_t max_msg_size) { return max_msg_size != 0 && max_msg_size != HB_NO_LIMIT; }
 // sovRaft: varint length (raft/raftpb/raft.pb.go)
 __device__ __forceinline__ uint64_t sov(uint64_t x) { return x ? (uint64_t)(70 - __clzll(x)) / 7 : 1; }
@@ -125,27 +128,36 @@ __device__ __forceinline__ uint64_t ent_size(uint32_t desc, uint64_t term, uint6
   }
   return n;
 }
-__device__ __forceinline__ uint64_t* szp_at(const DevState& S, uint32_t g, uint64_t i) {
-  return S.szp + (size_t)(i & SZ_MASK) * S.G + g;
+// the cumulative size of entry i in the group's ring (extent word x)
+__device__ __forceinline__ uint64_t* cum_at(uint64_t x, uint64_t i) { return lx_base(x) + (i & (lx_cap(x) - 1)); }
+// The ring keeps cum(i) for i in [szlo, last] as long as that span fits its
+// capacity; appending past it drops the oldest (szlo moves up).  The host
+// reserves a capacity that covers [firstIndex - 1, lastIndex] plus what a batch
+// can append (hb_reserve_log), so only entries below firstIndex - 1 ever leave.
+__device__ __forceinline__ void sz_keep(const DevState& S, uint32_t g, uint64_t x, uint64_t last) {
+  const uint64_t cap = lx_cap(x);
+  if (last >= cap && S.szlo[g] < last - (cap - 1)) S.szlo[g] = last - (cap - 1);
 }
 // appendEntry's entries (last0, last0 + k] at Term `term`: their sizes enter the
-// window (d = their descriptors; null = the becomeLeader noop, pb.Entry{})
+// ring (d = their descriptors; null = the becomeLeader noop, pb.Entry{})
 __device__ __forceinline__ void sz_append(const DevState& S, uint32_t g, uint64_t last0, uint64_t k, uint64_t term,
                                           const uint32_t* d) {
   if (!sz_on(S.max_msg_size)) return;
-  uint64_t acc = *szp_at(S, g, last0);
+  const uint64_t x = S.szx[g];
+  const uint64_t cap = lx_cap(x);
+  uint64_t acc = *cum_at(x, last0);
   for (uint64_t j = 1; j <= k; ++j) {
     acc += ent_size(d ? d[j - 1] : 0u, term, last0 + j);
-    if (j + HB_SIZE_WINDOW > k) *szp_at(S, g, last0 + j) = acc;
+    if (j + cap > k) *cum_at(x, last0 + j) = acc;
   }
-  const uint64_t last = last0 + k;
-  if (last >= HB_SIZE_WINDOW && S.szlo[g] < last - (HB_SIZE_WINDOW - 1)) S.szlo[g] = last - (HB_SIZE_WINDOW - 1);
+  sz_keep(S, g, x, last0 + k);
 }
 // sendAppend's entries(next, maxMsgSize) (raft/raft.go:265, raft/log.go:219-224)
 // cut by limitSize (raft/util.go:97-110): the last index sent, next <= last.
 // The first entry always goes; each further one while the running sum of
 // Entry.Size() stays <= maxSize (a binary search over the cumulative sizes).
-// *ok = false when the window does not reach back to next - 1.
+// *ok = false when the ring does not reach back to next - 1 (the caller did
+// not load the group's sizes: hb_load_entry_sizes / hb_reserve_log).
 __device__ __forceinline__ uint64_t sz_limit(const DevState& S, uint32_t g, uint64_t next, uint64_t last, bool* ok) {
   if (S.max_msg_size == 0) return next;
   if (S.max_msg_size == HB_NO_LIMIT) return last;
@@ -153,14 +165,74 @@ __device__ __forceinline__ uint64_t sz_limit(const DevState& S, uint32_t g, uint
     *ok = false;
     return next;
   }
-  const uint64_t base = *szp_at(S, g, next - 1);
+  const uint64_t x = S.szx[g];
+  const uint64_t base = *cum_at(x, next - 1);
   uint64_t lo = next, hi = last;
   while (lo < hi) {
     const uint64_t mid = lo + (hi - lo + 1) / 2;
-    if (*szp_at(S, g, mid) - base <= S.max_msg_size) lo = mid;
+    if (*cum_at(x, mid) - base <= S.max_msg_size) lo = mid;
     else hi = mid - 1;
   }
   return lo;
+}
+
+// ---- term runs (follower side) ---------------------------------------------------
+// The log's runs below the current-term run, oldest first, as a ring of
+// {start index, term} pairs: run k covers [start_k, start_k+1).  push adds a
+// newer run (a full ring drops its oldest; the host reserves enough that only
+// runs wholly below firstIndex - 1 can leave), cut drops the runs starting at
+// or after an index, find returns the newest run starting at or before i.
+struct Runs {
+  uint64_t* R;
+  uint64_t mask;
+  uint32_t n, h;
+  __device__ __forceinline__ void open(const DevState& S, uint32_t g) {
+    const uint64_t x = S.trx[g], c = S.trc[g];
+    R = lx_base(x);
+    mask = lx_cap(x) - 1;
+    n = (uint32_t)c;
+    h = (uint32_t)(c >> 32);
+  }
+  __device__ __forceinline__ uint64_t* at(uint32_t k) const { return R + 2 * ((h + k) & mask); }
+  __device__ __forceinline__ void close(const DevState& S, uint32_t g) const {
+    S.trc[g] = (uint64_t)n | ((uint64_t)h << 32);
+  }
+  __device__ __forceinline__ void push(uint64_t start, uint64_t t) {
+    if (n > 0 && at(n - 1)[1] == t) return;  // the run goes on
+    if ((uint64_t)n == mask + 1) {           // full: the oldest run leaves
+      h = (uint32_t)((h + 1) & mask);
+      --n;
+    }
+    uint64_t* r = at(n);
+    r[0] = start;
+    r[1] = t;
+    ++n;
+  }
+  __device__ __forceinline__ void cut(uint64_t ci) {
+    while (n > 0 && at(n - 1)[0] >= ci) --n;
+  }
+  // the term of index i (binary search; starts increase), *ok = false below the oldest run
+  __device__ __forceinline__ uint64_t find(uint64_t i, bool* ok) const {
+    if (n == 0 || at(0)[0] > i) {
+      *ok = false;
+      return 0;
+    }
+    uint32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo + 1) / 2;
+      if (at(mid)[0] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    return at(lo)[1];
+  }
+};
+// reset of a group whose term changes: its current-term run becomes an older run
+__device__ __forceinline__ void tr_push(const DevState& S, uint32_t g, uint64_t start, uint64_t t) {
+  Runs r;
+  r.open(S, g);
+  const uint32_t n0 = r.n, h0 = r.h;
+  r.push(start, t);
+  if (r.n != n0 || r.h != h0) r.close(S, g);
 }
 
 // ---- event sink ---------------------------------------------------------------
@@ -585,36 +657,14 @@ struct Lane {
     ev(HB_EV_APP, s, 0, x);
   }
 
-  // ---------------------------------------------------------------- term runs
-  // The log's terms as the device keeps them: the current-term run [tfirst,
-  // last] (tfirst = HB_NO_INDEX: none) plus up to HB_TERM_RUNS older runs
-  // (start, term) in a ring [slot][G], count / head in meta.
-  __device__ __forceinline__ uint64_t* trs_at(uint32_t k) const { return S.trs + (size_t)k * S.G + g; }
-  __device__ __forceinline__ uint64_t* trt_at(uint32_t k) const { return S.trt + (size_t)k * S.G + g; }
-  __device__ __forceinline__ uint32_t tr_slot(uint32_t k) const { return (m_trh(meta) + k) & (HB_TERM_RUNS - 1); }
-  __device__ __forceinline__ void set_tr(uint32_t n, uint32_t h) {
-    meta = (meta & ~(0x7Full << 40)) | ((uint64_t)(n & 0xF) << 40) | ((uint64_t)(h & 7) << 44);
-    dirty |= D_META;
-  }
-  __device__ __forceinline__ void tr_push(uint64_t start, uint64_t t) {
-    uint32_t n = m_trn(meta), h = m_trh(meta);
-    if (n > 0 && *trt_at(tr_slot(n - 1)) == t) return;  // the run goes on
-    if (n == HB_TERM_RUNS) {  // the oldest run leaves the window
-      h = (h + 1) & (HB_TERM_RUNS - 1);
-      --n;
-    }
-    const uint32_t k = (h + n) & (HB_TERM_RUNS - 1);
-    *trs_at(k) = start;
-    *trt_at(k) = t;
-    set_tr(n + 1, h);
-  }
-
   // ---------------------------------------------------------------- transitions
-  // reset raft/raft.go:334-349
+  // reset raft/raft.go:334-349.  The log's terms as the device keeps them: the
+  // current-term run [tfirst, last] (tfirst = HB_NO_INDEX: none) plus the
+  // older runs (Runs, the log index).
   __device__ __forceinline__ void reset(uint64_t t) {
     if (term != t) {
 #ifndef HB_X_NOPUSH
-      if (tfirst != HB_NO_INDEX) tr_push(tfirst, term);  // the old current-term run becomes an older run
+      if (tfirst != HB_NO_INDEX) tr_push(S, g, tfirst, term);  // the old current-term run becomes an older run
 #endif
       term = t;
       set_vote(HB_REF_NONE);
@@ -672,14 +722,14 @@ struct Lane {
   // ---------------------------------------------------------------- follower side
   // raftLog.term(i) from what the device keeps: 0 outside [first-1, last]
   // (raft/log.go:198-203), Term in the current-term run, else the newest older
-  // run starting at or before i; *ok = false when the runs do not reach back.
+  // run starting at or before i; *ok = false when the loaded runs do not reach
+  // back (the caller did not load the group's runs: hb_load_term_runs).
   __device__ __forceinline__ uint64_t fterm(uint64_t i, bool* ok) const {
     if (i + 1 < first || i > last) return 0;
     if (tfirst != HB_NO_INDEX && i >= tfirst) return term;
-    for (int k = (int)m_trn(meta) - 1; k >= 0; --k)
-      if (*trs_at(tr_slot((uint32_t)k)) <= i) return *trt_at(tr_slot((uint32_t)k));
-    *ok = false;
-    return 0;
+    Runs r;
+    r.open(S, g);
+    return r.find(i, ok);
   }
   __device__ __forceinline__ void resp(uint32_t to, uint32_t kind, uint64_t x) { ev(HB_EV_RESP, to, kind, x); }
 
@@ -688,19 +738,19 @@ struct Lane {
   // cut at ci - 1 and takes entries ci .. index + ne (terms eterm[e0 ..]).
   __device__ __forceinline__ void follower_append(uint64_t ci, uint64_t index, uint64_t e0, uint64_t ne) {
     if (!prog) load_progress();  // M_SM derives the self Match from last: pin it before last moves
-    uint32_t nr = m_trn(meta);
-    const uint32_t h = m_trh(meta);
-    while (nr > 0 && *trs_at(tr_slot(nr - 1)) >= ci) --nr;
-    set_tr(nr, h);
+    Runs rr;
+    rr.open(S, g);
+    rr.cut(ci);
     if (tfirst != HB_NO_INDEX && tfirst >= ci) tfirst = HB_NO_INDEX;
     const bool sized = sz_on(S.max_msg_size);
-    uint64_t acc = 0;
+    uint64_t acc = 0, x = 0;
     if (sized) {
-      if (ci - 1 < S.szlo[g]) {
+      x = S.szx[g];
+      if (ci - 1 < S.szlo[g]) {  // the log (and its sizes) restart at ci - 1
         S.szlo[g] = ci - 1;
-        *szp_at(S, g, ci - 1) = 0;
+        *cum_at(x, ci - 1) = 0;
       }
-      acc = *szp_at(S, g, ci - 1);
+      acc = *cum_at(x, ci - 1);
     }
     const uint64_t lastnewi = index + ne;
 #pragma nounroll
@@ -711,21 +761,21 @@ struct Lane {
         if (tfirst == HB_NO_INDEX) tfirst = j;
       } else {
         if (tfirst != HB_NO_INDEX) {  // a lower term after Term entries
-          tr_push(tfirst, term);
+          rr.push(tfirst, term);
           tfirst = HB_NO_INDEX;
         }
-        tr_push(j, t);
+        rr.push(j, t);
       }
       if (sized) {
         acc += ent_size(S.edesc ? S.edesc[k] : 0u, t, j);
-        *szp_at(S, g, j) = acc;
+        *cum_at(x, j) = acc;
       }
     }
+    rr.close(S, g);
     last = lastnewi;
     tlast = tfirst != HB_NO_INDEX ? last : 0;
     dirty |= D_LAST | D_TRUN;
-    if (sized && last >= HB_SIZE_WINDOW && S.szlo[g] < last - (HB_SIZE_WINDOW - 1))
-      S.szlo[g] = last - (HB_SIZE_WINDOW - 1);
+    if (sized) sz_keep(S, g, x, last);
     ev(HB_EV_FOLLOW, 0, HB_FOLLOW_APPEND, arrival_x());
   }
 
@@ -797,15 +847,19 @@ struct Lane {
         committed = sidx;
         S.snap[g] = sidx;
         dirty |= D_FIRST | D_LAST | D_COMMIT | D_TRUN;
-        set_tr(0, 0);
         tfirst = HB_NO_INDEX;
         tlast = 0;
+        Runs rr;
+        rr.open(S, g);
+        rr.n = 0;
+        rr.h = 0;
         if (sterm == term) {
           tfirst = sidx;
           tlast = sidx;
         } else {
-          tr_push(sidx, sterm);
+          rr.push(sidx, sterm);
         }
+        rr.close(S, g);
         const uint32_t nn = n(), sf = self();
 #pragma unroll
         for (int s = 0; s < NMAX; ++s) {  // setProgress for every peer of the ConfState
@@ -819,7 +873,7 @@ struct Lane {
         prog = true;
         if (sz_on(S.max_msg_size)) {
           S.szlo[g] = sidx;
-          *szp_at(S, g, sidx) = 0;
+          *cum_at(S.szx[g], sidx) = 0;
         }
         ev(HB_EV_FOLLOW, 0, HB_FOLLOW_RESTORE, arrival_x());
       }

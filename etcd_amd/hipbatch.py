@@ -55,6 +55,8 @@ def lib():
         "hb_set_log_bounds": (C.c_int, [H, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
         "hb_load_entry_sizes": (C.c_int, [H, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
         "hb_load_term_runs": (C.c_int, [H, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
+        "hb_reserve_log": (C.c_int, [H, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
+        "hb_log_capacity": (C.c_int, [H, C.c_uint32, P(C.c_uint64), P(C.c_uint64)]),
         "hb_get_inflights": (C.c_int, [H, C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32), C.c_void_p]),
         "hb_step": (C.c_int, [H, P(abi.hb_batch), C.c_uint32]),
         "hb_load_timers": (C.c_int, [H, C.c_uint32, C.c_uint32, C.c_void_p]),
@@ -66,6 +68,10 @@ def lib():
                                 C.c_void_p]),
         "hb_events_device": (C.c_int, [H, P(C.c_void_p), P(C.c_void_p), P(C.c_void_p), P(C.c_uint32)]),
         "hb_copy_events": (C.c_int, [H, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
+        "hb_events_to_host": (C.c_int, [H, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+        "hb_event_words_chunks": (C.c_int, [H, P(C.c_uint32), P(C.c_uint32)]),
+        "hb_expand_event_words": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64,
+                                            P(C.c_uint64)]),
         "hb_stats_device": (C.c_int, [H, P(C.c_void_p)]),
         "hb_stats": (C.c_int, [H, C.c_void_p]),
         "hb_phase_ms": (C.c_int, [H, C.c_void_p, P(C.c_uint32)]),
@@ -120,6 +126,9 @@ class Engine:
         if getattr(self, "h", None):
             lib().hb_destroy(self.h)
             self.h = None
+        for p, _ in getattr(self, "_pins", {}).values():
+            lib().hb_free_pinned(p)
+        self._pins = {}
 
     def __del__(self):
         try:
@@ -172,7 +181,8 @@ class Engine:
                                                             s.ctypes.data))
 
     def load_entry_sizes(self, sizes):
-        """Finite max_msg_size: {group slot: Entry.Size() of its last n entries, oldest first}."""
+        """Finite max_msg_size: {group slot: Entry.Size() of its last n entries, oldest first}
+        (normally the whole log from firstIndex; the ring grows to hold them)."""
         gs = np.ascontiguousarray(sorted(sizes), dtype=np.uint32)
         ns = np.ascontiguousarray([len(sizes[int(g)]) for g in gs], dtype=np.uint32)
         flat = np.ascontiguousarray(np.concatenate([np.asarray(sizes[int(g)], dtype=np.uint32) for g in gs])
@@ -181,12 +191,31 @@ class Engine:
                                                                 flat.ctypes.data))
 
     def load_term_runs(self, runs):
-        """Follower side: {group slot: [(start index, term), ...] older term runs, oldest first}."""
+        """Follower side: {group slot: [(start index, term), ...] older term runs, oldest first}
+        (normally every run down to firstIndex - 1; the ring grows to hold them)."""
         gs = np.ascontiguousarray(sorted(runs), dtype=np.uint32)
         ns = np.ascontiguousarray([len(runs[int(g)]) for g in gs], dtype=np.uint32)
         flat = np.ascontiguousarray([x for g in gs for r in runs[int(g)] for x in r] or [0], dtype=np.uint64)
         _check("hb_load_term_runs", lib().hb_load_term_runs(self.h, len(gs), gs.ctypes.data, ns.ctypes.data,
                                                             flat.ctypes.data))
+
+    def reserve_log(self, groups, size_cap=None, run_cap=None):
+        """Grow the log-index rings of the given group slots to hold at least
+        size_cap entry sizes / run_cap term runs (hb_reserve_log; None = unchanged)."""
+        g = np.ascontiguousarray(groups, dtype=np.uint32)
+        if not len(g):
+            return
+        sc = None if size_cap is None else np.ascontiguousarray(np.broadcast_to(size_cap, g.shape), dtype=np.uint64)
+        rc = None if run_cap is None else np.ascontiguousarray(np.broadcast_to(run_cap, g.shape), dtype=np.uint64)
+        _check("hb_reserve_log", lib().hb_reserve_log(self.h, len(g), g.ctypes.data,
+                                                      None if sc is None else sc.ctypes.data,
+                                                      None if rc is None else rc.ctypes.data))
+
+    def log_capacity(self, group):
+        """(size ring capacity, term-run ring capacity) of one group slot."""
+        a, b = C.c_uint64(), C.c_uint64()
+        _check("hb_log_capacity", lib().hb_log_capacity(self.h, group, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     def get_inflights(self, group, slot):
         out = np.zeros(self.max_inflight, dtype=np.uint64)
@@ -274,6 +303,64 @@ class Engine:
         n = C.c_uint64()
         _check("hb_copy_events", lib().hb_copy_events(self.h, C.c_void_p(host_ptr), cap, C.byref(n)))
         return n.value
+
+    def n_chunks(self):
+        n, per = C.c_uint32(), C.c_uint32()
+        _check("hb_event_words_chunks", lib().hb_event_words_chunks(self.h, C.byref(n), C.byref(per)))
+        return n.value, per.value
+
+    def events_to_host(self, words_ptr, cap, counts_ptr, total_ptr):
+        """Asynchronous compact delta (hb_events_to_host) into pinned buffers
+        (hb_alloc_pinned / torch pin_memory): read them after sync()."""
+        _check("hb_events_to_host", lib().hb_events_to_host(self.h, C.c_void_p(words_ptr), cap,
+                                                            C.c_void_p(counts_ptr), C.c_void_p(total_ptr)))
+
+    def event_words(self):
+        """The last step's compact event words and per-chunk counts (host copies;
+        synchronizes), via hb_events_to_host into pinned buffers."""
+        nc, _ = self.n_chunks()
+        L = lib()
+        pins = getattr(self, "_pins", None)
+        if pins is None:
+            pins = self._pins = {}
+
+        def pinned(name, nbytes):
+            p, cap = pins.get(name, (None, 0))
+            if cap < nbytes:
+                if p:
+                    L.hb_free_pinned(p)
+                q = C.c_void_p()
+                _check("hb_alloc_pinned", L.hb_alloc_pinned(max(nbytes, 64), C.byref(q)))
+                pins[name] = (q.value, max(nbytes, 64))
+            return pins[name][0]
+        cnt = pinned("counts", 4 * nc)
+        tot = pinned("total", 8)
+        cap = pins.get("words", (None, 0))[1] // 8
+        for _ in range(2):
+            w = pinned("words", 8 * max(cap, 1))
+            self.events_to_host(w, cap, cnt, tot)
+            self.sync()
+            total = C.c_uint64.from_address(tot).value
+            if total <= cap:
+                break
+            cap = total
+        words = np.ctypeslib.as_array((C.c_uint64 * max(total, 1)).from_address(w))[:total].copy()
+        counts = np.ctypeslib.as_array((C.c_uint32 * nc).from_address(cnt)).copy()
+        return words, counts
+
+    @staticmethod
+    def expand_words(words, counts):
+        """hb_expand_event_words: compact words -> hb_event records (CPU)."""
+        L = lib()
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        c = np.ascontiguousarray(counts, dtype=np.uint32)
+        n = C.c_uint64()
+        _check("hb_expand_event_words", L.hb_expand_event_words(w.ctypes.data, len(w), c.ctypes.data, len(c), None,
+                                                                0, C.byref(n)))
+        out = np.zeros(max(n.value, 1), dtype=abi.EVENT_DTYPE)
+        _check("hb_expand_event_words", L.hb_expand_event_words(w.ctypes.data, len(w), c.ctypes.data, len(c),
+                                                                out.ctypes.data, len(out), C.byref(n)))
+        return out[: n.value]
 
     def stats(self):
         out = np.zeros(abi.HB_STAT_COUNT, dtype=np.uint64)

@@ -258,40 +258,49 @@ def attach_entry_descs(batch, G, seed=3, max_len=64, nil_p=0.2, conf_p=0.1):
 def window_sizes(groups, runs, seed=4, max_len=64, frac_full=0.7):
     """Entry.Size() of each group's latest entries (hb_load_entry_sizes): random
     payloads for the entries the log already holds, their Term from the log's
-    term runs; most groups get their whole log (up to HB_SIZE_WINDOW - 1), the
-    rest only a few entries (sends further back fault HB_FAULT_SIZE_WINDOW)."""
+    term runs; most groups get their whole log (firstIndex .. lastIndex), the
+    rest only a few entries (a caller that loads less than the log: sends
+    further back fault HB_FAULT_SIZE_WINDOW, the engine's precondition)."""
     rng = np.random.default_rng(seed)
     out = {}
     for g in range(len(groups)):
         first, last = int(groups["first_index"][g]), int(groups["last_index"][g])
-        avail = min(last - (first - 1), A.HB_SIZE_WINDOW - 1)
+        avail = last - (first - 1)
         k = avail if rng.random() < frac_full else int(rng.integers(0, avail + 1))
-        rr = runs[g]
-        z = []
-        for i in range(last - k + 1, last + 1):
-            term = 0
-            for idx, t in rr:
-                if idx <= i:
-                    term = t
-            ln = int(rng.integers(0, max_len + 1))
-            d = A.hb_ent_desc(ln, int(rng.random() < 0.1), rng.random() >= 0.2)
-            z.append(A.entry_size(d, term, i))
-        out[g] = z
+        rr = np.asarray(runs[g], dtype=np.uint64).reshape(-1, 2)
+        idx = np.arange(last - k + 1, last + 1, dtype=np.uint64)
+        term = rr[np.searchsorted(rr[:, 0], idx, side="right") - 1, 1] if k else idx
+        ln = rng.integers(0, max_len + 1, k).astype(np.uint64)
+        typ = (rng.random(k) < 0.1).astype(np.uint64)
+        has = rng.random(k) >= 0.2
+        z = 3 + _sov(typ) + _sov(term) + _sov(idx) + np.where(has, 1 + ln + _sov(ln), 0)
+        out[g] = z.astype(np.uint32).tolist()
     return out
 
 
-def older_runs(groups, runs, keep=A.HB_TERM_RUNS):
-    """The log term runs below each group's current-term run (term_first), the
-    newest `keep` of them: what hb_load_term_runs takes (follower side)."""
+def _sov(x):
+    """sovRaft (varint length) of a uint64 array."""
+    x = np.asarray(x, dtype=np.uint64)
+    n = np.ones(x.shape, dtype=np.uint64)
+    y = x >> np.uint64(7)
+    while y.any():
+        n += (y > 0).astype(np.uint64)
+        y >>= np.uint64(7)
+    return n
+
+
+def older_runs(groups, runs, keep=None):
+    """The log term runs below each group's current-term run (term_first), all
+    of them or the newest `keep`: what hb_load_term_runs takes (follower side)."""
     out = {}
     for g in range(len(groups)):
         tf = int(groups["term_first"][g])
         rr = [(int(i), int(t)) for i, t in runs[g] if tf == A.HB_NO_INDEX or int(i) < tf]
-        out[g] = rr[-keep:]
+        out[g] = rr if keep is None else rr[max(len(rr) - keep, 0):]
     return out
 
 
-def follower_messages(now, term_of, nmsg, seed=5, nonmember=0.05, max_ents=4):
+def follower_messages(now, term_of, nmsg, seed=5, nonmember=0.05, max_ents=4, deep=0.0):
     """Random follower-side messages (MsgApp with entries / MsgHeartbeat /
     MsgSnap / MsgVote) against the groups' current state `now`; term_of(g, i)
     gives a group's log term (the oracle's).  Mostly well-formed (matching
@@ -323,6 +332,8 @@ def follower_messages(now, term_of, nmsg, seed=5, nonmember=0.05, max_ents=4):
         ents = []
         if t == A.HB_MSG_APP:
             x = max(0, last + int(rng.integers(-3, 2)))
+            if rng.random() < deep:  # a probe anywhere in the log (a leader backing up after rejections)
+                x = int(rng.integers(0, last + 1))
             h = term_of(g, x) if rng.random() < 0.8 else int(rng.integers(0, gt + 2))
             if x > 0 and h == 0:  # LogTerm 0 names index 0 only: a leader holds the entry it sends after
                 h = int(rng.integers(1, gt + 2))
@@ -352,6 +363,68 @@ def follower_messages(now, term_of, nmsg, seed=5, nonmember=0.05, max_ents=4):
     return dict(group=np.array(grp, np.uint32), info=np.array(info, np.uint32), term=np.array(term, np.uint64),
                 index=np.array(index, np.uint64), hint=np.array(hint, np.uint64), commit=np.array(commit, np.uint64),
                 eoff=np.array(eoff, np.uint64), eterm=np.array(eterm or [0], np.uint64)[:len(eterm)], props=None)
+
+
+def many_runs_groups(G, n=3, seed=9, runs_lo=18, runs_hi=30, run_len=40):
+    """Followers whose logs hold runs_lo..runs_hi term runs of 1..run_len
+    entries (the follower side's raftLog.term at any depth); every group's
+    Progress in its reset form.  Returns (groups, runs)."""
+    rng = np.random.default_rng(seed)
+    g = np.zeros(G, dtype=A.GROUP_DTYPE)
+    runs = []
+    for i in range(G):
+        k = int(rng.integers(runs_lo, runs_hi + 1))
+        lens = rng.integers(1, run_len + 1, k)
+        first = int(rng.integers(1, 50))
+        t = int(rng.integers(0, 3))
+        rr, pos = [], first - 1
+        for L in lens:
+            rr.append((pos, t))
+            pos += int(L)
+            t += int(rng.integers(1, 4))
+        last = pos - 1
+        top = rr[-1][1]
+        term = top + int(rng.integers(0, 3))
+        runs.append(rr)
+        r = g[i]
+        r["term"], r["first_index"], r["last_index"] = term, first, last
+        r["committed"] = int(rng.integers(first - 1, max(first - 1, last - 5) + 1))
+        r["snap_index"] = first - 1
+        r["term_first"], r["term_last"] = (rr[-1][0], last) if top == term else (A.HB_NO_INDEX, 0)
+        r["state"], r["n"], r["self_slot"] = A.HB_STATE_FOLLOWER, n, 0
+        r["lead"] = 1 if rng.random() < 0.7 else A.HB_REF_NONE
+        r["vote"] = int(rng.choice([A.HB_REF_NONE, 1, 0]))
+        for s in range(n):
+            r["pr"][s]["match"] = last if s == 0 else 0
+            r["pr"][s]["next"] = last + 1
+    return g, runs
+
+
+def deep_lag_leaders(G, n=3, seed=10, last_lo=6000, last_hi=9000, lag_min=5000):
+    """Leaders with long logs whose followers are far behind (Probe, or
+    Replicate with an empty window), Match at least lag_min entries below
+    lastIndex: every sendAppend to them cuts entries(Next, maxMsgSize) deep in
+    the log.  Returns (groups, runs)."""
+    rng = np.random.default_rng(seed)
+    g = np.zeros(G, dtype=A.GROUP_DTYPE)
+    last = rng.integers(last_lo, last_hi + 1, G)
+    term = rng.integers(2, 50, G)
+    tf = np.maximum(last - rng.integers(0, 3000, G), 1)
+    g["term"], g["first_index"], g["last_index"], g["committed"] = term, 1, last, last - rng.integers(0, 50, G)
+    g["term_first"], g["term_last"], g["snap_index"] = tf, last, 0
+    g["state"], g["n"], g["self_slot"], g["lead"], g["vote"] = A.HB_STATE_LEADER, n, 0, 0, 0
+    runs = []
+    for i in range(G):
+        runs.append([(0, int(term[i]) - 1), (int(tf[i]), int(term[i]))])
+        for s in range(n):
+            p = g[i]["pr"][s]
+            if s == 0:
+                p["match"], p["next"] = last[i], last[i] + 1
+                continue
+            m = int(rng.integers(0, last[i] - lag_min + 1))
+            p["match"], p["next"] = m, m + 1
+            p["state"] = A.HB_PR_PROBE if rng.random() < 0.5 else A.HB_PR_REPLICATE
+    return g, runs
 
 
 def merge_batches(a, b, seed=6):

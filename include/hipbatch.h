@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define HB_ABI_VERSION 3
+#define HB_ABI_VERSION 4
 
 /* ---- error codes -------------------------------------------------------- */
 #define HB_OK          0
@@ -48,8 +48,12 @@ extern "C" {
 #define HB_MAX_INFLIGHT   1024   /* Config.MaxInflightMsgs upper bound on device       */
 #define HB_NO_LIMIT       UINT64_MAX  /* raft noLimit (raft/raft.go:30)                */
 #define HB_NO_INDEX       UINT64_MAX
-#define HB_SIZE_WINDOW    1024   /* entries whose sizes the device keeps per group (finite MaxSizePerMsg) */
-#define HB_TERM_RUNS      8      /* older log term runs the device keeps per group (follower side) */
+/* The log index (hb_reserve_log): per group, the cumulative Entry.Size() of
+ * its log (finite MaxSizePerMsg) and its older term runs (follower side), in
+ * rings of any power-of-two capacity; these are the capacities hb_create
+ * starts every group with (128 bytes per ring). */
+#define HB_SIZE_RING_MIN  16
+#define HB_TERM_RING_MIN  8
 
 /* ---- raft enums (values equal the reference's) --------------------------- */
 /* StateType raft/raft.go:35-39 */
@@ -211,12 +215,16 @@ typedef struct hb_group {
 #define HB_FAULT_FOLLOWER_LEADER 8  /* "invalid transition [follower -> leader]" raft/raft.go:409 (oracle KATs only) */
 #define HB_FAULT_RAND_EXHAUSTED  9  /* engine-defined, no reference panic: hb_tick needed draw
                                        rand_pos of the group but hb_set_rand supplied fewer */
-#define HB_FAULT_SIZE_WINDOW    10  /* engine-defined, no reference panic: with a finite
-                                       max_msg_size, sendAppend needed the size of an entry
-                                       older than the device's HB_SIZE_WINDOW - 1 latest */
-#define HB_FAULT_TERM_WINDOW    11  /* engine-defined, no reference panic: the follower side
-                                       needed the term of an entry older than the device's
-                                       HB_TERM_RUNS older term runs (hb_load_term_runs) */
+#define HB_FAULT_SIZE_WINDOW    10  /* engine precondition, no reference panic: with a finite
+                                       max_msg_size, sendAppend needed the size of an entry the
+                                       caller never loaded into the log index
+                                       (hb_load_entry_sizes), or one a ring smaller than the
+                                       log dropped (hb_reserve_log).  libhbnode loads and
+                                       reserves both, so it never sees this code. */
+#define HB_FAULT_TERM_WINDOW    11  /* engine precondition, no reference panic: the follower side
+                                       needed the term of an entry the caller never loaded
+                                       (hb_load_term_runs) or a too-small ring dropped; as above,
+                                       unreachable through libhbnode */
 #define HB_FAULT_CONFLICT_COMMITTED 12  /* "entry %d conflict with committed entry" raft/log.go:79 */
 
 /* ---- events (the sparse delta list) ---------------------------------------
@@ -327,8 +335,12 @@ typedef struct hb_handle hb_handle;
  * `max_replicas` peers, MaxInflightMsgs = max_inflight (Config.MaxInflightMsgs,
  * raft/raft.go:98) and MaxSizePerMsg = max_msg_size (raft/raft.go:93; any
  * value: HB_NO_LIMIT, 0, or a finite size, for which the device keeps the
- * sizes of each group's last HB_SIZE_WINDOW entries, see
- * hb_load_entry_sizes).  `max_batch` bounds hb_step's n. */
+ * cumulative sizes of each group's log, see hb_load_entry_sizes /
+ * hb_reserve_log).  `max_batch` bounds hb_step's n.
+ * Device memory: per group ~100 B + nmax x (28 + 8 max_inflight) B of state,
+ * 16 B + a 128-byte term-run ring, and for a finite max_msg_size 16 B + a
+ * 128-byte size ring (rings grow with hb_reserve_log: 8 B per log entry,
+ * 16 B per term run). */
 int  hb_create(int device, uint32_t capacity, uint32_t max_replicas,
                uint32_t max_inflight, uint64_t max_msg_size, uint64_t max_batch,
                hb_handle** out);
@@ -370,25 +382,50 @@ int  hb_remove_groups(hb_handle* h, uint32_t first, uint32_t count);
  * `count` group slots (host arrays). */
 int  hb_set_log_bounds(hb_handle* h, uint32_t count, const uint32_t* groups,
                        const uint64_t* first_index, const uint64_t* snap_index);
-/* Finite max_msg_size only: the protobuf sizes (Entry.Size()) of the latest
- * entries of `count` loaded groups, so that sendAppend can cut entries(Next,
- * maxMsgSize) with limitSize.  groups[i] takes n_sizes[i] sizes (at most
- * HB_SIZE_WINDOW - 1): the entries (last_index - n_sizes[i], last_index], in
- * index order, concatenated over i in `sizes` (host arrays).  hb_load_groups
+/* ---- the log index ---------------------------------------------------------
+ * What the device needs of a group's log besides its current-term run: the
+ * entries' protobuf sizes (a finite MaxSizePerMsg: sendAppend cuts
+ * entries(Next, maxMsgSize) with limitSize, raft/raft.go:265,
+ * raft/log.go:219-224, raft/util.go:97-110, for ANY Next in the log) and the
+ * terms below the current-term run (follower side: raftLog.term(i) for any i,
+ * raft/log.go:198-217).  The host owns the log (it holds the payloads and
+ * Storage) and loads both once per group; the device keeps them up to date as
+ * it appends, truncates and restores.  Each lives in a per-group ring whose
+ * capacity the host reserves: the ring drops its oldest element only when it
+ * is full, so a capacity covering [firstIndex - 1, lastIndex] plus what the
+ * next step can append (entries of MsgProp / props / MsgApp, one noop per
+ * election) means nothing the reference can read is ever missing.
+ *
+ * Finite max_msg_size only: the Entry.Size() of the entries (last_index -
+ * n_sizes[i], last_index] of group groups[i] (any n_sizes[i] <= last_index;
+ * normally the whole log from first_index), in index order, concatenated over
+ * i in `sizes` (host arrays); the ring grows to hold them.  hb_load_groups
  * leaves a group with none (only a follower at Next = last_index + 1 can be
- * served); a send that needs an older entry faults HB_FAULT_SIZE_WINDOW. */
+ * served); a send that needs an entry never loaded faults HB_FAULT_SIZE_WINDOW. */
 int  hb_load_entry_sizes(hb_handle* h, uint32_t count, const uint32_t* groups,
                          const uint32_t* n_sizes, const uint32_t* sizes);
 /* Follower side: the terms of a loaded group's log below its current-term run
  * (term_first), which raftLog.term() lookups of MsgApp / MsgVote / MsgSnap
  * need (matchTerm, findConflict, isUpToDate; raft/log.go:72-123, 249-251).
- * groups[i] takes n_runs[i] <= HB_TERM_RUNS runs (start index, term), oldest
- * first, the pairs of all groups concatenated in `runs` (host arrays): run k
- * covers [start_k, start_k+1) and the last one reaches term_first - 1 (or
- * last_index when term_first = HB_NO_INDEX).  hb_load_groups leaves a group
- * with none: a lookup below term_first then faults HB_FAULT_TERM_WINDOW. */
+ * groups[i] takes n_runs[i] runs (start index, term), oldest first, the pairs
+ * of all groups concatenated in `runs` (host arrays): run k covers [start_k,
+ * start_k+1) and the last one reaches term_first - 1 (or last_index when
+ * term_first = HB_NO_INDEX); normally every run down to first_index - 1.  The
+ * ring grows to hold them plus one.  hb_load_groups leaves a group with none:
+ * a lookup below term_first then faults HB_FAULT_TERM_WINDOW. */
 int  hb_load_term_runs(hb_handle* h, uint32_t count, const uint32_t* groups,
                        const uint32_t* n_runs, const uint64_t* runs);
+/* Grow the rings of groups[i] to hold at least size_cap[i] cumulative sizes
+ * (the span [oldest needed index, lastIndex] including firstIndex - 1; ignored
+ * unless max_msg_size is finite) and run_cap[i] term runs (every run of the log
+ * plus the runs the next step can start); a NULL array or 0 leaves that ring
+ * as is.  Capacities round up to a power of two and never shrink; the content
+ * is kept.  Synchronous (one copy kernel for the groups that grow).  Call it
+ * before an hb_step / hb_tick that could outgrow a ring. */
+int  hb_reserve_log(hb_handle* h, uint32_t count, const uint32_t* groups,
+                    const uint64_t* size_cap, const uint64_t* run_cap);
+/* The current ring capacities of one group (0 sizes: max_msg_size not finite). */
+int  hb_log_capacity(hb_handle* h, uint32_t group, uint64_t* size_cap, uint64_t* run_cap);
 /* Inflight window of (group, slot): buffer[(start + i) % max_inflight] = vals[i]. */
 int  hb_set_inflights(hb_handle* h, uint32_t group, uint32_t slot,
                       uint32_t start, uint32_t count, const uint64_t* vals);
@@ -480,6 +517,24 @@ int  hb_events_device(hb_handle* h, const uint64_t** base, const uint64_t** chun
 /* Gather the last step's events densely into host memory (synchronizes).
  * *n = number of events; returns HB_EINVAL if cap is too small. */
 int  hb_copy_events(hb_handle* h, hb_event* out, uint64_t cap, uint64_t* n);
+/* The compact delta list for a host consumer: the last
+ * step's event words exactly as the device wrote them (format above), densely
+ * in chunk order, written by the device into pinned host memory from
+ * hb_alloc_pinned: words[0 .. *total) when *total <= cap (else only counts and
+ * total are written: call again with a larger buffer, the step's events stay
+ * valid until the next hb_step / hb_tick), counts[c] = the words of chunk c for
+ * every chunk (hb_event_words_chunks).  Asynchronous on the handle's stream
+ * (8 bytes per word over PCIe instead of hb_copy_events' 16 per event, one
+ * word per bcastAppend): the host reads the buffers after hb_sync.  A group's
+ * events are its words in chunk 2p, then chunk 2p + 1, in order, p = group /
+ * groups_per_chunk; hb_expand_event_words turns them into hb_event records. */
+int  hb_events_to_host(hb_handle* h, uint64_t* words, uint64_t cap, uint32_t* counts, uint64_t* total);
+int  hb_event_words_chunks(hb_handle* h, uint32_t* n_chunks, uint32_t* groups_per_chunk);
+/* Host-side expansion of hb_events_to_host's output into hb_event records
+ * (*n_out = the number of records; HB_EINVAL if cap is too small; out NULL
+ * only counts).  Pure CPU, no handle. */
+int  hb_expand_event_words(const uint64_t* words, uint64_t n_words, const uint32_t* counts, uint32_t n_chunks,
+                           hb_event* out, uint64_t cap, uint64_t* n_out);
 /* Statistics of the last step: device pointer to HB_STAT_COUNT u64 (for an
  * RCCL all-reduce on the same stream) or a synchronous host copy. */
 int  hb_stats_device(hb_handle* h, uint64_t** dev_stats);

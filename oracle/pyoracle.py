@@ -107,9 +107,7 @@ class orc_raft(C.Structure):
         ("ev", C.c_void_p), ("nev", C.c_uint64), ("ev_cap", C.c_uint64), ("group", C.c_uint32),
         ("arrival", C.c_uint64), ("fault", C.c_int), ("n_won", C.c_uint64), ("n_lost", C.c_uint64),
         ("szc", C.c_void_p), ("szc_base", C.c_uint64), ("szc_n", C.c_uint64), ("szc_cap", C.c_uint64),
-        ("sz_lo", C.c_uint64),
-        ("tw_start", C.c_uint64 * abi.HB_TERM_RUNS), ("tw_term", C.c_uint64 * abi.HB_TERM_RUNS), ("tw_n", C.c_int),
-        ("tw_tfirst", C.c_uint64),
+        ("sz_lo", C.c_uint64), ("tw_lo", C.c_uint64), ("tw_tfirst", C.c_uint64),
     ]
 
 
@@ -175,6 +173,7 @@ def lib():
             "orc_groups_at": (R, [R, C.c_uint32]),
             "orc_groups_load": (C.c_int, [R, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_uint64]),
             "orc_groups_export": (None, [R, C.c_uint32, C.c_void_p]),
+            "orc_groups_log_info": (None, [R, C.c_uint32, C.c_void_p]),
             "orc_raft_tick": (C.c_int, [R, P(C.c_uint64), C.c_uint64]),
             "orc_unmarshal_message": (C.c_int, [C.c_char_p, C.c_int64, P(orc_wire_msg)]),
             "orc_decode_batch": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
@@ -561,6 +560,14 @@ class OracleGroups:
     def groups(self):
         out = np.zeros(self.G, dtype=abi.GROUP_DTYPE)
         lib().orc_groups_export(self.ptr, self.G, out.ctypes.data)
+        return out
+
+    def log_info(self):
+        """Per group [G, 4] u64: term runs of its log (covering [firstIndex-1, lastIndex]),
+        the oldest index whose size is loaded (sz_lo), firstIndex, lastIndex — what a
+        caller of the engine reserves its log index from (hb_reserve_log)."""
+        out = np.zeros((self.G, 4), dtype=np.uint64)
+        lib().orc_groups_log_info(self.ptr, self.G, out.ctypes.data)
         return out
 
     def load_sizes(self, sizes):

@@ -274,6 +274,7 @@ void orc_raft_init(orc_raft* r, uint64_t id, const uint64_t* peers, int npeers,
   }
   r->state = HB_STATE_FOLLOWER;
   r->tw_tfirst = HB_NO_INDEX;                             /* KAT rafts: the engine would know every run */
+  r->tw_lo = HB_NO_INDEX;
   for (int k = 0; k < r->log.nruns; k++) tw_push(r, r->log.runs[k].index, r->log.runs[k].term);
   orc_raft_become_follower(r, r->term, ORC_NONE);         /* :199 */
 }
@@ -355,19 +356,15 @@ void orc_raft_commit_to(orc_raft* r, uint64_t tocommit) { /* commitTo raft/log.g
   }
 }
 
-/* ---- the engine's term window (follower side) ---- */
+/* ---- what the engine's log index knows of the terms (follower side) ----
+ * The engine's term runs hold every run the caller loaded (hb_load_term_runs)
+ * plus the ones its own appends / resets started; the harness reserves ring
+ * capacity so none is dropped (hb_reserve_log).  All the oracle tracks is
+ * the oldest run start the engine knows (tw_lo) and its current-term run; the
+ * terms themselves come from `log`. */
 static void tw_push(orc_raft* r, uint64_t start, uint64_t term) {
-  if (r->tw_n > 0 && r->tw_term[r->tw_n - 1] == term) return;  /* the run goes on */
-  if (r->tw_n == HB_TERM_RUNS) {                          /* the oldest run leaves the window */
-    for (int k = 1; k < HB_TERM_RUNS; k++) {
-      r->tw_start[k - 1] = r->tw_start[k];
-      r->tw_term[k - 1] = r->tw_term[k];
-    }
-    r->tw_n--;
-  }
-  r->tw_start[r->tw_n] = start;
-  r->tw_term[r->tw_n] = term;
-  r->tw_n++;
+  (void)term;
+  if (r->tw_lo == HB_NO_INDEX) r->tw_lo = start;
 }
 
 static void tw_term_change(orc_raft* r, uint64_t old_term) {  /* reset to a new Term */
@@ -381,7 +378,7 @@ static void tw_leader_append(orc_raft* r, uint64_t first_new) {  /* entries at T
 
 /* the engine knows term(i) for every i >= this in [first-1, last] */
 static uint64_t tw_known_lo(const orc_raft* r) {
-  if (r->tw_n > 0) return r->tw_start[0];
+  if (r->tw_lo != HB_NO_INDEX) return r->tw_lo;
   if (r->tw_tfirst != HB_NO_INDEX) return r->tw_tfirst;
   return r->log.last_index + 1;
 }
@@ -398,13 +395,7 @@ static uint64_t f_term(orc_raft* r, uint64_t i) {
 }
 
 int orc_raft_load_term_runs(orc_raft* r, uint32_t n, const uint64_t* runs) {
-  if (n > HB_TERM_RUNS) return -1;
-  r->tw_n = 0;
-  for (uint32_t k = 0; k < n; k++) {
-    r->tw_start[r->tw_n] = runs[2 * k];
-    r->tw_term[r->tw_n] = runs[2 * k + 1];
-    r->tw_n++;
-  }
+  r->tw_lo = n > 0 ? runs[0] : HB_NO_INDEX;
   return 0;
 }
 
@@ -460,7 +451,7 @@ static void szc_reset(orc_raft* r, uint64_t base) {      /* no entry size known:
 }
 
 int orc_raft_load_sizes(orc_raft* r, uint32_t n, const uint32_t* sizes) {
-  if (!sized(r) || n >= HB_SIZE_WINDOW || n > r->log.last_index) return -1;
+  if (!sized(r) || n > r->log.last_index) return -1;
   szc_reset(r, r->log.last_index - n);
   uint64_t acc = 0;
   for (uint32_t j = 0; j < n; j++) szc_push(r, acc += sizes[j]);
@@ -473,8 +464,6 @@ static void szc_append(orc_raft* r, uint64_t last0, uint64_t k, const uint32_t* 
   if (r->szc_n == 0) szc_reset(r, last0);                 /* a raft built by orc_raft_init */
   uint64_t acc = r->szc[last0 - r->szc_base];
   for (uint64_t j = 1; j <= k; j++) szc_push(r, acc += orc_entry_size(desc ? desc[j - 1] : 0u, r->term, last0 + j));
-  uint64_t last = last0 + k;
-  if (last >= HB_SIZE_WINDOW && r->sz_lo < last - (HB_SIZE_WINDOW - 1)) r->sz_lo = last - (HB_SIZE_WINDOW - 1);
 }
 
 /* the last index of entries(next, maxMsgSize) (raft/log.go:219-224 + limitSize);
@@ -696,8 +685,9 @@ void orc_raft_campaign(orc_raft* r) {                     /* campaign raft/raft.
 static void follower_append(orc_raft* r, const orc_msg* m, uint64_t ci) {
   const uint64_t off = m->index + 1;
   orc_log_truncate(&r->log, ci - 1);                      /* unstable.truncateAndAppend */
-  /* the engine's term window: runs from ci on are gone */
-  while (r->tw_n > 0 && r->tw_start[r->tw_n - 1] >= ci) r->tw_n--;
+  /* the engine's term runs: those from ci on are gone (starts increase, so the
+   * oldest survives iff it starts below ci) */
+  if (r->tw_lo != HB_NO_INDEX && r->tw_lo >= ci) r->tw_lo = HB_NO_INDEX;
   if (r->tw_tfirst != HB_NO_INDEX && r->tw_tfirst >= ci) r->tw_tfirst = HB_NO_INDEX;
   if (sized(r)) {                                         /* and its entry sizes */
     if (r->szc_n == 0 || ci - 1 < r->sz_lo) szc_reset(r, ci - 1);
@@ -719,10 +709,6 @@ static void follower_append(orc_raft* r, const orc_msg* m, uint64_t ci) {
       szc_push(r, acc + orc_entry_size(m->edesc ? m->edesc[j - off] : 0u, t, j));
     }
     orc_log_push(&r->log, t, 1);
-  }
-  if (sized(r)) {
-    const uint64_t last = r->log.last_index;
-    if (last >= HB_SIZE_WINDOW && r->sz_lo < last - (HB_SIZE_WINDOW - 1)) r->sz_lo = last - (HB_SIZE_WINDOW - 1);
   }
   emit(r, HB_EV_FOLLOW, 0, r->arrival, HB_FOLLOW_APPEND);
 }
@@ -803,7 +789,7 @@ static int restore(orc_raft* r, uint64_t sindex, uint64_t sterm) {  /* raft/raft
     pr->match = r->ids[i] == r->id ? last : 0;
     orc_ins_init(&pr->ins, r->max_inflight);
   }
-  r->tw_n = 0;
+  r->tw_lo = HB_NO_INDEX;
   r->tw_tfirst = HB_NO_INDEX;
   if (sterm == r->term) r->tw_tfirst = sindex;
   else tw_push(r, sindex, sterm);
@@ -1116,7 +1102,7 @@ int orc_raft_from_group(orc_raft* r, const hb_group* g, const orc_run* runs, int
   }
   r->fault = (int)g->fault;
   if (sized(r)) szc_reset(r, r->log.last_index);            /* hb_load_groups: no entry size yet */
-  r->tw_n = 0;                                              /* hb_load_groups: no older term run yet */
+  r->tw_lo = HB_NO_INDEX;                                   /* hb_load_groups: no older term run yet */
   r->tw_tfirst = HB_NO_INDEX;
   for (int k = 0; k < r->log.nruns; k++)                    /* the current-term run (term_first) */
     if (r->log.runs[k].term == r->term) {
@@ -1446,4 +1432,14 @@ int orc_groups_load(orc_raft* gs, uint32_t n, const hb_group* recs, const orc_ru
 
 void orc_groups_export(const orc_raft* gs, uint32_t n, hb_group* out) {
   for (uint32_t i = 0; i < n; i++) orc_raft_to_group(&gs[i], &out[i]);
+}
+
+void orc_groups_log_info(const orc_raft* gs, uint32_t n, uint64_t* out) {
+  for (uint32_t i = 0; i < n; i++) {
+    const orc_raft* r = &gs[i];
+    out[4 * i] = (uint64_t)r->log.nruns;
+    out[4 * i + 1] = r->szc_n ? r->sz_lo : r->log.last_index;
+    out[4 * i + 2] = r->log.first_index;
+    out[4 * i + 3] = r->log.last_index;
+  }
 }

@@ -123,16 +123,17 @@ typedef struct orc_raft {
   uint64_t n_won, n_lost;         /* elections won (-> leader) / lost by poll (-> follower) */
   /* Entry.Size() of the log's entries, as cumulative sums (finite
    * max_msg_size): szc[i - szc_base] = sum of sizes of (szc_base, i].  sz_lo
-   * = the oldest index the engine keeps a size for (its HB_SIZE_WINDOW
-   * bound, mirrored so the engine-defined HB_FAULT_SIZE_WINDOW is checked). */
+   * = the oldest index whose size the caller loaded into the engine's log
+   * index (hb_load_entry_sizes), mirrored so that the engine precondition
+   * HB_FAULT_SIZE_WINDOW is checked too; the harness reserves ring capacity
+   * (hb_reserve_log), so the engine drops nothing the oracle keeps. */
   uint64_t* szc;
   uint64_t szc_base, szc_n, szc_cap, sz_lo;
-  /* The engine's view of the log terms on the follower side (mirrored so the
-   * engine-defined HB_FAULT_TERM_WINDOW is checked; the terms themselves come
-   * from `log`): at most HB_TERM_RUNS older runs (start, term) plus the
-   * current-term run [tw_tfirst, last_index] (HB_NO_INDEX: none). */
-  uint64_t tw_start[HB_TERM_RUNS], tw_term[HB_TERM_RUNS];
-  int tw_n;
+  /* What the engine's log index knows of the terms (follower side; the terms
+   * themselves come from `log`): the oldest older-run start it holds (tw_lo,
+   * HB_NO_INDEX: none) plus the current-term run [tw_tfirst, last_index];
+   * a lookup below both is the engine precondition HB_FAULT_TERM_WINDOW. */
+  uint64_t tw_lo;
   uint64_t tw_tfirst;
 } orc_raft;
 
@@ -266,6 +267,8 @@ void      orc_groups_free(orc_raft* g, uint32_t ngroups);
 int       orc_groups_load(orc_raft* gs, uint32_t n, const hb_group* recs, const orc_run* runs,
                           const uint64_t* run_off, int max_inflight, uint64_t max_msg_size);
 void      orc_groups_export(const orc_raft* gs, uint32_t n, hb_group* out);
+/* per group out[4i..4i+3] = log term runs, sz_lo (oldest loaded size), first_index, last_index */
+void      orc_groups_log_info(const orc_raft* gs, uint32_t n, uint64_t* out);
 orc_raft* orc_groups_at(orc_raft* g, uint32_t i);
 size_t    orc_sizeof_raft(void);
 

@@ -70,16 +70,46 @@ class Pair:
         self.eng.load_groups(init)
         for (g, s), vals in (ins or {}).items():
             self.eng.set_inflights(g, s, int(init[g]["pr"][s]["ins_start"]), vals)
-        if sizes:  # finite max_msg_size: the latest entries' sizes on both sides
+        self.sized = max_msg_size not in (0, abi.HB_NO_LIMIT)
+        if sizes:  # finite max_msg_size: the entries' sizes on both sides
             self.og.load_sizes(sizes)
             self.eng.load_entry_sizes(sizes)
-        if term_runs:  # follower side: the older term runs on both sides (True: all the log's, newest first)
+        if term_runs:  # follower side: the older term runs on both sides (True: all the log's)
             if term_runs is True:
                 from etcd_amd import synth
                 term_runs = synth.older_runs(init, runs)
             self.og.load_term_runs(term_runs)
             self.eng.load_term_runs(term_runs)
         assert_groups_equal(self.eng.get_groups(), init, "load")
+
+    def reserve(self, batch=None, extra=0):
+        """What a caller of the engine does before every step (hb_reserve_log):
+        ring capacity for every group's log index covering its log plus what
+        the batch can append — entries of its MsgProps / props / MsgApps, and
+        one noop or new term run per message (`extra` per group for a tick)."""
+        info = self.og.log_info().astype(np.int64)  # runs, sz_lo, first, last
+        G = len(info)
+        add = np.full(G, extra, dtype=np.int64)
+        top = info[:, 3].copy()
+        if batch is not None and len(batch["group"]):
+            grp = np.asarray(batch["group"], dtype=np.int64)
+            ok = grp < G
+            add += np.bincount(grp[ok], minlength=G)[:G]
+            t = np.asarray(batch["info"]) & 0xF
+            idx = np.asarray(batch["index"], dtype=np.int64)
+            prop = ok & (t == abi.HB_MSG_PROP)
+            add += np.bincount(grp[prop], weights=idx[prop], minlength=G)[:G].astype(np.int64)
+            if batch.get("eterm") is not None and batch.get("eoff") is not None:
+                eoff = np.asarray(batch["eoff"], dtype=np.int64)
+                ne = np.diff(np.append(eoff, len(batch["eterm"])))
+                app = ok & (t == abi.HB_MSG_APP)
+                add += np.bincount(grp[app], weights=ne[app], minlength=G)[:G].astype(np.int64)
+                np.maximum.at(top, grp[app], idx[app] + ne[app])
+        if batch is not None and batch.get("props") is not None:
+            add += np.asarray(batch["props"], dtype=np.int64)[:G]
+        runs = info[:, 0] + add + 1
+        szc = (np.maximum(top, info[:, 3]) + add - info[:, 1] + 1) if self.sized else None
+        self.eng.reserve_log(np.arange(G, dtype=np.uint32), szc, runs)
 
     def set_timers(self, timers, draws):
         self.draws = np.ascontiguousarray(draws, dtype=np.uint64)
@@ -89,6 +119,7 @@ class Pair:
 
     def tick(self, ctx="", check_inflights=False):
         """One MultiNode.Tick on both sides; events, stats, groups and timers equal."""
+        self.reserve(extra=1)
         self.eng.tick()
         dev_ev = self.eng.events()
         dev_st = self.eng.stats()
@@ -106,9 +137,13 @@ class Pair:
         return dev_ev, dev_st, ora_g
 
     def step(self, batch, ctx="", check_inflights=True):
+        self.reserve(batch)
         self.eng.step_batch(batch, host=True)
         dev_ev = self.eng.events()
         dev_st = self.eng.stats()
+        # the compact delta (hb_events_to_host words, expanded on the host) is the same stream
+        words, counts = self.eng.event_words()
+        assert np.array_equal(self.eng.expand_words(words, counts), dev_ev), f"{ctx}: compact words differ"
         ora_ev, ora_st = self.og.step(batch)
         assert_events_equal(dev_ev, ora_ev, ctx)
         assert np.array_equal(dev_st, ora_st), \

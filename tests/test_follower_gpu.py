@@ -189,14 +189,15 @@ def test_vote_from_sender_outside_prs():
 
 # ---------------------------------------------------------------- clusters
 class Cluster:
-    def __init__(self, G, ids=(1, 2, 3), seed=0, election=10, W=256):
+    def __init__(self, G, ids=(1, 2, 3), seed=0, election=10, W=256, max_msg_size=abi.HB_NO_LIMIT):
         self.rng = random.Random(seed)
         self.ids = list(ids)
         self.G = G
-        self.nodes = {i: StartMultiNode(i, capacity=G + 4, max_inflight=W) for i in ids}
-        for i in ids:
-            r = random.Random(seed * 1000 + i)
-            self.nodes[i].SetRand([r.getrandbits(63) for _ in range(1 << 15)])
+        self.seed, self.election, self.W, self.max_msg_size = seed, election, W, max_msg_size
+        self.down = set()  # stopped nodes: no Ready, no Tick, messages to them are lost
+        self.sent = []  # (group, MsgApp) delivered, when self.record
+        self.record = False
+        self.nodes = {i: self._start(i) for i in ids}
         self.st = {(i, g): MemoryStorage() for i in ids for g in range(1, G + 1)}
         for i in ids:
             for g in range(1, G + 1):
@@ -206,8 +207,37 @@ class Cluster:
         self.inbox = []
         self.proposed = {g: set() for g in range(1, G + 1)}
 
+    def _start(self, i):
+        mn = StartMultiNode(i, capacity=self.G + 4, max_inflight=self.W, max_msg_size=self.max_msg_size)
+        r = random.Random(self.seed * 1000 + i)
+        mn.SetRand([r.getrandbits(63) for _ in range(1 << 15)])
+        return mn
+
+    def stop_node(self, i):
+        """Node i crashes: its MultiNode is gone, its storages stay."""
+        self.nodes[i].Stop()
+        self.down.add(i)
+
+    def restart_node(self, i):
+        """Node i restarts from its storages (raft/multinode_test.go:302-370):
+        a snapshot at its applied index carries the ConfState (CreateGroup takes
+        the peers from it, raft/raft.go:164-172), Config.Applied = that index."""
+        mn = self._start(i)
+        for g in range(1, self.G + 1):
+            st = self.st[i, g]
+            ap = [e for e in self.applied[i, g] if e[0] != "snap"]
+            at = ap[-1][0] if ap else 0
+            if at > st.Snapshot().Index:
+                _, err = st.CreateSnapshot(at, self.ids, b"restart@%d" % at)
+                assert err is None
+            mn.CreateGroup(g, Config(self.election, 1, applied=st.Snapshot().Index), st)
+        self.nodes[i] = mn
+        self.down.discard(i)
+
     def ready_round(self):
         for i in self.ids:
+            if i in self.down:
+                continue
             rds = self.nodes[i].Ready()
             for g, rd in rds.items():
                 assert rd.fault == 0, (i, g, rd.fault)
@@ -240,25 +270,32 @@ class Cluster:
         box, self.inbox = self.inbox, []
         self.rng.shuffle(box)
         for g, m in box:
-            if self.rng.random() < drop:
+            if self.rng.random() < drop or m.To in self.down:
                 continue
+            if self.record and m.Type == APP:
+                self.sent.append((g, m))
             self.nodes[m.To].Step(g, m)
 
-    def propose(self, k, tag):
+    def propose(self, k, tag, pad=0):
         for _ in range(k):
             g = self.rng.randint(1, self.G)
-            i = self.rng.choice(self.ids)
+            i = self.rng.choice([x for x in self.ids if x not in self.down])
             data = f"{tag}-{g}-{i}-{self.rng.getrandbits(32)}".encode()
+            if pad:
+                data += b"p" * self.rng.randint(0, pad)
             self.proposed[g].add(data)
             self.nodes[i].Propose(g, data)
 
     def tick(self):
         for i in self.ids:
-            self.nodes[i].Tick()
+            if i not in self.down:
+                self.nodes[i].Tick()
 
     def compact(self, keep=3):
         """The application's CreateSnapshot + Compact at its applied index."""
         for (i, g), st in self.st.items():
+            if i in self.down:
+                continue
             ents = [e for e in self.applied[i, g] if e[0] != "snap"]
             if len(ents) < keep + 2:
                 continue
@@ -283,8 +320,9 @@ class Cluster:
                     assert seen.setdefault(idx, e) == e, f"group {g} index {idx}: {seen[idx]} vs {e} on {i}"
 
     def stop(self):
-        for n in self.nodes.values():
-            n.Stop()
+        for i, n in self.nodes.items():
+            if i not in self.down:
+                n.Stop()
 
 
 @pytest.mark.parametrize("G,seed", [(16, 1), (64, 2)])
@@ -335,4 +373,153 @@ def test_cluster_safety_under_loss_and_elections(G, seed, drop):
     c.check_safety()
     committed = sum(len(c.applied[1, g]) for g in range(1, G + 1))
     assert committed > G * 10
+    c.stop()
+
+
+def test_probe_into_log_with_twenty_term_runs():
+    """raftLog.term(i) at any depth of the log (raft/log.go:198-217): a
+    restarted follower whose storage holds 60 entries in 20 term runs (libhbnode
+    loads every run into the device's log index) answers a leader probing at
+    any index (handleAppendEntries raft/raft.go:651-665, maybeAppend
+    raft/log.go:72-88): a matching LogTerm is accepted and the log is cut and
+    appended after it, a wrong one is rejected with RejectHint = lastIndex."""
+    ents = [(i + 1, i // 3 + 1) for i in range(60)]
+    for idx in (1, 2, 4, 17, 31, 44, 58, 60):
+        t = ents[idx - 1][1]
+        mn, st = follower(ents, 25)
+        mn.Step(1, Message(Type=APP, From=2, To=1, Term=25, LogTerm=t, Index=idx,
+                           Entries=[Entry(Term=25, Index=idx + 1, Data=b"x")], Commit=0))
+        rd = one_ready(mn, st)
+        assert rd.fault == 0
+        assert [(m.Type, m.Index, m.Reject) for m in rd.Messages] == [(APPRESP, idx + 1, False)], idx
+        assert [(e.Index, e.Term) for e in rd.Entries] == [(idx + 1, 25)], idx
+        mn.Stop()
+        mn, st = follower(ents, 25)
+        mn.Step(1, Message(Type=APP, From=2, To=1, Term=25, LogTerm=t + 1, Index=idx, Commit=0))
+        rd = one_ready(mn, st)
+        assert rd.fault == 0
+        assert [(m.Type, m.Index, m.Reject, m.RejectHint) for m in rd.Messages] == [(APPRESP, idx, True, 60)], idx
+        mn.Stop()
+    # isUpToDate over the 20-run log (raft/log.go:235-237): MsgVote from a
+    # candidate whose last entry is one term older is rejected
+    mn, st = follower(ents, 25)
+    mn.Step(1, Message(Type=VOTE, From=2, To=1, Term=26, LogTerm=19, Index=100))
+    rd = one_ready(mn, st)
+    assert [(m.Type, m.Reject) for m in rd.Messages] == [(VOTERESP, True)]
+    mn.Stop()
+
+
+def test_restarted_follower_catches_up_5000_behind_under_1mib():
+    """etcdserver's MaxSizePerMsg = 1 MiB (etcdserver/raft.go:229): node 3
+    crashes, every group commits > 5,000 more entries of random payload sizes
+    on nodes 1 and 2, node 3 restarts from its storage.  The leaders probe it
+    back (rejections, maybeDecrTo) and send entries(Next, 1 MiB) from more than
+    5,000 entries behind (raft/raft.go:265, limitSize raft/util.go:97-110): no
+    group faults, every MsgApp is cut exactly by limitSize, and node 3 applies
+    every entry in the same order as the others."""
+    from etcd_amd.multinode import entry_size
+    G, lim = 3, 1 << 20
+    c = Cluster(G, seed=11, max_msg_size=lim)
+    for g in range(1, G + 1):
+        c.nodes[1].Campaign(g)
+    for _ in range(4):
+        c.ready_round()
+        c.deliver()
+    c.stop_node(3)
+    for r in range(13):  # > 5,000 entries per group while node 3 is down
+        for g in range(1, G + 1):
+            for _ in range(450):
+                c.nodes[1].Propose(g, b"e%d-%d-" % (g, r) + b"z" * c.rng.randint(0, 900))
+        c.ready_round()
+        c.deliver()
+        c.tick()
+    for _ in range(6):
+        c.ready_round()
+        c.deliver()
+        c.tick()
+    last = {g: c.nodes[1].Status(g).HardState.Commit for g in range(1, G + 1)}
+    behind = {g: last[g] - c.st[3, g].LastIndex() for g in range(1, G + 1)}
+    assert min(behind.values()) > 5000, behind
+    c.restart_node(3)
+    c.record = True
+    for _ in range(40):
+        c.ready_round()
+        c.deliver()
+        c.tick()
+        if all(c.st[3, g].LastIndex() >= last[g] for g in range(1, G + 1)):
+            break
+    for _ in range(4):
+        c.ready_round()
+        c.deliver()
+    c.check_safety()
+    deep = 0
+    for g, m in c.sent:
+        if m.To != 3 or not m.Entries:
+            continue
+        sz = [entry_size(e) for e in m.Entries]
+        assert len(sz) == 1 or sum(sz) <= lim, (g, m.Index, len(sz), sum(sz))
+        deep = max(deep, last[g] - m.Index)
+    assert deep > 5000, deep
+    for g in range(1, G + 1):
+        assert c.st[3, g].LastIndex() >= last[g]
+        a1 = [e for e in c.applied[1, g] if e[0] != "snap"]
+        a3 = {e[0]: e for e in c.applied[3, g] if e[0] != "snap"}
+        assert all(a3[e[0]] == e for e in a1 if e[0] in a3) and max(a3) >= last[g], g
+    c.stop()
+
+
+def test_cluster_with_restarted_follower():
+    """A 3-node cluster where node 3 crashes and restarts twice from its
+    storage (snapshot ConfState, Config.Applied) while proposals, elections (of
+    the groups it led) and compaction go on: safety holds throughout, and once
+    the cluster is whole again every later proposal commits on every node and
+    node 3 holds every committed index."""
+    G = 12
+    c = Cluster(G, seed=21, election=8)
+    for g in range(1, G + 1):
+        c.nodes[c.ids[g % 3]].Campaign(g)
+    for r in range(45):
+        if r in (8, 26):
+            c.stop_node(3)
+        if r in (17, 35):
+            c.restart_node(3)
+        c.ready_round()
+        c.deliver()
+        c.propose(2 * G, f"r{r}", pad=200)
+        c.tick()
+        if r == 30:
+            c.compact(keep=20)
+
+    def leaders():
+        return {g for g in range(1, G + 1) for i in c.ids
+                if c.nodes[i].Status(g).SoftState.RaftState == StateLeader}
+    # without pre-vote a group can take many election rounds (a candidate with a
+    # shorter log loses, raft/log.go:235-237); proposals to a group with no
+    # leader are dropped (raft/raft.go:619-621), so the late ones wait for leaders
+    for _ in range(80):
+        if len(leaders()) == G:
+            break
+        c.ready_round()
+        c.deliver()
+        c.tick()
+    assert len(leaders()) == G
+    for r in range(6):
+        c.ready_round()
+        c.deliver()
+        c.propose(2 * G, f"late{r}", pad=200)
+        c.tick()
+    for _ in range(25):
+        c.ready_round()
+        c.deliver()
+        c.tick()
+    c.check_safety()
+    for g in range(1, G + 1):
+        late = {d for d in c.proposed[g] if d.startswith(b"late")}
+        top = set()
+        for i in c.ids:
+            ap = [e for e in c.applied[i, g] if e[0] != "snap"]
+            got = {e[2] for e in ap if e[2]}
+            assert late <= got, f"group {g} node {i}: {len(late - got)} late proposals missing"
+            top.add(ap[-1][0])
+        assert len(top) == 1, f"group {g}: applied up to {top}"
     c.stop()

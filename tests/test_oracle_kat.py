@@ -5,6 +5,7 @@ the oracle (oracle/raft_oracle.c).  The Go toolchain is absent from this image,
 so these tables ARE the oracle's pin (DESIGN.md "Parity").  Substitutions are
 named where a test drives a follower-side path the engine does not cover.
 """
+import numpy as np
 import pytest
 
 from etcd_amd import abi
@@ -673,10 +674,40 @@ def test_send_append_cut_by_max_size_per_msg():
         assert r.pr(2).Next == want + 1 and r.fault == 0
 
 
-def test_send_append_beyond_size_window_faults():
-    """Engine-defined bound (not a reference panic): with a finite MaxSizePerMsg
-    the engine keeps the sizes of the latest HB_SIZE_WINDOW - 1 entries; a send
-    that starts before them faults HB_FAULT_SIZE_WINDOW (oracle and engine alike)."""
+def test_send_append_from_any_depth():
+    """With a finite MaxSizePerMsg the engine's log index holds the size of
+    every entry of the log (hb_load_entry_sizes + hb_reserve_log), so
+    sendAppend cuts entries(Next, maxMsgSize) for a follower at any depth: here
+    5,000 entries behind under etcdserver's 1 MiB limit (etcdserver/raft.go:229;
+    raft/raft.go:265, raft/util.go:97-110)."""
+    n = 6000
+    ents = [(i + 1, 1) for i in range(n)]
+    r = Raft(1, [1, 2], ents=ents, max_msg_size=1 << 20)
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 600, n)
+    sizes = [abi.entry_size(abi.hb_ent_desc(int(d), 0, True), 1, i + 1) for i, d in enumerate(data)]
+    r.load_sizes(sizes)
+    r.becomeCandidate()
+    r.becomeLeader()  # noop at n + 1 (Term 2)
+    r.readMessages()
+    allsz = sizes + [abi.entry_size(0, 2, n + 1)]
+    for nxt in (n + 1 - 5000, 2, 1, n - 1):
+        r.setProgress(2, nxt - 1, nxt)
+        r.pr(2).State = abi.HB_PR_REPLICATE
+        r.sendAppend(2)
+        ms = r.readMessages()
+        tot, k = allsz[nxt - 1], 1
+        while nxt - 1 + k < len(allsz) and tot + allsz[nxt - 1 + k] <= (1 << 20):
+            tot += allsz[nxt - 1 + k]
+            k += 1
+        assert r.fault == 0 and len(ms) == 1 and ms[0].Index == nxt - 1 and ms[0].nents == k, (nxt, ms)
+
+
+def test_send_append_before_loaded_sizes_faults():
+    """Engine precondition (not a reference panic): the engine computes
+    limitSize from the sizes its caller loaded; a send that starts before them
+    faults HB_FAULT_SIZE_WINDOW (oracle and engine alike).  libhbnode always
+    loads the whole log, so MultiNode never sees it."""
     r = Raft(1, [1, 2], ents=[(1, 1), (2, 1), (3, 1), (4, 1)], max_msg_size=100)
     r.load_sizes([6, 6])  # only entries 3 and 4 are known: next - 1 >= 2 can be served
     r.becomeCandidate()
@@ -887,16 +918,21 @@ def test_restore_snapshot_via_msg_snap():
     assert [(m.Type, m.Index) for m in r2.readMessages()] == [(APPRESP, 2)]
 
 
-def test_follower_term_window_fault():
-    """Engine-defined bound: the engine keeps HB_TERM_RUNS older term runs; a
-    follower-side lookup below them faults HB_FAULT_TERM_WINDOW."""
-    ents = [(i + 1, i + 1) for i in range(abi.HB_TERM_RUNS + 2)]  # one run per entry
-    r = Raft(1, [1, 2], ents=ents)
-    r.becomeFollower(20, 2)
-    r.Step(Msg(APP, From=2, To=1, Term=20, LogTerm=2, Index=2))  # term(2): dropped from the window
-    assert r.fault == abi.HB_FAULT_TERM_WINDOW
-    r2 = Raft(1, [1, 2], ents=ents)
-    r2.becomeFollower(20, 2)
-    last = len(ents)
-    r2.Step(Msg(APP, From=2, To=1, Term=20, LogTerm=last, Index=last, Commit=0))
-    assert r2.fault == 0 and [m.Index for m in r2.readMessages()] == [last]
+def test_follower_term_lookup_at_any_depth():
+    """raftLog.term(i) for any i of the log (raft/log.go:198-217): with every
+    older term run in the engine's log index (hb_load_term_runs), a leader
+    probing a follower whose log holds 20 term runs is answered from any of
+    them — a matching LogTerm deep in the log is accepted, a wrong one rejected."""
+    ents = [(i + 1, i // 3 + 1) for i in range(60)]  # 20 runs of 3 entries
+    for idx in (2, 5, 31, 59, 60):
+        r = Raft(1, [1, 2], ents=ents)
+        r.becomeFollower(25, 2)
+        t = ents[idx - 1][1]
+        r.Step(Msg(APP, From=2, To=1, Term=25, LogTerm=t, Index=idx, Entries=[(idx + 1, 25)], Commit=0))
+        ms = r.readMessages()
+        assert r.fault == 0 and [(m.Index, bool(m.Reject)) for m in ms] == [(idx + 1, False)], idx
+        r2 = Raft(1, [1, 2], ents=ents)
+        r2.becomeFollower(25, 2)
+        r2.Step(Msg(APP, From=2, To=1, Term=25, LogTerm=t + 1, Index=idx, Commit=0))
+        ms = r2.readMessages()
+        assert r2.fault == 0 and [(m.Index, bool(m.Reject)) for m in ms] == [(idx, True)], idx

@@ -288,8 +288,8 @@ def test_fuzz_finite_max_msg_size(seed, nmax, W, max_size):
     fuzzed states and messages, MsgProps and dense proposals carrying entries of
     random payload sizes; every MsgApp's last entry (optimisticUpdate /
     inflights.add) follows limitSize over the entries' gogo sizes.  Groups whose
-    size window does not reach a follower's Next fault HB_FAULT_SIZE_WINDOW on
-    both sides."""
+    caller loaded only part of the log's sizes fault HB_FAULT_SIZE_WINDOW (the
+    engine's precondition) on both sides where a send reaches below them."""
     g, runs, ins = synth.random_groups(1200, nmax, seed=seed, W=W)
     sizes = synth.window_sizes(g, runs, seed=seed + 1)
     pair = Pair(g, runs, nmax, W, ins=ins, max_msg_size=max_size, sizes=sizes, max_batch=1 << 14)
@@ -365,3 +365,85 @@ def test_follower_replication_stream():
         last = last + k
         assert np.array_equal(now["last_index"], last)
         assert st[abi.HB_STAT_COMMITS] == G and st[abi.HB_STAT_FAULTS] == 0
+
+
+# ---------------------------------------------------------------- the log index at depth
+def test_deep_lag_finite_max_msg_size():
+    """etcdserver's MaxSizePerMsg = 1 MiB (etcdserver/raft.go:229) with
+    followers 5,000+ entries behind leaders whose logs hold 6,000-9,000
+    entries of random payload sizes: heartbeat responses, rejections
+    (maybeDecrTo to a random RejectHint) and acks make sendAppend cut
+    entries(Next, 1 MiB) anywhere in the log (raft/raft.go:265, limitSize
+    raft/util.go:97-110).  The log index holds every entry's size
+    (hb_load_entry_sizes + hb_reserve_log), so no group faults and events,
+    records and inflights equal the oracle's."""
+    G, n = 500, 3
+    g, runs = synth.deep_lag_leaders(G, n, seed=91)
+    sizes = synth.window_sizes(g, runs, seed=92, max_len=900, frac_full=1.0)
+    pair = Pair(g, runs, n, 64, max_msg_size=1 << 20, sizes=sizes, max_batch=1 << 14)
+    rng = np.random.default_rng(93)
+    for step in range(4):
+        now = pair.og.groups()
+        grp, info, term, index, hint = [], [], [], [], []
+        for i in range(G):
+            for s in range(1, n):
+                p = now[i]["pr"][s]
+                u = rng.random()
+                rej = 0
+                if u < 0.35:  # MsgHeartbeatResp: Match < lastIndex -> sendAppend
+                    t, x, h = abi.HB_MSG_HEARTBEAT_RESP, 0, 0
+                elif u < 0.6:  # reject of the last probe, follower far behind
+                    t, x, h = abi.HB_MSG_APP_RESP, int(p["next"]) - 1, int(rng.integers(0, max(1, int(p["next"]))))
+                    rej = 1
+                else:  # ack of what was sent (or a stale ack)
+                    t, x, h = abi.HB_MSG_APP_RESP, max(int(p["next"]) - 1, int(p["match"])), 0
+                grp.append(i)
+                info.append(t | (s << 4) | (rej << 8))
+                term.append(int(now[i]["term"]))
+                index.append(x)
+                hint.append(h)
+        order = rng.permutation(len(grp))
+        b = dict(group=np.array(grp, np.uint32)[order], info=np.array(info, np.uint32)[order],
+                 term=np.array(term, np.uint64)[order], index=np.array(index, np.uint64)[order],
+                 hint=np.array(hint, np.uint64)[order], props=(rng.random(G) < 0.3).astype(np.uint32))
+        b = synth.attach_entry_descs(b, G, seed=94 + step, max_len=900)
+        _, st, ora = pair.step(b, ctx=f"deep lag step {step}")
+        assert st[abi.HB_STAT_FAULTS] == 0 and (ora["fault"] == 0).all()
+    sc, rc = pair.eng.log_capacity(0)
+    assert sc >= 6000 and rc >= abi.HB_TERM_RING_MIN
+
+
+@pytest.mark.parametrize("seed,nmax", [(95, 3), (96, 5)])
+def test_follower_side_many_term_runs(seed, nmax):
+    """Followers whose logs hold 18-30 term runs, probed by MsgApps anywhere in
+    the log (matching and wrong LogTerms, conflicts that cut the log deep),
+    MsgVote (isUpToDate) and MsgSnap: every raftLog.term lookup is answered from
+    the log index (all runs loaded), no group faults, and the engine equals the
+    oracle."""
+    g, runs = synth.many_runs_groups(800, nmax, seed=seed)
+    pair = Pair(g, runs, nmax, 16, max_batch=1 << 15, term_runs=True)
+    for k in range(4):
+        b = synth.follower_messages(pair.og.groups(), pair.og.term, 3000, seed=seed * 10 + k, deep=0.6)
+        _, st, ora = pair.step(b, ctx=f"many runs n={nmax} step {k}")
+        assert not (ora["fault"] == abi.HB_FAULT_TERM_WINDOW).any()
+
+
+def test_log_index_precondition_faults():
+    """Engine precondition, checked on both sides: a caller that loads no
+    entry sizes (finite MaxSizePerMsg) or no older term runs gets
+    HB_FAULT_SIZE_WINDOW / HB_FAULT_TERM_WINDOW exactly where the log index
+    lacks the data (libhbnode always loads both, see test_follower_gpu.py)."""
+    g, runs = synth.deep_lag_leaders(200, 3, seed=97, last_lo=300, last_hi=600, lag_min=200)
+    pair = Pair(g, runs, 3, 16, max_msg_size=4096, max_batch=1 << 12)  # no sizes loaded
+    grp = np.repeat(np.arange(200, dtype=np.uint32), 2)
+    info = np.tile(np.array([abi.HB_MSG_HEARTBEAT_RESP | (1 << 4), abi.HB_MSG_HEARTBEAT_RESP | (2 << 4)],
+                            np.uint32), 200)
+    b = dict(group=grp, info=info, term=g["term"][grp].astype(np.uint64), index=np.zeros(400, np.uint64),
+             hint=np.zeros(400, np.uint64), props=None, eoff=np.zeros(400, np.uint64))
+    _, st, ora = pair.step(b, ctx="no sizes")
+    assert (ora["fault"] == abi.HB_FAULT_SIZE_WINDOW).all()
+    g2, runs2 = synth.many_runs_groups(300, 3, seed=98)
+    pair2 = Pair(g2, runs2, 3, 16, max_batch=1 << 13)  # no term runs loaded
+    b2 = synth.follower_messages(pair2.og.groups(), pair2.og.term, 1500, seed=99, deep=1.0)
+    _, st2, ora2 = pair2.step(b2, ctx="no runs")
+    assert (ora2["fault"] == abi.HB_FAULT_TERM_WINDOW).sum() > 50
