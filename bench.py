@@ -253,11 +253,15 @@ def run_multinode(args):
     G = args.groups or 1000
     n = args.replicas or 3
     L = C.CDLL(os.path.join(ROOT, "etcd_amd", "libhbnode_bench.so"))
-    L.hbnb_run.restype = C.c_int
-    L.hbnb_run.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]
-    out = (C.c_double * 8)()
+    L.hbnb_run2.restype = C.c_int
+    L.hbnb_run2.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                            C.POINTER(C.c_double)]
+    out = (C.c_double * 24)()
+    bulk = args.mn_mode == "bulk"
+    flags = 3 if bulk else 0  # HBNB_BULK | HBNB_PAR_APP
+    threads = args.mn_threads if bulk else 1
     t0 = time.perf_counter()
-    rc = L.hbnb_run(int(os.environ.get("LOCAL_RANK", "0")), G, n, args.warmup, args.steps, out)
+    rc = L.hbnb_run2(int(os.environ.get("LOCAL_RANK", "0")), G, n, args.warmup, args.steps, flags, threads, out)
     wall = time.perf_counter() - t0
     if rc != 0:
         raise SystemExit(f"hbnb_run failed: {rc}")
@@ -271,9 +275,16 @@ def run_multinode(args):
                                   f"shape{' = BASELINE.json configs[0]' if G == 1000 and n == 3 else ''})",
                       "groups": G, "replicas": n, "max_inflight": 256},
            "commits_per_s": adv / secs,
+           "api": ("hbn_step_many + hbn_propose_many, host threads "
+                   f"{threads or 'default (min(16, cores))'}, application persists from the same number of threads"
+                   if bulk else "one hbn_step / hbn_propose call per message, one host thread"),
            "split_s_per_step": {"ready": out[3] / args.steps, "step_and_propose": out[4] / args.steps,
                                 "append_and_advance": out[5] / args.steps},
            "parity_sanity": bool(adv == G * args.steps and out[7] == 0),
+           "host_phases_s_per_step": {k: round(out[8 + i] / args.steps, 6) for i, k in enumerate(
+               ["load_sync", "log_reserve", "hb_step_call", "event_fetch", "event_replay", "stepped_marks",
+                "ready_build", "ready_merge", "advance", "bulk_lookup", "bulk_responses", "bulk_proposals",
+                "batch_reset"])},
            "wall_s": wall}
     if not args.no_cpu_baseline:
         cb = cpu_baseline(n, groups=min(G, args.cpu_groups), budget_s=min(args.cpu_seconds, 5.0))
@@ -341,6 +352,10 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="batch inputs on their own stream: the prep stage of step k+1 (bucket sort + routing) "
                          "overlaps the apply stage of step k (hb_set_input_stream); default: stages serialized")
+    ap.add_argument("--mn-mode", choices=["bulk", "percall"], default="bulk",
+                    help="multinode: bulk = hbn_step_many / hbn_propose_many + host threads (default), "
+                         "percall = one API call per message on one thread (the r01/r02 path, for A/B)")
+    ap.add_argument("--mn-threads", type=int, default=0, help="multinode bulk: host threads (0 = library default)")
     ap.add_argument("--traffic-json", default=None,
                     help="profiles/<tag>_traffic.json from tools/profile_round.sh (default: newest in profiles/)")
     args = ap.parse_args()

@@ -22,10 +22,17 @@
 #include "../../include/hbnode.h"
 
 #include <algorithm>
-#include <stdexcept>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <exception>
+#include <functional>
 #include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -471,7 +478,8 @@ struct Group {
   // and what the pending batch can add: entries and messages (each may start a
   // run or append a noop), and the top of its MsgApps' entries
   uint64_t lx_sz = 0, lx_tr = 0, lx_runs = 0;
-  uint64_t bx = 0, bx_top = 0;
+  uint64_t bx = 0, bx_top = 0;  // entries the batch can append (sizes)
+  uint64_t bxr = 0;             // term runs it can start: a noop per VoteResp / MsgHup, a MsgApp entry, a restore
   bool in_bx = false;
 
   hbn_hard_state hard() const { return hbn_hard_state{term, vote, hs_commit}; }
@@ -483,9 +491,146 @@ struct Group {
   }
 };
 
+// ---------------------------------------------------------------- host threads
+// Groups are independent (raft/multinode.go:125-131), so the per-group host
+// work of a Ready cycle — replaying the device's events, assembling Ready,
+// Advance, bulk ingestion — runs on a pool of host threads, each owning a
+// disjoint set of groups; the node's membership lists are appended per thread
+// and merged in thread order.  The calling thread is worker 0.
+class Pool {
+ public:
+  explicit Pool(unsigned n) : n_(n ? n : 1) {
+    for (unsigned t = 1; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  unsigned size() const { return n_; }
+  // f(tid) for tid in [0, size()); returns once every worker finished; the
+  // first exception (lowest tid) is rethrown on the calling thread
+  template <class F>
+  void run(F&& f, unsigned use = 0) {
+    const unsigned k = use && use < n_ ? use : n_;
+    std::vector<std::exception_ptr> err(k);
+    auto body = [&](unsigned t) {
+      try {
+        f(t);
+      } catch (...) {
+        err[t] = std::current_exception();
+      }
+    };
+    if (k > 1) {
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        job_ = body;
+        k_ = k;
+        left_ = k - 1;
+        ++gen_;
+      }
+      cv_.notify_all();
+      body(0);
+      std::unique_lock<std::mutex> lk(mu_);
+      done_.wait(lk, [&] { return left_ == 0; });
+      job_ = nullptr;
+    } else {
+      body(0);
+    }
+    for (auto& e : err)
+      if (e) std::rethrow_exception(e);
+  }
+
+ private:
+  void loop(unsigned t) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void(unsigned)> job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        if (t >= k_) continue;
+        job = job_;
+      }
+      job(t);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--left_ == 0) done_.notify_one();
+    }
+  }
+  unsigned n_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::function<void(unsigned)> job_;
+  uint64_t gen_ = 0;
+  unsigned k_ = 0, left_ = 0;
+  bool stop_ = false;
+};
+
+// [lo, hi) of n items for worker t of k
+inline void split(size_t n, unsigned k, unsigned t, size_t* lo, size_t* hi) {
+  *lo = n * t / k;
+  *hi = n * (t + 1) / k;
+}
+// set a membership flag; true for the one caller that set it
+inline bool flag_set(bool& f) { return !__atomic_exchange_n(&f, true, __ATOMIC_RELAXED); }
+
+// membership lists a parallel phase appends to, one per worker
+struct Lists {
+  std::vector<Group*> touched, content, delivered, reload, stepped, bx;
+  void clear() {
+    touched.clear();
+    content.clear();
+    delivered.clear();
+    reload.clear();
+    stepped.clear();
+    bx.clear();
+  }
+};
+
+// one worker's part of the last Ready (valid until the next call on the node)
+struct Arena {
+  std::vector<hbn_group_ready> out;
+  std::vector<hbn_entry> ents;
+  std::vector<uint64_t> ent_off;  // byte offset of each ents[i].data in bytes
+  std::vector<hbn_message> msgs;
+  std::vector<uint8_t> bytes;
+  std::vector<uint64_t> off;  // per out: entries, committed, messages offsets
+  std::deque<Snap> snaps;
+  void clear() {
+    out.clear();
+    ents.clear();
+    ent_off.clear();
+    msgs.clear();
+    bytes.clear();
+    off.clear();
+    snaps.clear();
+  }
+};
+
+// host phase timers (hbn_profile): seconds and calls per phase
+enum : uint32_t {
+  PH_SYNC_LOADS, PH_RESERVE, PH_HB_STEP, PH_FETCH, PH_REPLAY, PH_STEPPED, PH_BUILD, PH_MERGE, PH_ADVANCE,
+  PH_BULK_LOOKUP, PH_BULK_RESP, PH_BULK_PROP, PH_CLEAR, PH_COUNT_
+};
+struct PhaseClock {
+  double* acc;
+  std::chrono::steady_clock::time_point t0;
+  PhaseClock(double* a) : acc(a), t0(std::chrono::steady_clock::now()) {}
+  ~PhaseClock() { *acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
+};
+#define HBN_PHASE(n, ph) PhaseClock phase_clock_##ph(&(n)->prof[ph])
+
 }  // namespace
 
 struct hbn_node {
+  double prof[PH_COUNT_] = {};
   hb_handle* h = nullptr;
   uint64_t id = 0;
   uint32_t capacity = 0, nmax = 0, W = 0;
@@ -513,8 +658,17 @@ struct hbn_node {
   std::vector<Group*> pend_tr;  // ... and whose older log term runs are still to push
   std::vector<Group*> stepped;  // groups whose raft.Step runs in the pending batch
   std::vector<Group*> bx;       // groups with messages in the pending batch (Group::bx)
-  hb_event* evbuf = nullptr;  // pinned (hb_alloc_pinned): the event copy lands straight in it
-  uint64_t evcap = 0;
+  // the step's compact event words (hb_events_to_host, pinned: the device writes them)
+  uint64_t* w_words = nullptr;
+  uint64_t w_cap = 0;
+  uint32_t* w_counts = nullptr;
+  uint64_t* w_total = nullptr;
+  uint32_t n_chunks = 0, chunk_groups = 0;
+  std::vector<uint64_t> w_off;  // first word of each chunk
+  // host threads (hbn_set_threads) and their per-phase lists
+  std::unique_ptr<Pool> pool;
+  std::vector<Lists> lists;
+  std::vector<Arena> arenas;
   // CreateGroup loads, coalesced into one hb_load_groups / hb_load_timers per slot run
   std::vector<std::pair<uint32_t, hb_group>> pend_rec;
   std::vector<std::pair<uint32_t, hb_timer>> pend_tm;
@@ -524,14 +678,9 @@ struct hbn_node {
   std::vector<Group*> content;    // groups whose state-derived Ready may be non-empty (lazy, Group::content)
   std::vector<Group*> delivered;  // groups of the last Ready (Group::delivered)
   bool awaiting_advance = false;
-  // flat arena of the last Ready (valid until the next call); pointers patched at the end
+  // the last Ready: one record per group (contiguous), its entries / messages in
+  // the arena of the worker that built it
   std::vector<hbn_group_ready> r_out;
-  std::vector<hbn_entry> r_ents;
-  std::vector<uint64_t> r_ent_off;  // byte offset of each r_ents[i].data in r_bytes
-  std::vector<hbn_message> r_msgs;
-  std::vector<uint8_t> r_bytes;
-  std::vector<uint64_t> r_off;  // per r_out: entries, committed, messages offsets; per r_msgs: entries offset
-  std::deque<Snap> r_snaps;
 };
 
 namespace {
@@ -598,16 +747,23 @@ uint32_t alloc_slot(hbn_node* n) {
 }
 
 // ---------------------------------------------------------------- event replay
-void touch(hbn_node* n, Group& g) {
-  if (!g.touched) {
-    g.touched = true;
-    n->touched.push_back(&g);
-  }
+void touch_into(std::vector<Group*>& v, Group& g) {
+  if (flag_set(g.touched)) v.push_back(&g);
 }
+void touch(hbn_node* n, Group& g) { touch_into(n->touched, g); }
 
-void mark_stepped(hbn_node* n, Group& g) {
+void mark_stepped(std::vector<Group*>& touched, Group& g) {
   g.hs_commit = g.log.committed;  // r.Commit = r.raftLog.committed after Step (raft/raft.go:488)
-  touch(n, g);
+  touch_into(touched, g);
+}
+void mark_stepped(hbn_node* n, Group& g) { mark_stepped(n->touched, g); }
+
+// worker lists merged into the node's, in worker order
+void merge(std::vector<Group*>& dst, std::vector<Lists>& ls, std::vector<Group*> Lists::*m) {
+  for (Lists& l : ls) {
+    dst.insert(dst.end(), (l.*m).begin(), (l.*m).end());
+    (l.*m).clear();
+  }
 }
 
 // r.msgs entries are read from the log when the Ready is built; before the log
@@ -648,7 +804,7 @@ void follower_append(hbn_node* n, Group& g, uint64_t x) {
 }
 
 // HB_FOLLOW_RESTORE: restore of batch message x's snapshot (raft/raft.go:684-707)
-void follower_restore(hbn_node* n, Group& g, uint64_t x) {
+void follower_restore(hbn_node* n, Group& g, uint64_t x, Lists& L) {
   if (x >= n->b_snapi.size() || n->b_snapi[x] == NO_SLOT) panicf("device restored a snapshot the host does not hold");
   const Snap& s = n->b_snaps[n->b_snapi[x]];
   materialize(g);
@@ -662,7 +818,7 @@ void follower_restore(hbn_node* n, Group& g, uint64_t x) {
     g.reload_nodes = s.nodes;
     if (!g.reload) {
       g.reload = true;
-      n->reload.push_back(&g);
+      L.reload.push_back(&g);
     }
   }
 }
@@ -682,7 +838,7 @@ void follower_resp(hbn_node* n, Group& g, const hb_event& e) {
   g.msgs.push_back(std::move(m));
 }
 
-void on_event(hbn_node* n, Group& g, const hb_event& e) {
+void on_event(hbn_node* n, Group& g, const hb_event& e, Lists& L) {
   if (g.fault) return;
   switch (e.type) {
     case HB_EV_TERM:  // reset (raft/raft.go:334-349)
@@ -743,7 +899,7 @@ void on_event(hbn_node* n, Group& g, const hb_event& e) {
     case HB_EV_APP: {  // sendAppend (raft/raft.go:261-281)
       Msg m = base_msg(n, g, HB_MSG_APP, g.peers.at(e.to));
       m.index = e.x;
-      m.log_term = g.log.term(e.x);
+      m.log_term = (e.aux & 1u) ? g.term : g.log.term(e.x);  // aux 1: the device saw term(Index) == Term
       // entries(Index+1, maxMsgSize): (Index, last] under noLimit, one entry under 0
       const uint64_t li = g.log.last_index();
       m.owned = false;
@@ -799,7 +955,7 @@ void on_event(hbn_node* n, Group& g, const hb_event& e) {
       } else if (e.aux == HB_FOLLOW_APPEND) {
         follower_append(n, g, e.x);
       } else if (e.aux == HB_FOLLOW_RESTORE) {
-        follower_restore(n, g, e.x);
+        follower_restore(n, g, e.x, L);
       }
       break;
     case HB_EV_RESP:
@@ -810,30 +966,96 @@ void on_event(hbn_node* n, Group& g, const hb_event& e) {
   }
 }
 
+// The step's events: the device's compact words (hb_events_to_host; one word
+// per bcastAppend), replayed per group in order.  Partition p's groups have
+// their words in chunks 2p and 2p+1, so workers take contiguous partition
+// ranges (balanced by words) and never share a group.
 void consume_events(hbn_node* n) {
-  // one copy call per cycle: into the pinned buffer, grown (and the call
-  // repeated) only when the step produced more events than it holds
-  uint64_t cnt = 0;
-  int rc = hb_copy_events(n->h, n->evbuf, n->evcap, &cnt);
-  if (rc == HB_EINVAL && cnt > n->evcap) {
-    if (n->evbuf) (void)hb_free_pinned(n->evbuf);
-    n->evbuf = nullptr;
-    n->evcap = 0;
-    const uint64_t cap = cnt + cnt / 4 + 1024;
+  if (!n->w_counts) {
+    check(hb_event_words_chunks(n->h, &n->n_chunks, &n->chunk_groups));
     void* p = nullptr;
-    check(hb_alloc_pinned(cap * sizeof(hb_event), &p));
-    n->evbuf = static_cast<hb_event*>(p);
-    n->evcap = cap;
-    rc = hb_copy_events(n->h, n->evbuf, n->evcap, &cnt);
+    check(hb_alloc_pinned(n->n_chunks * 4ull + 64, &p));
+    n->w_counts = static_cast<uint32_t*>(p);
+    check(hb_alloc_pinned(64, &p));
+    n->w_total = static_cast<uint64_t*>(p);
   }
-  check(rc);
-  for (uint64_t i = 0; i < cnt; ++i) {
-    const hb_event& e = n->evbuf[i];
-    if (e.group >= n->by_slot.size() || !n->by_slot[e.group]) continue;
-    Group& g = *n->by_slot[e.group];
-    on_event(n, g, e);
-    mark_stepped(n, g);
+  auto fetch0 = std::chrono::steady_clock::now();
+  for (int attempt = 0;; ++attempt) {
+    check(hb_events_to_host(n->h, n->w_words, n->w_cap, n->w_counts, n->w_total));
+    check(hb_sync(n->h));
+    if (*n->w_total <= n->w_cap) break;
+    if (attempt) panicf("device event words exceed their buffer");
+    if (n->w_words) (void)hb_free_pinned(n->w_words);
+    n->w_words = nullptr;
+    n->w_cap = 0;
+    const uint64_t cap = *n->w_total + *n->w_total / 4 + 4096;
+    void* p = nullptr;
+    check(hb_alloc_pinned(cap * 8, &p));
+    n->w_words = static_cast<uint64_t*>(p);
+    n->w_cap = cap;
   }
+  n->prof[PH_FETCH] += std::chrono::duration<double>(std::chrono::steady_clock::now() - fetch0).count();
+  const uint64_t total = *n->w_total;
+  if (total == 0) return;
+  HBN_PHASE(n, PH_REPLAY);
+  const uint32_t nc = n->n_chunks, np = nc / 2;
+  n->w_off.resize(nc + 1);
+  uint64_t run = 0;
+  for (uint32_t c = 0; c < nc; ++c) {
+    n->w_off[c] = run;
+    run += n->w_counts[c];
+  }
+  n->w_off[nc] = run;
+  if (run != total) panicf("device event word counts disagree");
+  const unsigned k = total < 32768 ? 1 : n->pool->size();
+  n->pool->run(
+      [&](unsigned t) {
+        // partitions [p0, p1) of worker t: an equal share of the words
+        uint32_t p0 = 0, p1 = np;
+        if (k > 1) {
+          const uint64_t w0 = total * t / k, w1 = total * (t + 1) / k;
+          auto at = [&](uint64_t w) {  // first partition whose words start at or after w
+            return (uint32_t)(std::lower_bound(n->w_off.begin(), n->w_off.begin() + nc, w) - n->w_off.begin() + 1) / 2;
+          };
+          p0 = t == 0 ? 0 : at(w0);
+          p1 = t + 1 == k ? np : at(w1);
+        }
+        Lists& L = n->lists[t];
+        const uint64_t* W = n->w_words;
+        for (uint32_t p = p0; p < p1; ++p) {
+          for (uint64_t i = n->w_off[2 * p], end = n->w_off[2 * p + 2]; i < end; ++i) {
+            const uint64_t w = W[i];
+            const uint32_t type = (uint32_t)w & 0xF;
+            if (type == HB_EVW_CONT) continue;
+            const uint32_t slot = p * n->chunk_groups + ((uint32_t)(w >> 16) & 0xFF);
+            if (slot >= n->by_slot.size() || !n->by_slot[slot]) continue;
+            Group& g = *n->by_slot[slot];
+            hb_event e;
+            e.group = slot;
+            e.x = w >> 24;
+            if (((w >> 11) & 1u) && i + 1 < end) e.x |= (W[i + 1] >> 4) << 40;
+            const uint32_t to = (uint32_t)(w >> 4) & 0x7F;
+            if (type == HB_EVW_BCAST) {  // an HB_EV_APP to every slot of the mask, in slot order
+              e.type = HB_EV_APP;
+              e.aux = (uint16_t)((w >> 12) & 0xF);
+              for (uint32_t s = 0; s < 7; ++s)
+                if ((to >> s) & 1u) {
+                  e.to = (uint8_t)s;
+                  on_event(n, g, e, L);
+                }
+            } else {
+              e.type = (uint8_t)type;
+              e.to = (uint8_t)to;
+              e.aux = (uint16_t)((w >> 12) & 0xF);
+              on_event(n, g, e, L);
+            }
+            mark_stepped(L.touched, g);
+          }
+        }
+      },
+      k);
+  merge(n->touched, n->lists, &Lists::touched);
+  merge(n->reload, n->lists, &Lists::reload);
 }
 
 // Push the queued CreateGroup records and timers to the device, one call per
@@ -884,19 +1106,22 @@ uint64_t pow2_at_least(uint64_t x) {
   return p;
 }
 
-// Capacity for g's rings before a step that can add up to g.bx entries / runs
-// (and MsgApp entries up to g.bx_top): sizes cover [firstIndex - 1, the new
-// lastIndex], runs every run of the log plus the new ones.  Requested with 2x
-// headroom (amortised); the exact run count is taken only when the bound grows
-// past the reserved capacity.
-void want_log(const hbn_node* n, Group& g, uint64_t extra, std::vector<uint32_t>& slots,
+// Capacity for g's rings before a step that can append up to extra_sz entries
+// (and MsgApp entries up to g.bx_top) and start up to extra_runs term runs:
+// sizes cover [firstIndex - 1, the new lastIndex], runs every run of the log
+// plus the new ones.  Requested with 2x headroom (amortised); the exact run
+// count is taken only when the bound grows past the reserved capacity.
+void want_log(const hbn_node* n, Group& g, uint64_t extra_sz, uint64_t extra_runs, std::vector<uint32_t>& slots,
               std::vector<uint64_t>& szc, std::vector<uint64_t>& trc) {
-  const uint64_t lo = g.log.first_index() - 1;
-  const uint64_t need_sz = n->sized ? std::max(g.log.last_index(), g.bx_top) + extra - lo + 1 : 0;
-  uint64_t need_tr = g.lx_runs + extra + 1;
+  uint64_t need_sz = 0;
+  if (n->sized) {
+    const uint64_t lo = g.log.first_index() - 1;
+    need_sz = std::max(g.log.last_index(), g.bx_top) + extra_sz - lo + 1;
+  }
+  uint64_t need_tr = g.lx_runs + extra_runs + 1;
   if (need_tr > g.lx_tr) {
     g.lx_runs = count_runs(g);
-    need_tr = g.lx_runs + extra + 1;
+    need_tr = g.lx_runs + extra_runs + 1;
   }
   const bool gs = need_sz > g.lx_sz, gt = need_tr > g.lx_tr;
   if (!gs && !gt) return;
@@ -928,7 +1153,7 @@ void push_sizes(hbn_node* n) {
     cnt.push_back((uint32_t)k);
     g->log.visit(fi, li + 1, [&](const Ent& x) { sizes.push_back((uint32_t)ent_size(x)); });
     g->lx_sz = 0;  // a reload: reserve afresh
-    want_log(n, *g, 0, rs, rz, rt);
+    want_log(n, *g, 0, 0, rs, rz, rt);
   }
   n->pend_sz.clear();
   reserve(n, rs, rz, rt);
@@ -960,7 +1185,7 @@ void push_term_runs(hbn_node* n) {
     }
     g->lx_tr = 0;  // a reload: reserve afresh, with the exact count
     g->lx_runs = rr.size() + (tf != HB_NO_INDEX ? 1 : 0);
-    want_log(n, *g, 0, rs, rz, rt);
+    want_log(n, *g, 0, 0, rs, rz, rt);
   }
   n->pend_tr.clear();
   reserve(n, rs, rz, rt);
@@ -968,18 +1193,32 @@ void push_term_runs(hbn_node* n) {
     check(hb_load_term_runs(n->h, (uint32_t)slots.size(), slots.data(), cnt.data(), runs.data()));
 }
 
-// Before hb_step: room in every batch group's rings for what the batch can add.
+// Before hb_step: room in every batch group's rings for what the batch can add
+// (workers over disjoint ranges of the batch's groups).
 void reserve_batch(hbn_node* n) {
-  std::vector<uint32_t> rs;
-  std::vector<uint64_t> rz, rt;
-  for (Group* g : n->bx)
-    if (g->slot != NO_SLOT) want_log(n, *g, g->bx, rs, rz, rt);
-  reserve(n, rs, rz, rt);
-  for (Group* g : n->bx) {  // after the step: the bound on the log's runs grows by what it could add
-    g->lx_runs += g->bx;
-    g->bx = g->bx_top = 0;
-    g->in_bx = false;
+  const size_t nb = n->bx.size();
+  const unsigned k = nb < 8192 ? 1 : n->pool->size();
+  std::vector<std::vector<uint32_t>> rs(k);
+  std::vector<std::vector<uint64_t>> rz(k), rt(k);
+  n->pool->run(
+      [&](unsigned t) {
+        size_t lo, hi;
+        split(nb, k, t, &lo, &hi);
+        for (size_t i = lo; i < hi; ++i) {
+          Group& g = *n->bx[i];
+          if (g.slot != NO_SLOT) want_log(n, g, g.bx, g.bxr, rs[t], rz[t], rt[t]);
+          g.lx_runs += g.bxr;  // after the step: the bound on the log's runs grows by what it could add
+          g.bx = g.bx_top = g.bxr = 0;
+          g.in_bx = false;
+        }
+      },
+      k);
+  for (unsigned t = 1; t < k; ++t) {
+    rs[0].insert(rs[0].end(), rs[t].begin(), rs[t].end());
+    rz[0].insert(rz[0].end(), rz[t].begin(), rz[t].end());
+    rt[0].insert(rt[0].end(), rt[t].begin(), rt[t].end());
   }
+  reserve(n, rs[0], rz[0], rt[0]);
   n->bx.clear();
 }
 
@@ -1008,7 +1247,10 @@ void reload_prs(hbn_node* n, Group& g, const std::vector<uint64_t>& new_peers,
                 const std::vector<std::pair<uint64_t, uint64_t>>& fresh, bool restored);
 
 void flush(hbn_node* n) {
-  sync_loads(n);
+  {
+    HBN_PHASE(n, PH_SYNC_LOADS);
+    sync_loads(n);
+  }
   if (n->b_group.empty()) return;
   hb_batch b{};
   b.n = n->b_group.size();
@@ -1025,14 +1267,24 @@ void flush(hbn_node* n) {
     if (n->b_app) b.eterm = n->b_eterm.data();
   }
   if (n->b_follow) b.commit = n->b_commit.data();
-  reserve_batch(n);
-  check(hb_step(n->h, &b, HB_STEP_HOST_PTRS));
-  consume_events(n);
-  for (Group* g : n->stepped) {
-    g->stepped = false;
-    mark_stepped(n, *g);
+  {
+    HBN_PHASE(n, PH_RESERVE);
+    reserve_batch(n);
   }
-  n->stepped.clear();
+  {
+    HBN_PHASE(n, PH_HB_STEP);
+    check(hb_step(n->h, &b, HB_STEP_HOST_PTRS));
+  }
+  consume_events(n);
+  {
+    HBN_PHASE(n, PH_STEPPED);
+    for (Group* g : n->stepped) {
+      g->stepped = false;
+      mark_stepped(n, *g);
+    }
+    n->stepped.clear();
+  }
+  HBN_PHASE(n, PH_CLEAR);
   n->b_group.clear();
   n->b_info.clear();
   n->b_term.clear();
@@ -1087,7 +1339,8 @@ void push(hbn_node* n, Group& g, uint32_t type, uint64_t from, bool reject, uint
   n->b_commit.push_back(commit);
   n->b_from.push_back(from);
   n->b_snapi.push_back(NO_SLOT);
-  g.bx++;  // a noop (becomeLeader) or a new term run at most
+  g.bx++;  // a noop (becomeLeader) at most
+  if (type == HB_MSG_HUP || type == HB_MSG_VOTE_RESP || type == HB_MSG_SNAP) g.bxr++;  // a noop's / restore's run
   if (!g.in_bx) {
     g.in_bx = true;
     n->bx.push_back(&g);
@@ -1104,10 +1357,175 @@ Group& group_of(hbn_node* n, uint64_t id) {
   return *it->second;
 }
 
+// ---- bulk ingestion (hbn_step_many / hbn_propose_many) ----
+// Pass 1 (parallel): each message's group, and whether it takes the bulk path
+// (an existing, unfaulted group; for steps a response type).  The rest go one
+// by one through the single-message path, which raises the reference's errors
+// at the right position.
+struct BulkRun {
+  std::vector<Group*> gp;
+  std::vector<uint8_t> fast;
+};
+template <class Ok>
+void bulk_lookup(hbn_node* n, uint64_t count, const uint64_t* gids, BulkRun& br, Ok&& ok) {
+  HBN_PHASE(n, PH_BULK_LOOKUP);
+  br.gp.assign(count, nullptr);
+  br.fast.assign(count, 0);
+  const unsigned k = count < 8192 ? 1 : n->pool->size();
+  n->pool->run(
+      [&](unsigned t) {
+        size_t lo, hi;
+        split(count, k, t, &lo, &hi);
+        for (size_t i = lo; i < hi; ++i) {
+          auto it = n->groups.find(gids[i]);
+          if (it == n->groups.end()) continue;
+          Group* g = it->second.get();
+          br.gp[i] = g;
+          br.fast[i] = !g->fault && ok(i, *g);
+        }
+      },
+      k);
+}
+
+// Bulk push() of response messages [a, b) (all fast): rows at fixed batch
+// positions, group flags by atomic exchange, lists per worker.  The batch has
+// room for b - a rows.
+void push_responses(hbn_node* n, const BulkRun& br, const hbn_message* m, size_t a, size_t b) {
+  HBN_PHASE(n, PH_BULK_RESP);
+  const size_t cnt = b - a;
+  const unsigned k = cnt < 8192 ? 1 : n->pool->size();
+  std::vector<size_t> rows(k + 1, 0);  // rows of each worker's range (groups with a device slot)
+  n->pool->run(
+      [&](unsigned t) {
+        size_t lo, hi, c = 0;
+        split(cnt, k, t, &lo, &hi);
+        for (size_t i = a + lo; i < a + hi; ++i) c += br.gp[i]->slot != NO_SLOT;
+        rows[t + 1] = c;
+      },
+      k);
+  for (unsigned t = 0; t < k; ++t) rows[t + 1] += rows[t];
+  const size_t base = n->b_group.size(), add = rows[k];
+  for (auto* v : {&n->b_term, &n->b_index, &n->b_hint, &n->b_eoff, &n->b_commit, &n->b_from}) v->resize(base + add);
+  n->b_group.resize(base + add);
+  n->b_info.resize(base + add);
+  n->b_snapi.resize(base + add, NO_SLOT);
+  n->pool->run(
+      [&](unsigned t) {
+        size_t lo, hi;
+        split(cnt, k, t, &lo, &hi);
+        Lists& L = n->lists[t];
+        size_t r = base + rows[t];
+        for (size_t i = a + lo; i < a + hi; ++i) {
+          Group& g = *br.gp[i];
+          const hbn_message& x = m[i];
+          touch_into(L.touched, g);
+          if (g.slot == NO_SLOT) continue;  // prs is empty: responses are filtered (raft/multinode.go:235)
+          const int s = g.slot_of(x.from);
+          n->b_group[r] = g.slot;
+          n->b_info[r] = HB_INFO(x.type, s >= 0 ? (uint32_t)s : HB_SLOT_NONE, x.reject != 0);
+          n->b_term[r] = x.term;
+          n->b_index[r] = x.index;
+          n->b_hint[r] = x.reject_hint;
+          n->b_eoff[r] = n->b_nent;
+          n->b_commit[r] = 0;
+          n->b_from[r] = x.from;
+          ++r;
+          __atomic_fetch_add(&g.bx, 1, __ATOMIC_RELAXED);
+          if (x.type == HB_MSG_VOTE_RESP) __atomic_fetch_add(&g.bxr, 1, __ATOMIC_RELAXED);
+          if (flag_set(g.in_bx)) L.bx.push_back(&g);
+          if (s >= 0 && flag_set(g.stepped)) L.stepped.push_back(&g);
+        }
+      },
+      k);
+  merge(n->touched, n->lists, &Lists::touched);
+  merge(n->bx, n->lists, &Lists::bx);
+  merge(n->stepped, n->lists, &Lists::stepped);
+}
+
+// Bulk propose() of one-entry proposals [a, b) (all fast: groups with a device
+// slot).  A group's proposals keep their order in g.props, so each group
+// belongs to one worker (slot % k); rows and entry positions are fixed.
+void push_proposals(hbn_node* n, const BulkRun& br, const uint8_t* const* data, const uint64_t* len, size_t a,
+                    size_t b) {
+  HBN_PHASE(n, PH_BULK_PROP);
+  const size_t cnt = b - a, base = n->b_group.size(), e0 = n->b_nent;
+  const unsigned k = cnt < 8192 ? 1 : n->pool->size();
+  for (auto* v : {&n->b_term, &n->b_index, &n->b_hint, &n->b_eoff, &n->b_commit, &n->b_from}) v->resize(base + cnt);
+  n->b_group.resize(base + cnt);
+  n->b_info.resize(base + cnt);
+  n->b_snapi.resize(base + cnt, NO_SLOT);
+  n->b_eterm.resize(e0 + cnt, 0);
+  n->b_ents.resize(e0 + cnt);
+  if (n->sized) n->b_edesc.resize(e0 + cnt);
+  std::vector<uint32_t> sl(cnt);
+  for (size_t i = 0; i < cnt; ++i) sl[i] = br.gp[a + i]->slot;
+  n->pool->run(
+      [&](unsigned t) {
+        Lists& L = n->lists[t];
+        for (size_t j = 0; j < cnt; ++j) {
+          if (k > 1 && sl[j] % k != t) continue;
+          const size_t i = a + j, r = base + j;
+          Group& g = *br.gp[i];
+          Msg msg;
+          msg.type = HB_MSG_PROP;
+          msg.from = n->id;  // raft/multinode.go:228
+          Ent e;
+          e.has_data = data[i] != nullptr;
+          if (len[i]) e.data.assign(reinterpret_cast<const char*>(data[i]), len[i]);
+          if (n->sized) n->b_edesc[e0 + j] = ent_desc(e);
+          msg.entries.push_back(std::move(e));
+          g.props.push_back(std::move(msg));
+          const int s = g.slot_of(n->id);
+          n->b_group[r] = g.slot;
+          n->b_info[r] = HB_INFO(HB_MSG_PROP, s >= 0 ? (uint32_t)s : HB_SLOT_NONE, false);
+          n->b_term[r] = 0;
+          n->b_index[r] = 1;
+          n->b_hint[r] = 0;
+          n->b_eoff[r] = e0 + j;
+          n->b_commit[r] = 0;
+          n->b_from[r] = n->id;
+          g.bx += 2;  // the message and its entry
+          if (flag_set(g.touched)) L.touched.push_back(&g);
+          if (flag_set(g.in_bx)) L.bx.push_back(&g);
+          if (flag_set(g.stepped)) L.stepped.push_back(&g);
+        }
+      },
+      k);
+  n->b_nent = e0 + cnt;
+  merge(n->touched, n->lists, &Lists::touched);
+  merge(n->bx, n->lists, &Lists::bx);
+  merge(n->stepped, n->lists, &Lists::stepped);
+}
+
+// Runs of bulk messages in [0, count), each cut to the batch's free rows (the
+// batch is stepped when full, as push() does); the others one at a time.
+template <class Bulk, class One>
+void bulk_runs(hbn_node* n, uint64_t count, const BulkRun& br, uint64_t* done, Bulk&& bulk, One&& one) {
+  size_t i = 0;
+  while (i < count) {
+    if (!br.fast[i]) {
+      one(i);
+      *done = ++i;
+      continue;
+    }
+    size_t j = i;
+    while (j < count && br.fast[j]) ++j;
+    while (i < j) {
+      if (n->b_group.size() >= n->max_batch) flush(n);
+      const size_t room = n->max_batch - n->b_group.size();
+      const size_t e = std::min(j, i + room);
+      bulk(i, e);
+      *done = i = e;
+    }
+  }
+}
+
 // One entry of the last pushed message (its descriptor for the device's
 // limitSize, its term for the follower side; `keep`: the payload for the replay).
 void push_entry(hbn_node* n, const Ent& x, bool keep) {
-  n->by_slot[n->b_group.back()]->bx++;  // one more entry (and possibly term run) the step can append
+  Group* g = n->by_slot[n->b_group.back()];
+  g->bx++;  // one more entry the step can append
+  if (keep) g->bxr++;  // a MsgApp entry can start a term run (a MsgProp entry continues the leader's)
   if (n->sized) n->b_edesc.push_back(ent_desc(x));
   n->b_eterm.push_back(x.term);
   if (keep) n->b_ents.push_back(x);
@@ -1166,7 +1584,8 @@ void step_follower(hbn_node* n, Group& g, const hbn_message* m) {
 }
 
 // ---------------------------------------------------------------- Ready
-void arena_entry(hbn_node* n, const Ent& x) {
+void refresh_content(std::vector<Group*>& content, Group& g);
+void arena_entry(Arena& A, const Ent& x) {
   hbn_entry e;
   e.term = x.term;
   e.index = x.index;
@@ -1174,19 +1593,98 @@ void arena_entry(hbn_node* n, const Ent& x) {
   e.has_data = x.has_data;
   e.data = nullptr;
   e.data_len = x.data.size();
-  n->r_ent_off.push_back(n->r_bytes.size());
-  if (!x.data.empty()) n->r_bytes.insert(n->r_bytes.end(), x.data.begin(), x.data.end());
-  n->r_ents.push_back(e);
+  A.ent_off.push_back(A.bytes.size());
+  if (!x.data.empty()) A.bytes.insert(A.bytes.end(), x.data.begin(), x.data.end());
+  A.ents.push_back(e);
 }
 
 void clear_arena(hbn_node* n) {
   n->r_out.clear();
-  n->r_ents.clear();
-  n->r_ent_off.clear();
-  n->r_msgs.clear();
-  n->r_bytes.clear();
-  n->r_off.clear();
-  n->r_snaps.clear();
+  for (Arena& A : n->arenas) A.clear();
+}
+
+// newReady (raft/node.go:447-463) of g into arena A when it containsUpdates
+// (raft/node.go:96-100); the delivered part is remembered for commitReady.
+void build_ready(Group& g, Arena& A, Lists& L) {
+  g.touched = false;
+  refresh_content(L.content, g);
+  if (!g.content && g.msgs.empty() && !g.fault) return;
+  hbn_group_ready r;
+  std::memset(&r, 0, sizeof(r));
+  r.group = g.id;
+  Delivered& d = g.dlv;
+  d = Delivered{};
+  if (!(g.soft() == g.prev_soft)) {
+    r.has_soft_state = 1;
+    r.raft_state = g.state;
+    r.lead = g.lead;
+    d.has_soft = true;
+    d.soft = g.soft();
+  }
+  if (!hs_equal(g.hard(), g.prev_hard)) r.hard_state = d.hard = g.hard();
+  if (g.log.has_usnap) {
+    A.snaps.push_back(g.log.usnap);
+    snap_view(A.snaps.back(), &r.snapshot);
+    d.snap_index = g.log.usnap.index;
+  }
+  A.off.push_back(A.ents.size());  // Entries = unstableEntries
+  for (const Ent& x : g.log.unstable) arena_entry(A, x);
+  r.n_entries = g.log.unstable.size();
+  if (r.n_entries) {
+    d.has_last = true;
+    d.last_index = g.log.unstable.back().index;
+    d.last_term = g.log.unstable.back().term;
+  }
+  A.off.push_back(A.ents.size());  // CommittedEntries = nextEnts (raft/log.go:135-141)
+  const uint64_t lo = std::max(g.log.applied + 1, g.log.first_index());
+  if (g.log.committed + 1 > lo) g.log.visit(lo, g.log.committed + 1, [&](const Ent& x) { arena_entry(A, x); });
+  r.n_committed = A.ents.size() - A.off.back();
+  A.off.push_back(A.msgs.size());  // Messages = r.msgs, then cleared (raft/multinode.go:277-281)
+  for (Msg& m : g.msgs) {
+    hbn_message x;
+    std::memset(&x, 0, sizeof(x));
+    x.type = m.type;
+    x.reject = m.reject;
+    x.to = m.to;
+    x.from = m.from;
+    x.term = m.term;
+    x.log_term = m.log_term;
+    x.index = m.index;
+    x.commit = m.commit;
+    x.reject_hint = m.reject_hint;
+    const size_t e0 = A.ents.size();
+    if (m.owned)
+      for (const Ent& e : m.entries) arena_entry(A, e);
+    else if (m.ent_hi > m.ent_lo)
+      g.log.visit(m.ent_lo, m.ent_hi, [&](const Ent& e) { arena_entry(A, e); });
+    x.n_entries = A.ents.size() - e0;
+    x.entries = reinterpret_cast<const hbn_entry*>(e0);  // offset, patched below
+    if (m.has_snap) {
+      A.snaps.push_back(m.snap);
+      snap_view(A.snaps.back(), &x.snapshot);
+    }
+    A.msgs.push_back(x);
+  }
+  r.n_messages = g.msgs.size();
+  g.msgs.clear();
+  r.fault = g.fault;
+  g.delivered = true;
+  L.delivered.push_back(&g);
+  A.out.push_back(r);
+}
+
+// once no vector of A grows any more: offsets become pointers
+void patch_arena(Arena& A) {
+  for (size_t i = 0; i < A.ents.size(); ++i)
+    if (A.ents[i].data_len) A.ents[i].data = A.bytes.data() + A.ent_off[i];
+  for (hbn_message& x : A.msgs)
+    x.entries = x.n_entries ? A.ents.data() + reinterpret_cast<uintptr_t>(x.entries) : nullptr;
+  for (size_t i = 0; i < A.out.size(); ++i) {
+    hbn_group_ready& r = A.out[i];
+    r.entries = r.n_entries ? A.ents.data() + A.off[3 * i] : nullptr;
+    r.committed_entries = r.n_committed ? A.ents.data() + A.off[3 * i + 1] : nullptr;
+    r.messages = r.n_messages ? A.msgs.data() + A.off[3 * i + 2] : nullptr;
+  }
 }
 
 // commitReady raft/multinode.go:137-164
@@ -1210,9 +1708,9 @@ bool has_updates(const Group& g) {
   return g.log.committed + 1 > std::max(g.log.applied + 1, g.log.first_index());
 }
 
-void refresh_content(hbn_node* n, Group& g) {
+void refresh_content(std::vector<Group*>& content, Group& g) {
   const bool c = has_updates(g);
-  if (c && !g.content) n->content.push_back(&g);
+  if (c && !g.content) content.push_back(&g);
   g.content = c;
 }
 
@@ -1363,6 +1861,47 @@ int guarded(F&& f) {
     g_err = e.what();
     return HBN_EPANIC;
   }
+}
+
+// Step (raft/multinode.go:431-439) of one message; throws the reference's errors.
+void step_one(hbn_node* n, uint64_t group, const hbn_message* m) {
+  const uint32_t t = m->type;
+  // IsLocalMsg (raft/util.go:49-51): ignored when received over the network
+  if (t == HB_MSG_HUP || t == HB_MSG_BEAT || t == HB_MSG_UNREACHABLE || t == HB_MSG_SNAP_STATUS) return;
+  Group& g = group_of(n, group);
+  if (t == HB_MSG_PROP) {
+    Msg p;
+    p.type = t;
+    p.to = m->to;
+    p.term = m->term;
+    p.log_term = m->log_term;
+    p.index = m->index;
+    p.commit = m->commit;
+    p.reject = m->reject;
+    p.reject_hint = m->reject_hint;
+    for (uint64_t i = 0; i < m->n_entries; ++i) p.entries.push_back(ent_from(m->entries[i]));
+    propose(n, g, std::move(p));
+    return;
+  }
+  if (t == HB_MSG_APP || t == HB_MSG_HEARTBEAT || t == HB_MSG_SNAP || t == HB_MSG_VOTE) {
+    step_follower(n, g, m);
+    return;
+  }
+  if (t != HB_MSG_APP_RESP && t != HB_MSG_VOTE_RESP && t != HB_MSG_HEARTBEAT_RESP) throw Fail{HBN_EUNSUPPORTED};
+  if (g.fault) throw Fail{HBN_EPANIC};
+  push(n, g, t, m->from, m->reject != 0, m->term, m->index, m->reject_hint);
+}
+
+// Propose (raft/multinode.go:377-385) of one entry.
+void propose_one(hbn_node* n, uint64_t group, const uint8_t* data, uint64_t len) {
+  Group& g = group_of(n, group);
+  Msg m;
+  m.type = HB_MSG_PROP;
+  Ent e;
+  e.has_data = data != nullptr;
+  if (len) e.data.assign(reinterpret_cast<const char*>(data), len);
+  m.entries.push_back(std::move(e));
+  propose(n, g, std::move(m));
 }
 
 }  // namespace
@@ -1563,6 +2102,11 @@ int hbn_start(int device, uint64_t id, uint32_t capacity, uint32_t max_replicas,
     n->max_msg = max_msg_size;
     n->sized = max_msg_size != 0 && max_msg_size != HB_NO_LIMIT;
     n->max_batch = max_batch;
+    unsigned th = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    if (const char* e = std::getenv("HBN_THREADS")) th = std::max(1, std::atoi(e));
+    n->pool.reset(new Pool(th));
+    n->lists.resize(th);
+    n->arenas.resize(th);
     n->by_slot.assign(capacity, nullptr);
     n->free_slots.reserve(capacity);
     for (uint32_t s = capacity; s > 0; --s) n->free_slots.push_back(s - 1);
@@ -1574,7 +2118,9 @@ int hbn_stop(hbn_node* n) {
   if (!n) return HB_EINVAL;
   for (auto& kv : n->groups)
     if (kv.second->log.st) drop_user(kv.second->log.st, n, kv.first);
-  if (n->evbuf) (void)hb_free_pinned(n->evbuf);
+  if (n->w_words) (void)hb_free_pinned(n->w_words);
+  if (n->w_counts) (void)hb_free_pinned(n->w_counts);
+  if (n->w_total) (void)hb_free_pinned(n->w_total);
   const int rc = hb_destroy(n->h);
   delete n;
   return rc;
@@ -1700,7 +2246,7 @@ int hbn_tick(hbn_node* n) {
       std::vector<uint64_t> rz, rt;
       for (Group* g : n->by_slot)
         if (g && g->peers.size() == 1) {
-          want_log(n, *g, 1, rs, rz, rt);
+          want_log(n, *g, 1, 1, rs, rz, rt);
           g->lx_runs += 1;
         }
       reserve(n, rs, rz, rt);
@@ -1728,16 +2274,23 @@ int hbn_campaign(hbn_node* n, uint64_t group) {
 
 int hbn_propose(hbn_node* n, uint64_t group, const uint8_t* data, uint64_t len) {
   if (!n || (len && !data)) return HB_EINVAL;
-  return guarded([&] {
-    Group& g = group_of(n, group);
-    Msg m;
-    m.type = HB_MSG_PROP;
-    Ent e;
-    e.has_data = data != nullptr;
-    if (len) e.data.assign(reinterpret_cast<const char*>(data), len);
-    m.entries.push_back(std::move(e));
-    propose(n, g, std::move(m));
+  return guarded([&] { propose_one(n, group, data, len); });
+}
+
+int hbn_propose_many(hbn_node* n, uint64_t count, const uint64_t* groups, const uint8_t* const* data,
+                     const uint64_t* len, uint64_t* done) {
+  if (!n || (count && (!groups || !data || !len))) return HB_EINVAL;
+  for (uint64_t i = 0; i < count; ++i)
+    if (len[i] && !data[i]) return HB_EINVAL;
+  uint64_t d = 0;
+  const int rc = guarded([&] {
+    BulkRun br;
+    bulk_lookup(n, count, groups, br, [](size_t, const Group& g) { return g.slot != NO_SLOT; });
+    bulk_runs(n, count, br, &d, [&](size_t a, size_t b) { push_proposals(n, br, data, len, a, b); },
+              [&](size_t i) { propose_one(n, groups[i], data[i], len[i]); });
   });
+  if (done) *done = d;
+  return rc;
 }
 
 int hbn_propose_conf_change(hbn_node* n, uint64_t group, uint64_t cc_id, uint32_t cc_type, uint64_t node_id,
@@ -1758,32 +2311,40 @@ int hbn_propose_conf_change(hbn_node* n, uint64_t group, uint64_t cc_id, uint32_
 
 int hbn_step(hbn_node* n, uint64_t group, const hbn_message* m) {
   if (!n || !m || (m->n_entries && !m->entries)) return HB_EINVAL;
-  const uint32_t t = m->type;
-  // IsLocalMsg (raft/util.go:49-51): ignored when received over the network
-  if (t == HB_MSG_HUP || t == HB_MSG_BEAT || t == HB_MSG_UNREACHABLE || t == HB_MSG_SNAP_STATUS) return HB_OK;
+  return guarded([&] { step_one(n, group, m); });
+}
+
+int hbn_step_many(hbn_node* n, uint64_t count, const uint64_t* groups, const hbn_message* msgs, uint64_t* done) {
+  if (!n || (count && (!groups || !msgs))) return HB_EINVAL;
+  for (uint64_t i = 0; i < count; ++i)
+    if (msgs[i].n_entries && !msgs[i].entries) return HB_EINVAL;
+  uint64_t d = 0;
+  const int rc = guarded([&] {
+    BulkRun br;
+    bulk_lookup(n, count, groups, br, [&](size_t i, const Group&) {
+      const uint32_t t = msgs[i].type;
+      return t == HB_MSG_APP_RESP || t == HB_MSG_VOTE_RESP || t == HB_MSG_HEARTBEAT_RESP;
+    });
+    bulk_runs(n, count, br, &d, [&](size_t a, size_t b) { push_responses(n, br, msgs, a, b); },
+              [&](size_t i) { step_one(n, groups[i], &msgs[i]); });
+  });
+  if (done) *done = d;
+  return rc;
+}
+
+int hbn_profile(hbn_node* n, double* out, uint32_t cap, uint32_t* count) {
+  if (!n) return HB_EINVAL;
+  if (count) *count = PH_COUNT_;
+  for (uint32_t i = 0; i < cap && i < PH_COUNT_ && out; ++i) out[i] = n->prof[i];
+  return HB_OK;
+}
+
+int hbn_set_threads(hbn_node* n, uint32_t threads) {
+  if (!n || threads == 0 || threads > 256) return HB_EINVAL;
   return guarded([&] {
-    Group& g = group_of(n, group);
-    if (t == HB_MSG_PROP) {
-      Msg p;
-      p.type = t;
-      p.to = m->to;
-      p.term = m->term;
-      p.log_term = m->log_term;
-      p.index = m->index;
-      p.commit = m->commit;
-      p.reject = m->reject;
-      p.reject_hint = m->reject_hint;
-      for (uint64_t i = 0; i < m->n_entries; ++i) p.entries.push_back(ent_from(m->entries[i]));
-      propose(n, g, std::move(p));
-      return;
-    }
-    if (t == HB_MSG_APP || t == HB_MSG_HEARTBEAT || t == HB_MSG_SNAP || t == HB_MSG_VOTE) {
-      step_follower(n, g, m);
-      return;
-    }
-    if (t != HB_MSG_APP_RESP && t != HB_MSG_VOTE_RESP && t != HB_MSG_HEARTBEAT_RESP) throw Fail{HBN_EUNSUPPORTED};
-    if (g.fault) throw Fail{HBN_EPANIC};
-    push(n, g, t, m->from, m->reject != 0, m->term, m->index, m->reject_hint);
+    n->pool.reset(new Pool(threads));
+    n->lists.resize(threads);
+    if (n->arenas.size() < threads) n->arenas.resize(threads);  // (the last Ready stays valid)
   });
 }
 
@@ -1861,91 +2422,32 @@ int hbn_ready(hbn_node* n, const hbn_group_ready** out, uint64_t* count) {
     }
     for (Group* g : n->delivered) g->delivered = false;
     n->delivered.clear();
-    for (Group* gp : n->touched) {
-      Group& g = *gp;
-      g.touched = false;
-      refresh_content(n, g);
-      if (!g.content && g.msgs.empty() && !g.fault) continue;  // containsUpdates (raft/node.go:96-100)
-      // newReady raft/node.go:447-463
-      hbn_group_ready r;
-      std::memset(&r, 0, sizeof(r));
-      r.group = g.id;
-      Delivered& d = g.dlv;
-      d = Delivered{};
-      if (!(g.soft() == g.prev_soft)) {
-        r.has_soft_state = 1;
-        r.raft_state = g.state;
-        r.lead = g.lead;
-        d.has_soft = true;
-        d.soft = g.soft();
-      }
-      if (!hs_equal(g.hard(), g.prev_hard)) r.hard_state = d.hard = g.hard();
-      if (g.log.has_usnap) {
-        n->r_snaps.push_back(g.log.usnap);
-        snap_view(n->r_snaps.back(), &r.snapshot);
-        d.snap_index = g.log.usnap.index;
-      }
-      n->r_off.push_back(n->r_ents.size());  // Entries = unstableEntries
-      for (const Ent& x : g.log.unstable) arena_entry(n, x);
-      r.n_entries = g.log.unstable.size();
-      if (r.n_entries) {
-        d.has_last = true;
-        d.last_index = g.log.unstable.back().index;
-        d.last_term = g.log.unstable.back().term;
-      }
-      n->r_off.push_back(n->r_ents.size());  // CommittedEntries = nextEnts (raft/log.go:135-141)
-      const uint64_t lo = std::max(g.log.applied + 1, g.log.first_index());
-      if (g.log.committed + 1 > lo) g.log.visit(lo, g.log.committed + 1, [&](const Ent& x) { arena_entry(n, x); });
-      r.n_committed = n->r_ents.size() - n->r_off.back();
-      n->r_off.push_back(n->r_msgs.size());  // Messages = r.msgs, then cleared (raft/multinode.go:277-281)
-      for (Msg& m : g.msgs) {
-        hbn_message x;
-        std::memset(&x, 0, sizeof(x));
-        x.type = m.type;
-        x.reject = m.reject;
-        x.to = m.to;
-        x.from = m.from;
-        x.term = m.term;
-        x.log_term = m.log_term;
-        x.index = m.index;
-        x.commit = m.commit;
-        x.reject_hint = m.reject_hint;
-        const size_t e0 = n->r_ents.size();
-        if (m.owned)
-          for (const Ent& e : m.entries) arena_entry(n, e);
-        else if (m.ent_hi > m.ent_lo)
-          g.log.visit(m.ent_lo, m.ent_hi, [&](const Ent& e) { arena_entry(n, e); });
-        x.n_entries = n->r_ents.size() - e0;
-        x.entries = reinterpret_cast<const hbn_entry*>(e0);  // offset, patched below
-        if (m.has_snap) {
-          n->r_snaps.push_back(m.snap);
-          snap_view(n->r_snaps.back(), &x.snapshot);
-        }
-        n->r_msgs.push_back(x);
-      }
-      r.n_messages = g.msgs.size();
-      g.msgs.clear();
-      r.fault = g.fault;
-      g.delivered = true;
-      n->delivered.push_back(&g);
-      n->r_out.push_back(r);
-    }
+    // newReady for every touched group, workers over disjoint ranges of them
+    const size_t nt = n->touched.size();
+    const unsigned k = nt < 4096 ? 1 : n->pool->size();
+    auto build0 = std::chrono::steady_clock::now();
+    n->pool->run(
+        [&](unsigned t) {
+          size_t lo, hi;
+          split(nt, k, t, &lo, &hi);
+          Arena& A = n->arenas[t];
+          for (size_t i = lo; i < hi; ++i) build_ready(*n->touched[i], A, n->lists[t]);
+          patch_arena(A);
+        },
+        k);
     n->touched.clear();
-    if (n->r_out.empty()) {
+    n->prof[PH_BUILD] += std::chrono::duration<double>(std::chrono::steady_clock::now() - build0).count();
+    HBN_PHASE(n, PH_MERGE);
+    merge(n->content, n->lists, &Lists::content);
+    merge(n->delivered, n->lists, &Lists::delivered);
+    size_t tot = 0;
+    for (const Arena& A : n->arenas) tot += A.out.size();
+    if (tot == 0) {
       rc = HBN_EAGAIN;
       return;
     }
-    // patch the arena pointers now that no vector grows any more
-    for (size_t i = 0; i < n->r_ents.size(); ++i)
-      if (n->r_ents[i].data_len) n->r_ents[i].data = n->r_bytes.data() + n->r_ent_off[i];
-    for (hbn_message& x : n->r_msgs)
-      x.entries = x.n_entries ? n->r_ents.data() + reinterpret_cast<uintptr_t>(x.entries) : nullptr;
-    for (size_t i = 0; i < n->r_out.size(); ++i) {
-      hbn_group_ready& r = n->r_out[i];
-      r.entries = r.n_entries ? n->r_ents.data() + n->r_off[3 * i] : nullptr;
-      r.committed_entries = r.n_committed ? n->r_ents.data() + n->r_off[3 * i + 1] : nullptr;
-      r.messages = r.n_messages ? n->r_msgs.data() + n->r_off[3 * i + 2] : nullptr;
-    }
+    n->r_out.reserve(tot);
+    for (const Arena& A : n->arenas) n->r_out.insert(n->r_out.end(), A.out.begin(), A.out.end());
     n->awaiting_advance = true;
   });
   if (g0 != HB_OK) return g0;
@@ -1959,17 +2461,28 @@ int hbn_advance(hbn_node* n, const uint64_t* groups, uint64_t count) {
   if (!n || (count && !groups)) return HB_EINVAL;
   return guarded([&] {
     flush(n);
-    for (uint64_t i = 0; i < count; ++i) {
-      auto it = n->groups.find(groups[i]);
-      if (it == n->groups.end() || !it->second->delivered) continue;
-      Group& g = *it->second;
-      g.delivered = false;
-      materialize(g);  // messages stepped since the Ready still read the log
-      commit_ready(g, g.dlv);
-      // the recomputed Ready (raft/multinode.go:290-295) is a candidate again
-      refresh_content(n, g);
-      touch(n, g);
-    }
+    HBN_PHASE(n, PH_ADVANCE);
+    const unsigned k = count < 4096 ? 1 : n->pool->size();
+    n->pool->run(
+        [&](unsigned t) {
+          size_t lo, hi;
+          split(count, k, t, &lo, &hi);
+          Lists& L = n->lists[t];
+          for (size_t i = lo; i < hi; ++i) {
+            auto it = n->groups.find(groups[i]);
+            if (it == n->groups.end()) continue;
+            Group& g = *it->second;
+            if (!__atomic_exchange_n(&g.delivered, false, __ATOMIC_RELAXED)) continue;  // (a group listed twice)
+            materialize(g);  // messages stepped since the Ready still read the log
+            commit_ready(g, g.dlv);
+            // the recomputed Ready (raft/multinode.go:290-295) is a candidate again
+            refresh_content(L.content, g);
+            touch_into(L.touched, g);
+          }
+        },
+        k);
+    merge(n->content, n->lists, &Lists::content);
+    merge(n->touched, n->lists, &Lists::touched);
     n->awaiting_advance = false;
   });
 }

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "../../include/hbnode.h"
@@ -25,13 +26,31 @@ extern "C" {
 
 // out[0] timed seconds, [1] MsgAppResp stepped, [2] commit advances (groups x rounds),
 // [3] seconds in hbn_ready, [4] seconds in hbn_step/hbn_propose, [5] seconds in
-// storage append + hbn_advance, [6] entries committed seen in Ready, [7] faults.
+// storage append + hbn_advance, [6] entries committed seen in Ready, [7] faults,
+// [8 .. 8 + 16) the node's host phase seconds over the timed rounds (hbn_profile).
+// flags: HBNB_BULK = the round's acks and proposals through hbn_step_many /
+// hbn_propose_many (one call each) instead of one call per message;
+// HBNB_PAR_APP = the application persists a Ready's entries to the groups'
+// storages from `threads` threads (storages are independent).  threads: the
+// node's host threads too (hbn_set_threads; 0 = the library default).
+#define HBNB_BULK 1u
+#define HBNB_PAR_APP 2u
+int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t rounds, uint32_t flags,
+              uint32_t threads, double* out);
 int hbnb_run(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t rounds, double* out) {
+  return hbnb_run2(device, G, n, warmup, rounds, 0, 0, out);
+}
+
+int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t rounds, uint32_t flags,
+              uint32_t threads, double* out) {
   if (G == 0 || n < 2 || n > HB_MAX_REPLICAS || !out) return HB_EINVAL;
   hbn_node* mn = nullptr;
   const uint64_t max_batch = (uint64_t)G * n + 16;
   int rc = hbn_start(device, 1, G, n, 256, HB_NO_LIMIT, max_batch, &mn);
   if (rc) return rc;
+  if (threads) rc = hbn_set_threads(mn, threads);
+  const uint32_t app_threads =
+      (flags & HBNB_PAR_APP) ? (threads ? threads : std::min(16u, std::max(1u, std::thread::hardware_concurrency()))) : 1;
   std::vector<hbn_storage*> st(G, nullptr);
   std::vector<uint64_t> peers(n), last(G, 0), commit(G, 0), ids(G);
   for (uint32_t i = 0; i < n; ++i) peers[i] = i + 1;
@@ -64,21 +83,42 @@ int hbnb_run(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t round
     if (r == HBN_EAGAIN) return 0;
     if (r) return r;
     std::vector<uint64_t> adv(cnt);
-    for (uint64_t i = 0; i < cnt; ++i) {
-      const hbn_group_ready& rd = rds[i];
-      const uint64_t g = rd.group - 1;
-      faults += rd.fault != 0;
-      if (rd.n_entries) {
-        r = hbn_storage_append(st[g], rd.entries, rd.n_entries);
-        if (r) return r;
-        last[g] = rd.entries[rd.n_entries - 1].index;
+    // the application's part: persist each group's entries (MemoryStorage.Append)
+    auto persist = [&](uint64_t lo, uint64_t hi, uint64_t* f, uint64_t* ce, uint64_t* av) -> int {
+      for (uint64_t i = lo; i < hi; ++i) {
+        const hbn_group_ready& rd = rds[i];
+        const uint64_t g = rd.group - 1;
+        *f += rd.fault != 0;
+        if (rd.n_entries) {
+          const int e = hbn_storage_append(st[g], rd.entries, rd.n_entries);
+          if (e) return e;
+          last[g] = rd.entries[rd.n_entries - 1].index;
+        }
+        *ce += rd.n_committed;
+        if (rd.hard_state.commit > commit[g]) {
+          commit[g] = rd.hard_state.commit;
+          ++*av;
+        }
+        adv[i] = rd.group;
       }
-      committed_entries += rd.n_committed;
-      if (rd.hard_state.commit > commit[g]) {
-        commit[g] = rd.hard_state.commit;
-        ++advances;
+      return 0;
+    };
+    if (app_threads > 1 && cnt >= 4096) {
+      std::vector<uint64_t> f(app_threads), ce(app_threads), av(app_threads);
+      std::vector<int> er(app_threads);
+      std::vector<std::thread> th;
+      for (uint32_t t = 0; t < app_threads; ++t)
+        th.emplace_back([&, t] { er[t] = persist(cnt * t / app_threads, cnt * (t + 1) / app_threads, &f[t], &ce[t], &av[t]); });
+      for (auto& x : th) x.join();
+      for (uint32_t t = 0; t < app_threads; ++t) {
+        if (er[t]) return er[t];
+        faults += f[t];
+        committed_entries += ce[t];
+        advances += av[t];
       }
-      adv[i] = rd.group;
+    } else {
+      r = persist(0, cnt, &faults, &committed_entries, &advances);
+      if (r) return r;
     }
     r = hbn_advance(mn, adv.data(), cnt);
     t_adv += secs(b, clk::now());
@@ -92,8 +132,13 @@ int hbnb_run(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t round
   std::shuffle(order.begin(), order.end(), rng);
   m.type = HB_MSG_APP_RESP;
   static const uint8_t foo[3] = {'f', 'o', 'o'};
+  std::vector<uint64_t> bg(order.size());
+  std::vector<hbn_message> bm(order.size());
+  std::vector<const uint8_t*> pdata(G, foo);
+  std::vector<uint64_t> plen(G, 3);
   auto t0 = clk::now();
   uint64_t acks = 0;
+  double prof0[16] = {}, prof1[16] = {};
   for (uint32_t r = 0; r < warmup + rounds && !rc; ++r) {
     if (r == warmup) {
       t0 = clk::now();
@@ -101,16 +146,31 @@ int hbnb_run(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t round
       advances = 0;
       committed_entries = 0;
       t_ready = t_step = t_adv = 0;
+      hbn_profile(mn, prof0, 16, nullptr);
     }
     auto a = clk::now();
-    for (size_t i = 0; i < order.size() && !rc; ++i) {  // followers ack the last round's entries
-      const uint64_t g = order[i] / (n - 1);
-      m.from = 2 + order[i] % (n - 1);
-      m.index = last[g];
-      rc = hbn_step(mn, ids[g], &m);
-      ++acks;
+    if (flags & HBNB_BULK) {  // the round's network input and proposals, one call each
+      for (size_t i = 0; i < order.size(); ++i) {
+        const uint64_t g = order[i] / (n - 1);
+        bg[i] = ids[g];
+        bm[i] = m;
+        bm[i].from = 2 + order[i] % (n - 1);
+        bm[i].index = last[g];
+      }
+      uint64_t done = 0;
+      rc = hbn_step_many(mn, order.size(), bg.data(), bm.data(), &done);
+      acks += done;
+      if (!rc) rc = hbn_propose_many(mn, G, ids.data(), pdata.data(), plen.data(), &done);
+    } else {
+      for (size_t i = 0; i < order.size() && !rc; ++i) {  // followers ack the last round's entries
+        const uint64_t g = order[i] / (n - 1);
+        m.from = 2 + order[i] % (n - 1);
+        m.index = last[g];
+        rc = hbn_step(mn, ids[g], &m);
+        ++acks;
+      }
+      for (uint32_t g = 0; g < G && !rc; ++g) rc = hbn_propose(mn, ids[g], foo, 3);
     }
-    for (uint32_t g = 0; g < G && !rc; ++g) rc = hbn_propose(mn, ids[g], foo, 3);
     t_step += secs(a, clk::now());
     if (!rc) rc = cycle();
     if (G >= 100000) {  // progress for long runs
@@ -119,6 +179,8 @@ int hbnb_run(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t round
     }
   }
   const double total = secs(t0, clk::now());
+  hbn_profile(mn, prof1, 16, nullptr);
+  for (int i = 0; i < 16; ++i) out[8 + i] = prof1[i] - prof0[i];
   out[0] = total;
   out[1] = (double)acks;
   out[2] = (double)advances;

@@ -1968,7 +1968,7 @@ __global__ void __launch_bounds__(256) k_expand_events(const uint64_t* base, con
         while (m) {
           const uint32_t s = __ffs(m) - 1;
           m &= m - 1;
-          o[r++] = hb_event{x, group, (uint8_t)HB_EV_APP, (uint8_t)s, 0};
+          o[r++] = hb_event{x, group, (uint8_t)HB_EV_APP, (uint8_t)s, (uint16_t)aux};
         }
       } else {
         o[0] = hb_event{x, group, (uint8_t)type, (uint8_t)to, (uint16_t)aux};
@@ -3258,7 +3258,7 @@ int hb_expand_event_words(const uint64_t* words, uint64_t n_words, const uint32_
       if (type == EVC_BCAST) {
         for (uint32_t s = 0; s < 7; ++s)
           if ((to >> s) & 1u) {
-            if (out && k < cap) out[k] = hb_event{x, group, (uint8_t)HB_EV_APP, (uint8_t)s, 0};
+            if (out && k < cap) out[k] = hb_event{x, group, (uint8_t)HB_EV_APP, (uint8_t)s, (uint16_t)aux};
             ++k;
           }
       } else {

@@ -218,11 +218,12 @@ struct ElectLane {
     // rlast + 1 <= last: MsgApp{Index = rlast} and pause
     if (bcast) {  // one EVC_BCAST word for two or more sends (the same records once expanded)
       const uint32_t mask = ((1u << nn) - 1) & ~(1u << sf);
+      const uint32_t lt = (tfirst <= rlast && rlast <= tlast) ? 1u : 0u;  // aux: term(Index) == Term
       if (mask & (mask - 1)) {
-        emit_ev(E, g & (PART - 1), EVC_BCAST, mask, 0, rlast);
+        emit_ev(E, g & (PART - 1), EVC_BCAST, mask, lt, rlast);
         nev += __popc(mask);
       } else if (mask) {
-        ev(HB_EV_APP, __ffs(mask) - 1, 0, rlast);
+        ev(HB_EV_APP, __ffs(mask) - 1, lt, rlast);
       }
       sent = true;
     }

@@ -184,6 +184,9 @@ struct FastLane {
     set_pm(s, pm_make(pm_state(p), pm_paused(p), idx, cnt - i));
     head[s] = v;
   }
+  // an HB_EV_APP's aux: the entry at x (the MsgApp's Index) has the current Term
+  // (m.LogTerm == m.Term), so the host need not look it up
+  __device__ __forceinline__ uint32_t lt_cur(uint64_t x) const { return (tfirst <= x && x <= tlast) ? 1u : 0u; }
   // raftLog.term(i) == Term over the current-term run (raft/log.go:198-217)
   __device__ __forceinline__ bool term_eq(uint64_t i) const {
     if (i + 1 < first || i > last) return term == 0;
@@ -271,7 +274,7 @@ struct FastLane {
   __device__ __forceinline__ void send_append(int s) {
     uint64_t x = 0;
     const uint32_t k = send_decide(s, &x);
-    if (k != SEND_NONE) ev(k == SEND_APP ? HB_EV_APP : HB_EV_SNAP, s, 0, x);
+    if (k != SEND_NONE) ev(k == SEND_APP ? HB_EV_APP : HB_EV_SNAP, s, k == SEND_APP ? lt_cur(x) : 0u, x);
   }
   // bcastAppend raft/raft.go:303-310 (slot order, self skipped).  When every
   // message it sends is a MsgApp with the same Index (steady state), the sends
@@ -297,13 +300,14 @@ struct FastLane {
     }
     if (mask == 0) return;
     if (same && (mask & (mask - 1))) {
-      emit_ev(E, g & (PART - 1), EVC_BCAST, mask, 0, x0);
+      emit_ev(E, g & (PART - 1), EVC_BCAST, mask, lt_cur(x0), x0);
       nev += __popc(mask);
       return;
     }
 #pragma unroll
     for (int s = 0; s < NMAX; ++s)
-      if (kind[s] != SEND_NONE) ev(kind[s] == SEND_APP ? HB_EV_APP : HB_EV_SNAP, s, 0, xs[s]);
+      if (kind[s] != SEND_NONE)
+        ev(kind[s] == SEND_APP ? HB_EV_APP : HB_EV_SNAP, s, kind[s] == SEND_APP ? lt_cur(xs[s]) : 0u, xs[s]);
   }
 
   // ---- preconditions (checked per message by the kernel)

@@ -654,7 +654,7 @@ struct Lane {
         p.pm |= PM_PAUSED;                              // pause
       }
     }
-    ev(HB_EV_APP, s, 0, x);
+    ev(HB_EV_APP, s, (tfirst <= x && x <= tlast) ? 1u : 0u, x);  // aux: term(x) == Term (m.LogTerm)
   }
 
   // ---------------------------------------------------------------- transitions

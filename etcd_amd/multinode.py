@@ -204,6 +204,10 @@ def lib():
             "hbn_propose": (C.c_int, [vp, u64, vp, u64]),
             "hbn_propose_conf_change": (C.c_int, [vp, u64, u64, u32, u64, vp, u64]),
             "hbn_step": (C.c_int, [vp, u64, P(hbn_message)]),
+            "hbn_step_many": (C.c_int, [vp, u64, P(u64), P(hbn_message), P(u64)]),
+            "hbn_propose_many": (C.c_int, [vp, u64, P(u64), P(vp), P(u64), P(u64)]),
+            "hbn_set_threads": (C.c_int, [vp, u32]),
+            "hbn_profile": (C.c_int, [vp, P(C.c_double), u32, P(u32)]),
             "hbn_report_unreachable": (C.c_int, [vp, u64, u64]),
             "hbn_report_snapshot": (C.c_int, [vp, u64, u64, C.c_int]),
             "hbn_apply_conf_change": (C.c_int, [vp, u64, u32, u64, P(u64), P(u32)]),
@@ -438,6 +442,40 @@ class MultiNode:
         cm.entries, cm.n_entries = ents.arr, ents.n
         cm.snapshot, keep = _snap_in(m.Snapshot)
         _check("hbn_step", lib().hbn_step(self.p, group, C.byref(cm)))
+
+    def StepMany(self, items):
+        """[(group, Message), ...] in order through hbn_step_many (one call);
+        returns how many were taken (all of them unless it raises)."""
+        n = len(items)
+        gs = (C.c_uint64 * max(1, n))(*[g for g, _ in items])
+        arr = (hbn_message * max(1, n))()
+        keep = []
+        for i, (_, m) in enumerate(items):
+            ents = _EntryArray(m.Entries)
+            cm = arr[i]
+            cm.type, cm.reject, cm.to, cm.from_ = m.Type, int(m.Reject), m.To, m.From
+            cm.term, cm.log_term, cm.index, cm.commit, cm.reject_hint = m.Term, m.LogTerm, m.Index, m.Commit, \
+                m.RejectHint
+            cm.entries, cm.n_entries = ents.arr, ents.n
+            cm.snapshot, k = _snap_in(m.Snapshot)
+            keep.append((ents, k))
+        done = C.c_uint64()
+        _check("hbn_step_many", lib().hbn_step_many(self.p, n, gs, arr, C.byref(done)))
+        return done.value
+
+    def ProposeMany(self, items):
+        """[(group, data or None), ...] in order through hbn_propose_many."""
+        n = len(items)
+        gs = (C.c_uint64 * max(1, n))(*[g for g, _ in items])
+        bufs = [C.create_string_buffer(bytes(d), max(1, len(d))) if d is not None else None for _, d in items]
+        ptrs = (C.c_void_p * max(1, n))(*[C.cast(b, C.c_void_p).value if b is not None else None for b in bufs])
+        lens = (C.c_uint64 * max(1, n))(*[len(d or b"") for _, d in items])
+        done = C.c_uint64()
+        _check("hbn_propose_many", lib().hbn_propose_many(self.p, n, gs, ptrs, lens, C.byref(done)))
+        return done.value
+
+    def SetThreads(self, k):
+        _check("hbn_set_threads", lib().hbn_set_threads(self.p, k))
 
     def ReportUnreachable(self, id, group):
         _check("hbn_report_unreachable", lib().hbn_report_unreachable(self.p, id, group))

@@ -164,8 +164,9 @@ uint64_t hbn_entry_size(const hbn_entry* e);
 /* ---- MultiNode (raft/multinode.go:12-49) ---------------------------------- */
 /* StartMultiNode(id) on `device`: up to `capacity` groups of <= max_replicas
  * peers, Config.MaxInflightMsgs = max_inflight, MaxSizePerMsg = max_msg_size
- * (HB_NO_LIMIT or 0), at most max_batch messages per device step (the batch
- * is flushed early when it fills). */
+ * (any value: HB_NO_LIMIT, 0 or finite; the device's log index then holds
+ * every entry's size, loaded and reserved by this library), at most max_batch
+ * messages per device step (the batch is flushed early when it fills). */
 int hbn_start(int device, uint64_t id, uint32_t capacity, uint32_t max_replicas, uint32_t max_inflight,
               uint64_t max_msg_size, uint64_t max_batch, hbn_node** out);
 int hbn_stop(hbn_node* n);
@@ -189,6 +190,27 @@ int hbn_propose_conf_change(hbn_node* n, uint64_t group, uint64_t cc_id, uint32_
  * MsgVote) go to the device batch.  A MsgSnap whose ConfState differs from the
  * group's peers ends the batch (the restore reloads the group's prs). */
 int hbn_step(hbn_node* n, uint64_t group, const hbn_message* m);
+/* Bulk ingestion: exactly count calls of hbn_step(n, groups[i], &msgs[i]) /
+ * hbn_propose(n, groups[i], data[i], len[i]) in order (data[i] NULL = nil
+ * Data), in one call.  The reference hands each message to its run goroutine
+ * over a channel (raft/multinode.go:401-415), and a cgo call costs ~100 ns, so
+ * a binding collects a Ready cycle's network input and proposals and passes
+ * them together; responses and proposals are laid into the device batch by the
+ * node's host threads.  On an error, *done = the messages taken before the one
+ * that failed (its error is returned, as hbn_step would). */
+int hbn_step_many(hbn_node* n, uint64_t count, const uint64_t* groups, const hbn_message* msgs, uint64_t* done);
+int hbn_propose_many(hbn_node* n, uint64_t count, const uint64_t* groups, const uint8_t* const* data,
+                     const uint64_t* len, uint64_t* done);
+/* Host threads for the per-group work of a Ready cycle (event replay, Ready
+ * assembly, Advance, bulk ingestion); groups are independent, each worker owns
+ * a disjoint set.  Default min(16, cores), or the HBN_THREADS environment
+ * variable.  The calling thread is one of them. */
+int hbn_set_threads(hbn_node* n, uint32_t threads);
+/* Seconds the node's host side spent per phase since hbn_start (diagnostics;
+ * out[0..min(cap, *count)), order: load sync, log-index reserve, hb_step call,
+ * event fetch, event replay, stepped marks, Ready assembly, Ready merge,
+ * Advance, bulk lookup, bulk responses, bulk proposals, batch reset). */
+int hbn_profile(hbn_node* n, double* out, uint32_t cap, uint32_t* count);
 int hbn_report_unreachable(hbn_node* n, uint64_t id, uint64_t group);           /* :461-469 */
 int hbn_report_snapshot(hbn_node* n, uint64_t id, uint64_t group, int failure); /* :471-481 */
 /* ApplyConfChange (:401-430, run :239-262): node_id 0 only resets pendingConf.

@@ -250,7 +250,9 @@ typedef struct hb_group {
  *                   the current lastIndex (max_msg_size noLimit), x+1
  *                   (max_msg_size 0), or limitSize's cut of (x, lastIndex]
  *                   (finite max_msg_size); none if x+1 > lastIndex.  m.Commit =
- *                   current committed, m.Term = current term, m.LogTerm = term(x).
+ *                   current committed, m.Term = current term, m.LogTerm = term(x);
+ *                   aux = 1 when term(x) == m.Term (the host then needs no log
+ *                   lookup for LogTerm), else 0.
  *                   (raft.sendAppend, raft/raft.go:261-281)
  *   HB_EV_SNAP      to, x = snapshot index         (raft/raft.go:246-260)
  *   HB_EV_HEARTBEAT to, x = m.Commit              (raft.sendHeartbeat, raft/raft.go:285-299)
@@ -501,7 +503,7 @@ int  hb_step(hb_handle* h, const hb_batch* b, uint32_t flags);
  * at base + chunk_off[c].  A group's events are its words in chunk 2p, then
  * in chunk 2p+1, each in order.  Word format (bit ranges):
  *   [0:4)   type: HB_EV_*; 12 = an HB_EV_APP to every slot of the mask in
- *           `to` (same x, aux 0), in slot order; 15 = continuation word
+ *           `to` (same x and aux), in slot order; 15 = continuation word
  *   [4:11)  to (slot / node ref), or the slot mask of type 12
  *   [11]    x needs 64 bits: the next word is a continuation holding
  *           x bits 40..63 in its bits [4:28)

@@ -325,7 +325,7 @@ static void send(orc_raft* r, orc_msg m) {                /* send raft/raft.go:2
   r->msgs[r->nmsgs++] = m;
   int to = (int)orc_raft_ref(r, m.to);
   switch (m.type) {
-    case HB_MSG_APP: emit(r, HB_EV_APP, to, m.index, 0); break;
+    case HB_MSG_APP: emit(r, HB_EV_APP, to, m.index, m.log_term == r->term ? 1 : 0); break;  /* aux: LogTerm == Term */
     case HB_MSG_SNAP: emit(r, HB_EV_SNAP, to, m.snap_index, 0); break;
     case HB_MSG_HEARTBEAT: emit(r, HB_EV_HEARTBEAT, to, m.commit, 0); break;
     case HB_MSG_VOTE: emit(r, HB_EV_VOTE, to, m.index, 0); break;

@@ -12,7 +12,7 @@ from etcd_amd import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 FIXTURES = sorted(glob.glob(os.path.join(HERE, "golden", "*.npz")))
-BATCH_KEYS = ("group", "info", "term", "index", "hint", "props")
+BATCH_KEYS = ("group", "info", "term", "index", "hint", "props", "edesc", "eoff", "peoff", "commit", "eterm")
 
 
 def load(path):
@@ -34,20 +34,31 @@ def ins_of(d):
     return out
 
 
+def unflat(d, key, width):
+    if f"{key}_gs" not in d:
+        return None
+    out, o = {}, 0
+    for g, n in zip(d[f"{key}_gs"].tolist(), d[f"{key}_n"].tolist()):
+        v = d[f"{key}_vals"][o:o + n * width]
+        out[g] = v.tolist() if width == 1 else [tuple(x) for x in v.reshape(-1, 2).tolist()]
+        o += n * width
+    return out
+
+
 def test_fixtures_present():
     names = {os.path.basename(p) for p in FIXTURES}
-    assert {"cfg2_n3.npz", "cfg2_n5.npz", "storm_n7.npz", "fuzz_n5.npz"} <= names
+    assert {"cfg2_n3.npz", "cfg2_n5.npz", "storm_n7.npz", "fuzz_n5.npz", "sized_n3.npz",
+            "follower_n3.npz"} <= names
 
 
 @pytest.mark.parametrize("path", FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
 def test_oracle_reproduces_golden(path):
-    from tests.golden.make_golden import cases
+    from tests.golden.make_golden import cases, oracle_for
     name = os.path.basename(path)[:-4]
     case = next(c for c in cases() if c[0] == name)
     want = load(path)
-    from oracle.pyoracle import OracleGroups
-    _, nmax, W, groups, runs, ins, batches = case
-    og = OracleGroups(groups, runs, W, abi.HB_NO_LIMIT, ins)
+    _, nmax, W, groups, runs, ins, batches, extra = case
+    og = oracle_for(groups, runs, W, ins, extra)
     assert np.array_equal(og.groups(), want["init"])
     for k, b in enumerate(batches):
         ev, st = og.step(b)
@@ -63,8 +74,16 @@ def test_engine_reproduces_golden(path):
     from etcd_amd.hipbatch import Engine
     d = load(path)
     init = d["init"]
-    eng = Engine(len(init), max_replicas=int(d["nmax"]), max_inflight=int(d["W"]), max_batch=1 << 14)
+    eng = Engine(len(init), max_replicas=int(d["nmax"]), max_inflight=int(d["W"]),
+                 max_msg_size=int(d["max_msg_size"]), max_batch=1 << 14)
     eng.load_groups(init)
+    if unflat(d, "sz", 1):
+        eng.load_entry_sizes(unflat(d, "sz", 1))
+    if unflat(d, "tr", 2):
+        eng.load_term_runs(unflat(d, "tr", 2))
+    # the log index covers every group's log and anything a fixture step appends
+    sized = int(d["max_msg_size"]) not in (0, abi.HB_NO_LIMIT)
+    eng.reserve_log(np.arange(len(init), dtype=np.uint32), 4096 if sized else None, 256)
     for (g, s), vals in (ins_of(d) or {}).items():
         eng.set_inflights(g, s, int(init[g]["pr"][s]["ins_start"]), vals)
     name = os.path.basename(path)[:-4]

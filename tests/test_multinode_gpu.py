@@ -476,3 +476,96 @@ def test_max_size_per_msg_cuts_msgapp_entries():
     st = mn.Status(1)
     assert st.Progress[2].match == 3 + len(payloads)
     mn.Stop()
+
+
+# ---------------------------------------------------------------- bulk ingestion + host threads
+def test_bulk_and_threaded_ready_equal_per_call():
+    """hbn_step_many / hbn_propose_many with the node's host threads (event
+    replay, Ready assembly and Advance split over workers by group) produce the
+    same Ready as one hbn_step / hbn_propose call per message on one thread, on
+    every cycle: 6,000 groups (above the parallel thresholds), shuffled acks,
+    heartbeat responses, stale and rejected acks, and local / lower-term
+    messages that take the single-message path inside the bulk call."""
+    import random
+    G, ids = 6000, [1, 2, 3]
+    a = StartMultiNode(1, capacity=G + 8, max_batch=1 << 16)
+    b = StartMultiNode(1, capacity=G + 8, max_batch=1 << 16)
+    a.SetThreads(8)
+    b.SetThreads(1)
+    sa = {g: MemoryStorage() for g in range(1, G + 1)}
+    sb = {g: MemoryStorage() for g in range(1, G + 1)}
+    for g in range(1, G + 1):
+        a.CreateGroup(g, Config(10, 1), sa[g], peers=ids)
+        b.CreateGroup(g, Config(10, 1), sb[g], peers=ids)
+
+    def cycle():
+        ra, rb = a.Ready(), b.Ready()
+        assert ra == rb
+        for mn, st, rds in ((a, sa, ra), (b, sb, rb)):
+            for g, rd in rds.items():
+                st[g].Append(rd.Entries)
+            mn.Advance(rds)
+        return ra
+    cycle()
+    for g in range(1, G + 1):
+        a.Campaign(g)
+        b.Campaign(g)
+    cycle()
+    votes = [(g, Message(Type=abi.HB_MSG_VOTE_RESP, From=f, To=1, Term=2)) for g in range(1, G + 1) for f in (2, 3)]
+    assert a.StepMany(votes) == len(votes)
+    for g, m in votes:
+        b.Step(g, m)
+    cycle()
+    rng = random.Random(5)
+    for r in range(4):
+        props = [(g, b"r%d-%d" % (r, g) if rng.random() < 0.9 else None) for g in range(1, G + 1) if rng.random() < 0.8]
+        assert a.ProposeMany(props) == len(props)
+        for g, d in props:
+            b.Propose(g, d)
+        rd = cycle()
+        msgs = []
+        for g in range(1, G + 1):
+            last = sa[g].LastIndex()
+            for f in (2, 3):
+                u = rng.random()
+                if u < 0.7:
+                    msgs.append((g, Message(Type=abi.HB_MSG_APP_RESP, From=f, To=1, Term=2, Index=last)))
+                elif u < 0.8:
+                    msgs.append((g, Message(Type=abi.HB_MSG_HEARTBEAT_RESP, From=f, To=1, Term=2)))
+                elif u < 0.88:
+                    msgs.append((g, Message(Type=abi.HB_MSG_APP_RESP, From=f, To=1, Term=2, Index=last - 1,
+                                            Reject=True, RejectHint=last - 2)))
+                elif u < 0.94:
+                    msgs.append((g, Message(Type=abi.HB_MSG_APP_RESP, From=f, To=1, Term=1, Index=1)))  # lower term
+                else:
+                    msgs.append((g, Message(Type=abi.HB_MSG_BEAT, From=f, To=1)))  # local: ignored by Step
+        rng.shuffle(msgs)
+        assert a.StepMany(msgs) == len(msgs)
+        for g, m in msgs:
+            b.Step(g, m)
+        cycle()
+    def st(mn, g):
+        x = mn.Status(g)
+        return (x.HardState, x.SoftState, x.Applied,
+                {k: (p.match, p.next, p.state, p.paused, p.ins_count) for k, p in x.Progress.items()})
+    for g in rng.sample(range(1, G + 1), 50):
+        assert st(a, g) == st(b, g)
+    a.Stop()
+    b.Stop()
+
+
+def test_bulk_step_stops_at_the_first_error():
+    """hbn_step_many reports the messages it took before an error, as the same
+    sequence of hbn_step calls would have stopped: a message for a missing
+    group raises ENOGROUP and nothing after it is taken."""
+    from etcd_amd.multinode import HbnError
+    mn = StartMultiNode(1, capacity=16)
+    s = MemoryStorage()
+    mn.CreateGroup(1, Config(10, 1), s, peers=[1, 2, 3])
+    items = [(1, Message(Type=abi.HB_MSG_VOTE_RESP, From=2, To=1, Term=1))] * 3 + \
+            [(99, Message(Type=abi.HB_MSG_VOTE_RESP, From=2, To=1, Term=1))] + \
+            [(1, Message(Type=abi.HB_MSG_VOTE_RESP, From=3, To=1, Term=1))]
+    with pytest.raises(HbnError) as ei:
+        mn.StepMany(items)
+    assert "hbn_step_many" in str(ei.value)
+    mn.Stop()
