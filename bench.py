@@ -349,6 +349,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
                     help="shards of the parallel best-case CPU baseline (the GPU box's share is 16 cores)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-phase HIP events")
+    ap.add_argument("--e2e-events", choices=["words", "records"], default="words",
+                    help="e2e: delta list D2H as compact event words (default) or 16-byte hb_event records")
     ap.add_argument("--overlap", action="store_true",
                     help="batch inputs on their own stream: the prep stage of step k+1 (bucket sort + routing) "
                          "overlaps the apply stage of step k (hb_set_input_stream); default: stages serialized")
@@ -616,10 +618,15 @@ def run_e2e(args, world, rank, local, dev, torch, dist):
     """cfg2 end to end (SURVEY.md 7 "End-to-end vs kernel"; reported apart from
     the HBM-resident headline): every step's batch starts in pinned host memory
     (hb_step with HB_STEP_HOST_PTRS copies group / info / term / index and the
-    dense props to the device) and the step's events come back to pinned host
-    memory as public hb_event records (hb_copy_events), i.e. what a host
-    MultiNode hands over and gets back per Ready cycle.  Wall clock per step,
-    synchronised."""
+    dense props to the device) and the step's delta list comes back to pinned
+    host memory, i.e. what a host MultiNode hands over and gets back per Ready
+    cycle.  The delta list is the device's compact event words
+    (hb_events_to_host: 8 B per word, one word per bcastAppend, SURVEY.md 8(a)
+    a12), which libhbnode replays directly; `--e2e-events records` ships the
+    expanded 16-byte hb_event records instead (hb_copy_events), and the words'
+    host expansion (hb_expand_event_words) is timed apart as
+    `host_expand_ms_per_step` for a consumer that wants records.  Wall clock
+    per step, synchronised."""
     from etcd_amd import abi
     from etcd_amd.hipbatch import Engine
     n = args.replicas
@@ -629,6 +636,7 @@ def run_e2e(args, world, rank, local, dev, torch, dist):
     stream = torch.cuda.current_stream(dev)
     eng = Engine(G, max_replicas=n, max_inflight=256, max_batch=nmsg, device=local, stream=stream)
     eng.load_groups(groups)
+    words_mode = args.e2e_events == "words"
 
     def pinned(a):
         t = torch.from_numpy(np.ascontiguousarray(a).view({4: np.int32, 8: np.int64}[a.dtype.itemsize]))
@@ -637,53 +645,79 @@ def run_e2e(args, world, rank, local, dev, torch, dist):
     total = args.warmup + args.steps
     h_index = [pinned(batch["index"] + np.uint64(k)) for k in range(total)]
     ev_cap = G * (2 * n + 4)
-    h_ev = torch.empty(ev_cap * abi.EVENT_DTYPE.itemsize, dtype=torch.uint8).pin_memory()
+    nchunks, _ = eng.n_chunks()
+    if words_mode:
+        h_w = torch.empty(ev_cap, dtype=torch.int64).pin_memory()
+        h_cnt = torch.empty(nchunks, dtype=torch.int32).pin_memory()
+        h_tot = torch.zeros(1, dtype=torch.int64).pin_memory()
+    else:
+        h_ev = torch.empty(ev_cap * abi.EVENT_DTYPE.itemsize, dtype=torch.uint8).pin_memory()
     torch.cuda.synchronize()
     st_acc = np.zeros(abi.HB_STAT_COUNT, np.uint64)
-    nev_total = 0
+    nev_total = nword_total = 0
     t_step = t_ev = 0.0
     for k in range(total):
         if k == args.warmup:
             if world > 1:
                 dist.barrier()
             st_acc[:] = 0
-            nev_total = 0
+            nev_total = nword_total = 0
             t_step = t_ev = 0.0
         t0 = time.perf_counter()
         eng.step(h_group, h_info, h_term, h_index[k], None, h_props, host=True)
-        eng.sync()
-        t1 = time.perf_counter()
-        nev = eng.events_into(h_ev.data_ptr(), ev_cap)
-        t2 = time.perf_counter()
+        if words_mode:  # the words ride the same stream: one sync for step + delta
+            eng.events_to_host(h_w.data_ptr(), ev_cap, h_cnt.data_ptr(), h_tot.data_ptr())
+            eng.sync()
+            t1 = t2 = time.perf_counter()
+            nw = int(h_tot[0])
+            assert nw <= ev_cap
+            nword_total += nw
+        else:
+            eng.sync()
+            t1 = time.perf_counter()
+            nev_total += eng.events_into(h_ev.data_ptr(), ev_cap)
+            t2 = time.perf_counter()
         t_step += t1 - t0
         t_ev += t2 - t1
-        nev_total += nev
         st_acc += eng.stats()
     sec_t = torch.tensor([t_step + t_ev], dtype=torch.float64)
     if world > 1:
         sec_t = sec_t.to(dev)
         dist.all_reduce(sec_t, op=dist.ReduceOp.MAX)
     sec = float(sec_t.item())
-    appresp = int(st_acc[abi.HB_STAT_APPRESP])
+    expand = {}
+    if words_mode:  # the last step's words expanded on the host, untimed above
+        w = h_w.numpy()[: int(h_tot[0])].view(np.uint64)
+        c = h_cnt.numpy().view(np.uint32)
+        te = time.perf_counter()
+        recs = Engine.expand_words(w, c)
+        expand = {"host_expand_ms_per_step": round(1e3 * (time.perf_counter() - te), 3),
+                  "records_per_step": len(recs)}
+        nev_total = len(recs) * args.steps
     st_t = torch.from_numpy(st_acc.view(np.int64).copy()).to(dev)
     if world > 1:
         dist.all_reduce(st_t)
     st = st_t.cpu().numpy().view(np.uint64)
     ok = int(st[abi.HB_STAT_COMMITS]) == G_total * args.steps and int(st[abi.HB_STAT_FAULTS]) == 0
     h2d = nmsg * 24 + G * 4
-    out = {"metric": "MsgAppResp applied/sec end to end (cfg2 batch from host memory + events back to host)",
+    steps = max(args.steps, 1)
+    d2h = (nword_total // steps * 8 + nchunks * 4 + 8) if words_mode else nev_total // steps * 16
+    how = ("hb_events_to_host (compact 8-byte words) into pinned memory, one hb_sync" if words_mode
+           else "hb_sync, then hb_copy_events (16-byte hb_event records) into pinned memory")
+    out = {"metric": "MsgAppResp applied/sec end to end (cfg2 batch from host memory + delta list back to host)",
            "value": int(st[abi.HB_STAT_APPRESP]) / sec, "unit": "MsgAppResp/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * sec / args.steps,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
            "data": "synthetic (cfg2 stream in pinned host memory)",
-           "config": {"workload": f"e2e: cfg2 {args.groups} raft groups x {n} per GPU, batch H2D + events D2H "
-                                  f"every step", "groups_per_gpu": args.groups, "replicas": n},
-           "split_ms_per_step": {"h2d_and_step": 1e3 * t_step / args.steps,
-                                 "events_d2h": 1e3 * t_ev / args.steps},
-           "bytes_per_step": {"h2d_batch": h2d, "d2h_events": nev_total // max(args.steps, 1) * 16},
-           "pcie_gbs": round((h2d + nev_total / args.steps * 16) / (sec / args.steps) / 1e9, 2),
-           "events_per_step": nev_total // max(args.steps, 1), "parity_sanity": bool(ok),
-           "timing": "wall clock per step: hb_step (H2D inside) + hb_sync, then hb_copy_events into pinned memory",
+           "config": {"workload": f"e2e: cfg2 {args.groups} raft groups x {n} per GPU, batch H2D + delta D2H "
+                                  f"every step ({args.e2e_events})", "groups_per_gpu": args.groups, "replicas": n},
+           "split_ms_per_step": {"h2d_step_and_delta" if words_mode else "h2d_and_step": 1e3 * t_step / steps,
+                                 "events_d2h": 1e3 * t_ev / steps},
+           "bytes_per_step": {"h2d_batch": h2d, "d2h_delta": d2h},
+           "pcie_gbs": round((h2d + d2h) / (sec / steps) / 1e9, 2),
+           "events_per_step": nev_total // steps, "words_per_step": nword_total // steps if words_mode else None,
+           **expand, "parity_sanity": bool(ok),
+           "timing": "wall clock per step: hb_step (H2D inside) + " + how,
            "cpu_baseline": None}
     if world > 1:
         dist.barrier()
