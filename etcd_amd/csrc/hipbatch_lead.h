@@ -1,0 +1,267 @@
+// hipbatch_lead.h — the leader lane: Lane::step (hipbatch_kernels.h)
+// restricted to the responses a leader steps at its own term, with its
+// Progress in registers.
+//
+// k_apply_fast takes only accepted MsgAppResp from Replicate followers; any
+// other response on a leader hands the group to the general kernel.  On
+// BASELINE.json cfg3 (1M groups x 5, lagging followers) that is most groups:
+// rejected MsgAppResp (maybeDecrTo + becomeProbe + sendAppend), accepts from
+// Probe / Snapshot followers (becomeReplicate, maybeSnapshotAbort), stale and
+// lagging acks that pause or unpause a full window, MsgHeartbeatResp
+// (freeFirstOne + sendAppend), MsgUnreachable and MsgSnapStatus.  The general
+// kernel carries every role and message type and needs all 256 VGPRs plus
+// scratch; this lane is FastLane (its loads, Progress arrays indexed by
+// compile-time slots, maybeCommit network, sendAppend / bcastAppend with
+// limitSize) plus exactly those transitions, and its kernel (k_lead) runs at
+// several waves per SIMD without scratch.
+//
+// It steps a message when the group is a leader, the sender is a member and
+// the message's term is not higher than the group's (stepLeader
+// raft/raft.go:514-583; a lower non-zero term is ignored by the gate, :479-486).
+// Anything else — a higher term (step-down), proposals, MsgHup / MsgBeat,
+// follower-side types, a non-member MsgSnapStatus — hands the group over, at
+// that message, to k_apply.  Every event and state write is the one
+// Lane::step makes, in the same order; the GPU parity tests compare the
+// kernels with the oracle.
+#pragma once
+
+#include "hipbatch_fast.h"
+
+namespace hb {
+
+template <int NMAX>
+struct LeadLane : FastLane<NMAX> {
+  using B = FastLane<NMAX>;
+  using B::S;
+  using B::g;
+  using B::term;
+  using B::first;
+  using B::last;
+  using B::match;
+  using B::next;
+  using B::head;
+  using B::pm;
+  using B::dirty;
+  using B::faulted;
+
+  // Whether this lane steps the message (false: hand the group over here).
+  // The caller has dropped non-member responses (raft/multinode.go:235).
+  __device__ __forceinline__ bool takes(uint32_t type, uint32_t from, uint64_t mterm) const {
+    if (this->state() != HB_STATE_LEADER || from >= this->n() || mterm > term) return false;
+    return type == HB_MSG_APP_RESP || type == HB_MSG_HEARTBEAT_RESP || type == HB_MSG_UNREACHABLE ||
+           type == HB_MSG_SNAP_STATUS || type == HB_MSG_VOTE_RESP;
+  }
+
+  // One slot's Progress as scalars (a runtime slot: one select per slot and
+  // field, so the transitions below exist once in the code, not once per slot).
+  __device__ __forceinline__ Pr get(uint32_t s) const {
+    Pr p{match[0], next[0], head[0], pm[0]};
+#pragma unroll
+    for (int k = 1; k < NMAX; ++k) {
+      const bool h = (uint32_t)k == s;
+      p.match = h ? match[k] : p.match;
+      p.next = h ? next[k] : p.next;
+      p.head = h ? head[k] : p.head;
+      p.pm = h ? pm[k] : p.pm;
+    }
+    return p;
+  }
+  __device__ __forceinline__ void put(uint32_t s, const Pr& p) {
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k) {
+      const bool h = (uint32_t)k == s;
+      if (h && (p.match != match[k] || p.next != next[k])) dirty |= 1u << (D_SLOT0 + k);
+      if (h && p.pm != pm[k]) dirty |= 1u << (B::D_PM0 + k);
+      match[k] = h ? p.match : match[k];
+      next[k] = h ? p.next : next[k];
+      head[k] = h ? p.head : head[k];
+      pm[k] = h ? p.pm : pm[k];
+    }
+  }
+  __device__ __forceinline__ uint64_t pending_of(uint32_t s) const { return S.pending[(size_t)s * S.G + g]; }
+  __device__ __forceinline__ uint64_t* ring_at(uint32_t s, uint32_t idx) const {
+    return S.ring + ((size_t)s * S.W + idx) * S.G + g;
+  }
+
+  // inflights.freeTo raft/progress.go:204-224 (head entry from the register copy)
+  __device__ __forceinline__ void free_to(uint32_t s, Pr& p, uint64_t to) const {
+    const uint32_t cnt = pm_count(p.pm);
+    if (cnt == 0) return;
+    uint64_t v = p.head;
+    if (to < v) return;
+    uint32_t idx = pm_start(p.pm);
+    const uint32_t W = S.W;
+    uint32_t i = 0;
+    while (true) {
+      ++i;
+      if (++idx >= W) idx -= W;
+      if (i == cnt) break;
+      v = *ring_at(s, idx);
+      if (to < v) break;
+    }
+    p.pm = pm_make(pm_state(p.pm), pm_paused(p.pm), idx, cnt - i);
+    p.head = v;
+  }
+
+  // sendAppend raft/raft.go:239-282 to slot s: the progress side effects;
+  // returns what it sends (FastLane::SEND_*), its index in *xo.
+  __device__ __forceinline__ uint32_t send_decide(uint32_t s, Pr& p, uint64_t* xo) {
+    if (B::is_paused(p.pm)) return B::SEND_NONE;
+    if (p.next < first) {  // needSnapshot raft/raft.go:715-717
+      const uint64_t snapi = S.snap[g];
+      if (snapi == 0) {
+        this->fault(HB_FAULT_EMPTY_SNAPSHOT);
+        return B::SEND_NONE;
+      }
+      p.pm = pm_make(HB_PR_SNAPSHOT, 0, 0, 0);  // becomeSnapshot
+      S.pending[(size_t)s * S.G + g] = snapi;
+      *xo = snapi;
+      return B::SEND_SNAP;
+    }
+    const uint64_t x = p.next - 1;
+    if (p.next <= last) {
+      bool ok = true;
+      const uint64_t lastsent = sz_limit(S, g, p.next, last, &ok);
+      if (!ok) {
+        this->fault(HB_FAULT_SIZE_WINDOW);
+        return B::SEND_NONE;
+      }
+      const uint32_t st = pm_state(p.pm);
+      if (st == HB_PR_REPLICATE) {
+        const uint32_t cnt = pm_count(p.pm), start = pm_start(p.pm);
+        if (cnt == S.W) {
+          this->fault(HB_FAULT_INFLIGHTS_FULL);
+          return B::SEND_NONE;
+        }
+        uint32_t idx = start + cnt;
+        if (idx >= S.W) idx -= S.W;
+        *ring_at(s, idx) = lastsent;  // inflights.add
+        if (cnt == 0) p.head = lastsent;
+        p.next = lastsent + 1;        // optimisticUpdate
+        p.pm = pm_make(HB_PR_REPLICATE, pm_paused(p.pm), start, cnt + 1);
+      } else if (st == HB_PR_PROBE) {
+        p.pm |= PM_PAUSED;            // pause
+      }
+    }
+    *xo = x;
+    return B::SEND_APP;
+  }
+
+  // The sends of a bcastAppend (raft/raft.go:303-310, slot order, self
+  // skipped) or of one sendAppend, as runs: consecutive MsgApps with the same
+  // Index become one EVC_BCAST word (the same records once expanded).
+  uint32_t run_mask;
+  uint64_t run_x;
+  __device__ __forceinline__ void run_flush() {
+    if (run_mask & (run_mask - 1)) {
+      emit_ev(this->E, g & (PART - 1), EVC_BCAST, run_mask, this->lt_cur(run_x), run_x);
+      this->nev += __popc(run_mask);
+    } else if (run_mask) {
+      this->ev(HB_EV_APP, __ffs(run_mask) - 1, this->lt_cur(run_x), run_x);
+    }
+    run_mask = 0;
+  }
+  __device__ __forceinline__ void send(uint32_t s) {
+    Pr p = get(s);
+    uint64_t x = 0;
+    const uint32_t k = send_decide(s, p, &x);
+    put(s, p);
+    if (k == B::SEND_APP) {
+      if (run_mask && x != run_x) run_flush();
+      run_mask |= 1u << s;
+      run_x = x;
+    } else if (k == B::SEND_SNAP) {
+      run_flush();
+      this->ev(HB_EV_SNAP, s, 0, x);
+    }
+  }
+  __device__ __forceinline__ void bcast() {
+    const uint32_t nn = this->n(), sf = this->self();
+    run_mask = 0;
+#pragma nounroll
+    for (uint32_t s = 0; s < nn; ++s) {
+      if (faulted()) break;
+      if (s != sf) send(s);
+    }
+    run_flush();
+  }
+
+  // stepLeader (raft/raft.go:514-583) for the messages takes() accepts.
+  __device__ __forceinline__ void step(uint32_t type, uint32_t from, uint64_t mterm, uint64_t index, bool reject,
+                                       uint64_t hint) {
+    if (mterm != 0 && mterm < term) return;  // the gate ignores a lower term (:483-486)
+    bool updated = false, old_paused = false, send_one = false;
+    Pr p = get(from);
+    const uint32_t ps = pm_state(p.pm);
+    if (type == HB_MSG_APP_RESP) {  // :514-546
+      if (reject) {
+        bool dec = false;  // maybeDecrTo raft/progress.go:119-141
+        if (ps == HB_PR_REPLICATE) {
+          if (index > p.match) {
+            p.next = p.match + 1;
+            dec = true;
+          }
+        } else if (p.next - 1 == index) {
+          p.next = umin64(index, hint + 1);
+          if (p.next < 1) p.next = 1;
+          p.pm &= ~PM_PAUSED;
+          dec = true;
+        }
+        if (dec && ps == HB_PR_REPLICATE) {  // becomeProbe from Replicate raft/progress.go:76-88
+          p.pm = pm_make(HB_PR_PROBE, 0, 0, 0);
+          p.next = p.match + 1;
+        }
+        send_one = dec;
+      } else {
+        old_paused = B::is_paused(p.pm);
+        if (p.match < index) {  // maybeUpdate raft/progress.go:102-113
+          p.match = index;
+          p.pm &= ~PM_PAUSED;
+          updated = true;
+        }
+        if (p.next < index + 1) p.next = index + 1;
+        if (updated) {
+          if (ps == HB_PR_PROBE) {  // becomeReplicate :90-93
+            p.pm = pm_make(HB_PR_REPLICATE, 0, 0, 0);
+            p.next = p.match + 1;
+          } else if (ps == HB_PR_SNAPSHOT) {  // maybeSnapshotAbort -> becomeProbe
+            const uint64_t pend = pending_of(from);
+            if (p.match >= pend) {
+              p.pm = pm_make(HB_PR_PROBE, 0, 0, 0);
+              p.next = umax64(p.match + 1, pend + 1);
+            }
+          } else {  // ins.freeTo(m.Index)
+            free_to(from, p, index);
+          }
+        }
+      }
+    } else if (type == HB_MSG_HEARTBEAT_RESP) {  // :547-554
+      if (ps == HB_PR_REPLICATE && pm_count(p.pm) == S.W) free_to(from, p, p.head);  // freeFirstOne
+      send_one = p.match < last;
+    } else if (type == HB_MSG_SNAP_STATUS) {  // :559-574
+      if (ps == HB_PR_SNAPSHOT) {
+        p.next = reject ? p.match + 1                                 // snapshotFailure, becomeProbe
+                        : umax64(p.match + 1, pending_of(from) + 1);  // becomeProbe from Snapshot
+        p.pm = pm_make(HB_PR_PROBE, 1, 0, 0);                         // ... and pause
+      }
+    } else if (type == HB_MSG_UNREACHABLE) {  // :575-581
+      if (ps == HB_PR_REPLICATE) {
+        p.pm = pm_make(HB_PR_PROBE, 0, 0, 0);
+        p.next = p.match + 1;
+      }
+    }  // MsgVoteResp: a leader ignores it
+    put(from, p);
+    if (updated) {  // maybeCommit -> bcastAppend, else a paused follower gets sendAppend
+      if (this->maybe_commit()) bcast();
+      else if (old_paused) send_one = true;
+    }
+    if (send_one && !faulted()) {
+      run_mask = 0;
+      send(from);
+      run_flush();
+    }
+    if (faulted()) this->ev(HB_EV_FAULT, 0, faulted(), this->arrival_x());
+  }
+};
+
+}  // namespace hb

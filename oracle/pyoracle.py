@@ -600,3 +600,82 @@ class OracleGroups:
 
     def raft(self, g):
         return lib().orc_groups_at(self.ptr, g).contents
+
+
+class ShardedOracleGroups:
+    """The same groups as OracleGroups, split into `shards` contiguous ranges
+    that are stepped concurrently (one thread per shard; ctypes releases the
+    GIL inside the C oracle).  Groups are independent (raft/multinode.go:125-131)
+    and each shard steps its groups' messages in their arrival order, so the
+    result equals one OracleGroups over the whole batch: events are mapped
+    back to global group ids and global arrival positions, statistics summed.
+    Used for the full-size BASELINE configurations, where one core would take
+    minutes.  Supports the leader-side batch fields (group / info / term /
+    index / hint / props)."""
+
+    def __init__(self, groups, runs, max_inflight, max_msg_size=NO_LIMIT, shards=16):
+        G = len(groups)
+        self.G = G
+        self.max_inflight = max_inflight
+        per = -(-G // shards)
+        self.bounds = [(lo, min(G, lo + per)) for lo in range(0, G, per)]
+        flat, off = flat_runs(runs)
+        self.parts = []
+        for lo, hi in self.bounds:
+            o = off[lo:hi + 1]
+            sub_flat = flat[int(o[0]):int(o[-1])]
+            self.parts.append(OracleGroups(groups[lo:hi], (sub_flat, o - o[0]), max_inflight, max_msg_size))
+
+    def _map(self, fn):
+        import threading
+        out = [None] * len(self.parts)
+
+        def run(i):
+            out[i] = fn(i, self.parts[i])
+        th = [threading.Thread(target=run, args=(i,)) for i in range(len(self.parts))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return out
+
+    def step(self, b):
+        for k in ("edesc", "eoff", "peoff", "commit", "eterm"):
+            assert b.get(k) is None, f"ShardedOracleGroups: batch field {k} not supported"
+        grp = np.asarray(b["group"], dtype=np.uint32)
+        per = self.bounds[0][1] - self.bounds[0][0]
+        sid = np.minimum(grp // np.uint32(per), np.uint32(len(self.parts)))  # out-of-range ids: dropped below
+        order = np.argsort(sid, kind="stable")
+        cuts = np.searchsorted(sid[order], np.arange(len(self.parts) + 1))
+        drop_stats = np.zeros(abi.HB_STAT_COUNT, np.uint64)
+        assert np.all(grp < self.G), "ShardedOracleGroups: out-of-range group ids"
+
+        def run(i, og):
+            lo, hi = self.bounds[i]
+            idx = order[cuts[i]:cuts[i + 1]]
+            sub = {"group": grp[idx] - np.uint32(lo), "info": np.asarray(b["info"])[idx],
+                   "term": np.asarray(b["term"])[idx], "index": np.asarray(b["index"])[idx]}
+            if b.get("hint") is not None:
+                sub["hint"] = np.asarray(b["hint"])[idx]
+            if b.get("props") is not None:
+                sub["props"] = np.asarray(b["props"])[lo:hi]
+            ev, st = og.step(sub)
+            ev["group"] += np.uint32(lo)
+            arr = np.isin(ev["type"], [abi.HB_EV_PROP_FWD, abi.HB_EV_PROP_DROP, abi.HB_EV_FAULT]) & \
+                (ev["x"] != np.uint64(abi.HB_NO_INDEX))
+            ev["x"][arr] = idx[ev["x"][arr].astype(np.int64)].astype(np.uint64)
+            return ev, st
+        res = self._map(run)
+        return np.concatenate([r[0] for r in res]), sum((r[1] for r in res), drop_stats)
+
+    def groups(self):
+        return np.concatenate(self._map(lambda i, og: og.groups()))
+
+    def log_info(self):
+        return np.concatenate(self._map(lambda i, og: og.log_info()))
+
+    def inflights(self, g, slot):
+        for (lo, hi), og in zip(self.bounds, self.parts):
+            if lo <= g < hi:
+                return og.inflights(g - lo, slot)
+        raise IndexError(g)

@@ -3,7 +3,7 @@ oracle (oracle/, CPU) with identical batches and compare bit-exactly."""
 import numpy as np
 
 from etcd_amd import abi
-from oracle.pyoracle import OracleGroups
+from oracle.pyoracle import OracleGroups, ShardedOracleGroups
 
 
 def sort_events(ev):
@@ -61,9 +61,13 @@ class Pair:
     """An engine and an oracle loaded with the same groups."""
 
     def __init__(self, groups, runs, nmax, W, ins=None, max_msg_size=abi.HB_NO_LIMIT, max_batch=1 << 16,
-                 sizes=None, term_runs=None):
+                 sizes=None, term_runs=None, oracle_shards=1):
         from etcd_amd.hipbatch import Engine
-        self.og = OracleGroups(groups, runs, W, max_msg_size, ins)
+        if oracle_shards > 1:  # full-size configurations: the oracle's groups stepped on several cores
+            assert not ins and not sizes and not term_runs
+            self.og = ShardedOracleGroups(groups, runs, W, max_msg_size, shards=oracle_shards)
+        else:
+            self.og = OracleGroups(groups, runs, W, max_msg_size, ins)
         init = self.og.groups()  # canonical record (term run derived from the log)
         self.eng = Engine(len(groups), max_replicas=nmax, max_inflight=W, max_msg_size=max_msg_size,
                           max_batch=max_batch)

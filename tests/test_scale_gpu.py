@@ -27,7 +27,7 @@ def test_cfg5_shard_8m_groups():
     size-independent properties (one commit per group, every ack applied)."""
     G = 8 * 1024 * 1024
     g, runs = synth.steady_groups(G, 3, seed=61, with_runs="flat")
-    pair = Pair(g, runs, 3, 8, max_batch=2 * G + 16)
+    pair = Pair(g, runs, 3, 8, max_batch=2 * G + 16, oracle_shards=16)
     for step in range(2):
         _, st, now = pair.step(synth.cfg2_batch(g, step, seed=62 + step), ctx=f"cfg5 shard step {step}",
                                check_inflights=False)
@@ -49,10 +49,30 @@ def test_cfg4_storm_over_1m_groups():
     k_route<8> and k_apply<7>, three storms on the state the last one left."""
     G = 1_100_000
     g, runs = synth.election_groups(G, 7, seed=71, with_runs="flat")
-    pair = Pair(g, runs, 7, 8, max_batch=8 * G + 16)
+    pair = Pair(g, runs, 7, 8, max_batch=8 * G + 16, oracle_shards=16)
     b = synth.cfg4_storm_batch(g, seed=72)
     for k in range(3):
         _, st, _ = pair.step(dict(b, term=synth.storm_terms(b["term"], k)), ctx=f"storm 1.1M {k}",
+                             check_inflights=False)
+        assert st[abi.HB_STAT_VOTERESP] == G * 6
+        assert st[abi.HB_STAT_WON] > G // 4 and st[abi.HB_STAT_FAULTS] == 0
+
+
+@pytest.mark.timeout(900)
+def test_cfg4_storm_full_4m_groups():
+    """BASELINE.json configs[3] at its real size: 4,194,304 groups x 7, W = 8,
+    the bench's own storm (bench.py --workload cfg4: same seed, groups and
+    batch; 33.5M messages per step: a step-down, MsgHup and 6 MsgVoteResp per
+    group), two storms on the state the first left, against the oracle (16
+    shards on 16 cores): every event, statistic and group record."""
+    G = 4 * 1024 * 1024
+    seed = 0x5EED0004  # bench.py run_aux, rank 0
+    g, runs = synth.election_groups(G, 7, seed=seed, with_runs="flat")
+    pair = Pair(g, runs, 7, 8, max_batch=8 * G + 16, oracle_shards=16)
+    b = synth.cfg4_storm_batch(g, seed=seed)
+    del g, runs
+    for k in range(2):
+        _, st, _ = pair.step(dict(b, term=synth.storm_terms(b["term"], k)), ctx=f"storm 4M {k}",
                              check_inflights=False)
         assert st[abi.HB_STAT_VOTERESP] == G * 6
         assert st[abi.HB_STAT_WON] > G // 4 and st[abi.HB_STAT_FAULTS] == 0
@@ -65,7 +85,7 @@ def test_cfg3_open_loop_over_1m_groups():
     unreachable and 1-4 entries per group, through k_route<6> and k_apply<5>."""
     G = 1_100_000
     g, runs = synth.lagging_groups(G, 5, seed=0x5EED0003, W=8, with_runs="flat")
-    pair = Pair(g, runs, 5, 8, max_batch=12 * G)
+    pair = Pair(g, runs, 5, 8, max_batch=12 * G, oracle_shards=16)
     rng = np.random.default_rng(81)
     now = pair.og.groups()
     for k in range(3):
