@@ -109,7 +109,7 @@ constexpr uint32_t SIS_LOG_MAX = 4;
 // each on a 128-byte line of its own (CTR_STRIDE words): the returning atomics of every partition
 // on one line serialise at the memory side (~7 ns each; 16K partitions put 16K on a list)
 enum : uint32_t { CTR_STRIDE = 32, CTR_AP = 0, CTR_EL = 8 * CTR_STRIDE, CTR_FL = 16 * CTR_STRIDE,
-                  CTR_DONE = 17 * CTR_STRIDE, CTR_LD = 18 * CTR_STRIDE, CTR_WORDS = 26 * CTR_STRIDE };
+                  CTR_DONE = 17 * CTR_STRIDE, CTR_WORDS = 18 * CTR_STRIDE };
 // step statistics: NSH shards per value, each (value, shard) on a 128-byte line of its own
 constexpr uint32_t NSH = 8;
 constexpr uint64_t STAGE_MAX = 8ull << 20;  // host-pointer batches packed into one pinned copy up to this size  // (a shard per XCD slot; a finish lane per (value, shard))
@@ -401,9 +401,6 @@ struct ApplyArgs {
   uint32_t* eflag;          // [NB][PART/32] (n >= 5) handed-over groups k_elect should try: not a
   uint32_t* el_cnt;         // [8]   leader, or a leader with a higher-term message in its slots;
   uint32_t* el_list;        // [8][NB]  k_elect's work lists (per XCD slot, as ap_list)
-  uint32_t* lflag;          // [NB][PART/32] (n >= 5) handed-over leaders k_lead should try (leader at
-  uint32_t* ld_cnt;         // [8]   batch start, no higher-term message, all messages in its route
-  uint32_t* ld_list;        // [8][NB]  slots, no pending proposal); k_lead's work lists
   uint32_t grid;            // apply_grid: virtual workgroups of the partition mapping (part_of)
   uint32_t sis_log;         // partitions per bucket (log2)
   uint32_t* done;           // k_apply workgroups finished (the last one runs the finish)
@@ -814,7 +811,7 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FastLane<NMAX>& L,
                                           uint32_t (&s_info)[NMAX - 1], uint32_t (&s_orig)[NMAX - 1],
                                           uint64_t (&s_term)[NMAX - 1], uint64_t (&s_index)[NMAX - 1],
                                           uint64_t moff, uint32_t* l_pfill, uint32_t* l_fill, uint32_t* l_flag,
-                                          uint32_t* l_eflag, uint32_t* l_lflag, uint32_t (&vals)[ST_N + 1]) {
+                                          uint32_t* l_eflag, uint32_t (&vals)[ST_N + 1]) {
   constexpr uint32_t KMAX = NMAX - 1;
   const uint32_t g = part * PART + lane;
   const uint64_t last0 = L.last, commit0 = L.committed;
@@ -903,9 +900,6 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FastLane<NMAX>& L,
 #pragma unroll
     for (uint32_t k = 0; k < KMAX; ++k) higher |= k < cnt && s_term[k] > L.term;
     if (flagged && (!leader || higher)) atomicOr(&l_eflag[lane >> 5], 1u << (lane & 31));
-    // k_lead's: a leader that keeps its term, all its messages in route slots
-    else if (flagged && cnt <= route_kmax(NMAX) && (resume >> 31) == 0)
-      atomicOr(&l_lflag[lane >> 5], 1u << (lane & 31));
   }
   if (flagged) {
     atomicOr(&l_flag[lane >> 5], 1u << (lane & 31));
@@ -928,24 +922,20 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FastLane<NMAX>& L,
 // The partition's bookkeeping after its lanes (one lane: `lane == 0`'s thread):
 // event fills, and the k_apply / k_elect work lists of this XCD slot.
 __device__ __forceinline__ void fast_close(const ApplyArgs& a, uint32_t part, const uint32_t* l_flag,
-                                           const uint32_t* l_eflag, const uint32_t* l_lflag, uint32_t pfill,
-                                           uint32_t fill) {
+                                           const uint32_t* l_eflag, uint32_t pfill, uint32_t fill) {
   a.ev_counts[2 * part] = pfill;
   a.ev_counts[2 * part + 1] = fill;
-  uint32_t any = 0, eany = 0, lany = 0;
+  uint32_t any = 0, eany = 0;
 #pragma unroll
   for (uint32_t w = 0; w < FLAG_WORDS; ++w) {
     any |= l_flag[w];
     eany |= l_eflag ? l_eflag[w] : 0u;
-    lany |= l_lflag ? l_lflag[w] : 0u;
   }
   const uint32_t xs = blockIdx.x & 7;
   if (any)  // the partition joins k_apply's list of its XCD slot
     a.ap_list[(size_t)xs * a.NB + atomicAdd(&a.ap_cnt[xs * CTR_STRIDE], 1u)] = part;
   if (eany)  // ... and k_elect's
     a.el_list[(size_t)xs * a.NB + atomicAdd(&a.el_cnt[xs * CTR_STRIDE], 1u)] = part;
-  if (lany)  // ... and k_lead's
-    a.ld_list[(size_t)xs * a.NB + atomicAdd(&a.ld_cnt[xs * CTR_STRIDE], 1u)] = part;
 }
 
 template <int NMAX>
@@ -954,7 +944,6 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 
   __shared__ uint32_t l_fill, l_pfill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint32_t l_eflag[FLAG_WORDS];
-  __shared__ uint32_t l_lflag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
 
   const uint32_t part = block_part(a.sis_log);
@@ -964,7 +953,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 
   const bool gvalid = g < a.S.G;
   if (tid == 0) l_fill = l_pfill = 0;
   if (tid <= ST_N) l_stats[tid] = 0;
-  if (tid < FLAG_WORDS) l_flag[tid] = l_eflag[tid] = l_lflag[tid] = 0;
+  if (tid < FLAG_WORDS) l_flag[tid] = l_eflag[tid] = 0;
 
   // ---- every load of the lane, one round trip
   FastLane<NMAX> L;
@@ -1007,17 +996,13 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 
   }
   uint32_t vals[ST_N + 1];
   (void)fast_step<NMAX>(a, L, part, tid, live, lead, leader, prop_raw, cnt, s_info, s_orig, s_term, s_index,
-                        a.ev_off[2 * part + 1], &l_pfill, &l_fill, l_flag, l_eflag, l_lflag, vals);
+                        a.ev_off[2 * part + 1], &l_pfill, &l_fill, l_flag, l_eflag, vals);
   reduce_stats(a, l_stats, vals);
   if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
   if constexpr (NMAX >= 5) {
-    if (tid < FLAG_WORDS) {
-      a.eflag[(size_t)part * FLAG_WORDS + tid] = l_eflag[tid];
-      a.lflag[(size_t)part * FLAG_WORDS + tid] = l_lflag[tid];
-    }
+    if (tid < FLAG_WORDS) a.eflag[(size_t)part * FLAG_WORDS + tid] = l_eflag[tid];
   }
-  if (tid == 0)
-    fast_close(a, part, l_flag, NMAX >= 5 ? l_eflag : nullptr, NMAX >= 5 ? l_lflag : nullptr, l_pfill, l_fill);
+  if (tid == 0) fast_close(a, part, l_flag, NMAX >= 5 ? l_eflag : nullptr, l_pfill, l_fill);
 }
 
 // ---------------------------------------------------------------------------
@@ -1238,10 +1223,12 @@ __device__ __forceinline__ bool apply_part(const ApplyArgs& a, uint32_t part, Ge
 constexpr uint32_t FOLLOW_GRID = HB_FOLLOW_GRID;
 // k_apply's grid: 0 = one workgroup per partition (each takes at most one list
 // entry); else a persistent grid of that many (a multiple of 8).  Measured on
-// MI355X: 512 saves ~1.5 us on an empty cfg2 step but costs 5-7 % on cfg3 /
-// cfg4, where every partition is on the lists.
+// MI355X: 512 saves ~1.5 us on an empty cfg2 step but cost 5-7 % on cfg3 /
+// cfg4 while every partition was on the lists.  Since the leader lane
+// (k_apply_lead) the n >= 5 lists are short, and the per-partition grid of a
+// 256-VGPR, 31 KB-LDS kernel is itself ~40 us of dispatch (cfg3).
 #ifndef HB_GEN_GRID
-#define HB_GEN_GRID 0
+#define HB_GEN_GRID 1024
 #endif
 constexpr uint32_t GEN_GRID = HB_GEN_GRID;
 #ifndef HB_GEN_GRID3
@@ -1462,86 +1449,119 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
   }
 }
 
-// k_lead: the leader lane (hipbatch_lead.h) over its work lists (per XCD slot,
-// as k_elect's), after k_elect and before k_apply (n >= 5): a handed-over
-// leader whose messages all sit in its route slots (lflag: a leader at batch
-// start without a higher-term message, so k_elect never touched it) steps
-// them as far as LeadLane::takes allows — every
-// response a leader steps at its own term, with its Progress in registers.  A
-// group it finishes leaves the partition's flags; a group it hands over
-// resumes in k_apply at the first message it did not take.
 #ifndef HB_LEAD_WAVES
 #define HB_LEAD_WAVES 3
 #endif
+// ---------------------------------------------------------------------------
+// k_apply_lead (n >= 5, replaces k_apply_fast there): one workgroup per
+// partition, one lane per group, the leader lane (hipbatch_lead.h) for every
+// leader whose messages all sit in its route slots: the dense proposal, then
+// the slot messages in arrival order as far as LeadLane::takes allows — every
+// response a leader steps at its own term.  One load and one store of the
+// group's state for the whole batch.  What it cannot take is handed over as
+// k_apply_fast does (resume word, pflag; eflag for k_elect: a group that is no
+// leader, or a leader stopped by a higher-term message).  A leader without a
+// proposal and with more messages than n - 1 (an election storm's leader)
+// first reads only its Term and its slots' terms: with a higher term among
+// them it is handed over unloaded.
+// ---------------------------------------------------------------------------
 template <int NMAX>
-__global__ void __launch_bounds__(PART, HB_LEAD_WAVES) k_lead(ApplyArgs a) {
+__global__ void __launch_bounds__(PART, HB_LEAD_WAVES) k_apply_lead(ApplyArgs a) {
   constexpr uint32_t KS = route_kmax(NMAX);
-  __shared__ uint32_t l_fill;
+  __shared__ uint32_t l_fill, l_pfill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
-  __shared__ uint32_t l_lflag[FLAG_WORDS];
+  __shared__ uint32_t l_eflag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
+  const uint32_t part = block_part(a.sis_log);
+  if (part >= a.NB) return;  // uniform: grid padding
   const uint32_t tid = threadIdx.x;
-  const uint32_t xs = blockIdx.x & 7, stride = gridDim.x >> 3;
-  const uint32_t nl = __hip_atomic_load(&a.ld_cnt[xs * CTR_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (uint32_t i = blockIdx.x >> 3; i < nl; i += stride) {  // uniform
-    const uint32_t part = a.ld_list[(size_t)xs * a.NB + i];
-    const uint32_t g = part * PART + tid;
-    if (tid < FLAG_WORDS) {
-      l_flag[tid] = a.pflag[(size_t)part * FLAG_WORDS + tid];
-      l_lflag[tid] = a.lflag[(size_t)part * FLAG_WORDS + tid];
-    }
-    if (tid == 0) l_fill = a.ev_counts[2 * part + 1];  // after k_apply_fast's / k_elect's events
-    if (tid <= ST_N) l_stats[tid] = 0;
-    __syncthreads();
-    const bool flagged = (l_lflag[tid >> 5] >> (tid & 31)) & 1u;  // live, not faulted when handed over
-    LeadLane<NMAX> L;
-    L.S = a.S;
-    L.E.chunk = a.ev + a.ev_off[2 * part + 1];
-    L.E.fill = &l_fill;
-    L.g = g;
-    L.mlo = flagged ? reinterpret_cast<const uint32_t*>(a.S.meta)[2 * (size_t)g] : 0u;
-    const uint32_t cnt = flagged ? a.cnt[g] : 0u;
-    const uint32_t resume = flagged ? a.resume[g] : 0u;
-    const uint32_t skip = resume & 0x3FFFFFFFu;
-    // (a pending dense proposal means the group was no leader with a self slot
-    // at k_apply_fast; it stays with k_apply)
-    const bool mine = flagged && cnt <= KS && skip < cnt && (resume >> 31) == 0 &&
-                      L.state() == HB_STATE_LEADER && L.faulted() == 0;
-    uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
-    bool done = false;
-    uint64_t commit0 = 0;
-    L.nev = 0;
-    L.dirty = 0;
-    L.committed = 0;
-    if (mine) {
+  const uint32_t g = part * PART + tid;
+  const bool gvalid = g < a.S.G;
+  if (tid == 0) l_fill = l_pfill = 0;
+  if (tid <= ST_N) l_stats[tid] = 0;
+  if (tid < FLAG_WORDS) l_flag[tid] = l_eflag[tid] = 0;
+
+  LeadLane<NMAX> L;
+  L.S = a.S;
+  L.g = g;
+  L.mlo = gvalid ? reinterpret_cast<const uint32_t*>(a.S.meta)[2 * (size_t)g] : 0u;
+  const uint32_t prop_raw = (a.props && gvalid) ? a.props[g] : 0u;
+  const uint32_t cnt = gvalid ? a.cnt[g] : 0u;
+  const bool live = gvalid && L.n() != 0 && L.faulted() == 0;
+  const bool leader = live && L.state() == HB_STATE_LEADER;
+  const bool fits = cnt <= KS;  // every message of the group is in its slots
+  // a leader with a proposal or at most one message per follower loads at once
+  const bool spec = leader && (prop_raw != 0 || (fits && cnt <= (uint32_t)NMAX - 1));
+  L.dirty = 0;
+  L.nev = 0;
+  L.last = L.committed = 0;
+  L.term = 0;
+  if (spec) L.load();
+  uint32_t key[KS];
+  uint32_t perm = 0;
+  const bool slots = leader && fits;
+#pragma unroll
+  for (uint32_t k = 0; k < KS; ++k) {
+    key[k] = (slots && k < cnt) ? a.slot_orig[(size_t)k * a.S.G + g] : 0xFFFFFFFFu;
+    perm |= k << (4 * k);
+  }
+  bool loaded = spec, higher = false;
+  if (slots && !spec) {  // a busy leader without a proposal: load it unless a higher term steps it down
+    const uint64_t t = a.S.term[g];
+#pragma unroll
+    for (uint32_t k = 0; k < KS; ++k) higher |= k < cnt && a.slot_term[(size_t)k * a.S.G + g] > t;
+    if (!higher) {
       L.load();
-      commit0 = ((resume >> 30) & 1u) ? L.committed : a.commit0[g];
-      // arrival order of the slots (odd-even transposition, slot numbers as nibbles)
-      uint32_t key[KS];
-      uint32_t perm = 0;
+      loaded = true;
+    }
+  }
+  // arrival order of the slots (odd-even transposition, slot numbers as nibbles)
 #pragma unroll
-      for (uint32_t k = 0; k < KS; ++k) {
-        key[k] = k < cnt ? a.slot_orig[(size_t)k * a.S.G + g] : 0xFFFFFFFFu;
-        perm |= k << (4 * k);
-      }
+  for (uint32_t r = 0; r < KS; ++r) {
 #pragma unroll
-      for (uint32_t r = 0; r < KS; ++r) {
-#pragma unroll
-        for (uint32_t k = (r & 1); k + 1 < KS; k += 2) {
-          const uint32_t k0 = key[k], k1 = key[k + 1];
-          const bool sw = k1 < k0;
-          key[k] = sw ? k1 : k0;
-          key[k + 1] = sw ? k0 : k1;
-          const uint32_t p0 = (perm >> (4 * k)) & 0xF, p1 = (perm >> (4 * (k + 1))) & 0xF;
-          const uint32_t swp = (perm & ~(0xFFu << (4 * k))) | (p1 << (4 * k)) | (p0 << (4 * (k + 1)));
-          perm = sw ? swp : perm;
-        }
-      }
-      uint32_t x = skip;
-      uint32_t inf_n = 0, orig_n = 0;
-      uint64_t term_n = 0, index_n = 0;
+    for (uint32_t k = (r & 1); k + 1 < KS; k += 2) {
+      const uint32_t k0 = key[k], k1 = key[k + 1];
+      const bool sw = k1 < k0;
+      key[k] = sw ? k1 : k0;
+      key[k + 1] = sw ? k0 : k1;
+      const uint32_t p0 = (perm >> (4 * k)) & 0xF, p1 = (perm >> (4 * (k + 1))) & 0xF;
+      const uint32_t swp = (perm & ~(0xFFu << (4 * k))) | (p1 << (4 * k)) | (p0 << (4 * (k + 1)));
+      perm = sw ? swp : perm;
+    }
+  }
+  const uint64_t last0 = L.last, commit0 = L.committed;
+  bool flagged = false;
+  uint32_t resume = 0;
+  uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
+
+  // ---- the dense proposal: the partition's P chunk (fixed slot), before any message event
+  const uint64_t poff = (uint64_t)part * PART * a.ev_per_msg;
+  if (tid == 0) a.ev_off[2 * part] = poff;
+  L.E.chunk = a.ev + poff;
+  L.E.fill = &l_pfill;
+  const uint32_t prop_k = live ? prop_raw : 0u;
+  if (prop_k) {
+    if (loaded && L.prop_ok(prop_k)) {
+      L.arrival = 0xFFFFFFFFu;
+      L.prop(prop_k);
+    } else {
+      flagged = true;
+      resume = 1u << 31;  // the proposal itself is pending (stepped by k_apply into the M chunk)
+    }
+  }
+  // ---- the slot messages in arrival order (M chunk reserved by k_route)
+  L.E.chunk = a.ev + a.ev_off[2 * part + 1];
+  L.E.fill = &l_fill;
+  if (live && cnt > 0 && !flagged && !L.faulted()) {
+    if (!loaded || !fits) {  // all to k_apply (or k_elect)
+      flagged = true;
+      resume = 0;
+    } else {
+      uint32_t x = 0;
+      uint32_t inf_n, orig_n;
+      uint64_t term_n, index_n;
       {
-        const size_t o = (size_t)((perm >> (4 * x)) & 0xF) * a.S.G + g;
+        const size_t o = (size_t)(perm & 0xF) * a.S.G + g;
         inf_n = a.slot_info[o];
         orig_n = a.slot_orig[o];
         term_n = a.slot_term[o];
@@ -1565,7 +1585,12 @@ __global__ void __launch_bounds__(PART, HB_LEAD_WAVES) k_lead(ApplyArgs a) {
           st_drop++;
           continue;
         }
-        if (!L.takes(type, from, mterm)) break;
+        if (!L.takes(type, from, mterm)) {
+          flagged = true;
+          resume = x;
+          higher = mterm > L.term;
+          break;
+        }
         L.arrival = morig;
         L.step(type, from, mterm, mindex, reject,
                (reject && type == HB_MSG_APP_RESP && a.hint) ? a.hint[morig] : 0ull);
@@ -1573,32 +1598,32 @@ __global__ void __launch_bounds__(PART, HB_LEAD_WAVES) k_lead(ApplyArgs a) {
         st_app += type == HB_MSG_APP_RESP;
         st_vote += type == HB_MSG_VOTE_RESP;
       }
-      if (x > skip) {
-        L.store();
-        if (x == cnt || L.faulted()) {
-          done = true;  // the group's batch ends here (a fault freezes it)
-          atomicAnd(&l_flag[tid >> 5], ~(1u << (tid & 31)));
-        } else {  // k_apply resumes at message x, loading what was stored
-          a.resume[g] = x;
-          a.commit0[g] = commit0;
-        }
-      }
     }
-    const uint64_t vals[ST_N + 1] = {st_msgs,
-                                     st_app,
-                                     st_vote,
-                                     st_drop,
-                                     (uint64_t)(done && L.committed != commit0),
-                                     0,
-                                     0,
-                                     (uint64_t)(done && L.faulted() != 0),
-                                     0,
-                                     L.nev};
-    reduce_stats(a, l_stats, vals);  // (ends with a barrier: l_flag and l_fill are final)
-    if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
-    if (tid == 0) a.ev_counts[2 * part + 1] = l_fill;
-    __syncthreads();  // the next partition reuses the LDS
   }
+  if (loaded) L.store();
+  // k_elect's candidates: no leader, or a leader a higher term steps down
+  if (flagged && (!leader || higher)) atomicOr(&l_eflag[tid >> 5], 1u << (tid & 31));
+  if (flagged) {
+    atomicOr(&l_flag[tid >> 5], 1u << (tid & 31));
+    a.resume[g] = resume | (loaded ? 0u : 1u << 30);
+    if (loaded) a.commit0[g] = commit0;
+  }
+  const uint32_t vals[ST_N + 1] = {st_msgs,
+                                   st_app,
+                                   st_vote,
+                                   st_drop,
+                                   (uint32_t)(!flagged && L.committed != commit0),
+                                   0,
+                                   0,
+                                   (uint32_t)(L.faulted() != 0 && live),
+                                   (uint32_t)(L.last - last0),
+                                   L.nev};
+  reduce_stats(a, l_stats, vals);
+  if (tid < FLAG_WORDS) {
+    a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
+    a.eflag[(size_t)part * FLAG_WORDS + tid] = l_eflag[tid];
+  }
+  if (tid == 0) fast_close(a, part, l_flag, l_eflag, l_pfill, l_fill);
 }
 
 // k_follow: the follower-capable lane (Lane<NMAX, true>) for the groups
@@ -2304,8 +2329,6 @@ struct hb_handle {
   uint32_t* fl_list = nullptr;    // [NB]
   uint32_t* eflag = nullptr;      // [NB][PART/32] k_elect's groups (n >= 5)
   uint32_t* el_list = nullptr;    // [8][NB]
-  uint32_t* lflag = nullptr;      // [NB][PART/32] k_lead's groups (n >= 5)
-  uint32_t* ld_list = nullptr;    // [8][NB]
   uint32_t* done = nullptr;       // k_apply workgroups finished this step
   uint32_t* resume = nullptr;     // [G]
   uint64_t* commit0 = nullptr;    // [G]
@@ -2440,7 +2463,8 @@ template <int NMAX>
 void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
   const uint32_t grid = apply_grid(h);
   if (ev) (void)hipEventRecord(ev[2], h->stream);
-  hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
+  if constexpr (NMAX >= 5) hipLaunchKernelGGL(k_apply_lead<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
+  else hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
   if (ev) (void)hipEventRecord(ev[3], h->stream);
   if constexpr (NMAX >= 5) {  // the general kernel spills at n >= 5: elections go first
 #ifndef HB_X_NO_ELECT
@@ -2450,11 +2474,6 @@ void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
 #endif
       hipLaunchKernelGGL(k_elect<NMAX>, dim3(ELECT_GRID ? std::min(grid, ELECT_GRID) : grid), dim3(PART), 0,
                          h->stream, a);
-  }
-  if constexpr (NMAX >= 5) {  // leaders' other responses, before the spilling general kernel
-#ifndef HB_X_NO_LEAD
-    hipLaunchKernelGGL(k_lead<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
-#endif
   }
   if constexpr (NMAX <= 3) {  // chained follower pass; the last workgroup runs the finish
     const uint32_t gg = GEN_GRID3 ? std::min(grid, GEN_GRID3) : grid;
@@ -2591,8 +2610,6 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   if (h->nmax >= 5) {
     ALLOC(h->eflag, (size_t)h->NB * FLAG_WORDS);
     ALLOC(h->el_list, 8ull * h->NB);
-    ALLOC(h->lflag, (size_t)h->NB * FLAG_WORDS);
-    ALLOC(h->ld_list, 8ull * h->NB);
   }
   ALLOC(h->resume, G);
   ALLOC(h->commit0, G);
@@ -3275,9 +3292,6 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.eflag = h->eflag;
   aa.el_cnt = ps.ctr + CTR_EL;
   aa.el_list = h->el_list;
-  aa.lflag = h->lflag;
-  aa.ld_cnt = ps.ctr + CTR_LD;
-  aa.ld_list = h->ld_list;
   aa.grid = apply_grid(h);
   aa.sis_log = h->sis_log;
   aa.done = ps.ctr + CTR_DONE;

@@ -1,28 +1,29 @@
 // hipbatch_lead.h — the leader lane: Lane::step (hipbatch_kernels.h)
-// restricted to the responses a leader steps at its own term, with its
-// Progress in registers.
+// restricted to what a leader steps at its own term, with its Progress in
+// registers.  It runs in k_apply_lead, the n >= 5 apply kernel.
 //
-// k_apply_fast takes only accepted MsgAppResp from Replicate followers; any
-// other response on a leader hands the group to the general kernel.  On
-// BASELINE.json cfg3 (1M groups x 5, lagging followers) that is most groups:
-// rejected MsgAppResp (maybeDecrTo + becomeProbe + sendAppend), accepts from
-// Probe / Snapshot followers (becomeReplicate, maybeSnapshotAbort), stale and
-// lagging acks that pause or unpause a full window, MsgHeartbeatResp
-// (freeFirstOne + sendAppend), MsgUnreachable and MsgSnapStatus.  The general
-// kernel carries every role and message type and needs all 256 VGPRs plus
-// scratch; this lane is FastLane (its loads, Progress arrays indexed by
-// compile-time slots, maybeCommit network, sendAppend / bcastAppend with
-// limitSize) plus exactly those transitions, and its kernel (k_lead) runs at
-// several waves per SIMD without scratch.
+// FastLane (k_apply_fast, n = 3) takes only proposals and accepted MsgAppResp
+// from Replicate followers; any other response on a leader would hand the group
+// to the general kernel, which carries every role and message type and needs
+// all 256 VGPRs plus scratch.  On BASELINE.json cfg3 (1M groups x 5, lagging
+// followers) that is most groups: rejected MsgAppResp (maybeDecrTo +
+// becomeProbe + sendAppend), accepts from Probe / Snapshot followers
+// (becomeReplicate, maybeSnapshotAbort), stale and lagging acks that pause or
+// unpause a full window, MsgHeartbeatResp (freeFirstOne + sendAppend),
+// MsgUnreachable and MsgSnapStatus.  LeadLane is FastLane (its loads and
+// store, maybeCommit network, limitSize) plus exactly those transitions, with
+// one code path for every slot: the sender's Progress is selected into
+// scalars, stepped once and put back, and bcastAppend is a rolled loop whose
+// consecutive equal-Index MsgApps become one EVC_BCAST word.
 //
 // It steps a message when the group is a leader, the sender is a member and
 // the message's term is not higher than the group's (stepLeader
 // raft/raft.go:514-583; a lower non-zero term is ignored by the gate, :479-486).
-// Anything else — a higher term (step-down), proposals, MsgHup / MsgBeat,
-// follower-side types, a non-member MsgSnapStatus — hands the group over, at
-// that message, to k_apply.  Every event and state write is the one
-// Lane::step makes, in the same order; the GPU parity tests compare the
-// kernels with the oracle.
+// Anything else — a higher term (step-down), MsgProp messages, MsgHup /
+// MsgBeat, follower-side types, a non-member MsgSnapStatus — hands the group
+// over, at that message, to k_elect / k_apply.  Every event and state write is
+// the one Lane::step makes, in the same order; the GPU parity tests compare
+// the kernels with the oracle.
 #pragma once
 
 #include "hipbatch_fast.h"
@@ -184,6 +185,33 @@ struct LeadLane : FastLane<NMAX> {
       if (s != sf) send(s);
     }
     run_flush();
+  }
+
+  // MsgProp with k entries on a leader (FastLane::prop with the rolled
+  // bcastAppend): stepLeader raft/raft.go:500-513 -> appendEntry :351-360 ->
+  // maybeCommit :323-332 -> bcastAppend :303-310
+  __device__ __forceinline__ void prop(uint32_t k) {
+    const uint64_t old = last;
+    if (sz_on(S.max_msg_size)) sz_append(S, g, old, k, term, S.edesc + S.peoff[g]);  // dense proposal entries
+    last += k;
+    if (this->tfirst == HB_NO_INDEX) {
+      this->tfirst = old + 1;
+      dirty |= B::D_TFIRST;
+    }
+    this->tlast = last;
+    dirty |= D_LAST | D_TRUN;
+    this->ev(HB_EV_LAST, 0, 0, last);
+    const uint32_t sf = this->self();  // self maybeUpdate(lastIndex) raft/raft.go:358
+    Pr p = get(sf);
+    if (p.match < last) {
+      p.match = last;
+      p.pm &= ~PM_PAUSED;
+    }
+    if (p.next < last + 1) p.next = last + 1;
+    put(sf, p);
+    this->maybe_commit();
+    bcast();
+    if (faulted()) this->ev(HB_EV_FAULT, 0, faulted(), this->arrival_x());
   }
 
   // stepLeader (raft/raft.go:514-583) for the messages takes() accepts.
