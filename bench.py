@@ -223,23 +223,46 @@ def pmc_traffic(path, kernel, G, n, apply_us):
     profile was taken on the same workload and its average duration agrees with
     the live measurement within 15 % (same build); otherwise None."""
     import glob
-    if path is None:
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
-        if not cands:
-            return None, None
-        path = cands[-1]
-    try:
-        d = json.load(open(path))
-        k = d["kernels"][kernel]
-        cfg = d["bench"]["config"]
-    except (OSError, KeyError, ValueError):
-        return None, None
-    if cfg.get("groups_per_gpu") != G or cfg.get("replicas") != n or "traffic_bytes" not in k:
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")), reverse=True)
+    for path in cands:  # the newest profile of this configuration
+        try:
+            d = json.load(open(path))
+            k = d["kernels"][kernel]
+            cfg = d["bench"]["config"]
+        except (OSError, KeyError, ValueError):
+            continue
+        if cfg.get("groups_per_gpu") == G and cfg.get("replicas") == n and "traffic_bytes" in k:
+            break
+    else:
         return None, None
     src = os.path.relpath(path, ROOT)
     if abs(k["avg_us"] - apply_us) > 0.15 * apply_us:
         return None, f"{src}: profiled avg {k['avg_us']:.1f} us vs live {apply_us:.1f} us (stale, not used)"
     return float(k["traffic_bytes"]), f"{src}: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, avg {k['avg_us']:.1f} us"
+
+
+def step_traffic(path, workload, G, n, ms_per_step):
+    """Whole-step HBM bytes of an auxiliary line (cfg3 / cfg4 / tick) from the
+    newest committed profile of the same workload and configuration
+    (tools/profile_round.sh with WL=<workload>: FETCH_SIZE x 2 + WRITE_SIZE
+    summed over the step's kernels).  Used only when the traced run's step time
+    agrees with the live one within 15 %; otherwise None."""
+    import glob
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")), reverse=True)
+    for p in cands:
+        try:
+            d = json.load(open(p))
+            st, cfg, bms = d["step"], d["bench"]["config"], d["bench"]["ms_per_step"]
+        except (OSError, KeyError, ValueError, TypeError):
+            continue
+        if cfg.get("workload", "").startswith(workload + ":") and cfg.get("groups_per_gpu") == G and \
+                cfg.get("replicas") == n:
+            src = os.path.relpath(p, ROOT)
+            if abs(bms - ms_per_step) > 0.15 * ms_per_step:
+                return None, f"{src}: profiled step {bms:.3f} ms vs live {ms_per_step:.3f} ms (stale, not used)"
+            return float(st["traffic_bytes"]), (f"{src}: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE summed over the "
+                                                f"step's kernels, traced step {bms:.3f} ms")
+    return None, None
 
 
 def run_multinode(args):
@@ -861,10 +884,16 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         eng.load_groups(g)
         rng = np.random.default_rng(seed)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        mix = np.zeros(5, np.int64)  # timed steps: acks, rejects, heartbeat resps, unreachable, groups proposing
         for k in range(total):
             now = eng.get_groups()  # the stream is generated from the engine's state (untimed)
             b = synth.cfg3_open_batch(now, rng)
             del now
+            if k >= args.warmup:
+                t, rj = b["info"] & 0xF, (b["info"] >> 8) & 1
+                mix += [int(((t == abi.HB_MSG_APP_RESP) & (rj == 0)).sum()), int(((t == abi.HB_MSG_APP_RESP) & (rj == 1)).sum()),
+                        int((t == abi.HB_MSG_HEARTBEAT_RESP).sum()), int((t == abi.HB_MSG_UNREACHABLE).sum()),
+                        int((b["props"] > 0).sum())]
             d = [torch.from_numpy(b[f].view(np.int32 if b[f].dtype == np.uint32 else np.int64)).to(dev)
                  for f in ("group", "info", "term", "index", "hint", "props")]
             torch.cuda.synchronize()
@@ -932,22 +961,37 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     else:
         metric, unit, val = "MsgAppResp applied/sec (cfg3 lagging followers)", "MsgAppResp/s", \
             int(st[abi.HB_STAT_APPRESP]) / sec
-        # SURVEY.md 8(d) cfg2 figures applied to cfg3: 66 B per stepped message (message 24,
-        # Match/Next/state/inflights), 80 B per group per batch, 21 B per follower per appended entry
-        alg = (int(st[abi.HB_STAT_MSGS]) * 66 + world * G * args.steps * 80 +
-               int(st[abi.HB_STAT_ENTRIES]) * (n - 1) * 21) / world
-        alg_note = "66 B per stepped message + 80 B per group + 21 B per follower per appended entry"
+        # Per message type, the SURVEY.md 8(d) rule (each field the reference reads once R / writes
+        # once if changed W): MsgAppResp accept 66 B (message 24, Match 8R+8W, Next 8R, State+Paused
+        # 2R, ins start/count 4R+4W, freed ring slot 8R); reject 64 B (message 24 + RejectHint 8,
+        # Match 8R, Next 8R+8W, State 2R+2W, ins 4W: maybeDecrTo + becomeProbe); MsgHeartbeatResp
+        # 43 B (message 24, State+count 3R, Match 8R, ring head 8R: freeFirstOne test); MsgUnreachable
+        # 36 B (message 24, State 2R+2W, Next 8W); per group per batch 80 B (Term, committed R+W,
+        # lastIndex R+W, termFirst, self Match R+W, delta 16 B); per MsgApp sent 21 B (State+count
+        # 3R, Next 8W, ring slot 8W, count 2W) = events - commits - LAST events (one per proposing group)
+        n_ack, n_rej, n_hb, n_unr, n_prop = (int(x) for x in mix)
+        sends = max(int(st[abi.HB_STAT_EVENTS]) - int(st[abi.HB_STAT_COMMITS]) - world * n_prop, 0)
+        alg = (n_ack * 66 + n_rej * 64 + n_hb * 43 + n_unr * 36 + world * G * args.steps * 80 + sends * 21) / world
+        alg_note = ("per message type: MsgAppResp accept 66 B, reject 64 B, MsgHeartbeatResp 43 B, MsgUnreachable 36 B; "
+                    "80 B per group per batch; 21 B per MsgApp sent (events - commits - proposing groups)")
+        extra_mix = {"acks": n_ack // args.steps, "rejects": n_rej // args.steps, "heartbeat_resps": n_hb // args.steps,
+                     "unreachable": n_unr // args.steps, "msgapp_sent": sends // args.steps // world}
 
-        extra = {"msgs_per_s": int(st[abi.HB_STAT_MSGS]) / sec, "commits_per_s": int(st[abi.HB_STAT_COMMITS]) / sec}
+        extra = {"msgs_per_s": int(st[abi.HB_STAT_MSGS]) / sec, "commits_per_s": int(st[abi.HB_STAT_COMMITS]) / sec,
+                 "mix_per_step_rank0": extra_mix}
         ok = int(st[abi.HB_STAT_FAULTS]) == 0
         wl = f"cfg3: {G} raft groups x {n} per GPU, lagging followers (W={W})"
         data = "synthetic (seeded open-loop cfg3 stream generated from the engine state each step)"
     if args.workload in ("cfg3", "cfg4", "tick"):
         # whole-step roofline (several kernels share the step; per-kernel times: profiles/*kernel_stats.csv)
         ach = alg / (ms / args.steps * 1e-3) / args.steps / 1e9 if ms > 0 else 0.0
+        tr, tsrc = step_traffic(args.traffic_json, args.workload, G, n, ms / args.steps) \
+            if args.workload != "tick" else (None, None)
         extra["roofline"] = {"bound": "hbm", "kernel": "hb_step (whole step)" if args.workload != "tick" else
                              "hb_tick (k_tick + finish)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr,
+                             "traffic_source": tsrc,
+                             "traffic_over_alg": round(tr / (alg / args.steps), 3) if tr else None,
                              "alg_bytes_per_step": round(alg / args.steps), "alg_bytes_note": alg_note}
     out = {"metric": metric, "value": val, "unit": unit, "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": ms / args.steps, "higher_is_better": True, "scaling": "weak",

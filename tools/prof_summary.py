@@ -99,6 +99,25 @@ def main():
                       f"2 x FETCH_SIZE = {cal['fetch_bytes']:.4g} B (ratio {cal['fetch_bytes'] / exp:.3f})."]
         out["calibration"] = {"kernel": "k_radix_hist", "expected_read_bytes": exp,
                               "measured_read_bytes": cal["fetch_bytes"]}
+    # the whole step (every kernel hb_step launches, per step; k_route runs once per step)
+    step_k = ("k_radix_hist", "k_scan_rows", "k_radix_scatter", "k_bucket_bounds", "k_route", "k_apply", "k_elect",
+              "k_follow", "k_finish")
+    steps = sum(s["calls"] for k, s in ks.items() if k.startswith("k_route"))
+    if steps:
+        tb = us = 0.0
+        missing = []
+        for k, s in ks.items():
+            if not k.startswith(step_k):
+                continue
+            us += s["avg_us"] * s["calls"] / steps
+            t = traffic(k)
+            if t:
+                tb += t["traffic_bytes"] * s["calls"] / steps
+            else:
+                missing.append(k)
+        out["step"] = {"traffic_bytes": tb, "kernel_us": us, "steps": steps, "kernels_without_pmc": missing}
+        lines += ["", f"Whole step ({steps} steps traced): kernels {us:.1f} us, HBM traffic {tb:.4g} B per step "
+                      f"(FETCH_SIZE x 2 + WRITE_SIZE summed over the step's kernels)"]
     if bench:
         out["bench"] = {"value": bench["value"], "ms_per_step": bench["ms_per_step"], "phases": bench.get("phases"),
                         "config": bench["config"]}

@@ -4,6 +4,7 @@
 #   2. PMC pass FETCH_SIZE  (own run, MI355X_MICROARCH.md: one counter group per pass)
 #   3. PMC pass WRITE_SIZE
 #   4. plain bench.py (the JSON line, with the traffic the passes measured)
+# WL=<workload> (default cfg2) profiles another bench line (cfg3 / cfg4 / cfg5 / tick).
 # Outputs under gpurun_out/<tag>/; tools/prof_summary.py folds them into profiles/.
 set -euo pipefail
 TAG=${1:-r01}
@@ -13,17 +14,18 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT"
 STEPS=${STEPS:-20}
+WA="--workload ${WL:-cfg2}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 bench.py --steps "$STEPS" --warmup 5 --no-cpu-baseline > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
+    python3 bench.py $WA --steps "$STEPS" --warmup 5 --no-cpu-baseline > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
 echo "trace done"
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > "$OUT/pmc_fetch.log" 2>&1
+    python3 bench.py $WA --steps 5 --warmup 2 --no-cpu-baseline --no-profile > "$OUT/pmc_fetch.log" 2>&1
 echo "fetch done"
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile > "$OUT/pmc_write.log" 2>&1
+    python3 bench.py $WA --steps 5 --warmup 2 --no-cpu-baseline --no-profile > "$OUT/pmc_write.log" 2>&1
 echo "write done"
 python3 tools/prof_summary.py "$OUT" --tag "$TAG" --out "$OUT/summary" > "$OUT/summary.log"
 echo "summary done"
-timeout -k 10 300 python3 bench.py --traffic-json "$OUT/summary/${TAG}_traffic.json" > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 300 python3 bench.py $WA --no-cpu-baseline --traffic-json "$OUT/summary/${TAG}_traffic.json" > "$OUT/bench.json" 2> "$OUT/bench.err"
 echo "bench done"
 tail -1 "$OUT/bench.json"
