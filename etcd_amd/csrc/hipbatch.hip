@@ -116,9 +116,15 @@ constexpr uint64_t STAGE_MAX = 8ull << 20;  // host-pointer batches packed into 
 __host__ __device__ constexpr uint32_t shard_at(uint32_t k, uint32_t sh) { return (k * NSH + sh) * 16; }
 constexpr uint32_t RDX_BITS = 8;
 constexpr uint32_t RDX_BINS = 1u << RDX_BITS;
-constexpr uint32_t RDX_THREADS = 512;
+#ifndef HB_RDX_THREADS  // measured (cfg2 / cfg5 A/B): 1024 x 2 beat 512 x 4 (-3 us / -46 us per step),
+#define HB_RDX_THREADS 1024  // 256 x 4, 512 x 2, 512 x 8 and 1024 x 4
+#endif
+#ifndef HB_RDX_ROUNDS
+#define HB_RDX_ROUNDS 2
+#endif
+constexpr uint32_t RDX_THREADS = HB_RDX_THREADS;
 constexpr uint32_t RDX_WAVES = RDX_THREADS / 64;
-constexpr uint32_t RDX_ROUNDS = 4;
+constexpr uint32_t RDX_ROUNDS = HB_RDX_ROUNDS;
 constexpr uint32_t RDX_TILE = RDX_THREADS * RDX_ROUNDS;  // 2048
 
 struct MsgRec {      // apply input record (24 B)
@@ -693,7 +699,10 @@ constexpr uint32_t ROUTE_THREADS = 1024;
 #define HB_ROUTE_UNROLL 4
 #endif
 constexpr uint32_t ROUTE_UNROLL = HB_ROUTE_UNROLL;  // records in flight per lane
-constexpr uint32_t route_rg_log(uint32_t kmax) { return kmax <= 2 ? 11 : (kmax <= 4 ? 10 : 9); }
+#ifndef HB_RG2_LOG  // route groups per workgroup for KMAX = 2 (log2): 1024 (4 sisters per 4096-group
+#define HB_RG2_LOG 10  // bucket, 53 KB LDS) measured faster than 2048 (2 sisters, 106 KB)
+#endif
+constexpr uint32_t route_rg_log(uint32_t kmax) { return kmax <= 2 ? HB_RG2_LOG : (kmax <= 4 ? 10 : 9); }
 template <int KMAX> struct RouteGeom {
   static constexpr uint32_t RG_LOG = route_rg_log(KMAX);
   static constexpr uint32_t RG = 1u << RG_LOG;     // groups per workgroup

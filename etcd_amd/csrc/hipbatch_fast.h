@@ -41,6 +41,7 @@ struct FastLane {
   uint64_t match[NMAX], next[NMAX], head[NMAX];
   uint32_t pm[NMAX];
   uint32_t dirty;
+  uint32_t hv;       // bit s: head[s] holds inflights.buffer[start] of slot s (read lazily)
   uint32_t nev;      // public events emitted (an EVC_BCAST word counts once per slot)
 
   __device__ __forceinline__ uint32_t n() const { return (mlo >> 2) & 7; }
@@ -101,12 +102,16 @@ struct FastLane {
       pm[s] = S.pm[(size_t)s * S.G + g];
     }
 #endif
-#ifdef HB_X_NOHEAD
-#pragma unroll
-    for (int s = 0; s < NMAX; ++s) head[s] = pm_count(pm[s]) ? last : 0;  // diagnostic: no ring read
-#else
+    // The ring heads are loaded with the state (one more round trip, beside
+    // nothing else); free_to reads one lazily if a lane has none.  Loading them
+    // only on demand (-DHB_X_LAZY_HEAD: an ack at or past Next - 1 frees the
+    // whole window unread) measured 1-3 % slower on cfg2 / cfg3 / cfg5.
+#ifndef HB_X_LAZY_HEAD
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) head[s] = pm_count(pm[s]) ? *ring_at(s, pm_start(pm[s])) : 0;
+    hv = (1u << NMAX) - 1;
+#else
+    hv = 0;
 #endif
     dirty = 0;
   }
@@ -163,16 +168,30 @@ struct FastLane {
     if (st == HB_PR_REPLICATE) return pm_count(p) == S.W;
     return true;
   }
-  // inflights.freeTo raft/progress.go:204-224 (head entry from the register copy)
-  // (s is a compile-time constant after the callers' unrolled slot loops)
-  __device__ __forceinline__ void free_to(int s, uint64_t to) {
+  // inflights.freeTo raft/progress.go:204-224 (s is a compile-time constant
+  // after the callers' unrolled slot loops).  nx0 = Next before the ack: in
+  // Replicate every entry is below Next (inflights.add of the last index sent,
+  // then Next = that + 1, raft/raft.go:270-273; Next only grows until the
+  // window is reset), so to >= nx0 - 1 pops the whole window without reading
+  // it; otherwise the head entry comes from the register copy, read once.
+  __device__ __forceinline__ void free_to(int s, uint64_t to, uint64_t nx0) {
     const uint32_t p = pm[s];
     const uint32_t cnt = pm_count(p);
     if (cnt == 0) return;
-    uint64_t v = head[s];
-    if (to < v) return;
     uint32_t idx = pm_start(p);
     const uint32_t W = S.W;
+    if (nx0 != 0 && to >= nx0 - 1) {
+      idx += cnt;
+      if (idx >= W) idx -= W;
+      set_pm(s, pm_make(pm_state(p), pm_paused(p), idx, 0));
+      return;
+    }
+    if (!((hv >> s) & 1u)) {
+      head[s] = *ring_at(s, idx);
+      hv |= 1u << s;
+    }
+    uint64_t v = head[s];
+    if (to < v) return;
     uint32_t i = 0;
     while (true) {
       ++i;
@@ -260,7 +279,10 @@ struct FastLane {
         uint32_t idx = start + cnt;
         if (idx >= S.W) idx -= S.W;
         *ring_at(s, idx) = lastsent;              // inflights.add
-        if (cnt == 0) head[s] = lastsent;
+        if (cnt == 0) {
+          head[s] = lastsent;
+          hv |= 1u << s;
+        }
         next[s] = lastsent + 1;                   // optimisticUpdate
         dirty |= 1u << (D_SLOT0 + s);
         set_pm(s, pm_make(HB_PR_REPLICATE, pm_paused(p), start, cnt + 1));
@@ -358,12 +380,13 @@ struct FastLane {
     for (int s = 0; s < NMAX; ++s) {
       if ((uint32_t)s == from) {
         old_paused = pm_count(pm[s]) == S.W;      // isPaused() in Replicate, before maybeUpdate
+        const uint64_t nx0 = next[s];
         if (next[s] < index + 1) next[s] = index + 1;
         if (match[s] < index) {                   // maybeUpdate raft/progress.go:102-113
           match[s] = index;
           set_pm(s, pm[s] & ~PM_PAUSED);
           updated = true;
-          free_to(s, index);                      // Replicate: ins.freeTo(m.Index)
+          free_to(s, index, nx0);                 // Replicate: ins.freeTo(m.Index)
         }
         dirty |= 1u << (D_SLOT0 + s);
       }

@@ -84,14 +84,26 @@ struct LeadLane : FastLane<NMAX> {
     return S.ring + ((size_t)s * S.W + idx) * S.G + g;
   }
 
-  // inflights.freeTo raft/progress.go:204-224 (head entry from the register copy)
-  __device__ __forceinline__ void free_to(uint32_t s, Pr& p, uint64_t to) const {
+  // inflights.freeTo raft/progress.go:204-224; nx0 = Next before the ack
+  // (FastLane::free_to: to >= nx0 - 1 pops the whole window unread; else the
+  // head entry is read once into the register copy)
+  __device__ __forceinline__ void free_to(uint32_t s, Pr& p, uint64_t to, uint64_t nx0) {
     const uint32_t cnt = pm_count(p.pm);
     if (cnt == 0) return;
-    uint64_t v = p.head;
-    if (to < v) return;
     uint32_t idx = pm_start(p.pm);
     const uint32_t W = S.W;
+    if (nx0 != 0 && to >= nx0 - 1) {
+      idx += cnt;
+      if (idx >= W) idx -= W;
+      p.pm = pm_make(pm_state(p.pm), pm_paused(p.pm), idx, 0);
+      return;
+    }
+    if (!((this->hv >> s) & 1u)) {
+      p.head = *ring_at(s, idx);
+      this->hv |= 1u << s;
+    }
+    uint64_t v = p.head;
+    if (to < v) return;
     uint32_t i = 0;
     while (true) {
       ++i;
@@ -137,7 +149,10 @@ struct LeadLane : FastLane<NMAX> {
         uint32_t idx = start + cnt;
         if (idx >= S.W) idx -= S.W;
         *ring_at(s, idx) = lastsent;  // inflights.add
-        if (cnt == 0) p.head = lastsent;
+        if (cnt == 0) {
+          p.head = lastsent;
+          this->hv |= 1u << s;
+        }
         p.next = lastsent + 1;        // optimisticUpdate
         p.pm = pm_make(HB_PR_REPLICATE, pm_paused(p.pm), start, cnt + 1);
       } else if (st == HB_PR_PROBE) {
@@ -242,6 +257,7 @@ struct LeadLane : FastLane<NMAX> {
         send_one = dec;
       } else {
         old_paused = B::is_paused(p.pm);
+        const uint64_t nx0 = p.next;
         if (p.match < index) {  // maybeUpdate raft/progress.go:102-113
           p.match = index;
           p.pm &= ~PM_PAUSED;
@@ -259,12 +275,17 @@ struct LeadLane : FastLane<NMAX> {
               p.next = umax64(p.match + 1, pend + 1);
             }
           } else {  // ins.freeTo(m.Index)
-            free_to(from, p, index);
+            free_to(from, p, index, nx0);
           }
         }
       }
     } else if (type == HB_MSG_HEARTBEAT_RESP) {  // :547-554
-      if (ps == HB_PR_REPLICATE && pm_count(p.pm) == S.W) free_to(from, p, p.head);  // freeFirstOne
+      if (ps == HB_PR_REPLICATE && pm_count(p.pm) == S.W) {  // freeFirstOne: entries increase, so one pops
+        uint32_t idx = pm_start(p.pm) + 1;
+        if (idx >= S.W) idx -= S.W;
+        p.pm = pm_make(HB_PR_REPLICATE, pm_paused(p.pm), idx, S.W - 1);
+        this->hv &= ~(1u << from);
+      }
       send_one = p.match < last;
     } else if (type == HB_MSG_SNAP_STATUS) {  // :559-574
       if (ps == HB_PR_SNAPSHOT) {
