@@ -94,6 +94,7 @@ HB_FOLLOW_STEP = 0
 HB_FOLLOW_APPEND = 1
 HB_FOLLOW_RESTORE = 2
 HB_EVW_BCAST = 12  # device event word: HB_EV_APP to every slot of a mask
+HB_EVW_VBCAST = 0  # device event word: HB_EV_VOTE to every slot of a mask
 HB_EVW_CONT = 15  # device event word: continuation (x bits 40..63)
 
 # wire ingestion record status (hb_decode)

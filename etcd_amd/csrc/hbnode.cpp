@@ -1035,8 +1035,8 @@ void consume_events(hbn_node* n) {
             e.x = w >> 24;
             if (((w >> 11) & 1u) && i + 1 < end) e.x |= (W[i + 1] >> 4) << 40;
             const uint32_t to = (uint32_t)(w >> 4) & 0x7F;
-            if (type == HB_EVW_BCAST) {  // an HB_EV_APP to every slot of the mask, in slot order
-              e.type = HB_EV_APP;
+            if (type == HB_EVW_BCAST || type == HB_EVW_VBCAST) {  // to every slot of the mask, in slot order
+              e.type = type == HB_EVW_BCAST ? HB_EV_APP : HB_EV_VOTE;
               e.aux = (uint16_t)((w >> 12) & 0xF);
               for (uint32_t s = 0; s < 7; ++s)
                 if ((to >> s) & 1u) {

@@ -2115,7 +2115,7 @@ __global__ void k_get_ins(DevState S, uint32_t g, uint32_t s, uint64_t* vals, ui
 __device__ __forceinline__ uint32_t evc_outputs(uint64_t w) {
   const uint32_t t = (uint32_t)w & 0xF;
   if (t == EVC_CONT) return 0;
-  if (t == EVC_BCAST) return __popc((uint32_t)(w >> 4) & 0x7F);
+  if (t == EVC_BCAST || t == EVC_VBCAST) return __popc((uint32_t)(w >> 4) & 0x7F);
   return 1;
 }
 __global__ void __launch_bounds__(256) k_chunk_events(const uint64_t* base, const uint32_t* counts,
@@ -2159,12 +2159,13 @@ __global__ void __launch_bounds__(256) k_expand_events(const uint64_t* base, con
       uint64_t x = w >> 24;
       if ((w >> 11) & 1u) x |= (src[i + 1] >> 4) << 40;
       hb_event* o = out + run + ex;
-      if (type == EVC_BCAST) {
+      if (type == EVC_BCAST || type == EVC_VBCAST) {
+        const uint8_t et = type == EVC_BCAST ? (uint8_t)HB_EV_APP : (uint8_t)HB_EV_VOTE;
         uint32_t m = to, r = 0;
         while (m) {
           const uint32_t s = __ffs(m) - 1;
           m &= m - 1;
-          o[r++] = hb_event{x, group, (uint8_t)HB_EV_APP, (uint8_t)s, (uint16_t)aux};
+          o[r++] = hb_event{x, group, et, (uint8_t)s, (uint16_t)aux};
         }
       } else {
         o[0] = hb_event{x, group, (uint8_t)type, (uint8_t)to, (uint16_t)aux};
@@ -3452,10 +3453,11 @@ int hb_expand_event_words(const uint64_t* words, uint64_t n_words, const uint32_
       const uint32_t group = (c >> 1) * PART + ((uint32_t)(x0 >> 16) & 0xFF);
       uint64_t x = x0 >> 24;
       if (((x0 >> 11) & 1u) && w + 1 < end) x |= (words[w + 1] >> 4) << 40;
-      if (type == EVC_BCAST) {
+      if (type == EVC_BCAST || type == EVC_VBCAST) {
+        const uint8_t et = type == EVC_BCAST ? (uint8_t)HB_EV_APP : (uint8_t)HB_EV_VOTE;
         for (uint32_t s = 0; s < 7; ++s)
           if ((to >> s) & 1u) {
-            if (out && k < cap) out[k] = hb_event{x, group, (uint8_t)HB_EV_APP, (uint8_t)s, (uint16_t)aux};
+            if (out && k < cap) out[k] = hb_event{x, group, et, (uint8_t)s, (uint16_t)aux};
             ++k;
           }
       } else {

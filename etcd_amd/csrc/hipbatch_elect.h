@@ -182,10 +182,20 @@ struct ElectLane {
       if (q == poll(sf, true)) {
         won++;
         win = true;
-      } else {
+      } else {  // the MsgVotes (slot order) as one EVC_VBCAST word when there are two or more
+        const uint32_t mask = ((1u << nn) - 1) & ~(1u << sf);
+#ifndef HB_X_NO_VBCAST
+        if (mask & (mask - 1)) {
+#else
+        if (false) {
+#endif
+          emit_ev(E, g & (PART - 1), EVC_VBCAST, mask, 0, last);
+          nev += __popc(mask);
+        } else {
 #pragma nounroll
-        for (uint32_t s = 0; s < nn; ++s)
-          if (s != sf) ev(HB_EV_VOTE, s, 0, last);
+          for (uint32_t s = 0; s < nn; ++s)
+            if (s != sf) ev(HB_EV_VOTE, s, 0, last);
+        }
       }
     } else if (state() == HB_STATE_CANDIDATE && type == HB_MSG_VOTE_RESP) {  // :603-612
       const uint32_t gr = poll(from, !reject);

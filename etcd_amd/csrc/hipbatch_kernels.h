@@ -240,6 +240,7 @@ __device__ __forceinline__ void tr_push(const DevState& S, uint32_t g, uint64_t 
 // stream is expanded from them by hb_copy_events, see hipbatch.hip):
 //
 //   [0:4)   type: HB_EV_*, or EVC_BCAST (an HB_EV_APP to every slot in the
+//           mask, same x), or EVC_VBCAST (an HB_EV_VOTE to every slot in the
 //           mask, same x), or EVC_CONT (second word of a long record)
 //   [4:11)  to (slot / node ref), or the slot mask of EVC_BCAST
 //   [11]    long: x >= 2^40, its high 24 bits follow in an EVC_CONT word
@@ -252,6 +253,7 @@ __device__ __forceinline__ void tr_push(const DevState& S, uint32_t g, uint64_t 
 // by every lane from kernel arguments (a global-address-space pointer, so the
 // stores are global_store, not flat) and the fill cursor is one LDS word.
 constexpr uint32_t EVC_BCAST = HB_EVW_BCAST;
+constexpr uint32_t EVC_VBCAST = HB_EVW_VBCAST;  // an HB_EV_VOTE to every slot in the mask, same x
 constexpr uint32_t EVC_CONT = HB_EVW_CONT;
 constexpr uint32_t EVC_WORDS_MAX = 2;  // words per event (long records)
 

@@ -503,8 +503,10 @@ int  hb_step(hb_handle* h, const hb_batch* b, uint32_t flags);
  * at base + chunk_off[c].  A group's events are its words in chunk 2p, then
  * in chunk 2p+1, each in order.  Word format (bit ranges):
  *   [0:4)   type: HB_EV_*; 12 = an HB_EV_APP to every slot of the mask in
- *           `to` (same x and aux), in slot order; 15 = continuation word
- *   [4:11)  to (slot / node ref), or the slot mask of type 12
+ *           `to` (same x and aux), in slot order; 0 = an HB_EV_VOTE to every
+ *           slot of the mask (same x, aux 0: campaign's MsgVotes), in slot
+ *           order; 15 = continuation word
+ *   [4:11)  to (slot / node ref), or the slot mask of types 12 and 0
  *   [11]    x needs 64 bits: the next word is a continuation holding
  *           x bits 40..63 in its bits [4:28)
  *   [12:16) aux
@@ -513,6 +515,7 @@ int  hb_step(hb_handle* h, const hb_batch* b, uint32_t flags);
  * hb_copy_events expands them into hb_event records.  Device pointers; valid
  * until the next hb_step. */
 #define HB_EVW_BCAST 12
+#define HB_EVW_VBCAST 0
 #define HB_EVW_CONT  15
 int  hb_events_device(hb_handle* h, const uint64_t** base, const uint64_t** chunk_off,
                       const uint32_t** counts, uint32_t* n_chunks);
