@@ -1334,6 +1334,9 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
 #ifndef HB_ELECT_WAVES
 #define HB_ELECT_WAVES 4
 #endif
+#ifndef HB_ELECT_PF  // slot messages in flight ahead of the one stepped (1 or 2)
+#define HB_ELECT_PF 1  // measured: 2 neutral on cfg4
+#endif
 #ifndef HB_ELECT_GRID
 #define HB_ELECT_GRID 0  // as HB_GEN_GRID
 #endif
@@ -1403,21 +1406,26 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
       }
       const uint32_t skip = resume & 0x3FFFFFFFu;
       uint32_t x = skip;
-      uint32_t inf_n = 0;
-      uint64_t term_n = 0;
-      if (x < cnt) {
-        const size_t o = (size_t)((perm >> (4 * x)) & 0xF) * a.S.G + g;
-        inf_n = a.slot_info[o];
-        term_n = a.slot_term[o];
-      }
+      // the next HB_ELECT_PF messages' loads are in flight while one is stepped
+      uint32_t inf_n = 0, inf_m = 0;
+      uint64_t term_n = 0, term_m = 0;
+      auto ld = [&](uint32_t y, uint32_t& inf, uint64_t& tm) {
+        const size_t o = (size_t)((perm >> (4 * y)) & 0xF) * a.S.G + g;
+        inf = a.slot_info[o];
+        tm = a.slot_term[o];
+      };
+      if (x < cnt) ld(x, inf_n, term_n);
+      if (HB_ELECT_PF >= 2 && x + 1 < cnt) ld(x + 1, inf_m, term_m);
 #pragma nounroll
       for (; x < cnt; ++x) {
         const uint32_t inf = inf_n;
         const uint64_t mterm = term_n;
-        if (x + 1 < cnt) {  // the next message's loads before this one is stepped
-          const size_t o = (size_t)((perm >> (4 * (x + 1))) & 0xF) * a.S.G + g;
-          inf_n = a.slot_info[o];
-          term_n = a.slot_term[o];
+        if (HB_ELECT_PF >= 2) {
+          inf_n = inf_m;
+          term_n = term_m;
+          if (x + 2 < cnt) ld(x + 2, inf_m, term_m);
+        } else if (x + 1 < cnt) {
+          ld(x + 1, inf_n, term_n);
         }
         const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
         if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
@@ -1460,6 +1468,9 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
 
 #ifndef HB_LEAD_WAVES
 #define HB_LEAD_WAVES 3
+#endif
+#ifndef HB_LEAD_PF  // slot messages in flight ahead of the one stepped (1 or 2)
+#define HB_LEAD_PF 1  // measured: 2 costs 3 % on cfg3 (more scratch)
 #endif
 // ---------------------------------------------------------------------------
 // k_apply_lead (n >= 5, replaces k_apply_fast there): one workgroup per
@@ -1567,26 +1578,31 @@ __global__ void __launch_bounds__(PART, HB_LEAD_WAVES) k_apply_lead(ApplyArgs a)
       resume = 0;
     } else {
       uint32_t x = 0;
-      uint32_t inf_n, orig_n;
-      uint64_t term_n, index_n;
-      {
-        const size_t o = (size_t)(perm & 0xF) * a.S.G + g;
-        inf_n = a.slot_info[o];
-        orig_n = a.slot_orig[o];
-        term_n = a.slot_term[o];
-        index_n = a.slot_index[o];
-      }
+      // the next HB_LEAD_PF messages' loads are in flight while one is stepped
+      uint32_t inf_n = 0, orig_n = 0, inf_m = 0, orig_m = 0;
+      uint64_t term_n = 0, index_n = 0, term_m = 0, index_m = 0;
+      auto ld = [&](uint32_t y, uint32_t& inf, uint32_t& org, uint64_t& tm, uint64_t& ix) {
+        const size_t o = (size_t)((perm >> (4 * y)) & 0xF) * a.S.G + g;
+        inf = a.slot_info[o];
+        org = a.slot_orig[o];
+        tm = a.slot_term[o];
+        ix = a.slot_index[o];
+      };
+      ld(0, inf_n, orig_n, term_n, index_n);
+      if (HB_LEAD_PF >= 2 && 1 < cnt) ld(1, inf_m, orig_m, term_m, index_m);
 #pragma nounroll
       for (; x < cnt; ++x) {
         if (L.faulted()) break;
         const uint32_t inf = inf_n, morig = orig_n;
         const uint64_t mterm = term_n, mindex = index_n;
-        if (x + 1 < cnt) {  // the next message's loads before this one is stepped
-          const size_t o = (size_t)((perm >> (4 * (x + 1))) & 0xF) * a.S.G + g;
-          inf_n = a.slot_info[o];
-          orig_n = a.slot_orig[o];
-          term_n = a.slot_term[o];
-          index_n = a.slot_index[o];
+        if (HB_LEAD_PF >= 2) {
+          inf_n = inf_m;
+          orig_n = orig_m;
+          term_n = term_m;
+          index_n = index_m;
+          if (x + 2 < cnt) ld(x + 2, inf_m, orig_m, term_m, index_m);
+        } else if (x + 1 < cnt) {
+          ld(x + 1, inf_n, orig_n, term_n, index_n);
         }
         const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
         const bool reject = (inf >> 8) & 1u;
