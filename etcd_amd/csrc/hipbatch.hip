@@ -912,8 +912,8 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FastLane<NMAX>& L,
   }
   if (flagged) {
     atomicOr(&l_flag[lane >> 5], 1u << (lane & 31));
-    a.resume[g] = resume | (lead ? 0u : 1u << 30);
-    if (lead) a.commit0[g] = commit0;
+    at32(a.resume, g) = resume | (lead ? 0u : 1u << 30);
+    if (lead) at32(a.commit0, g) = commit0;
   }
   vals[ST_MSGS] = st_msgs;
   vals[ST_APPRESP] = st_msgs;  // every fast message is a MsgAppResp
@@ -968,9 +968,9 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 
   FastLane<NMAX> L;
   L.S = a.S;
   L.g = g;
-  L.mlo = gvalid ? reinterpret_cast<const uint32_t*>(a.S.meta)[2 * (size_t)g] : 0u;
-  const uint32_t prop_raw = (a.props && gvalid) ? a.props[g] : 0u;
-  const uint32_t cnt = gvalid ? a.cnt[g] : 0u;
+  L.mlo = gvalid ? at32(reinterpret_cast<uint32_t*>(a.S.meta), 2 * g) : 0u;
+  const uint32_t prop_raw = (a.props && gvalid) ? at32(a.props, g) : 0u;
+  const uint32_t cnt = gvalid ? at32(a.cnt, g) : 0u;
   // A group takes part when its slot is live (n > 0) and not faulted.
   const bool live = gvalid && L.n() != 0 && L.faulted() == 0;
   // Only a leader has fast-path work: any other live group is handed to
@@ -987,7 +987,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 
   L.last = L.committed = 0;
   L.term = 0;
   if (lead) L.load();
-  else if (NMAX >= 5 && leader) L.term = a.S.term[g];
+  else if (NMAX >= 5 && leader) L.term = at32(a.S.term, g);
   uint32_t s_info[KMAX], s_orig[KMAX];
   uint64_t s_term[KMAX], s_index[KMAX];
   // a leader's used slots, in the state loads' round trip (both wait for meta
@@ -995,13 +995,13 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 
   const bool slots = lead && cnt <= KMAX;
 #pragma unroll
   for (uint32_t k = 0; k < KMAX; ++k) {
-    const size_t o = (size_t)k * a.S.G + g;
+    const uint32_t o = k * a.S.G + g;
     const bool u = slots && k < cnt;
-    s_info[k] = u ? a.slot_info[o] : 0u;
-    s_orig[k] = u ? a.slot_orig[o] : 0u;
+    s_info[k] = u ? at32(a.slot_info, o) : 0u;
+    s_orig[k] = u ? at32(a.slot_orig, o) : 0u;
     // (n >= 5: a busier leader's terms too, for k_elect's step-down test below)
-    s_term[k] = (NMAX >= 5 ? leader && k < cnt : u) ? a.slot_term[o] : 0ull;
-    s_index[k] = u ? a.slot_index[o] : 0ull;
+    s_term[k] = (NMAX >= 5 ? leader && k < cnt : u) ? at32(a.slot_term, o) : 0ull;
+    s_index[k] = u ? at32(a.slot_index, o) : 0ull;
   }
   uint32_t vals[ST_N + 1];
   (void)fast_step<NMAX>(a, L, part, tid, live, lead, leader, prop_raw, cnt, s_info, s_orig, s_term, s_index,
@@ -1626,8 +1626,8 @@ __global__ void __launch_bounds__(PART, HB_LEAD_WAVES) k_apply_lead(ApplyArgs a)
     }
   }
   if (loaded) L.store();
-  // k_elect's candidates: no leader, or a leader a higher term steps down
-  if (flagged && (!leader || higher)) atomicOr(&l_eflag[tid >> 5], 1u << (tid & 31));
+  // k_elect's candidates (n >= 5): no leader, or a leader a higher term steps down
+  if (NMAX >= 5 && flagged && (!leader || higher)) atomicOr(&l_eflag[tid >> 5], 1u << (tid & 31));
   if (flagged) {
     atomicOr(&l_flag[tid >> 5], 1u << (tid & 31));
     a.resume[g] = resume | (loaded ? 0u : 1u << 30);
@@ -1646,9 +1646,9 @@ __global__ void __launch_bounds__(PART, HB_LEAD_WAVES) k_apply_lead(ApplyArgs a)
   reduce_stats(a, l_stats, vals);
   if (tid < FLAG_WORDS) {
     a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
-    a.eflag[(size_t)part * FLAG_WORDS + tid] = l_eflag[tid];
+    if (NMAX >= 5) a.eflag[(size_t)part * FLAG_WORDS + tid] = l_eflag[tid];
   }
-  if (tid == 0) fast_close(a, part, l_flag, l_eflag, l_pfill, l_fill);
+  if (tid == 0) fast_close(a, part, l_flag, NMAX >= 5 ? l_eflag : nullptr, l_pfill, l_fill);
 }
 
 // k_follow: the follower-capable lane (Lane<NMAX, true>) for the groups
@@ -2489,7 +2489,11 @@ template <int NMAX>
 void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
   const uint32_t grid = apply_grid(h);
   if (ev) (void)hipEventRecord(ev[2], h->stream);
+#ifdef HB_X_LEAD3
+  if constexpr (true) hipLaunchKernelGGL(k_apply_lead<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
+#else
   if constexpr (NMAX >= 5) hipLaunchKernelGGL(k_apply_lead<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
+#endif
   else hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
   if (ev) (void)hipEventRecord(ev[3], h->stream);
   if constexpr (NMAX >= 5) {  // the general kernel spills at n >= 5: elections go first

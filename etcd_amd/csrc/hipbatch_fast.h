@@ -66,11 +66,11 @@ struct FastLane {
 
   // All state loads of the lane are independent, so they are in flight together.
   __device__ __forceinline__ void load() {
-    term = S.term[g];
-    committed = S.commit[g];
-    first = S.first[g];
-    last = S.last[g];
-    tfirst = S.tfirst[g];
+    term = at32(S.term, g);
+    committed = at32(S.commit, g);
+    first = at32(S.first, g);
+    last = at32(S.last, g);
+    tfirst = at32(S.tfirst, g);
     // arrays the meta flags mark as not kept are not read (M_TL / M_SM,
     // hipbatch_kernels.h); these loads issue once meta is in, beside the
     // ring heads, which wait for pm anyway
@@ -93,13 +93,13 @@ struct FastLane {
       }
     }
 #else
-    tlast = (mlo & (uint32_t)M_TL) ? last : S.tlast[g];
+    tlast = (mlo & (uint32_t)M_TL) ? last : at32(S.tlast, g);
     const uint32_t sf = (mlo & (uint32_t)M_SM) ? self() : 0xFFu;
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) {
-      match[s] = ((uint32_t)s == sf) ? last : S.match[(size_t)s * S.G + g];
-      next[s] = ((uint32_t)s == sf) ? last + 1 : S.next[(size_t)s * S.G + g];
-      pm[s] = S.pm[(size_t)s * S.G + g];
+      match[s] = ((uint32_t)s == sf) ? last : at32(S.match, s * S.G + g);
+      next[s] = ((uint32_t)s == sf) ? last + 1 : at32(S.next, s * S.G + g);
+      pm[s] = at32(S.pm, s * S.G + g);
     }
 #endif
     // The ring heads are loaded with the state (one more round trip, beside
@@ -142,18 +142,18 @@ struct FastLane {
         dirty |= D_META | (1u << (D_SLOT0 + s0));
       }
     }
-    if (dirty & D_META) reinterpret_cast<uint32_t*>(S.meta)[2 * (size_t)g] = mlo;  // little-endian low word
-    if (dirty & D_COMMIT) S.commit[g] = committed;
-    if (dirty & D_LAST) S.last[g] = last;
-    if (dirty & D_TFIRST) S.tfirst[g] = tfirst;
-    if ((dirty & D_TRUN) && !tl) S.tlast[g] = tlast;
+    if (dirty & D_META) at32(reinterpret_cast<uint32_t*>(S.meta), 2 * g) = mlo;  // little-endian low word
+    if (dirty & D_COMMIT) at32(S.commit, g) = committed;
+    if (dirty & D_LAST) at32(S.last, g) = last;
+    if (dirty & D_TFIRST) at32(S.tfirst, g) = tfirst;
+    if ((dirty & D_TRUN) && !tl) at32(S.tlast, g) = tlast;
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) {
       if ((dirty & (1u << (D_SLOT0 + s))) && (uint32_t)s != sf) {
-        S.match[(size_t)s * S.G + g] = match[s];
-        S.next[(size_t)s * S.G + g] = next[s];
+        at32(S.match, s * S.G + g) = match[s];
+        at32(S.next, s * S.G + g) = next[s];
       }
-      if (dirty & (1u << (D_PM0 + s))) S.pm[(size_t)s * S.G + g] = pm[s];
+      if (dirty & (1u << (D_PM0 + s))) at32(S.pm, s * S.G + g) = pm[s];
     }
   }
   __device__ __forceinline__ void set_pm(int s, uint32_t v) {

@@ -109,6 +109,20 @@ struct DevState {
   uint64_t bn;                // hb_batch.n
 };
 
+// Element i of a device array addressed by a 32-bit byte offset from the
+// array's (uniform) base: one global_load / global_store with an SGPR base and a
+// 32-bit VGPR offset instead of a 64-bit address per lane.  For the [G] and
+// [slot][G] arrays (at most 8 x 2^24 x 8 B = 1 GiB, hb_create caps capacity at
+// 2^24), not for the inflight rings.
+template <class T>
+__device__ __forceinline__ T& at32(T* base, uint32_t i) {
+  return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + i * (uint32_t)sizeof(T));
+}
+template <class T>
+__device__ __forceinline__ const T& at32(const T* base, uint32_t i) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + i * (uint32_t)sizeof(T));
+}
+
 // ---- log-pool extents ------------------------------------------------------------
 constexpr uint64_t LX_TAG = 0x3F;  // low bits of an extent word: log2(capacity)
 __host__ __device__ inline uint64_t lx_word(uint64_t addr, uint32_t log2cap) { return addr | log2cap; }
