@@ -680,6 +680,42 @@ __device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_sta
     atomicAdd((unsigned long long*)&a.stats_shard[shard_at(tid, blockIdx.x & (NSH - 1))], (unsigned long long)v);
 }
 
+// The fast and leader kernels' lane statistics are small per-lane counts
+// (messages, responses, drops: at most the route slots; commits, faults: 0 or
+// 1): four 16-bit fields per word keep a wave's sums exact (< 2^16 while each
+// lane's count is < 1024), so ten values take four wave reductions, not ten.
+#ifndef HB_X_WIDE_STATS
+template <>
+__device__ __forceinline__ void reduce_stats<uint32_t>(const ApplyArgs& a, uint64_t* l_stats,
+                                                       const uint32_t (&vals)[ST_N + 1]) {
+  const uint32_t tid = threadIdx.x;
+  uint64_t w[4] = {(uint64_t)vals[ST_MSGS] | (uint64_t)vals[ST_APPRESP] << 16 | (uint64_t)vals[ST_DROPPED] << 32 |
+                       (uint64_t)vals[ST_COMMITS] << 48,
+                   (uint64_t)vals[ST_VOTERESP] | (uint64_t)vals[ST_WON] << 16 | (uint64_t)vals[ST_LOST] << 32 |
+                       (uint64_t)vals[ST_FAULTS] << 48,
+                   (uint64_t)vals[ST_ENTRIES], (uint64_t)vals[ST_N]};
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) w[k] += __shfl_xor(w[k], d);
+  if ((tid & 63) == 0) {
+    const uint64_t v[ST_N + 1] = {w[0] & 0xFFFF, (w[0] >> 16) & 0xFFFF, w[1] & 0xFFFF, (w[0] >> 32) & 0xFFFF,
+                                  w[0] >> 48,    (w[1] >> 16) & 0xFFFF, (w[1] >> 32) & 0xFFFF, w[1] >> 48,
+                                  w[2],          w[3]};
+    static_assert(ST_MSGS == 0 && ST_APPRESP == 1 && ST_VOTERESP == 2 && ST_DROPPED == 3 && ST_COMMITS == 4 &&
+                      ST_WON == 5 && ST_LOST == 6 && ST_FAULTS == 7 && ST_ENTRIES == 8 && ST_N == 9,
+                  "the unpacking above follows the ST_ order");
+#pragma unroll
+    for (int k = 0; k <= ST_N; ++k)
+      if (v[k]) atomicAdd((unsigned long long*)&l_stats[k], (unsigned long long)v[k]);
+  }
+  __syncthreads();
+  const uint64_t v = tid <= ST_N ? l_stats[tid] : 0ull;
+  if (tid <= ST_N && v)
+    atomicAdd((unsigned long long*)&a.stats_shard[shard_at(tid, blockIdx.x & (NSH - 1))], (unsigned long long)v);
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // k_route<KMAX>: W = BK / RG workgroups per bucket, each owning RG groups
 // (RG x KMAX message slots fit in LDS: RG = 2048 / 1024 / 512 for KMAX =
