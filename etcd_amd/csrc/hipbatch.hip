@@ -1553,23 +1553,26 @@ __global__ void __launch_bounds__(PART, HB_LEAD_WAVES) k_apply_lead(ApplyArgs a)
   L.last = L.committed = 0;
   L.term = 0;
   if (spec) L.load();
-  uint32_t key[KS];
-  uint32_t perm = 0;
   const bool slots = leader && fits;
-#pragma unroll
-  for (uint32_t k = 0; k < KS; ++k) {
-    key[k] = (slots && k < cnt) ? a.slot_orig[(size_t)k * a.S.G + g] : 0xFFFFFFFFu;
-    perm |= k << (4 * k);
-  }
   bool loaded = spec, higher = false;
   if (slots && !spec) {  // a busy leader without a proposal: load it unless a higher term steps it down
-    const uint64_t t = a.S.term[g];
+    const uint64_t t = at32(a.S.term, g);
 #pragma unroll
-    for (uint32_t k = 0; k < KS; ++k) higher |= k < cnt && a.slot_term[(size_t)k * a.S.G + g] > t;
+    for (uint32_t k = 0; k < KS; ++k) higher |= k < cnt && at32(a.slot_term, k * a.S.G + g) > t;
     if (!higher) {
       L.load();
       loaded = true;
     }
+  }
+  // the slots' arrival indices, only for a group this kernel steps (an election
+  // storm's leaders go to k_elect without them)
+  uint32_t key[KS];
+  uint32_t perm = 0;
+  const bool keys = slots && loaded;
+#pragma unroll
+  for (uint32_t k = 0; k < KS; ++k) {
+    key[k] = (keys && k < cnt) ? at32(a.slot_orig, k * a.S.G + g) : 0xFFFFFFFFu;
+    perm |= k << (4 * k);
   }
   // arrival order of the slots (odd-even transposition, slot numbers as nibbles)
 #pragma unroll
