@@ -2048,10 +2048,11 @@ __global__ void k_gather(DevState S, uint32_t first, uint32_t count, hb_group* d
   r.votes_grant = m_grant(m);
   for (uint32_t s = 0; s < S.nmax && s < r.n; ++s) {
     const size_t o = (size_t)s * S.G + g;
-    const uint32_t p = S.pm[o];
+    uint32_t p = S.pm[o];
     const bool kept = !((m & M_SM) && s == r.self_slot);  // M_SM: materialized from last
     r.pr[s].match = kept ? S.match[o] : r.last_index;
     r.pr[s].next = kept ? S.next[o] : r.last_index + 1;
+    if (m & M_RS) rs_progress(m, s, r.last_index, r.term_first, &r.pr[s].match, &r.pr[s].next, &p);
     r.pr[s].state = pm_state(p);
     r.pr[s].paused = pm_paused(p);
     r.pr[s].ins_start = pm_start(p);
@@ -2142,6 +2143,21 @@ __global__ void k_set_ins(DevState S, uint32_t g, uint32_t s, uint32_t start, ui
     S.ring[((size_t)s * S.W + idx) * S.G + g] = vals[i];
   }
   if (threadIdx.x == 0) {
+    const uint64_t m = S.meta[g];
+    if (m & M_RS) {  // the reset form written out first: this slot's window changes alone
+      for (uint32_t k = 0; k < m_n(m); ++k) {
+        const size_t ok = (size_t)k * S.G + g;
+        uint64_t mt, nx;
+        uint32_t pk;
+        rs_progress(m, k, S.last[g], S.tfirst[g], &mt, &nx, &pk);
+        if (!((m & M_SM) && k == m_self(m))) {
+          S.match[ok] = mt;
+          S.next[ok] = nx;
+        }
+        S.pm[ok] = pk;
+      }
+      S.meta[g] = m & ~M_RS;
+    }
     const size_t o = (size_t)s * S.G + g;
     const uint32_t p = S.pm[o];
     S.pm[o] = pm_make(pm_state(p), pm_paused(p), start, count);
@@ -2150,7 +2166,7 @@ __global__ void k_set_ins(DevState S, uint32_t g, uint32_t s, uint32_t start, ui
 
 __global__ void k_get_ins(DevState S, uint32_t g, uint32_t s, uint64_t* vals, uint32_t* sc) {
   const size_t o = (size_t)s * S.G + g;
-  const uint32_t p = S.pm[o];
+  const uint32_t p = (S.meta[g] & M_RS) ? 0u : S.pm[o];  // the reset form: an empty window
   const uint32_t start = pm_start(p), count = pm_count(p);
   for (uint32_t i = threadIdx.x; i < count; i += blockDim.x) {
     uint32_t idx = start + i;

@@ -84,7 +84,13 @@ struct ElectLane {
     // reset form: the self slot's Match = lastIndex, Next = lastIndex + 1 (the
     // noop's maybeUpdate keeps both so); as loaded, nothing touched it
     const bool sm = rst ? sf < nn : (meta0 & M_SM) != 0;
-    const uint64_t m2 = (meta & ~(M_TL | M_SM)) | (tl ? M_TL : 0ull) | (sm ? M_SM : 0ull);
+    // after a reset the n Progress entries are the reset form: M_RS instead of n x 20 bytes, when
+    // rs_progress derives this reset's lastIndex (a leader's noop opened its term: tfirst = rlast + 1)
+    // and its pauses (a leader with peers sent to them); otherwise they are written out
+    const bool leader = state() == HB_STATE_LEADER;
+    const bool rs = rst && (leader ? (tfirst == rlast + 1 && (sent || nn <= 1)) : (rlast == last && !sent));
+    const uint64_t m2 = (meta & ~(M_TL | M_SM | M_RS)) | (tl ? M_TL : 0ull) | (sm ? M_SM : 0ull) |
+                        (rs ? M_RS : (rst ? 0ull : (meta & M_RS)));
     if (m2 != meta) {
       meta = m2;
       dirty |= D_META;
@@ -99,7 +105,7 @@ struct ElectLane {
       S.tlast[g] = tlast;
     }
     if (dirty & D_ELAPSED) S.elapsed[g] = 0;
-    if (rst) {
+    if (rst && !rs) {
       const uint32_t peer_pm = pm_make(HB_PR_PROBE, sent ? 1u : 0u, 0, 0);
 #pragma unroll
       for (int s = 0; s < NMAX; ++s) {

@@ -102,6 +102,20 @@ struct FastLane {
       pm[s] = at32(S.pm, s * S.G + g);
     }
 #endif
+    if (mlo & (uint32_t)M_RS) {  // a group k_elect left in the reset form: every slot written back
+      const uint32_t nn = n();
+#pragma unroll
+      for (int s = 0; s < NMAX; ++s) {
+        if ((uint32_t)s < nn) {
+          uint64_t mt, nx;
+          uint32_t p;
+          rs_progress(mlo, (uint32_t)s, last, tfirst, &mt, &nx, &p);
+          match[s] = mt;
+          next[s] = nx;
+          pm[s] = p;
+        }
+      }
+    }
     // The ring heads are loaded with the state (one more round trip, beside
     // nothing else); free_to reads one lazily if a lane has none.  Loading them
     // only on demand (-DHB_X_LAZY_HEAD: an ack at or past Next - 1 frees the
@@ -114,6 +128,13 @@ struct FastLane {
     hv = 0;
 #endif
     dirty = 0;
+    if (mlo & (uint32_t)M_RS) {
+      mlo &= ~(uint32_t)M_RS;
+      dirty |= D_META;
+#pragma unroll
+      for (int s = 0; s < NMAX; ++s)
+        if ((uint32_t)s < n()) dirty |= (1u << (D_SLOT0 + s)) | (1u << (D_PM0 + s));
+    }
   }
   // Dirty bits (hipbatch_kernels.h) plus, lane-local to the fast path:
   // D_TFIRST (tfirst alone; D_TRUN then means tlast) and per-slot D_PM0 + s

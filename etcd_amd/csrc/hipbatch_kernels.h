@@ -46,6 +46,15 @@ __host__ __device__ inline uint64_t meta_make(uint32_t state, uint32_t n, uint32
 }
 constexpr uint64_t M_TL = 1ull << 21;
 constexpr uint64_t M_SM = 1ull << 22;
+// M_RS: every Progress is in the form an election leaves it (k_elect does not
+// write the n entries): reset (raft/raft.go:334-349) at lastIndex rl — Match 0,
+// Next rl + 1, Probe, an empty window; the self slot Match = lastIndex, Next =
+// lastIndex + 1 (M_SM) — plus, for a leader, becomeLeader's noop at rl + 1 (so
+// rl = tfirst - 1) and bcastAppend's pause of every peer (:406-427, :239-282).
+// A non-leader's rl is its lastIndex (anything that moves a follower's
+// lastIndex loads its Progress first).  Readers materialize it (rs_progress),
+// writers of Progress clear it.
+constexpr uint64_t M_RS = 1ull << 23;
 __host__ __device__ inline uint32_t m_state(uint64_t m) { return (uint32_t)(m & 3); }
 __host__ __device__ inline uint32_t m_n(uint64_t m) { return (uint32_t)((m >> 2) & 7); }
 __host__ __device__ inline uint32_t m_self(uint64_t m) { return (uint32_t)((m >> 5) & 0xF); }
@@ -65,6 +74,17 @@ __host__ __device__ inline uint32_t pm_paused(uint32_t p) { return (p >> 2) & 1;
 __host__ __device__ inline uint32_t pm_start(uint32_t p) { return (p >> 3) & 0x3FF; }
 __host__ __device__ inline uint32_t pm_count(uint32_t p) { return (p >> 13) & 0x7FF; }
 constexpr uint32_t PM_PAUSED = 1u << 2;
+
+// Slot s's Progress under M_RS (meta m, the group's lastIndex and term_first).
+__device__ __forceinline__ void rs_progress(uint64_t m, uint32_t s, uint64_t last, uint64_t tfirst, uint64_t* match,
+                                            uint64_t* next, uint32_t* pm) {
+  const bool leader = m_state(m) == HB_STATE_LEADER;
+  const uint64_t rl = leader ? tfirst - 1 : last;
+  const bool me = s == m_self(m);
+  *match = me ? last : 0ull;
+  *next = me ? last + 1 : rl + 1;
+  *pm = pm_make(HB_PR_PROBE, (!me && leader) ? 1u : 0u, 0, 0);
+}
 
 // ---- device state (SoA in HBM) -------------------------------------------------
 struct DevState {
@@ -465,6 +485,23 @@ struct Lane {
       next[s] = S.next[(size_t)s * S.G + g];
       pm[s] = S.pm[(size_t)s * S.G + g];
     }
+    if (meta & M_RS) {  // the reset form (every slot rewritten by store)
+      const uint32_t nn = n();
+#pragma unroll
+      for (int s = 0; s < NMAX; ++s) {
+        if ((uint32_t)s < nn) {
+          uint64_t mt, nx;
+          uint32_t p;
+          rs_progress(meta, (uint32_t)s, last, tfirst, &mt, &nx, &p);
+          match[s] = mt;
+          next[s] = nx;
+          pm[s] = p;
+          dirty |= 1u << (D_SLOT0 + s);
+        }
+      }
+      meta &= ~M_RS;
+      dirty |= D_META;
+    }
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) head[s] = pm_count(pm[s]) ? *ring_at(s, pm_start(pm[s])) : 0;
     if (meta0 & M_SM) {  // as loaded: the self arrays are stale, last (unchanged so far) is their value
@@ -702,6 +739,7 @@ struct Lane {
         dirty |= 1u << (D_SLOT0 + s);
       }
     }
+    if (meta & M_RS) set_field(23, 1, 0);  // every slot is written
     prog = true;
   }
   // becomeFollower :384-391 / becomeCandidate :393-404 / becomeLeader :406-427.
@@ -886,6 +924,7 @@ struct Lane {
             dirty |= 1u << (D_SLOT0 + s);
           }
         }
+        if (meta & M_RS) set_field(23, 1, 0);  // every slot is written
         prog = true;
         if (sz_on(S.max_msg_size)) {
           S.szlo[g] = sidx;
