@@ -179,24 +179,39 @@ __device__ __forceinline__ uint32_t excl_scan256(uint32_t v, uint32_t* sh4, uint
   return before + incl - v;
 }
 
+// Per-tile digit counts, HIST_TPB tiles per workgroup: every group id of the
+// workgroup's tiles is loaded at once (more loads in flight per lane than one
+// 2048-message tile gives), then counted tile by tile in LDS.
+#ifndef HB_HIST_TPB
+#define HB_HIST_TPB 4
+#endif
+constexpr uint32_t HIST_TPB = HB_HIST_TPB;
 __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t G, uint32_t shift, uint32_t ntiles,
                                                            uint32_t* hist) {
-  __shared__ uint32_t cnt[RDX_BINS];
+  __shared__ uint32_t cnt[HIST_TPB][RDX_BINS];
   const uint32_t tid = threadIdx.x;
-  if (tid < RDX_BINS) cnt[tid] = 0;
+  for (uint32_t i = tid; i < HIST_TPB * RDX_BINS; i += RDX_THREADS) (&cnt[0][0])[i] = 0;
   __syncthreads();
   const uint32_t n = src_n(s);
-  const uint32_t base = blockIdx.x * RDX_TILE;
+  const uint32_t t0 = blockIdx.x * HIST_TPB;
+  uint32_t gv[HIST_TPB][RDX_ROUNDS];
 #pragma unroll
-  for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
-    const uint32_t i = base + r * RDX_THREADS + tid;
-    if (i < n) {
-      const uint32_t g = s.group[i];
-      if (g < G) atomicAdd(&cnt[rdx_digit(g, shift)], 1u);
+  for (uint32_t t = 0; t < HIST_TPB; ++t)
+#pragma unroll
+    for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+      const uint32_t i = (t0 + t) * RDX_TILE + r * RDX_THREADS + tid;
+      gv[t][r] = i < n ? s.group[i] : 0xFFFFFFFFu;
     }
-  }
+#pragma unroll
+  for (uint32_t t = 0; t < HIST_TPB; ++t)
+#pragma unroll
+    for (uint32_t r = 0; r < RDX_ROUNDS; ++r)
+      if (gv[t][r] < G) atomicAdd(&cnt[t][rdx_digit(gv[t][r], shift)], 1u);
   __syncthreads();
-  if (tid < RDX_BINS) hist[(size_t)blockIdx.x * RDX_BINS + tid] = cnt[tid];  // [tile][digit]: one 1 KB row per tile
+  for (uint32_t i = tid; i < HIST_TPB * RDX_BINS; i += RDX_THREADS) {
+    const uint32_t t = i / RDX_BINS;
+    if (t0 + t < ntiles) hist[(size_t)(t0 + t) * RDX_BINS + (i % RDX_BINS)] = (&cnt[0][0])[i];  // [tile][digit]
+  }
 }
 
 // Column scan: workgroup b turns column d of hist ([ntiles][RDX_BINS] tile
@@ -205,6 +220,10 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t
 // scanned by workgroups of one XCD (blockIdx % 8), so each line is fetched
 // into one L2 once.  It also clears the per-bucket event-chunk cursors for
 // the coming apply.
+#ifndef HB_SCAN_PER
+#define HB_SCAN_PER 16
+#endif
+constexpr uint32_t SCAN_PER = HB_SCAN_PER;
 __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t ntiles, uint32_t* totals,
                                                     uint32_t* bk_fill, uint32_t NBK, uint32_t* ctr) {
   __shared__ uint32_t sh16[16];
@@ -213,16 +232,20 @@ __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t nti
   for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < NBK; i += gridDim.x * 1024) bk_fill[i * CTR_STRIDE] = 0;
   if (blockIdx.x == 0)
     for (uint32_t i = threadIdx.x; i < CTR_WORDS; i += blockDim.x) ctr[i] = 0;
+  // SCAN_PER consecutive tiles per lane, all loads of a chunk in flight at once
   uint32_t carry = 0;
-  for (uint32_t base = 0; base < ntiles; base += 4096) {
-    const uint32_t i0 = base + threadIdx.x * 4;
-    uint32_t v[4];
+  for (uint32_t base = 0; base < ntiles; base += 1024 * SCAN_PER) {
+    const uint32_t i0 = base + threadIdx.x * SCAN_PER;
+    uint32_t v[SCAN_PER], sum = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = i0 + k < ntiles ? col[(size_t)(i0 + k) * RDX_BINS] : 0u;
+    for (uint32_t k = 0; k < SCAN_PER; ++k) {
+      v[k] = i0 + k < ntiles ? col[(size_t)(i0 + k) * RDX_BINS] : 0u;
+      sum += v[k];
+    }
     uint32_t tot;
-    uint32_t run = carry + block_excl_scan(v[0] + v[1] + v[2] + v[3], sh16, &tot);
+    uint32_t run = carry + block_excl_scan(sum, sh16, &tot);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (uint32_t k = 0; k < SCAN_PER; ++k) {
       if (i0 + k < ntiles) col[(size_t)(i0 + k) * RDX_BINS] = run;
       run += v[k];
     }
@@ -3344,7 +3367,8 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
       const bool last_pass = p + 1 == h->passes;
       const RadixDst& dst = h->tmp[p & 1];
       const uint32_t shift = PART_LOG + h->sis_log + p * RDX_BITS;
-      hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, h->G, shift, ntiles, h->hist);
+      hipLaunchKernelGGL(k_radix_hist, dim3((ntiles + HIST_TPB - 1) / HIST_TPB), dim3(RDX_THREADS), 0, ps_st, src, h->G,
+                         shift, ntiles, h->hist);
       hipLaunchKernelGGL(k_scan_rows, dim3(RDX_BINS), dim3(1024), 0, ps_st, h->hist, ntiles, h->totals, ps.bk_fill,
                          h->NBK, ps.ctr);
       if (last_pass)
