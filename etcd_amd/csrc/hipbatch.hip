@@ -1528,6 +1528,9 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
 #ifndef HB_LEAD_WAVES
 #define HB_LEAD_WAVES 3
 #endif
+#ifndef HB_LEAD7_WAVES  // k_apply_lead<7> (measured on cfg4: 2 waves +3 %, 4 waves -0.6 % with 128 B/lane of scratch)
+#define HB_LEAD7_WAVES 3
+#endif
 #ifndef HB_LEAD_PF  // slot messages in flight ahead of the one stepped (1 or 2)
 #define HB_LEAD_PF 1  // measured: 2 costs 3 % on cfg3 (more scratch)
 #endif
@@ -1545,7 +1548,7 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
 // them it is handed over unloaded.
 // ---------------------------------------------------------------------------
 template <int NMAX>
-__global__ void __launch_bounds__(PART, HB_LEAD_WAVES) k_apply_lead(ApplyArgs a) {
+__global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAVES) k_apply_lead(ApplyArgs a) {
   constexpr uint32_t KS = route_kmax(NMAX);
   __shared__ uint32_t l_fill, l_pfill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
