@@ -125,6 +125,13 @@ constexpr uint32_t RDX_BINS = 1u << RDX_BITS;
 constexpr uint32_t RDX_THREADS = HB_RDX_THREADS;
 constexpr uint32_t RDX_WAVES = RDX_THREADS / 64;
 constexpr uint32_t RDX_ROUNDS = HB_RDX_ROUNDS;
+#ifndef HB_RDX_SPLIT  // 0: the first of two passes takes a full 8-bit digit
+#define HB_RDX_SPLIT 1
+#endif
+#ifndef HB_RDX_SKEW  // first-pass bits = bucket bits / 2 + skew
+#define HB_RDX_SKEW 0
+#endif
+constexpr bool RDX_SPLIT = HB_RDX_SPLIT != 0;
 constexpr uint32_t RDX_TILE = RDX_THREADS * RDX_ROUNDS;  // 2048
 
 struct MsgRec {      // apply input record (24 B)
@@ -163,7 +170,10 @@ struct FinalDst {  // final pass output = apply input
 
 __device__ __forceinline__ uint32_t src_n(const RadixSrc& s) { return s.n_dev ? *s.n_dev : s.n; }
 // shift = the bucket's log2 size + the pass's digit offset
-__device__ __forceinline__ uint32_t rdx_digit(uint32_t g, uint32_t shift) { return (g >> shift) & (RDX_BINS - 1); }
+// dbits = the pass's digit width (<= RDX_BITS; the first of two passes takes half the bits)
+__device__ __forceinline__ uint32_t rdx_digit(uint32_t g, uint32_t shift, uint32_t dbits) {
+  return (g >> shift) & ((1u << dbits) - 1u);
+}
 
 // Exclusive scan over the first 256 threads of the block (all threads call it).
 __device__ __forceinline__ uint32_t excl_scan256(uint32_t v, uint32_t* sh4, uint32_t* total) {
@@ -186,8 +196,8 @@ __device__ __forceinline__ uint32_t excl_scan256(uint32_t v, uint32_t* sh4, uint
 #define HB_HIST_TPB 4
 #endif
 constexpr uint32_t HIST_TPB = HB_HIST_TPB;
-__global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t G, uint32_t shift, uint32_t ntiles,
-                                                           uint32_t* hist) {
+__global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t G, uint32_t shift, uint32_t dbits,
+                                                           uint32_t ntiles, uint32_t* hist) {
   __shared__ uint32_t cnt[HIST_TPB][RDX_BINS];
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < HIST_TPB * RDX_BINS; i += RDX_THREADS) (&cnt[0][0])[i] = 0;
@@ -206,7 +216,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t
   for (uint32_t t = 0; t < HIST_TPB; ++t)
 #pragma unroll
     for (uint32_t r = 0; r < RDX_ROUNDS; ++r)
-      if (gv[t][r] < G) atomicAdd(&cnt[t][rdx_digit(gv[t][r], shift)], 1u);
+      if (gv[t][r] < G) atomicAdd(&cnt[t][rdx_digit(gv[t][r], shift, dbits)], 1u);
   __syncthreads();
   for (uint32_t i = tid; i < HIST_TPB * RDX_BINS; i += RDX_THREADS) {
     const uint32_t t = i / RDX_BINS;
@@ -256,7 +266,7 @@ __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t nti
 
 template <bool FINAL>
 __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, RadixDst d, FinalDst f, uint32_t G,
-                                                              uint32_t shift, uint32_t ntiles, const uint32_t* off,
+                                                              uint32_t shift, uint32_t dbits, uint32_t ntiles, const uint32_t* off,
                                                               const uint32_t* totals, uint32_t* n_valid) {
   __shared__ uint32_t s_off[RDX_BINS];
   __shared__ uint32_t s_wcnt[RDX_WAVES][RDX_BINS];
@@ -313,7 +323,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
       vt[r] = vv[r] ? s.term[i] : 0ull;
       vx[r] = vv[r] ? s.index[i] : 0ull;
     }
-    vd[r] = rdx_digit(vg[r], shift);
+    vd[r] = rdx_digit(vg[r], shift, dbits);
   }
   // stable rank inside the wave: rounds in order, lanes in order
 #pragma unroll
@@ -321,6 +331,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
     uint64_t peers = __ballot(vv[r]);
 #pragma unroll
     for (uint32_t k = 0; k < RDX_BITS; ++k) {
+      if (k >= dbits) break;
       const bool bit = (vd[r] >> k) & 1u;
       const uint64_t bk = __ballot(bit);
       peers &= bit ? bk : ~bk;
@@ -366,7 +377,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
     const uint32_t p = r * RDX_THREADS + tid;
     if (p < valid) {
       const uint32_t g = st_group[p];
-      const uint32_t dg = rdx_digit(g, shift);
+      const uint32_t dg = rdx_digit(g, shift, dbits);
       const uint32_t o = s_off[dg] + (p - s_dstart[dg]);
       if (FINAL) {
         MsgRec m;
@@ -2404,6 +2415,7 @@ struct hb_handle {
   uint32_t NBK = 0;               // buckets
   uint32_t sis_log = SIS_LOG_MAX;  // partitions per bucket (log2)
   uint32_t passes = 1;
+  uint32_t bk_bits = 1;            // bits of a bucket id
   // host-pointer staging
   uint32_t* s_group = nullptr;
   uint32_t* s_info = nullptr;
@@ -2676,6 +2688,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
 #endif
   h->NBK = nbk_for(h->sis_log);
   h->passes = passes_for(h->sis_log);
+  h->bk_bits = std::max<uint32_t>(ceil_log2(h->NBK), 1);
   const size_t tiles_max = (mb + RDX_TILE - 1) / RDX_TILE;
   ALLOC(h->hist, (size_t)RDX_BINS * tiles_max);
   ALLOC(h->n_valid, 4);
@@ -3366,21 +3379,26 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     const uint32_t ntiles = (uint32_t)((b->n + RDX_TILE - 1) / RDX_TILE);
     RadixSrc src{bd.group, bd.info, bd.term, bd.index, nullptr, nullptr, (uint32_t)b->n};
     const FinalDst fin{ps.rec, ps.bucket, h->passes == 1 ? ps.bk_off : nullptr, h->NBK, h->sis_log};
+    uint32_t shift = PART_LOG + h->sis_log;
     for (uint32_t p = 0; p < h->passes; ++p) {
       const bool last_pass = p + 1 == h->passes;
       const RadixDst& dst = h->tmp[p & 1];
-      const uint32_t shift = PART_LOG + h->sis_log + p * RDX_BITS;
+      // two passes split the bucket id's bits evenly (the first takes the low
+      // half): 5 + 5 bits for 1,024 buckets write 64-message digit runs in both
+      // passes, where 8 + 2 wrote 8-message runs (partial lines) in the first
+      const uint32_t dbits = last_pass ? RDX_BITS : RDX_SPLIT ? h->bk_bits / 2 + HB_RDX_SKEW : RDX_BITS;
       hipLaunchKernelGGL(k_radix_hist, dim3((ntiles + HIST_TPB - 1) / HIST_TPB), dim3(RDX_THREADS), 0, ps_st, src, h->G,
-                         shift, ntiles, h->hist);
+                         shift, dbits, ntiles, h->hist);
       hipLaunchKernelGGL(k_scan_rows, dim3(RDX_BINS), dim3(1024), 0, ps_st, h->hist, ntiles, h->totals, ps.bk_fill,
                          h->NBK, ps.ctr);
       if (last_pass)
         hipLaunchKernelGGL(k_radix_scatter<true>, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
-                           shift, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
+                           shift, dbits, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
       else
         hipLaunchKernelGGL(k_radix_scatter<false>, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
-                           shift, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
+                           shift, dbits, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
       src = RadixSrc{dst.group, nullptr, nullptr, nullptr, dst.rec, h->n_valid, (uint32_t)b->n};
+      shift += dbits;
     }
     if (h->passes > 1)
       hipLaunchKernelGGL(k_bucket_bounds, dim3((h->NBK + 1 + 255) / 256), dim3(256), 0, ps_st,
