@@ -218,13 +218,14 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t
     for (uint32_t r = 0; r < RDX_ROUNDS; ++r)
       if (gv[t][r] < G) atomicAdd(&cnt[t][rdx_digit(gv[t][r], shift, dbits)], 1u);
   __syncthreads();
-  for (uint32_t i = tid; i < HIST_TPB * RDX_BINS; i += RDX_THREADS) {
-    const uint32_t t = i / RDX_BINS;
-    if (t0 + t < ntiles) hist[(size_t)(t0 + t) * RDX_BINS + (i % RDX_BINS)] = (&cnt[0][0])[i];  // [tile][digit]
+  const uint32_t nb = 1u << dbits;  // row width: the pass's digits only
+  for (uint32_t i = tid; i < (HIST_TPB << dbits); i += RDX_THREADS) {
+    const uint32_t t = i >> dbits, dg = i & (nb - 1);
+    if (t0 + t < ntiles) hist[((size_t)(t0 + t) << dbits) + dg] = cnt[t][dg];  // [tile][digit]
   }
 }
 
-// Column scan: workgroup b turns column d of hist ([ntiles][RDX_BINS] tile
+// Column scan: workgroup b turns column d of hist ([ntiles][nb] tile
 // counts) into exclusive per-tile prefixes and writes the column total to
 // totals[d].  The 32 digits of one 128-byte line of every tile row are
 // scanned by workgroups of one XCD (blockIdx % 8), so each line is fetched
@@ -234,10 +235,11 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t
 #define HB_SCAN_PER 16
 #endif
 constexpr uint32_t SCAN_PER = HB_SCAN_PER;
-__global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t ntiles, uint32_t* totals,
+__global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t ntiles, uint32_t dbits, uint32_t* totals,
                                                     uint32_t* bk_fill, uint32_t NBK, uint32_t* ctr) {
   __shared__ uint32_t sh16[16];
-  const uint32_t d = (blockIdx.x & 7) * (RDX_BINS / 8) + (blockIdx.x >> 3);
+  const uint32_t nb = 1u << dbits;
+  const uint32_t d = nb >= 8 ? (blockIdx.x & 7) * (nb / 8) + (blockIdx.x >> 3) : blockIdx.x;
   uint32_t* col = hist + d;
   for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < NBK; i += gridDim.x * 1024) bk_fill[i * CTR_STRIDE] = 0;
   if (blockIdx.x == 0)
@@ -249,14 +251,14 @@ __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t nti
     uint32_t v[SCAN_PER], sum = 0;
 #pragma unroll
     for (uint32_t k = 0; k < SCAN_PER; ++k) {
-      v[k] = i0 + k < ntiles ? col[(size_t)(i0 + k) * RDX_BINS] : 0u;
+      v[k] = i0 + k < ntiles ? col[(size_t)(i0 + k) << dbits] : 0u;
       sum += v[k];
     }
     uint32_t tot;
     uint32_t run = carry + block_excl_scan(sum, sh16, &tot);
 #pragma unroll
     for (uint32_t k = 0; k < SCAN_PER; ++k) {
-      if (i0 + k < ntiles) col[(size_t)(i0 + k) * RDX_BINS] = run;
+      if (i0 + k < ntiles) col[(size_t)(i0 + k) << dbits] = run;
       run += v[k];
     }
     carry += tot;
@@ -281,11 +283,12 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
   const uint32_t tile = blockIdx.x;
   {
     // digit base = exclusive scan of the digit totals; + this tile's row prefix
-    const uint32_t t = tid < RDX_BINS ? totals[tid] : 0u;
+    const uint32_t nb = 1u << dbits;  // the pass's digits (totals / off rows hold nb)
+    const uint32_t t = tid < nb ? totals[tid] : 0u;
     uint32_t all;
     const uint32_t excl = excl_scan256(t, sh4, &all);
-    if (tid < RDX_BINS) {
-      s_off[tid] = excl + off[(size_t)tile * RDX_BINS + tid];
+    if (tid < nb) {
+      s_off[tid] = excl + off[((size_t)tile << dbits) + tid];
       if (FINAL && f.bk_off && tile == 0 && tid <= f.NBK) f.bk_off[tid] = excl;
     }
     if (tile == 0 && tid == 0) {
@@ -3386,10 +3389,11 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
       // two passes split the bucket id's bits evenly (the first takes the low
       // half): 5 + 5 bits for 1,024 buckets write 64-message digit runs in both
       // passes, where 8 + 2 wrote 8-message runs (partial lines) in the first
-      const uint32_t dbits = last_pass ? RDX_BITS : RDX_SPLIT ? h->bk_bits / 2 + HB_RDX_SKEW : RDX_BITS;
+      const uint32_t b0 = RDX_SPLIT ? h->bk_bits / 2 + HB_RDX_SKEW : RDX_BITS;
+      const uint32_t dbits = h->passes == 1 ? RDX_BITS : p == 0 ? b0 : h->bk_bits - b0;
       hipLaunchKernelGGL(k_radix_hist, dim3((ntiles + HIST_TPB - 1) / HIST_TPB), dim3(RDX_THREADS), 0, ps_st, src, h->G,
                          shift, dbits, ntiles, h->hist);
-      hipLaunchKernelGGL(k_scan_rows, dim3(RDX_BINS), dim3(1024), 0, ps_st, h->hist, ntiles, h->totals, ps.bk_fill,
+      hipLaunchKernelGGL(k_scan_rows, dim3(1u << dbits), dim3(1024), 0, ps_st, h->hist, ntiles, dbits, h->totals, ps.bk_fill,
                          h->NBK, ps.ctr);
       if (last_pass)
         hipLaunchKernelGGL(k_radix_scatter<true>, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
