@@ -266,10 +266,49 @@ __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t nti
   if (threadIdx.x == 0) totals[d] = carry;
 }
 
+// Tile loads of k_radix_scatter (coalesced: round r, lane l -> element wave*256 + r*64 + l).
+struct ScatTile {
+  uint32_t g[RDX_ROUNDS], i[RDX_ROUNDS], o[RDX_ROUNDS];
+  uint64_t t[RDX_ROUNDS], x[RDX_ROUNDS];
+  bool v[RDX_ROUNDS];
+};
+__device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_t G, uint32_t base, uint32_t wave,
+                                          uint32_t lane, ScatTile& T) {
+#pragma unroll
+  for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+    const uint32_t i = base + wave * (64 * RDX_ROUNDS) + r * 64 + lane;
+    bool v = i < n;
+    T.g[r] = v ? s.group[i] : 0u;
+    v = v && T.g[r] < G;
+    T.v[r] = v;
+    if (s.rec) {
+      MsgRec m{};
+      if (v) m = s.rec[i];
+      T.i[r] = m.info;
+      T.o[r] = m.orig;
+      T.t[r] = m.term;
+      T.x[r] = m.index;
+    } else {
+      T.i[r] = v ? s.info[i] : 0u;
+      T.o[r] = v ? i : 0u;
+      T.t[r] = v ? s.term[i] : 0ull;
+      T.x[r] = v ? s.index[i] : 0ull;
+    }
+  }
+}
+
+// One workgroup scatters SCAT_TPW consecutive tiles; the next tile's loads
+// are issued before the current tile is ranked, staged and written, so they
+// are in flight during its LDS phases and stores.
+#ifndef HB_SCAT_TPW
+#define HB_SCAT_TPW 2
+#endif
+constexpr uint32_t SCAT_TPW = HB_SCAT_TPW;
 template <bool FINAL>
 __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, RadixDst d, FinalDst f, uint32_t G,
                                                               uint32_t shift, uint32_t dbits, uint32_t ntiles, const uint32_t* off,
                                                               const uint32_t* totals, uint32_t* n_valid) {
+  __shared__ uint32_t s_base[RDX_BINS];  // digit base in the pass output (exclusive scan of the totals)
   __shared__ uint32_t s_off[RDX_BINS];
   __shared__ uint32_t s_wcnt[RDX_WAVES][RDX_BINS];
   __shared__ uint32_t s_dstart[RDX_BINS + 1];
@@ -280,126 +319,113 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
   __shared__ uint64_t st_term[RDX_TILE];
   __shared__ uint64_t st_index[RDX_TILE];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t tile = blockIdx.x;
+  const uint32_t nb = 1u << dbits;  // the pass's digits (totals / off rows hold nb)
+  const uint32_t n = src_n(s);
+  const uint32_t tile0 = blockIdx.x * SCAT_TPW;
+  ScatTile cur, nxt;
+  scat_load(s, n, G, tile0 * RDX_TILE, wave, lane, cur);
   {
-    // digit base = exclusive scan of the digit totals; + this tile's row prefix
-    const uint32_t nb = 1u << dbits;  // the pass's digits (totals / off rows hold nb)
     const uint32_t t = tid < nb ? totals[tid] : 0u;
     uint32_t all;
     const uint32_t excl = excl_scan256(t, sh4, &all);
-    if (tid < nb) {
-      s_off[tid] = excl + off[((size_t)tile << dbits) + tid];
-      if (FINAL && f.bk_off && tile == 0 && tid <= f.NBK) f.bk_off[tid] = excl;
-    }
-    if (tile == 0 && tid == 0) {
-      *n_valid = all;
-      if (FINAL && f.bk_off && f.NBK == RDX_BINS) f.bk_off[RDX_BINS] = all;
-    }
-  }
-#pragma unroll
-  for (uint32_t k = 0; k < RDX_WAVES * RDX_BINS / RDX_THREADS; ++k) (&s_wcnt[0][0])[tid + k * RDX_THREADS] = 0;
-  __syncthreads();
-  const uint32_t n = src_n(s);
-  const uint32_t base = tile * RDX_TILE;
-  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  uint32_t vg[RDX_ROUNDS], vi[RDX_ROUNDS], vo[RDX_ROUNDS], vd[RDX_ROUNDS], vr[RDX_ROUNDS];
-  uint64_t vt[RDX_ROUNDS], vx[RDX_ROUNDS];
-  bool vv[RDX_ROUNDS];
-  // load (coalesced: round r, lane l -> element wave*256 + r*64 + l)
-#pragma unroll
-  for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
-    const uint32_t e = wave * (64 * RDX_ROUNDS) + r * 64 + lane;
-    const uint32_t i = base + e;
-    vv[r] = i < n;
-    vg[r] = vv[r] ? s.group[i] : 0u;
-    vv[r] = vv[r] && vg[r] < G;
-    if (s.rec) {
-      MsgRec m{};
-      if (vv[r]) m = s.rec[i];
-      vi[r] = m.info;
-      vo[r] = m.orig;
-      vt[r] = m.term;
-      vx[r] = m.index;
-    } else {
-      vi[r] = vv[r] ? s.info[i] : 0u;
-      vo[r] = vv[r] ? i : 0u;
-      vt[r] = vv[r] ? s.term[i] : 0ull;
-      vx[r] = vv[r] ? s.index[i] : 0ull;
-    }
-    vd[r] = rdx_digit(vg[r], shift, dbits);
-  }
-  // stable rank inside the wave: rounds in order, lanes in order
-#pragma unroll
-  for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
-    uint64_t peers = __ballot(vv[r]);
-#pragma unroll
-    for (uint32_t k = 0; k < RDX_BITS; ++k) {
-      if (k >= dbits) break;
-      const bool bit = (vd[r] >> k) & 1u;
-      const uint64_t bk = __ballot(bit);
-      peers &= bit ? bk : ~bk;
-    }
-    const uint32_t rank = (uint32_t)__popcll(peers & lt);
-    const uint32_t before = vv[r] ? s_wcnt[wave][vd[r]] : 0u;
-    vr[r] = before + rank;
-    if (vv[r] && rank == 0) s_wcnt[wave][vd[r]] = before + (uint32_t)__popcll(peers);
-  }
-  __syncthreads();
-  // per digit: prefix over waves, then digit starts inside the tile
-  uint32_t run = 0;
-  if (tid < RDX_BINS) {
-#pragma unroll
-    for (uint32_t w = 0; w < RDX_WAVES; ++w) {
-      const uint32_t c = s_wcnt[w][tid];
-      s_wcnt[w][tid] = run;
-      run += c;
-    }
-  }
-  {
-    uint32_t all;
-    const uint32_t excl = excl_scan256(tid < RDX_BINS ? run : 0u, sh4, &all);
-    if (tid < RDX_BINS) s_dstart[tid] = excl;
-    if (tid == 0) s_dstart[RDX_BINS] = all;
-  }
-  __syncthreads();
-#pragma unroll
-  for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
-    if (vv[r]) {
-      const uint32_t p = s_dstart[vd[r]] + s_wcnt[wave][vd[r]] + vr[r];
-      st_group[p] = vg[r];
-      st_info[p] = vi[r];
-      st_orig[p] = vo[r];
-      st_term[p] = vt[r];
-      st_index[p] = vx[r];
-    }
-  }
-  __syncthreads();
-  const uint32_t valid = s_dstart[RDX_BINS];
-#pragma unroll
-  for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
-    const uint32_t p = r * RDX_THREADS + tid;
-    if (p < valid) {
-      const uint32_t g = st_group[p];
-      const uint32_t dg = rdx_digit(g, shift, dbits);
-      const uint32_t o = s_off[dg] + (p - s_dstart[dg]);
-      if (FINAL) {
-        MsgRec m;
-        m.info = (st_info[p] & 0xFFFFu) | ((g & (PART - 1)) << 16) | (((g >> PART_LOG) & ((1u << f.sis_log) - 1)) << 24);
-        m.orig = st_orig[p];
-        m.term = st_term[p];
-        m.index = st_index[p];
-        f.rec[o] = m;
-        if (f.bucket) f.bucket[o] = g >> (PART_LOG + f.sis_log);
-      } else {
-        d.group[o] = g;
-        MsgRec m;
-        m.info = st_info[p];
-        m.orig = st_orig[p];
-        m.term = st_term[p];
-        m.index = st_index[p];
-        d.rec[o] = m;
+    if (tid < RDX_BINS) s_base[tid] = excl;
+    if (blockIdx.x == 0) {
+      if (FINAL && f.bk_off && tid <= f.NBK && tid < RDX_BINS) f.bk_off[tid] = excl;
+      if (tid == 0) {
+        *n_valid = all;
+        if (FINAL && f.bk_off && f.NBK == RDX_BINS) f.bk_off[RDX_BINS] = all;
       }
     }
+  }
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (uint32_t j = 0; j < SCAT_TPW; ++j) {
+    const uint32_t tile = tile0 + j;
+    if (tile >= ntiles) break;  // uniform
+    // this tile's digit starts in the output; per-wave digit counters cleared
+    if (tid < nb) s_off[tid] = s_base[tid] + off[((size_t)tile << dbits) + tid];
+#pragma unroll
+    for (uint32_t k = 0; k < RDX_WAVES * RDX_BINS / RDX_THREADS; ++k) (&s_wcnt[0][0])[tid + k * RDX_THREADS] = 0;
+    __syncthreads();
+    uint32_t vd[RDX_ROUNDS], vr[RDX_ROUNDS];
+#pragma unroll
+    for (uint32_t r = 0; r < RDX_ROUNDS; ++r) vd[r] = rdx_digit(cur.g[r], shift, dbits);
+    // the next tile's loads go out now
+    if (j + 1 < SCAT_TPW && tile + 1 < ntiles) scat_load(s, n, G, (tile + 1) * RDX_TILE, wave, lane, nxt);
+    // stable rank inside the wave: rounds in order, lanes in order
+#pragma unroll
+    for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+      uint64_t peers = __ballot(cur.v[r]);
+#pragma unroll
+      for (uint32_t k = 0; k < RDX_BITS; ++k) {
+        if (k >= dbits) break;
+        const bool bit = (vd[r] >> k) & 1u;
+        const uint64_t bk = __ballot(bit);
+        peers &= bit ? bk : ~bk;
+      }
+      const uint32_t rank = (uint32_t)__popcll(peers & lt);
+      const uint32_t before = cur.v[r] ? s_wcnt[wave][vd[r]] : 0u;
+      vr[r] = before + rank;
+      if (cur.v[r] && rank == 0) s_wcnt[wave][vd[r]] = before + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    // per digit: prefix over waves, then digit starts inside the tile
+    uint32_t run = 0;
+    if (tid < RDX_BINS) {
+#pragma unroll
+      for (uint32_t w = 0; w < RDX_WAVES; ++w) {
+        const uint32_t c = s_wcnt[w][tid];
+        s_wcnt[w][tid] = run;
+        run += c;
+      }
+    }
+    {
+      uint32_t all;
+      const uint32_t excl = excl_scan256(tid < RDX_BINS ? run : 0u, sh4, &all);
+      if (tid < RDX_BINS) s_dstart[tid] = excl;
+      if (tid == 0) s_dstart[RDX_BINS] = all;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+      if (cur.v[r]) {
+        const uint32_t p = s_dstart[vd[r]] + s_wcnt[wave][vd[r]] + vr[r];
+        st_group[p] = cur.g[r];
+        st_info[p] = cur.i[r];
+        st_orig[p] = cur.o[r];
+        st_term[p] = cur.t[r];
+        st_index[p] = cur.x[r];
+      }
+    }
+    __syncthreads();
+    const uint32_t valid = s_dstart[RDX_BINS];
+#pragma unroll
+    for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+      const uint32_t p = r * RDX_THREADS + tid;
+      if (p < valid) {
+        const uint32_t g = st_group[p];
+        const uint32_t dg = rdx_digit(g, shift, dbits);
+        const uint32_t o = s_off[dg] + (p - s_dstart[dg]);
+        if (FINAL) {
+          MsgRec m;
+          m.info = (st_info[p] & 0xFFFFu) | ((g & (PART - 1)) << 16) | (((g >> PART_LOG) & ((1u << f.sis_log) - 1)) << 24);
+          m.orig = st_orig[p];
+          m.term = st_term[p];
+          m.index = st_index[p];
+          f.rec[o] = m;
+          if (f.bucket) f.bucket[o] = g >> (PART_LOG + f.sis_log);
+        } else {
+          d.group[o] = g;
+          MsgRec m;
+          m.info = st_info[p];
+          m.orig = st_orig[p];
+          m.term = st_term[p];
+          m.index = st_index[p];
+          d.rec[o] = m;
+        }
+      }
+    }
+    __syncthreads();  // the next tile reuses s_off / s_wcnt / s_dstart / the staging
+    cur = nxt;
   }
 }
 
@@ -3396,10 +3422,10 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
       hipLaunchKernelGGL(k_scan_rows, dim3(1u << dbits), dim3(1024), 0, ps_st, h->hist, ntiles, dbits, h->totals, ps.bk_fill,
                          h->NBK, ps.ctr);
       if (last_pass)
-        hipLaunchKernelGGL(k_radix_scatter<true>, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
+        hipLaunchKernelGGL(k_radix_scatter<true>, dim3((ntiles + SCAT_TPW - 1) / SCAT_TPW), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
                            shift, dbits, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
       else
-        hipLaunchKernelGGL(k_radix_scatter<false>, dim3(ntiles), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
+        hipLaunchKernelGGL(k_radix_scatter<false>, dim3((ntiles + SCAT_TPW - 1) / SCAT_TPW), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
                            shift, dbits, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
       src = RadixSrc{dst.group, nullptr, nullptr, nullptr, dst.rec, h->n_valid, (uint32_t)b->n};
       shift += dbits;
