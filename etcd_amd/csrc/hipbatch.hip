@@ -798,6 +798,9 @@ constexpr uint32_t ROUTE_THREADS = 1024;
 #define HB_ROUTE_UNROLL 4
 #endif
 constexpr uint32_t ROUTE_UNROLL = HB_ROUTE_UNROLL;  // records in flight per lane
+#ifndef HB_ROUTE_PF  // 1: the next ROUTE_UNROLL records are loaded while the current ones are ranked
+#define HB_ROUTE_PF 0  // measured: cfg3 -1 %, cfg2 +1 us, cfg4 +0.5 %, cfg5 neutral
+#endif
 #ifndef HB_RG2_LOG  // route groups per workgroup for KMAX = 2 (log2): 1024 (4 sisters per 4096-group
 #define HB_RG2_LOG 10  // bucket, 53 KB LDS) measured faster than 2048 (2 sisters, 106 KB)
 #endif
@@ -831,15 +834,41 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   const uint32_t G = a.S.G;
   const uint32_t lg0 = w * RG;  // first group (in the bucket) of this workgroup
   const uint32_t sub_lo = lg0 >> PART_LOG, sub_hi = (lg0 + RG) >> PART_LOG;
+#if HB_ROUTE_PF
+  // the next chunk's records are loaded before this chunk is ranked
+  MsgRec mn[ROUTE_UNROLL];
+#pragma unroll
+  for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
+    const uint32_t p = lo + u * ROUTE_THREADS + tid;
+    if (p < hi) mn[u] = a.rec[p];
+  }
+#endif
   for (uint32_t base = lo; base < hi; base += ROUTE_THREADS * ROUTE_UNROLL) {
     MsgRec m[ROUTE_UNROLL];
     uint32_t sub[ROUTE_UNROLL];
+#if HB_ROUTE_PF
+#pragma unroll
+    for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) m[u] = mn[u];
+    if (base + ROUTE_THREADS * ROUTE_UNROLL < hi) {
+#pragma unroll
+      for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
+        const uint32_t p = base + (ROUTE_UNROLL + u) * ROUTE_THREADS + tid;
+        if (p < hi) mn[u] = a.rec[p];
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
+      const uint32_t p = base + u * ROUTE_THREADS + tid;
+      sub[u] = p < hi ? (m[u].info >> 24) & 0xFu : 0xFFu;  // the partition in the bucket
+    }
+#else
 #pragma unroll
     for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
       const uint32_t p = base + u * ROUTE_THREADS + tid;
       if (p < hi) m[u] = a.rec[p];
       sub[u] = p < hi ? (m[u].info >> 24) & 0xFu : 0xFFu;  // the partition in the bucket
     }
+#endif
     if (w == 0) {  // the key bytes the general kernel's bucket walk scans (one coalesced store per lane)
 #pragma unroll
       for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
