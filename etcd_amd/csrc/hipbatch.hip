@@ -195,6 +195,9 @@ __device__ __forceinline__ uint32_t excl_scan256(uint32_t v, uint32_t* sh4, uint
 #ifndef HB_HIST_TPB
 #define HB_HIST_TPB 4
 #endif
+#ifndef HB_HIST_COLMAJOR  // tile counts stored [digit][tile]: k_scan_rows reads each column contiguously
+#define HB_HIST_COLMAJOR 0
+#endif
 constexpr uint32_t HIST_TPB = HB_HIST_TPB;
 __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t G, uint32_t shift, uint32_t dbits,
                                                            uint32_t ntiles, uint32_t* hist) {
@@ -218,18 +221,22 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t
     for (uint32_t r = 0; r < RDX_ROUNDS; ++r)
       if (gv[t][r] < G) atomicAdd(&cnt[t][rdx_digit(gv[t][r], shift, dbits)], 1u);
   __syncthreads();
-  const uint32_t nb = 1u << dbits;  // row width: the pass's digits only
-  for (uint32_t i = tid; i < (HIST_TPB << dbits); i += RDX_THREADS) {
-    const uint32_t t = i >> dbits, dg = i & (nb - 1);
+  for (uint32_t i = tid; i < (HIST_TPB << dbits); i += RDX_THREADS) {  // the pass's digits only
+#if HB_HIST_COLMAJOR
+    const uint32_t t = i % HIST_TPB, dg = i / HIST_TPB;
+    if (t0 + t < ntiles) hist[(size_t)dg * ntiles + t0 + t] = cnt[t][dg];  // [digit][tile]
+#else
+    const uint32_t t = i >> dbits, dg = i & ((1u << dbits) - 1);
     if (t0 + t < ntiles) hist[((size_t)(t0 + t) << dbits) + dg] = cnt[t][dg];  // [tile][digit]
+#endif
   }
 }
 
-// Column scan: workgroup b turns column d of hist ([ntiles][nb] tile
-// counts) into exclusive per-tile prefixes and writes the column total to
-// totals[d].  The 32 digits of one 128-byte line of every tile row are
-// scanned by workgroups of one XCD (blockIdx % 8), so each line is fetched
-// into one L2 once.  It also clears the per-bucket event-chunk cursors for
+// Column scan: workgroup d turns column d of hist (tile counts, [nb][ntiles]:
+// each column contiguous) into exclusive per-tile prefixes and writes the
+// column total to totals[d].  (With HB_HIST_COLMAJOR=0, [ntiles][nb] rows:
+// the digits of one 128-byte line of every row are scanned by workgroups of
+// one XCD, so each line is fetched into one L2 once.)  It also clears the per-bucket event-chunk cursors for
 // the coming apply.
 #ifndef HB_SCAN_PER
 #define HB_SCAN_PER 16
@@ -238,9 +245,16 @@ constexpr uint32_t SCAN_PER = HB_SCAN_PER;
 __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t ntiles, uint32_t dbits, uint32_t* totals,
                                                     uint32_t* bk_fill, uint32_t NBK, uint32_t* ctr) {
   __shared__ uint32_t sh16[16];
+#if HB_HIST_COLMAJOR
+  const uint32_t d = blockIdx.x;
+  uint32_t* col = hist + (size_t)d * ntiles;  // the column is contiguous
+  constexpr uint32_t CS = 0;
+#else
   const uint32_t nb = 1u << dbits;
   const uint32_t d = nb >= 8 ? (blockIdx.x & 7) * (nb / 8) + (blockIdx.x >> 3) : blockIdx.x;
   uint32_t* col = hist + d;
+  const uint32_t CS = dbits;
+#endif
   for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < NBK; i += gridDim.x * 1024) bk_fill[i * CTR_STRIDE] = 0;
   if (blockIdx.x == 0)
     for (uint32_t i = threadIdx.x; i < CTR_WORDS; i += blockDim.x) ctr[i] = 0;
@@ -251,14 +265,14 @@ __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t nti
     uint32_t v[SCAN_PER], sum = 0;
 #pragma unroll
     for (uint32_t k = 0; k < SCAN_PER; ++k) {
-      v[k] = i0 + k < ntiles ? col[(size_t)(i0 + k) << dbits] : 0u;
+      v[k] = i0 + k < ntiles ? col[(size_t)(i0 + k) << CS] : 0u;
       sum += v[k];
     }
     uint32_t tot;
     uint32_t run = carry + block_excl_scan(sum, sh16, &tot);
 #pragma unroll
     for (uint32_t k = 0; k < SCAN_PER; ++k) {
-      if (i0 + k < ntiles) col[(size_t)(i0 + k) << dbits] = run;
+      if (i0 + k < ntiles) col[(size_t)(i0 + k) << CS] = run;
       run += v[k];
     }
     carry += tot;
@@ -342,7 +356,11 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
     const uint32_t tile = tile0 + j;
     if (tile >= ntiles) break;  // uniform
     // this tile's digit starts in the output; per-wave digit counters cleared
+#if HB_HIST_COLMAJOR
+    if (tid < nb) s_off[tid] = s_base[tid] + off[(size_t)tid * ntiles + tile];
+#else
     if (tid < nb) s_off[tid] = s_base[tid] + off[((size_t)tile << dbits) + tid];
+#endif
 #pragma unroll
     for (uint32_t k = 0; k < RDX_WAVES * RDX_BINS / RDX_THREADS; ++k) (&s_wcnt[0][0])[tid + k * RDX_THREADS] = 0;
     __syncthreads();
