@@ -481,6 +481,7 @@ struct Group {
   uint64_t bx = 0, bx_top = 0;  // entries the batch can append (sizes)
   uint64_t bxr = 0;             // term runs it can start: a noop per VoteResp / MsgHup, a MsgApp entry, a restore
   bool in_bx = false;
+  bool solo = false;  // on hbn_node::solo (one peer: its tick can win an election)
 
   hbn_hard_state hard() const { return hbn_hard_state{term, vote, hs_commit}; }
   Soft soft() const { return Soft{lead, state}; }
@@ -658,6 +659,7 @@ struct hbn_node {
   std::vector<Group*> pend_tr;  // ... and whose older log term runs are still to push
   std::vector<Group*> stepped;  // groups whose raft.Step runs in the pending batch
   std::vector<Group*> bx;       // groups with messages in the pending batch (Group::bx)
+  std::vector<Group*> solo;     // groups that had one peer when listed (Group::solo; pruned by hbn_tick)
   // the step's compact event words (hb_events_to_host, pinned: the device writes them)
   uint64_t* w_words = nullptr;
   uint64_t w_cap = 0;
@@ -737,6 +739,14 @@ hb_group make_record(const hbn_node* n, const Group& g, const std::vector<hb_pro
   r.vote = ref_of(g, n->id, g.vote);
   for (size_t s = 0; s < prs.size(); ++s) r.pr[s] = prs[s];
   return r;
+}
+
+// list a one-peer group for hbn_tick's noop reservation
+void note_solo(hbn_node* n, Group& g) {
+  if (g.peers.size() == 1 && !g.solo) {
+    g.solo = true;
+    n->solo.push_back(&g);
+  }
 }
 
 uint32_t alloc_slot(hbn_node* n) {
@@ -1498,9 +1508,14 @@ void push_proposals(hbn_node* n, const BulkRun& br, const uint8_t* const* data, 
 }
 
 // Runs of bulk messages in [0, count), each cut to the batch's free rows (the
-// batch is stepped when full, as push() does); the others one at a time.
-template <class Bulk, class One>
-void bulk_runs(hbn_node* n, uint64_t count, const BulkRun& br, uint64_t* done, Bulk&& bulk, One&& one) {
+// batch is stepped when full, as push() does); the others one at a time.  A
+// flush replays device events, which can fault a group or move its slot (a
+// restore reload).  The message whose push triggers the flush was checked
+// before it, as in push(); from the next one on, the run is re-checked with
+// `still`, and a message that no longer qualifies goes through one(i), which
+// raises the reference's error at its position, as hbn_step / hbn_propose do.
+template <class Bulk, class One, class Still>
+void bulk_runs(hbn_node* n, uint64_t count, BulkRun& br, uint64_t* done, Bulk&& bulk, One&& one, Still&& still) {
   size_t i = 0;
   while (i < count) {
     if (!br.fast[i]) {
@@ -1511,7 +1526,15 @@ void bulk_runs(hbn_node* n, uint64_t count, const BulkRun& br, uint64_t* done, B
     size_t j = i;
     while (j < count && br.fast[j]) ++j;
     while (i < j) {
-      if (n->b_group.size() >= n->max_batch) flush(n);
+      if (n->b_group.size() >= n->max_batch) {
+        flush(n);
+        for (size_t k = i + 1; k < j; ++k)
+          if (!still(k)) {
+            br.fast[k] = 0;
+            j = k;
+            break;
+          }
+      }
       const size_t room = n->max_batch - n->b_group.size();
       const size_t e = std::min(j, i + room);
       bulk(i, e);
@@ -1719,6 +1742,7 @@ void refresh_content(std::vector<Group*>& content, Group& g) {
 void reload_prs(hbn_node* n, Group& g, const std::vector<uint64_t>& new_peers,
                 const std::vector<std::pair<uint64_t, uint64_t>>& fresh /* id -> (match 0, next) */,
                 bool restored) {
+  if (new_peers.size() > n->nmax) throw Fail{HBN_EUNSUPPORTED};  // the engine's limit (hbn_start max_replicas <= 7)
   hb_group old;
   std::memset(&old, 0, sizeof(old));
   hb_timer tm;
@@ -1740,8 +1764,8 @@ void reload_prs(hbn_node* n, Group& g, const std::vector<uint64_t>& new_peers,
       ins_start[s] = st;
     }
   }
-  if (new_peers.size() > n->nmax) throw Fail{HB_EINVAL};
   g.peers = new_peers;
+  note_solo(n, g);
   if (new_peers.empty()) {
     if (g.slot != NO_SLOT) {
       check(hb_remove_groups(n->h, g.slot, 1));
@@ -2103,7 +2127,7 @@ int hbn_start(int device, uint64_t id, uint32_t capacity, uint32_t max_replicas,
     n->sized = max_msg_size != 0 && max_msg_size != HB_NO_LIMIT;
     n->max_batch = max_batch;
     unsigned th = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-    if (const char* e = std::getenv("HBN_THREADS")) th = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("HBN_THREADS")) th = (unsigned)std::min(256, std::max(1, std::atoi(e)));  // as hbn_set_threads
     n->pool.reset(new Pool(th));
     n->lists.resize(th);
     n->arenas.resize(th);
@@ -2178,7 +2202,7 @@ int hbn_create_group(hbn_node* n, uint64_t group, const hbn_config* cfg, hbn_sto
         g.peers.push_back(peer_ids[i]);
       }
     }
-    if (g.peers.size() > n->nmax) throw Fail{HB_EINVAL};
+    if (g.peers.size() > n->nmax) throw Fail{HBN_EUNSUPPORTED};  // the engine's limit (hbn_start max_replicas <= 7)
     // Progress after reset / addNode: Next = lastIndex+1; Match = lastIndex for self
     // after reset, 0 after addNode (the bootstrap path).
     std::vector<hb_progress> prs(g.peers.size());
@@ -2201,6 +2225,7 @@ int hbn_create_group(hbn_node* n, uint64_t group, const hbn_config* cfg, hbn_sto
       if (n->sized) n->pend_sz.push_back(&g);
       n->pend_tr.push_back(&g);
     }
+    note_solo(n, g);
     // the initial hard and soft states (:213-215)
     g.prev_soft = g.soft();
     g.prev_hard = g.hard();
@@ -2224,7 +2249,7 @@ int hbn_remove_group(hbn_node* n, uint64_t group) {
     }
     if (g.log.st) drop_user(g.log.st, n, group);
     for (auto* v : {&n->touched, &n->content, &n->delivered, &n->stepped, &n->bounds, &n->pend_sz, &n->pend_tr,
-                    &n->reload, &n->bx})
+                    &n->reload, &n->bx, &n->solo})
       v->erase(std::remove(v->begin(), v->end(), &g), v->end());
     n->groups.erase(it);
   });
@@ -2241,14 +2266,21 @@ int hbn_tick(hbn_node* n) {
   if (!n) return HB_EINVAL;
   return guarded([&] {
     flush(n);  // (also pushes queued loads)
-    {  // a one-peer group's tick can win an election at once and append its noop
+    if (!n->solo.empty()) {  // a one-peer group's tick can win an election at once and append its noop
       std::vector<uint32_t> rs;
       std::vector<uint64_t> rz, rt;
-      for (Group* g : n->by_slot)
-        if (g && g->peers.size() == 1) {
-          want_log(n, *g, 1, 1, rs, rz, rt);
-          g->lx_runs += 1;
+      size_t k = 0;
+      for (Group* g : n->solo) {
+        if (g->peers.size() != 1) {  // no longer one peer: off the list
+          g->solo = false;
+          continue;
         }
+        n->solo[k++] = g;
+        if (g->slot == NO_SLOT || g->state == HB_STATE_LEADER) continue;  // a leader's tick only beats
+        want_log(n, *g, 1, 1, rs, rz, rt);
+        g->lx_runs += 1;
+      }
+      n->solo.resize(k);
       reserve(n, rs, rz, rt);
     }
     check(hb_tick(n->h, 0));
@@ -2287,7 +2319,8 @@ int hbn_propose_many(hbn_node* n, uint64_t count, const uint64_t* groups, const 
     BulkRun br;
     bulk_lookup(n, count, groups, br, [](size_t, const Group& g) { return g.slot != NO_SLOT; });
     bulk_runs(n, count, br, &d, [&](size_t a, size_t b) { push_proposals(n, br, data, len, a, b); },
-              [&](size_t i) { propose_one(n, groups[i], data[i], len[i]); });
+              [&](size_t i) { propose_one(n, groups[i], data[i], len[i]); },
+              [&](size_t i) { return !br.gp[i]->fault && br.gp[i]->slot != NO_SLOT; });
   });
   if (done) *done = d;
   return rc;
@@ -2326,7 +2359,7 @@ int hbn_step_many(hbn_node* n, uint64_t count, const uint64_t* groups, const hbn
       return t == HB_MSG_APP_RESP || t == HB_MSG_VOTE_RESP || t == HB_MSG_HEARTBEAT_RESP;
     });
     bulk_runs(n, count, br, &d, [&](size_t a, size_t b) { push_responses(n, br, msgs, a, b); },
-              [&](size_t i) { step_one(n, groups[i], &msgs[i]); });
+              [&](size_t i) { step_one(n, groups[i], &msgs[i]); }, [&](size_t i) { return !br.gp[i]->fault; });
   });
   if (done) *done = d;
   return rc;

@@ -125,13 +125,6 @@ constexpr uint32_t RDX_BINS = 1u << RDX_BITS;
 constexpr uint32_t RDX_THREADS = HB_RDX_THREADS;
 constexpr uint32_t RDX_WAVES = RDX_THREADS / 64;
 constexpr uint32_t RDX_ROUNDS = HB_RDX_ROUNDS;
-#ifndef HB_RDX_SPLIT  // 0: the first of two passes takes a full 8-bit digit
-#define HB_RDX_SPLIT 1
-#endif
-#ifndef HB_RDX_SKEW  // first-pass bits = bucket bits / 2 + skew
-#define HB_RDX_SKEW 0
-#endif
-constexpr bool RDX_SPLIT = HB_RDX_SPLIT != 0;
 constexpr uint32_t RDX_TILE = RDX_THREADS * RDX_ROUNDS;  // 2048
 
 struct MsgRec {      // apply input record (24 B)
@@ -195,9 +188,6 @@ __device__ __forceinline__ uint32_t excl_scan256(uint32_t v, uint32_t* sh4, uint
 #ifndef HB_HIST_TPB
 #define HB_HIST_TPB 4
 #endif
-#ifndef HB_HIST_COLMAJOR  // tile counts stored [digit][tile]: k_scan_rows reads each column contiguously
-#define HB_HIST_COLMAJOR 0
-#endif
 constexpr uint32_t HIST_TPB = HB_HIST_TPB;
 __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t G, uint32_t shift, uint32_t dbits,
                                                            uint32_t ntiles, uint32_t* hist) {
@@ -222,21 +212,15 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t
       if (gv[t][r] < G) atomicAdd(&cnt[t][rdx_digit(gv[t][r], shift, dbits)], 1u);
   __syncthreads();
   for (uint32_t i = tid; i < (HIST_TPB << dbits); i += RDX_THREADS) {  // the pass's digits only
-#if HB_HIST_COLMAJOR
-    const uint32_t t = i % HIST_TPB, dg = i / HIST_TPB;
-    if (t0 + t < ntiles) hist[(size_t)dg * ntiles + t0 + t] = cnt[t][dg];  // [digit][tile]
-#else
     const uint32_t t = i >> dbits, dg = i & ((1u << dbits) - 1);
     if (t0 + t < ntiles) hist[((size_t)(t0 + t) << dbits) + dg] = cnt[t][dg];  // [tile][digit]
-#endif
   }
 }
 
-// Column scan: workgroup d turns column d of hist (tile counts, [nb][ntiles]:
-// each column contiguous) into exclusive per-tile prefixes and writes the
-// column total to totals[d].  (With HB_HIST_COLMAJOR=0, [ntiles][nb] rows:
-// the digits of one 128-byte line of every row are scanned by workgroups of
-// one XCD, so each line is fetched into one L2 once.)  It also clears the per-bucket event-chunk cursors for
+// Column scan: workgroup d turns column d of hist (tile counts, [ntiles][nb]
+// rows) into exclusive per-tile prefixes and writes the column total to
+// totals[d]; the digits of one 128-byte line of every row are scanned by
+// workgroups of one XCD, so each line is fetched into one L2 once.  It also clears the per-bucket event-chunk cursors for
 // the coming apply.
 #ifndef HB_SCAN_PER
 #define HB_SCAN_PER 16
@@ -245,16 +229,10 @@ constexpr uint32_t SCAN_PER = HB_SCAN_PER;
 __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t ntiles, uint32_t dbits, uint32_t* totals,
                                                     uint32_t* bk_fill, uint32_t NBK, uint32_t* ctr) {
   __shared__ uint32_t sh16[16];
-#if HB_HIST_COLMAJOR
-  const uint32_t d = blockIdx.x;
-  uint32_t* col = hist + (size_t)d * ntiles;  // the column is contiguous
-  constexpr uint32_t CS = 0;
-#else
   const uint32_t nb = 1u << dbits;
   const uint32_t d = nb >= 8 ? (blockIdx.x & 7) * (nb / 8) + (blockIdx.x >> 3) : blockIdx.x;
   uint32_t* col = hist + d;
   const uint32_t CS = dbits;
-#endif
   for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < NBK; i += gridDim.x * 1024) bk_fill[i * CTR_STRIDE] = 0;
   if (blockIdx.x == 0)
     for (uint32_t i = threadIdx.x; i < CTR_WORDS; i += blockDim.x) ctr[i] = 0;
@@ -356,11 +334,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
     const uint32_t tile = tile0 + j;
     if (tile >= ntiles) break;  // uniform
     // this tile's digit starts in the output; per-wave digit counters cleared
-#if HB_HIST_COLMAJOR
-    if (tid < nb) s_off[tid] = s_base[tid] + off[(size_t)tid * ntiles + tile];
-#else
     if (tid < nb) s_off[tid] = s_base[tid] + off[((size_t)tile << dbits) + tid];
-#endif
 #pragma unroll
     for (uint32_t k = 0; k < RDX_WAVES * RDX_BINS / RDX_THREADS; ++k) (&s_wcnt[0][0])[tid + k * RDX_THREADS] = 0;
     __syncthreads();
@@ -519,6 +493,8 @@ struct ApplyArgs {
 constexpr uint32_t route_kmax(int nmax) {
   return nmax <= 3 ? 2u : (nmax <= 5 ? (uint32_t)HB_KS5 : (uint32_t)(nmax - 1 + HB_KS_EXTRA));
 }
+static_assert(route_kmax(3) <= 8 && route_kmax(5) <= 8 && route_kmax(7) <= 8,
+              "the slot sorts carry slot numbers as 4-bit nibbles of one uint32_t");
 
 // stats slots reduced per workgroup
 enum { ST_MSGS, ST_APPRESP, ST_VOTERESP, ST_DROPPED, ST_COMMITS, ST_WON, ST_LOST, ST_FAULTS, ST_ENTRIES, ST_N };
@@ -765,7 +741,6 @@ __device__ __forceinline__ void reduce_stats(const ApplyArgs& a, uint64_t* l_sta
 // (messages, responses, drops: at most the route slots; commits, faults: 0 or
 // 1): four 16-bit fields per word keep a wave's sums exact (< 2^16 while each
 // lane's count is < 1024), so ten values take four wave reductions, not ten.
-#ifndef HB_X_WIDE_STATS
 template <>
 __device__ __forceinline__ void reduce_stats<uint32_t>(const ApplyArgs& a, uint64_t* l_stats,
                                                        const uint32_t (&vals)[ST_N + 1]) {
@@ -795,7 +770,6 @@ __device__ __forceinline__ void reduce_stats<uint32_t>(const ApplyArgs& a, uint6
   if (tid <= ST_N && v)
     atomicAdd((unsigned long long*)&a.stats_shard[shard_at(tid, blockIdx.x & (NSH - 1))], (unsigned long long)v);
 }
-#endif
 
 // ---------------------------------------------------------------------------
 // k_route<KMAX>: W = BK / RG workgroups per bucket, each owning RG groups
@@ -816,9 +790,6 @@ constexpr uint32_t ROUTE_THREADS = 1024;
 #define HB_ROUTE_UNROLL 4
 #endif
 constexpr uint32_t ROUTE_UNROLL = HB_ROUTE_UNROLL;  // records in flight per lane
-#ifndef HB_ROUTE_PF  // 1: the next ROUTE_UNROLL records are loaded while the current ones are ranked
-#define HB_ROUTE_PF 0  // measured: cfg3 -1 %, cfg2 +1 us, cfg4 +0.5 %, cfg5 neutral
-#endif
 #ifndef HB_RG2_LOG  // route groups per workgroup for KMAX = 2 (log2): 1024 (4 sisters per 4096-group
 #define HB_RG2_LOG 10  // bucket, 53 KB LDS) measured faster than 2048 (2 sisters, 106 KB)
 #endif
@@ -852,41 +823,15 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   const uint32_t G = a.S.G;
   const uint32_t lg0 = w * RG;  // first group (in the bucket) of this workgroup
   const uint32_t sub_lo = lg0 >> PART_LOG, sub_hi = (lg0 + RG) >> PART_LOG;
-#if HB_ROUTE_PF
-  // the next chunk's records are loaded before this chunk is ranked
-  MsgRec mn[ROUTE_UNROLL];
-#pragma unroll
-  for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
-    const uint32_t p = lo + u * ROUTE_THREADS + tid;
-    if (p < hi) mn[u] = a.rec[p];
-  }
-#endif
   for (uint32_t base = lo; base < hi; base += ROUTE_THREADS * ROUTE_UNROLL) {
     MsgRec m[ROUTE_UNROLL];
     uint32_t sub[ROUTE_UNROLL];
-#if HB_ROUTE_PF
-#pragma unroll
-    for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) m[u] = mn[u];
-    if (base + ROUTE_THREADS * ROUTE_UNROLL < hi) {
-#pragma unroll
-      for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
-        const uint32_t p = base + (ROUTE_UNROLL + u) * ROUTE_THREADS + tid;
-        if (p < hi) mn[u] = a.rec[p];
-      }
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
-      const uint32_t p = base + u * ROUTE_THREADS + tid;
-      sub[u] = p < hi ? (m[u].info >> 24) & 0xFu : 0xFFu;  // the partition in the bucket
-    }
-#else
 #pragma unroll
     for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
       const uint32_t p = base + u * ROUTE_THREADS + tid;
       if (p < hi) m[u] = a.rec[p];
       sub[u] = p < hi ? (m[u].info >> 24) & 0xFu : 0xFFu;  // the partition in the bucket
     }
-#endif
     if (w == 0) {  // the key bytes the general kernel's bucket walk scans (one coalesced store per lane)
 #pragma unroll
       for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
@@ -1480,9 +1425,6 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
 #ifndef HB_ELECT_WAVES
 #define HB_ELECT_WAVES 4
 #endif
-#ifndef HB_ELECT_PF  // slot messages in flight ahead of the one stepped (1 or 2)
-#define HB_ELECT_PF 1  // measured: 2 neutral on cfg4
-#endif
 #ifndef HB_ELECT_GRID
 #define HB_ELECT_GRID 0  // as HB_GEN_GRID
 #endif
@@ -1552,27 +1494,20 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
       }
       const uint32_t skip = resume & 0x3FFFFFFFu;
       uint32_t x = skip;
-      // the next HB_ELECT_PF messages' loads are in flight while one is stepped
-      uint32_t inf_n = 0, inf_m = 0;
-      uint64_t term_n = 0, term_m = 0;
+      // the next message's loads are in flight while one is stepped
+      uint32_t inf_n = 0;
+      uint64_t term_n = 0;
       auto ld = [&](uint32_t y, uint32_t& inf, uint64_t& tm) {
         const size_t o = (size_t)((perm >> (4 * y)) & 0xF) * a.S.G + g;
         inf = a.slot_info[o];
         tm = a.slot_term[o];
       };
       if (x < cnt) ld(x, inf_n, term_n);
-      if (HB_ELECT_PF >= 2 && x + 1 < cnt) ld(x + 1, inf_m, term_m);
 #pragma nounroll
       for (; x < cnt; ++x) {
         const uint32_t inf = inf_n;
         const uint64_t mterm = term_n;
-        if (HB_ELECT_PF >= 2) {
-          inf_n = inf_m;
-          term_n = term_m;
-          if (x + 2 < cnt) ld(x + 2, inf_m, term_m);
-        } else if (x + 1 < cnt) {
-          ld(x + 1, inf_n, term_n);
-        }
+        if (x + 1 < cnt) ld(x + 1, inf_n, term_n);
         const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
         if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
           st_drop++;
@@ -1617,9 +1552,6 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
 #endif
 #ifndef HB_LEAD7_WAVES  // k_apply_lead<7> (measured on cfg4: 2 waves +3 %, 4 waves -0.6 % with 128 B/lane of scratch)
 #define HB_LEAD7_WAVES 3
-#endif
-#ifndef HB_LEAD_PF  // slot messages in flight ahead of the one stepped (1 or 2)
-#define HB_LEAD_PF 1  // measured: 2 costs 3 % on cfg3 (more scratch)
 #endif
 // ---------------------------------------------------------------------------
 // k_apply_lead (n >= 5, replaces k_apply_fast there): one workgroup per
@@ -1730,9 +1662,9 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
       resume = 0;
     } else {
       uint32_t x = 0;
-      // the next HB_LEAD_PF messages' loads are in flight while one is stepped
-      uint32_t inf_n = 0, orig_n = 0, inf_m = 0, orig_m = 0;
-      uint64_t term_n = 0, index_n = 0, term_m = 0, index_m = 0;
+      // the next message's loads are in flight while one is stepped
+      uint32_t inf_n = 0, orig_n = 0;
+      uint64_t term_n = 0, index_n = 0;
       auto ld = [&](uint32_t y, uint32_t& inf, uint32_t& org, uint64_t& tm, uint64_t& ix) {
         const size_t o = (size_t)((perm >> (4 * y)) & 0xF) * a.S.G + g;
         inf = a.slot_info[o];
@@ -1741,21 +1673,12 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
         ix = a.slot_index[o];
       };
       ld(0, inf_n, orig_n, term_n, index_n);
-      if (HB_LEAD_PF >= 2 && 1 < cnt) ld(1, inf_m, orig_m, term_m, index_m);
 #pragma nounroll
       for (; x < cnt; ++x) {
         if (L.faulted()) break;
         const uint32_t inf = inf_n, morig = orig_n;
         const uint64_t mterm = term_n, mindex = index_n;
-        if (HB_LEAD_PF >= 2) {
-          inf_n = inf_m;
-          orig_n = orig_m;
-          term_n = term_m;
-          index_n = index_m;
-          if (x + 2 < cnt) ld(x + 2, inf_m, orig_m, term_m, index_m);
-        } else if (x + 1 < cnt) {
-          ld(x + 1, inf_n, orig_n, term_n, index_n);
-        }
+        if (x + 1 < cnt) ld(x + 1, inf_n, orig_n, term_n, index_n);
         const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
         const bool reject = (inf >> 8) & 1u;
         if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
@@ -2658,19 +2581,11 @@ template <int NMAX>
 void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
   const uint32_t grid = apply_grid(h);
   if (ev) (void)hipEventRecord(ev[2], h->stream);
-#ifdef HB_X_LEAD3
-  if constexpr (true) hipLaunchKernelGGL(k_apply_lead<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
-#else
   if constexpr (NMAX >= 5) hipLaunchKernelGGL(k_apply_lead<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
-#endif
   else hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
   if (ev) (void)hipEventRecord(ev[3], h->stream);
   if constexpr (NMAX >= 5) {  // the general kernel spills at n >= 5: elections go first
-#ifndef HB_X_NO_ELECT
     if (!sz_on(h->max_msg_size))
-#else
-    if (false)
-#endif
       hipLaunchKernelGGL(k_elect<NMAX>, dim3(ELECT_GRID ? std::min(grid, ELECT_GRID) : grid), dim3(PART), 0,
                          h->stream, a);
   }
@@ -2758,10 +2673,8 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
     return (std::max<uint32_t>(ceil_log2(nbk_for(sl)), 1) + RDX_BITS - 1) / RDX_BITS;
   };
   h->sis_log = SIS_LOG_MAX;
-#ifndef HB_FIXED_SIS
   const uint32_t sl_min = route_rg_log(route_kmax(h->nmax)) - PART_LOG;
   while (h->sis_log > sl_min && passes_for(h->sis_log - 1) == passes_for(SIS_LOG_MAX)) --h->sis_log;
-#endif
   h->NBK = nbk_for(h->sis_log);
   h->passes = passes_for(h->sis_log);
   h->bk_bits = std::max<uint32_t>(ceil_log2(h->NBK), 1);
@@ -3462,7 +3375,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
       // two passes split the bucket id's bits evenly (the first takes the low
       // half): 5 + 5 bits for 1,024 buckets write 64-message digit runs in both
       // passes, where 8 + 2 wrote 8-message runs (partial lines) in the first
-      const uint32_t b0 = RDX_SPLIT ? h->bk_bits / 2 + HB_RDX_SKEW : RDX_BITS;
+      const uint32_t b0 = h->bk_bits / 2;
       const uint32_t dbits = h->passes == 1 ? RDX_BITS : p == 0 ? b0 : h->bk_bits - b0;
       hipLaunchKernelGGL(k_radix_hist, dim3((ntiles + HIST_TPB - 1) / HIST_TPB), dim3(RDX_THREADS), 0, ps_st, src, h->G,
                          shift, dbits, ntiles, h->hist);

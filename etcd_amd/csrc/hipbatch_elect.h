@@ -122,9 +122,7 @@ struct ElectLane {
   // Lane::reset / transition / poll (raft/raft.go:334-404, :445-460)
   __device__ __forceinline__ void reset(uint64_t t) {
     if (term != t) {
-#ifndef HB_X_NOPUSH
       if (tfirst != HB_NO_INDEX) tr_push(S, g, tfirst, term);
-#endif
       term = t;
       set_vote(HB_REF_NONE);
       tfirst = HB_NO_INDEX;
@@ -190,11 +188,7 @@ struct ElectLane {
         win = true;
       } else {  // the MsgVotes (slot order) as one EVC_VBCAST word when there are two or more
         const uint32_t mask = ((1u << nn) - 1) & ~(1u << sf);
-#ifndef HB_X_NO_VBCAST
         if (mask & (mask - 1)) {
-#else
-        if (false) {
-#endif
           emit_ev(E, g & (PART - 1), EVC_VBCAST, mask, 0, last);
           nev += __popc(mask);
         } else {

@@ -74,25 +74,6 @@ struct FastLane {
     // arrays the meta flags mark as not kept are not read (M_TL / M_SM,
     // hipbatch_kernels.h); these loads issue once meta is in, beside the
     // ring heads, which wait for pm anyway
-#ifdef HB_X_UNCOND
-    {
-      const uint64_t tl0 = S.tlast[g];
-      uint64_t m0[NMAX], n0[NMAX];
-#pragma unroll
-      for (int s = 0; s < NMAX; ++s) {
-        m0[s] = S.match[(size_t)s * S.G + g];
-        n0[s] = S.next[(size_t)s * S.G + g];
-        pm[s] = S.pm[(size_t)s * S.G + g];
-      }
-      tlast = (mlo & (uint32_t)M_TL) ? last : tl0;
-      const uint32_t sf = (mlo & (uint32_t)M_SM) ? self() : 0xFFu;
-#pragma unroll
-      for (int s = 0; s < NMAX; ++s) {
-        match[s] = ((uint32_t)s == sf) ? last : m0[s];
-        next[s] = ((uint32_t)s == sf) ? last + 1 : n0[s];
-      }
-    }
-#else
     tlast = (mlo & (uint32_t)M_TL) ? last : at32(S.tlast, g);
     const uint32_t sf = (mlo & (uint32_t)M_SM) ? self() : 0xFFu;
 #pragma unroll
@@ -101,7 +82,6 @@ struct FastLane {
       next[s] = ((uint32_t)s == sf) ? last + 1 : at32(S.next, s * S.G + g);
       pm[s] = at32(S.pm, s * S.G + g);
     }
-#endif
     if (mlo & (uint32_t)M_RS) {  // a group k_elect left in the reset form: every slot written back
       const uint32_t nn = n();
 #pragma unroll
@@ -117,16 +97,12 @@ struct FastLane {
       }
     }
     // The ring heads are loaded with the state (one more round trip, beside
-    // nothing else); free_to reads one lazily if a lane has none.  Loading them
-    // only on demand (-DHB_X_LAZY_HEAD: an ack at or past Next - 1 frees the
-    // whole window unread) measured 1-3 % slower on cfg2 / cfg3 / cfg5.
-#ifndef HB_X_LAZY_HEAD
+    // nothing else); free_to reads one lazily if a lane has none.  (Loading
+    // them only on demand — an ack at or past Next - 1 frees the whole window
+    // unread — measured 1-3 % slower on cfg2 / cfg3 / cfg5.)
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) head[s] = pm_count(pm[s]) ? *ring_at(s, pm_start(pm[s])) : 0;
     hv = (1u << NMAX) - 1;
-#else
-    hv = 0;
-#endif
     dirty = 0;
     if (mlo & (uint32_t)M_RS) {
       mlo &= ~(uint32_t)M_RS;

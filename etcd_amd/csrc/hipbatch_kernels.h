@@ -716,9 +716,7 @@ struct Lane {
   // older runs (Runs, the log index).
   __device__ __forceinline__ void reset(uint64_t t) {
     if (term != t) {
-#ifndef HB_X_NOPUSH
       if (tfirst != HB_NO_INDEX) tr_push(S, g, tfirst, term);  // the old current-term run becomes an older run
-#endif
       term = t;
       set_vote(HB_REF_NONE);
       tfirst = HB_NO_INDEX;  // no entry carries a term newer than the old Term

@@ -460,7 +460,11 @@ class MultiNode:
             cm.snapshot, k = _snap_in(m.Snapshot)
             keep.append((ents, k))
         done = C.c_uint64()
-        _check("hbn_step_many", lib().hbn_step_many(self.p, n, gs, arr, C.byref(done)))
+        try:
+            _check("hbn_step_many", lib().hbn_step_many(self.p, n, gs, arr, C.byref(done)))
+        except (RaftPanic, HbnError) as e:
+            e.done = done.value  # the messages taken before the one that failed
+            raise
         return done.value
 
     def ProposeMany(self, items):
@@ -471,7 +475,11 @@ class MultiNode:
         ptrs = (C.c_void_p * max(1, n))(*[C.cast(b, C.c_void_p).value if b is not None else None for b in bufs])
         lens = (C.c_uint64 * max(1, n))(*[len(d or b"") for _, d in items])
         done = C.c_uint64()
-        _check("hbn_propose_many", lib().hbn_propose_many(self.p, n, gs, ptrs, lens, C.byref(done)))
+        try:
+            _check("hbn_propose_many", lib().hbn_propose_many(self.p, n, gs, ptrs, lens, C.byref(done)))
+        except (RaftPanic, HbnError) as e:
+            e.done = done.value
+            raise
         return done.value
 
     def SetThreads(self, k):

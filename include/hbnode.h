@@ -41,8 +41,12 @@ extern "C" {
 #define HBN_EEXIST         -11  /* CreateGroup for an id that exists                        */
 #define HBN_EAGAIN         -12  /* Ready: nothing to report, or the last Ready is not
                                    advanced yet (the reference's readyc is nil then)        */
-#define HBN_EUNSUPPORTED   -13  /* a group whose prs is empty receiving a message the device
-                                   would have to step (MsgHup, MsgProp, MsgApp, MsgVote ...) */
+#define HBN_EUNSUPPORTED   -13  /* outside the engine's limits, where the reference proceeds:
+                                   a group with more members than hbn_start's max_replicas
+                                   (at most HB_MAX_REPLICAS = 7: CreateGroup, or an
+                                   ApplyConfChange / snapshot restore adding one), or a group
+                                   whose prs is empty receiving a message the device would
+                                   have to step (MsgHup, MsgProp, MsgApp, MsgVote ...)      */
 #define HBN_EPANIC         -14  /* the reference panics here; see hbn_last_error()          */
 /* MemoryStorage errors (raft/storage.go:25-31) */
 #define HBN_ECOMPACTED     -20  /* ErrCompacted */
@@ -164,6 +168,16 @@ uint64_t hbn_entry_size(const hbn_entry* e);
 /* ---- MultiNode (raft/multinode.go:12-49) ---------------------------------- */
 /* StartMultiNode(id) on `device`: up to `capacity` groups of <= max_replicas
  * peers, Config.MaxInflightMsgs = max_inflight, MaxSizePerMsg = max_msg_size
+ *
+ * Engine limits (the reference has none of these: raft/raft.go:101-123 only
+ * requires MaxInflightMsgs > 0, addNode raft/raft.go:729-738 takes any id):
+ *   max_replicas <= HB_MAX_REPLICAS (7): a group's prs (self included) is at
+ *     most max_replicas; CreateGroup with more peers, or an ApplyConfChange /
+ *     snapshot restore that would add one, returns HBN_EUNSUPPORTED and leaves
+ *     the group unchanged;
+ *   1 <= max_inflight <= HB_MAX_INFLIGHT (1024), capacity <= 2^24 groups,
+ *   max_batch < 2^31 messages per device step: hbn_start returns HB_EINVAL.
+ * Within them every result is the reference's, bit for bit.
  * (any value: HB_NO_LIMIT, 0 or finite; the device's log index then holds
  * every entry's size, loaded and reserved by this library), at most max_batch
  * messages per device step (the batch is flushed early when it fills). */

@@ -342,12 +342,12 @@ def test_random_multinode_vs_oracle(seed, n):
 
 
 # ---------------------------------------------------------------- storage compaction / snapshots
-def _lagging_leader():
+def _lagging_leader(**kw):
     """Group 1 on node 1 with peers 1, 2, 3: node 1 leads at term 2, follower 2
     acks every entry, follower 3 never answers (Probe, paused, Next 4).  Four
     proposals later the log is 1..8, all committed, all in storage."""
     s = MemoryStorage()
-    mn = StartMultiNode(1)
+    mn = StartMultiNode(1, **kw)
     mn.CreateGroup(1, Config(10, 1), s, peers=[1, 2, 3])
 
     def cycle():
@@ -568,4 +568,65 @@ def test_bulk_step_stops_at_the_first_error():
     with pytest.raises(HbnError) as ei:
         mn.StepMany(items)
     assert "hbn_step_many" in str(ei.value)
+    mn.Stop()
+
+
+def test_bulk_step_after_a_flush_faults_the_group():
+    """A bulk call longer than max_batch: the batch is stepped when it fills, and
+    that step can fault a group (here "need non-empty snapshot", raft/raft.go:
+    246-256: the leader's storage was compacted without a snapshot and a lagging
+    follower's heartbeat response makes it send one).  hbn_step_many must stop
+    where the same hbn_step calls stop: the message whose push flushed the batch
+    is taken (it was checked before the flush), the next one for the faulted
+    group raises HBN_EPANIC, and done counts the messages before it."""
+    from etcd_amd.multinode import RaftPanic
+    hb2 = lambda: (1, Message(Type=abi.HB_MSG_HEARTBEAT_RESP, From=2, To=1, Term=2))
+    items = [(1, Message(Type=abi.HB_MSG_HEARTBEAT_RESP, From=3, To=1, Term=2)), hb2(), hb2(), hb2(), hb2()]
+    got = []
+    for bulk in (False, True):
+        mn, s, cycle = _lagging_leader(max_batch=2)
+        assert s.Compact(8) is None  # no CreateSnapshot: the storage's snapshot stays empty
+        mn.Tick()  # MsgBeat -> bcastHeartbeat resumes follower 3
+        cycle()
+        taken = 0
+        with pytest.raises(RaftPanic) as ei:
+            if bulk:
+                mn.StepMany(items)
+            else:
+                for g, m in items:
+                    mn.Step(g, m)
+                    taken += 1
+        got.append(ei.value.done if bulk else taken)
+        rd = mn.Ready()[1]
+        assert rd.fault == abi.HB_FAULT_EMPTY_SNAPSHOT
+        mn.Stop()
+    assert got == [3, 3]
+
+
+def test_member_limit_is_unsupported_not_invalid():
+    """The engine keeps at most max_replicas (<= 7) members per group; the
+    reference has no such limit (raft/raft.go:729-738).  CreateGroup with more
+    peers, and an ApplyConfChange adding one past the limit, return
+    HBN_EUNSUPPORTED and leave the group as it was."""
+    from etcd_amd.multinode import HBN_EUNSUPPORTED, HbnError
+    mn = StartMultiNode(1, capacity=8, max_replicas=3)
+    with pytest.raises(HbnError) as ei:
+        mn.CreateGroup(1, Config(10, 1), MemoryStorage(), peers=[1, 2, 3, 4])
+    assert ei.value.code == HBN_EUNSUPPORTED
+    s = MemoryStorage()
+    mn.CreateGroup(2, Config(10, 1), s, peers=[1, 2, 3])
+    with pytest.raises(HbnError) as ei:
+        mn.ApplyConfChange(2, ConfChangeAddNode, 4)
+    assert ei.value.code == HBN_EUNSUPPORTED
+    assert mn.ApplyConfChange(2, ConfChangeRemoveNode, 3) == [1, 2]
+    assert mn.ApplyConfChange(2, ConfChangeAddNode, 4) == [1, 2, 4]
+    mn.Stop()
+    mn = StartMultiNode(1, capacity=8)  # max_replicas 7
+    with pytest.raises(HbnError) as ei:
+        mn.CreateGroup(1, Config(10, 1), MemoryStorage(), peers=list(range(1, 9)))
+    assert ei.value.code == HBN_EUNSUPPORTED
+    mn.CreateGroup(2, Config(10, 1), MemoryStorage(), peers=list(range(1, 8)))
+    with pytest.raises(HbnError) as ei:
+        mn.ApplyConfChange(2, ConfChangeAddNode, 8)
+    assert ei.value.code == HBN_EUNSUPPORTED
     mn.Stop()
