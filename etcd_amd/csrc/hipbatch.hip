@@ -84,12 +84,20 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh16, 
 // scattered single records.  Messages of groups >= capacity are dropped in
 // the first pass.  Arrival order is preserved within every bucket.
 //
-// The final pass writes the apply input: one 24-byte MsgRec per message
+// The final pass writes the apply input: one 16-byte MsgRec per message
 // (info with the group's lane in bits 16-23 and its partition in the bucket
-// in bits 24-27, arrival index, term, index).  k_route reads the records and
-// writes the partition once more as a key byte per message, contiguous, for
-// the general kernel's bucket walk (a separate key array written here took
-// 8-byte runs per digit per tile: partial lines).
+// in bits 24-27, arrival index, Term and Index packed into one word, below).
+// k_route reads the records and writes the partition once more as a key byte
+// per message, contiguous, for the general kernel's bucket walk (a separate
+// key array written here took 8-byte runs per digit per tile: partial lines).
+//
+// The 16-byte record: every pass over the messages (scatter write, route read
+// and write, apply read) moves 16 instead of 24 bytes.  Term and Index share
+// one u64 (Index in bits 0-39, Term in 40-63) when they fit, which is every
+// message a raft cluster sends below 2^24 terms and 2^40 entries; otherwise
+// the record is marked REC_LONG and the first pass keeps the full pair in
+// the prep set's side table at the message's arrival index, where every
+// reader takes it from (rec_unpack).  Bit-exact for every u64 value.
 // ============================================================================
 struct BatchDev {
   const uint32_t* group;
@@ -127,12 +135,38 @@ constexpr uint32_t RDX_WAVES = RDX_THREADS / 64;
 constexpr uint32_t RDX_ROUNDS = HB_RDX_ROUNDS;
 constexpr uint32_t RDX_TILE = RDX_THREADS * RDX_ROUNDS;  // 2048
 
-struct MsgRec {      // apply input record (24 B)
-  uint32_t info;     // type | from << 4 | reject << 8 | lane << 16
+struct MsgRec {      // apply input record (16 B)
+  uint32_t info;     // type | from << 4 | reject << 8 | voted << 9 | lane << 16 | sub << 24 | long << 28
   uint32_t orig;     // arrival index in the batch
-  uint64_t term;
-  uint64_t index;
+  uint64_t ti;       // Index | Term << 40 (REC_LONG: side[2 orig], side[2 orig + 1])
 };
+static_assert(sizeof(MsgRec) == 16, "one dwordx4 per record");
+constexpr uint32_t REC_LONG = 1u << 28;
+constexpr uint32_t REC_IDX_BITS = 40;
+constexpr uint64_t REC_IDX_MASK = (1ull << REC_IDX_BITS) - 1;
+// pack (term, index) into ti; false: does not fit (REC_LONG)
+__device__ __forceinline__ bool rec_pack(uint64_t term, uint64_t index, uint64_t* ti) {
+  *ti = index | (term << REC_IDX_BITS);
+  return index <= REC_IDX_MASK && term < (1ull << (64 - REC_IDX_BITS));
+}
+// a record's Term and Index (a long record's from the side table)
+__device__ __forceinline__ void rec_unpack(uint32_t info, uint32_t orig, uint64_t ti, const uint64_t* side,
+                                           uint64_t* term, uint64_t* index) {
+  if (info & REC_LONG) {
+    *term = side[2 * (size_t)orig];
+    *index = side[2 * (size_t)orig + 1];
+  } else {
+    *term = ti >> REC_IDX_BITS;
+    *index = ti & REC_IDX_MASK;
+  }
+}
+// a route slot (lane-major [k][G], one dwordx4): info, arrival index, ti
+__device__ __forceinline__ void slot_unpack(const uint4 r, const uint64_t* side, uint32_t* info, uint32_t* orig,
+                                            uint64_t* term, uint64_t* index) {
+  *info = r.x;
+  *orig = r.y;
+  rec_unpack(r.x, r.y, (uint64_t)r.z | ((uint64_t)r.w << 32), side, term, index);
+}
 
 struct RadixSrc {
   const uint32_t* group;
@@ -141,13 +175,14 @@ struct RadixSrc {
   const uint64_t* index;
   const MsgRec* rec;      // ... or an intermediate pass's records (info without lane bits, arrival index)
   const uint32_t* n_dev;  // null: n
+  uint64_t* side;         // first pass: the long records' (term, index) by arrival index
   uint32_t n;
 };
 
 // Intermediate pass output: the group ids (what the next pass's histogram
-// reads) plus one 24-byte record per message, so that a digit's run of a tile
-// is one contiguous ~190-byte store instead of five runs of 32-64 bytes (the
-// SoA layout wrote 1.6x its bytes as partial lines on cfg4).
+// reads) plus one 16-byte record per message, so that a digit's run of a tile
+// is one contiguous store instead of several runs of 32-64 bytes (the SoA
+// layout wrote 1.6x its bytes as partial lines on cfg4).
 struct RadixDst {
   uint32_t* group;
   MsgRec* rec;
@@ -261,7 +296,7 @@ __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t nti
 // Tile loads of k_radix_scatter (coalesced: round r, lane l -> element wave*256 + r*64 + l).
 struct ScatTile {
   uint32_t g[RDX_ROUNDS], i[RDX_ROUNDS], o[RDX_ROUNDS];
-  uint64_t t[RDX_ROUNDS], x[RDX_ROUNDS];
+  uint64_t t[RDX_ROUNDS];  // packed ti
   bool v[RDX_ROUNDS];
 };
 __device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_t G, uint32_t base, uint32_t wave,
@@ -278,13 +313,19 @@ __device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_
       if (v) m = s.rec[i];
       T.i[r] = m.info;
       T.o[r] = m.orig;
-      T.t[r] = m.term;
-      T.x[r] = m.index;
-    } else {
-      T.i[r] = v ? s.info[i] : 0u;
+      T.t[r] = m.ti;
+    } else {  // the batch: pack Term and Index (a long pair goes to the side table)
+      const uint32_t inf = v ? s.info[i] : 0u;
+      const uint64_t tm = v ? s.term[i] : 0ull, ix = v ? s.index[i] : 0ull;
+      uint64_t ti;
+      const bool fits = rec_pack(tm, ix, &ti);
+      if (v && !fits) {
+        s.side[2 * (size_t)i] = tm;
+        s.side[2 * (size_t)i + 1] = ix;
+      }
+      T.i[r] = (inf & 0xFFFFu) | (fits ? 0u : REC_LONG);
       T.o[r] = v ? i : 0u;
-      T.t[r] = v ? s.term[i] : 0ull;
-      T.x[r] = v ? s.index[i] : 0ull;
+      T.t[r] = ti;
     }
   }
 }
@@ -308,8 +349,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
   __shared__ uint32_t st_group[RDX_TILE];
   __shared__ uint32_t st_info[RDX_TILE];
   __shared__ uint32_t st_orig[RDX_TILE];
-  __shared__ uint64_t st_term[RDX_TILE];
-  __shared__ uint64_t st_index[RDX_TILE];
+  __shared__ uint64_t st_ti[RDX_TILE];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint32_t nb = 1u << dbits;  // the pass's digits (totals / off rows hold nb)
   const uint32_t n = src_n(s);
@@ -384,8 +424,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
         st_group[p] = cur.g[r];
         st_info[p] = cur.i[r];
         st_orig[p] = cur.o[r];
-        st_term[p] = cur.t[r];
-        st_index[p] = cur.x[r];
+        st_ti[p] = cur.t[r];
       }
     }
     __syncthreads();
@@ -399,10 +438,10 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
         const uint32_t o = s_off[dg] + (p - s_dstart[dg]);
         if (FINAL) {
           MsgRec m;
-          m.info = (st_info[p] & 0xFFFFu) | ((g & (PART - 1)) << 16) | (((g >> PART_LOG) & ((1u << f.sis_log) - 1)) << 24);
+          m.info = (st_info[p] & (0xFFFFu | REC_LONG)) | ((g & (PART - 1)) << 16) |
+                   (((g >> PART_LOG) & ((1u << f.sis_log) - 1)) << 24);
           m.orig = st_orig[p];
-          m.term = st_term[p];
-          m.index = st_index[p];
+          m.ti = st_ti[p];
           f.rec[o] = m;
           if (f.bucket) f.bucket[o] = g >> (PART_LOG + f.sis_log);
         } else {
@@ -410,8 +449,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
           MsgRec m;
           m.info = st_info[p];
           m.orig = st_orig[p];
-          m.term = st_term[p];
-          m.index = st_index[p];
+          m.ti = st_ti[p];
           d.rec[o] = m;
         }
       }
@@ -472,10 +510,8 @@ struct ApplyArgs {
   // k_route -> k_apply_fast / k_apply: each group's first kmax messages, lane-major
   uint32_t kmax;            // slots per group (= route_kmax(nmax))
   uint8_t* cnt;             // [G] messages of the group in this batch (saturated at 255)
-  uint32_t* slot_info;      // [kmax][G]
-  uint32_t* slot_orig;      // [kmax][G]
-  uint64_t* slot_term;      // [kmax][G]
-  uint64_t* slot_index;     // [kmax][G]
+  uint4* slot;              // [kmax][G] MsgRec {info, arrival index, ti} (slot_unpack)
+  const uint64_t* side;     // [2 n] (term, index) of the REC_LONG records, by arrival index
 };
 
 // Message slots k_route keeps per group: n - 1 (one MsgAppResp per follower,
@@ -679,12 +715,14 @@ __device__ __forceinline__ void gather_round(St& sl, const ApplyArgs& a, uint32_
   for (uint32_t k = 0; k < PER; ++k) {
     const uint32_t i = tid + k * PART;
     if (i < fill) {
+      uint64_t tm, ix;
+      rec_unpack(m[k].info, m[k].orig, m[k].ti, a.side, &tm, &ix);
       sl.w[0][i] = m[k].info;
       sl.w[1][i] = m[k].orig;
-      sl.w[2][i] = (uint32_t)m[k].term;
-      sl.w[3][i] = (uint32_t)(m[k].term >> 32);
-      sl.w[4][i] = (uint32_t)m[k].index;
-      sl.w[5][i] = (uint32_t)(m[k].index >> 32);
+      sl.w[2][i] = (uint32_t)tm;
+      sl.w[3][i] = (uint32_t)(tm >> 32);
+      sl.w[4][i] = (uint32_t)ix;
+      sl.w[5][i] = (uint32_t)(ix >> 32);
       atomicAdd(&sl.cnt[(m[k].info >> 16) & (PART - 1)], 1u);
     }
   }
@@ -806,10 +844,7 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   constexpr uint32_t RG = RGm::RG, NP = RG / PART;
   const uint32_t sl = a.sis_log, W = 1u << (PART_LOG + sl - RGm::RG_LOG);
   __shared__ uint32_t l_cnt[RG];
-  __shared__ uint32_t l_info[KMAX][RG];
-  __shared__ uint32_t l_orig[KMAX][RG];
-  __shared__ uint64_t l_term[KMAX][RG];
-  __shared__ uint64_t l_index[KMAX][RG];
+  __shared__ uint4 l_slot[KMAX][RG];  // the group's first KMAX records as they will be stored
   __shared__ uint32_t l_ptot[NP];
   // blockIdx -> (bucket, w): the W sisters of a bucket share blockIdx % 8 (one XCD)
   const uint32_t x = blockIdx.x, q = x >> 3;
@@ -846,12 +881,8 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
       const uint32_t l = own ? (((sub[u] - sub_lo) << PART_LOG) | ((m[u].info >> 16) & (PART - 1))) : RG;
       if (l < RG) {
         const uint32_t r = atomicAdd(&l_cnt[l], 1u);
-        if (r < (uint32_t)KMAX) {
-          l_info[r][l] = m[u].info;
-          l_orig[r][l] = m[u].orig;
-          l_term[r][l] = m[u].term;
-          l_index[r][l] = m[u].index;
-        }
+        if (r < (uint32_t)KMAX)
+          l_slot[r][l] = make_uint4(m[u].info, m[u].orig, (uint32_t)m[u].ti, (uint32_t)(m[u].ti >> 32));
       }
     }
   }
@@ -862,15 +893,8 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
     if (g < G) {
       a.cnt[g] = (uint8_t)(c < 255 ? c : 255);
 #pragma unroll
-      for (uint32_t k = 0; k < (uint32_t)KMAX; ++k) {
-        if (k < c) {
-          const size_t o = (size_t)k * G + g;
-          a.slot_info[o] = l_info[k][i];
-          a.slot_orig[o] = l_orig[k][i];
-          a.slot_term[o] = l_term[k][i];
-          a.slot_index[o] = l_index[k][i];
-        }
-      }
+      for (uint32_t k = 0; k < (uint32_t)KMAX; ++k)
+        if (k < c) at32(a.slot, k * G + g) = l_slot[k][i];
     }
     uint32_t s = c;  // the wave's 64 groups lie in one partition
 #pragma unroll
@@ -1084,16 +1108,15 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 
   // a leader's used slots, in the state loads' round trip (both wait for meta
   // and the count); a group the fast path cannot finish reads none
   const bool slots = lead && cnt <= KMAX;
+  uint4 raw[KMAX];
 #pragma unroll
   for (uint32_t k = 0; k < KMAX; ++k) {
-    const uint32_t o = k * a.S.G + g;
-    const bool u = slots && k < cnt;
-    s_info[k] = u ? at32(a.slot_info, o) : 0u;
-    s_orig[k] = u ? at32(a.slot_orig, o) : 0u;
     // (n >= 5: a busier leader's terms too, for k_elect's step-down test below)
-    s_term[k] = (NMAX >= 5 ? leader && k < cnt : u) ? at32(a.slot_term, o) : 0ull;
-    s_index[k] = u ? at32(a.slot_index, o) : 0ull;
+    const bool u = NMAX >= 5 ? leader && k < cnt : slots && k < cnt;
+    raw[k] = u ? at32(a.slot, k * a.S.G + g) : make_uint4(0, 0, 0, 0);
   }
+#pragma unroll
+  for (uint32_t k = 0; k < KMAX; ++k) slot_unpack(raw[k], a.side, &s_info[k], &s_orig[k], &s_term[k], &s_index[k]);
   uint32_t vals[ST_N + 1];
   (void)fast_step<NMAX>(a, L, part, tid, live, lead, leader, prop_raw, cnt, s_info, s_orig, s_term, s_index,
                         a.ev_off[2 * part + 1], &l_pfill, &l_fill, l_flag, l_eflag, vals);
@@ -1220,7 +1243,7 @@ __device__ __forceinline__ bool apply_part(const ApplyArgs& a, uint32_t part, Ge
     uint32_t perm = 0;
 #pragma unroll
     for (uint32_t k = 0; k < KS; ++k) {
-      key[k] = k < cnt ? a.slot_orig[(size_t)k * a.S.G + g] : 0xFFFFFFFFu;
+      key[k] = k < cnt ? at32(a.slot, k * a.S.G + g).y : 0xFFFFFFFFu;
       perm |= k << (4 * k);
     }
 #pragma unroll
@@ -1240,25 +1263,16 @@ __device__ __forceinline__ bool apply_part(const ApplyArgs& a, uint32_t part, Ge
     // rolled loop: Lane::step is inlined once per call site)
     uint32_t inf_n = 0, orig_n = 0;
     uint64_t term_n = 0, index_n = 0;
-    if (cnt > skip) {
-      const size_t o = (size_t)((perm >> (4 * skip)) & 0xF) * a.S.G + g;
-      inf_n = a.slot_info[o];
-      orig_n = a.slot_orig[o];
-      term_n = a.slot_term[o];
-      index_n = a.slot_index[o];
-    }
+    if (cnt > skip)
+      slot_unpack(at32(a.slot, ((perm >> (4 * skip)) & 0xF) * a.S.G + g), a.side, &inf_n, &orig_n, &term_n, &index_n);
 #pragma nounroll
     for (uint32_t x = skip; x < cnt; ++x) {
       if (L.faulted()) break;
       const uint32_t inf = inf_n, morig = orig_n;
       const uint64_t mterm = term_n, mindex = index_n;
-      if (x + 1 < cnt) {
-        const size_t o = (size_t)((perm >> (4 * (x + 1))) & 0xF) * a.S.G + g;
-        inf_n = a.slot_info[o];
-        orig_n = a.slot_orig[o];
-        term_n = a.slot_term[o];
-        index_n = a.slot_index[o];
-      }
+      if (x + 1 < cnt)
+        slot_unpack(at32(a.slot, ((perm >> (4 * (x + 1))) & 0xF) * a.S.G + g), a.side, &inf_n, &orig_n, &term_n,
+                    &index_n);
       if (!step_one(inf, morig, mterm, mindex, x)) break;
     }
   }
@@ -1476,7 +1490,7 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
       uint32_t perm = 0;
 #pragma unroll
       for (uint32_t k = 0; k < KS; ++k) {
-        key[k] = k < cnt ? a.slot_orig[(size_t)k * a.S.G + g] : 0xFFFFFFFFu;
+        key[k] = k < cnt ? at32(a.slot, k * a.S.G + g).y : 0xFFFFFFFFu;
         perm |= k << (4 * k);
       }
 #pragma unroll
@@ -1498,9 +1512,9 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
       uint32_t inf_n = 0;
       uint64_t term_n = 0;
       auto ld = [&](uint32_t y, uint32_t& inf, uint64_t& tm) {
-        const size_t o = (size_t)((perm >> (4 * y)) & 0xF) * a.S.G + g;
-        inf = a.slot_info[o];
-        tm = a.slot_term[o];
+        uint32_t org;
+        uint64_t ix;
+        slot_unpack(at32(a.slot, ((perm >> (4 * y)) & 0xF) * a.S.G + g), a.side, &inf, &org, &tm, &ix);
       };
       if (x < cnt) ld(x, inf_n, term_n);
 #pragma nounroll
@@ -1603,7 +1617,14 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   if (slots && !spec) {  // a busy leader without a proposal: load it unless a higher term steps it down
     const uint64_t t = at32(a.S.term, g);
 #pragma unroll
-    for (uint32_t k = 0; k < KS; ++k) higher |= k < cnt && at32(a.slot_term, k * a.S.G + g) > t;
+    for (uint32_t k = 0; k < KS; ++k) {
+      if (k < cnt) {
+        uint32_t inf, org;
+        uint64_t tm, ix;
+        slot_unpack(at32(a.slot, k * a.S.G + g), a.side, &inf, &org, &tm, &ix);
+        higher |= tm > t;
+      }
+    }
     if (!higher) {
       L.load();
       loaded = true;
@@ -1616,7 +1637,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   const bool keys = slots && loaded;
 #pragma unroll
   for (uint32_t k = 0; k < KS; ++k) {
-    key[k] = (keys && k < cnt) ? at32(a.slot_orig, k * a.S.G + g) : 0xFFFFFFFFu;
+    key[k] = (keys && k < cnt) ? at32(a.slot, k * a.S.G + g).y : 0xFFFFFFFFu;
     perm |= k << (4 * k);
   }
   // arrival order of the slots (odd-even transposition, slot numbers as nibbles)
@@ -1666,11 +1687,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
       uint32_t inf_n = 0, orig_n = 0;
       uint64_t term_n = 0, index_n = 0;
       auto ld = [&](uint32_t y, uint32_t& inf, uint32_t& org, uint64_t& tm, uint64_t& ix) {
-        const size_t o = (size_t)((perm >> (4 * y)) & 0xF) * a.S.G + g;
-        inf = a.slot_info[o];
-        org = a.slot_orig[o];
-        tm = a.slot_term[o];
-        ix = a.slot_index[o];
+        slot_unpack(at32(a.slot, ((perm >> (4 * y)) & 0xF) * a.S.G + g), a.side, &inf, &org, &tm, &ix);
       };
       ld(0, inf_n, orig_n, term_n, index_n);
 #pragma nounroll
@@ -2329,10 +2346,8 @@ struct PrepSet {
   uint8_t* cnt = nullptr;         // [G]
   uint8_t* dstage = nullptr;      // device copy of the packed host batch (grown on demand)
   uint64_t dstage_cap = 0;
-  uint32_t* slot_info = nullptr;  // [nmax-1][G]
-  uint32_t* slot_orig = nullptr;
-  uint64_t* slot_term = nullptr;
-  uint64_t* slot_index = nullptr;
+  uint4* slot = nullptr;          // [route_kmax][G]
+  uint64_t* side = nullptr;       // [2 max_batch] long records' (term, index)
   uint64_t* ev_off = nullptr;     // [2 NB] event chunk offsets (route writes the M chunks)
   uint32_t* ev_counts = nullptr;  // [2 NB]
   hipEvent_t prepped = nullptr;   // prep stream: this set is ready
@@ -2695,10 +2710,8 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
     ALLOC(ps.bk_fill, (size_t)h->NBK * CTR_STRIDE);
     ALLOC(ps.ctr, CTR_WORDS);
     ALLOC(ps.cnt, G);
-    ALLOC(ps.slot_info, route_kmax(R) * G);
-    ALLOC(ps.slot_orig, route_kmax(R) * G);
-    ALLOC(ps.slot_term, route_kmax(R) * G);
-    ALLOC(ps.slot_index, route_kmax(R) * G);
+    ALLOC(ps.slot, route_kmax(R) * G);
+    ALLOC(ps.side, 2 * mb);
     ALLOC(ps.ev_counts, 2ull * h->NB);
     ALLOC(ps.ev_off, 2ull * h->NB);
   }
@@ -3366,7 +3379,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     HB_CHECK(hipMemsetAsync(ps.ctr, 0, CTR_WORDS * 4ull, ps_st));
   } else {
     const uint32_t ntiles = (uint32_t)((b->n + RDX_TILE - 1) / RDX_TILE);
-    RadixSrc src{bd.group, bd.info, bd.term, bd.index, nullptr, nullptr, (uint32_t)b->n};
+    RadixSrc src{bd.group, bd.info, bd.term, bd.index, nullptr, nullptr, ps.side, (uint32_t)b->n};
     const FinalDst fin{ps.rec, ps.bucket, h->passes == 1 ? ps.bk_off : nullptr, h->NBK, h->sis_log};
     uint32_t shift = PART_LOG + h->sis_log;
     for (uint32_t p = 0; p < h->passes; ++p) {
@@ -3387,7 +3400,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
       else
         hipLaunchKernelGGL(k_radix_scatter<false>, dim3((ntiles + SCAT_TPW - 1) / SCAT_TPW), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
                            shift, dbits, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
-      src = RadixSrc{dst.group, nullptr, nullptr, nullptr, dst.rec, h->n_valid, (uint32_t)b->n};
+      src = RadixSrc{dst.group, nullptr, nullptr, nullptr, dst.rec, h->n_valid, nullptr, (uint32_t)b->n};
       shift += dbits;
     }
     if (h->passes > 1)
@@ -3436,10 +3449,8 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.commit0 = h->commit0;
   aa.kmax = route_kmax(h->nmax);
   aa.cnt = ps.cnt;
-  aa.slot_info = ps.slot_info;
-  aa.slot_orig = ps.slot_orig;
-  aa.slot_term = ps.slot_term;
-  aa.slot_index = ps.slot_index;
+  aa.slot = ps.slot;
+  aa.side = ps.side;
   switch (h->nmax) {
     case 3: launch_route<route_kmax(3)>(h, aa, ps_st); break;
     case 5: launch_route<route_kmax(5)>(h, aa, ps_st); break;
