@@ -185,6 +185,41 @@ def cpu_baseline_tick(n, groups=200_000, W=256, budget_s=10.0, max_steps=50):
                       f"{steps} ticks in {spent:.2f} s, one core"}
 
 
+FOLLOW_GROUP_BYTES = 196  # SURVEY.md 8(d) rule applied to the follow step (follow_alg_note)
+
+
+def follow_alg_note():
+    return ("per group per follow step (SURVEY.md 8(d) rule: each field read once R / written once W): "
+            "MsgApp 48 B (message 24, m.LogTerm 8, m.Commit 8, entry term 8), MsgHeartbeat 32 B (message 24, "
+            "m.Commit 8), group 116 B (Term 8R, meta 8R, committed 8R+8W, lastIndex 8R+8W, firstIndex 8R, "
+            "termFirst 8R, elapsed 4W, 6 event words 48W: two step markers, two responses, append, commit) "
+            "= 196 B = 98 B per message")
+
+
+def cpu_baseline_follow(n, groups=200_000, W=256, budget_s=10.0, max_steps=40):
+    """The C oracle on a bounded sample of the follow workload (stepFollower ->
+    handleAppendEntries / handleHeartbeat, raft/raft.go:616-669), one core."""
+    from etcd_amd import abi, synth
+    from oracle.pyoracle import OracleGroups
+    g, runs = synth.follow_groups(groups, n, seed=0x5EED0006, with_runs="flat")
+    og = OracleGroups(g, runs, W)
+    msgs = commits = 0
+    spent = 0.0
+    steps = 0
+    while spent < budget_s and steps < max_steps:
+        b = synth.follow_batch(g, steps)
+        t0 = time.perf_counter()
+        _, st = og.step(b)
+        spent += time.perf_counter() - t0
+        msgs += int(st[abi.HB_STAT_MSGS])
+        commits += int(st[abi.HB_STAT_COMMITS])
+        steps += 1
+    return {"value": msgs / spent, "unit": "msgs/s", "cores": 1, "kind": "port", "commits_per_s": commits / spent,
+            "sample": f"oracle/raft_oracle.c (C restatement, not the Go reference), {groups} groups x {n}, "
+                      f"{steps} follow steps (MsgApp + MsgHeartbeat per group), {msgs} messages in {spent:.2f} s, "
+                      f"one core"}
+
+
 def cpu_baseline_wire(n, groups=100_000, W=256, budget_s=10.0, max_steps=20):
     """The C oracle decoding the cfg2 wire records (orc_decode_batch, the
     reference's Unmarshal restated) and stepping them, one core."""
@@ -354,14 +389,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["cfg2", "cfg5", "e2e", "cfg3", "cfg4", "tick", "wire", "multinode"],
+    ap.add_argument("--workload", choices=["cfg2", "cfg5", "e2e", "cfg3", "cfg4", "tick", "wire", "multinode", "follow"],
                     default="cfg2",
                     help="cfg2 (headline: 1M groups x 3 per GPU), cfg5 (8M groups x 3 per GPU = BASELINE.json "
                          "configs[4] at 8 GPUs), e2e = cfg2 with the batch in host memory and the events copied "
                          "back every step, cfg3 lagging followers, cfg4 election storm, "
                          "tick = MultiNode.Tick over the cfg2 groups (SURVEY.md 8(f) rank 1), "
                          "wire = cfg2 from raftpb wire records: hb_decode + hb_step (8(f) rank 3), "
-                         "multinode = the MultiNode API end to end (Step/Propose/Ready/Advance, 8(f) rank 2)")
+                         "multinode = the MultiNode API end to end (Step/Propose/Ready/Advance, 8(f) rank 2), "
+                         "follow = the follower side of cfg2: 1M followed groups x 3, each receiving its "
+                         "leader's MsgApp (1 entry) and MsgHeartbeat per step (8(f) rank 4)")
     ap.add_argument("--groups", type=int, default=None,
                     help="groups per GPU (cfg2/cfg3/e2e: 1M, cfg5: 8M, cfg4: 4M)")
     ap.add_argument("--replicas", type=int, default=None, help="cfg2/cfg5: 3, cfg3: 5, cfg4: 7")
@@ -791,7 +828,8 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     from etcd_amd import abi, synth
     from etcd_amd.hipbatch import Engine
     n, W, G = args.replicas, args.inflight, args.groups
-    seed = {"cfg3": 0x5EED0003, "cfg4": 0x5EED0004, "tick": 0x5EED0002, "wire": 0x5EED0002}[args.workload] + rank
+    seed = {"cfg3": 0x5EED0003, "cfg4": 0x5EED0004, "tick": 0x5EED0002, "wire": 0x5EED0002,
+            "follow": 0x5EED0006}[args.workload] + rank
     stream = torch.cuda.current_stream(dev)
     total = args.warmup + args.steps
     st_acc = np.zeros(abi.HB_STAT_COUNT, np.uint64)
@@ -825,6 +863,46 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         torch.cuda.synchronize()
         ms_local = e0.elapsed_time(e1)
         st_acc = stats.cpu().numpy().astype(np.uint64)
+        timing = "K steps back to back, inputs resident in HBM"
+    elif args.workload == "follow":
+        g, _ = synth.follow_groups(G, n, seed=seed, with_runs=False)
+        b = synth.follow_batch(g, 0, seed=seed)
+        nmsg = len(b["group"])
+        eng = Engine(G, max_replicas=n, max_inflight=W, max_batch=nmsg, device=local, stream=stream)
+        eng.load_groups(g)
+        del g
+
+        def dv(a):
+            return torch.from_numpy(np.ascontiguousarray(a).view(np.int32 if a.dtype == np.uint32 else np.int64)).to(dev)
+        d_group, d_info, d_term, d_hint, d_eoff, d_eterm = (dv(b[k]) for k in ("group", "info", "term", "hint",
+                                                                            "eoff", "eterm"))
+        app = dv(((b["info"] & 0xF) == abi.HB_MSG_APP).astype(np.uint64))
+        i0, c0 = dv(b["index"]), dv(b["commit"])
+        # step k continues the stream: the follower's log is k entries longer (resident before timing)
+        d_index = [i0 + app * k for k in range(total)]
+        d_commit = [c0 + k for k in range(total)]
+        stats = torch.zeros(abi.HB_STAT_COUNT, dtype=torch.int64, device=dev)
+
+        def one(k, prof=False):
+            eng.step(d_group, d_info, d_term, d_index[k], d_hint, None, host=False, eoff=d_eoff, commit=d_commit[k],
+                     eterm=d_eterm, profile=prof)
+        for k in range(args.warmup):
+            one(k)
+        eng.set_stats_accum(stats)
+        eng.phase_reset()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for k in range(args.warmup, total):
+            one(k, "apply" if (k - args.warmup) % 4 == 0 else False)  # HIP events around k_apply_fast
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms_local = e0.elapsed_time(e1)
+        st_acc = stats.cpu().numpy().astype(np.uint64)
+        ph, nph = eng.phase_ms()
+        apply_us = float(ph[abi.HB_PHASE_APPLY]) * 1e3
         timing = "K steps back to back, inputs resident in HBM"
     elif args.workload == "tick":
         g, _ = synth.steady_groups(G, n, seed=seed, with_runs=False)
@@ -995,6 +1073,24 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         ok = int(st[abi.HB_STAT_VOTERESP]) == world * G * (n - 1) * args.steps and int(st[abi.HB_STAT_FAULTS]) == 0
         wl = f"cfg4: {G} raft groups x {n} per GPU, election storm (step-down, MsgHup, {n - 1} MsgVoteResp per group)"
         data = "synthetic (seeded cfg4 storm replayed at +4 terms per step)"
+    elif args.workload == "follow":
+        metric, unit, val = "follower-side messages stepped/sec (MsgApp + MsgHeartbeat, follow workload)", "msgs/s", \
+            int(st[abi.HB_STAT_MSGS]) / sec
+        alg = FOLLOW_GROUP_BYTES * G * args.steps  # per rank
+        alg_note = follow_alg_note()
+        kname = "k_apply_fast<3> (X mode: FollowLane)"
+        ach_k = FOLLOW_GROUP_BYTES * G / (apply_us * 1e-6) / 1e9 if apply_us > 0 else 0.0
+        tr, tsrc = pmc_traffic(args.traffic_json, "k_apply_fast<3, true>", G, n, apply_us)
+        extra = {"commits_per_s": int(st[abi.HB_STAT_COMMITS]) / sec, "entries_per_s": int(st[abi.HB_STAT_ENTRIES]) / sec,
+                 "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(ach_k, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(ach_k / HBM_PEAK_GBS, 4), "traffic": tr,
+                              "traffic_source": tsrc, "launch_us_timed": round(apply_us, 2),
+                              "alg_bytes_per_launch": FOLLOW_GROUP_BYTES * G, "alg_bytes_note": alg_note,
+                              "step_frac": round(alg / args.steps / (ms / args.steps * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+        ok = int(st[abi.HB_STAT_COMMITS]) == world * G * args.steps and \
+            int(st[abi.HB_STAT_MSGS]) == 2 * world * G * args.steps and int(st[abi.HB_STAT_FAULTS]) == 0
+        wl = f"follow: {G} raft groups x {n} per GPU that this node follows, MsgApp (1 entry) + MsgHeartbeat each"
+        data = "synthetic (seeded follow stream: every group's leader appends one entry and heartbeats per step)"
     else:
         metric, unit, val = "MsgAppResp applied/sec (cfg3 lagging followers)", "MsgAppResp/s", \
             int(st[abi.HB_STAT_APPRESP]) / sec
@@ -1043,7 +1139,8 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = {"cfg4": cpu_baseline_cfg4, "cfg3": cpu_baseline_cfg3,
-                                       "tick": cpu_baseline_tick, "wire": cpu_baseline_wire}[args.workload](n, W=W)
+                                       "tick": cpu_baseline_tick, "wire": cpu_baseline_wire,
+                                       "follow": cpu_baseline_follow}[args.workload](n, W=W)
             except Exception as e:  # report, never fake
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out))

@@ -142,6 +142,18 @@ struct MsgRec {      // apply input record (16 B)
 };
 static_assert(sizeof(MsgRec) == 16, "one dwordx4 per record");
 constexpr uint32_t REC_LONG = 1u << 28;
+// Follower-side batches (hb_batch.commit present, "X mode"): every record also
+// carries a 16-byte extension {hint (m.LogTerm / RejectHint), m.Commit} through
+// the partition and the route (recx / slotx), and a MsgApp's info says how
+// many entries it carries (bits 10-15) and REC_UNI when there are at most
+// REC_UNI_MAX and every one has the message's Term — what the follower fast
+// lane needs, with no gather by arrival index.
+constexpr uint32_t REC_UNI = 1u << 29;
+constexpr uint32_t REC_UNI_MAX = 8;
+constexpr uint32_t REC_NE_SHIFT = 10;
+__device__ __forceinline__ uint32_t rec_ne(uint32_t info) { return (info >> REC_NE_SHIFT) & 0x3Fu; }
+// the bits of a batch info word a record keeps (lane / partition bits are added by the final pass)
+constexpr uint32_t REC_KEEP = 0xFFFFu | REC_LONG | REC_UNI;
 constexpr uint32_t REC_IDX_BITS = 40;
 constexpr uint64_t REC_IDX_MASK = (1ull << REC_IDX_BITS) - 1;
 // pack (term, index) into ti; false: does not fit (REC_LONG)
@@ -177,6 +189,14 @@ struct RadixSrc {
   const uint32_t* n_dev;  // null: n
   uint64_t* side;         // first pass: the long records' (term, index) by arrival index
   uint32_t n;
+  // X mode (hb_batch.commit present): the batch's hint / commit / entry arrays
+  // (first pass) or the intermediate pass's extensions
+  const uint64_t* hint;
+  const uint64_t* mcommit;
+  const uint64_t* eoff;
+  const uint64_t* eterm;
+  uint64_t n_ent;
+  const uint4* recx;
 };
 
 // Intermediate pass output: the group ids (what the next pass's histogram
@@ -186,10 +206,12 @@ struct RadixSrc {
 struct RadixDst {
   uint32_t* group;
   MsgRec* rec;
+  uint4* recx;  // X mode
 };
 
 struct FinalDst {  // final pass output = apply input
   MsgRec* rec;
+  uint4* recx;       // X mode: {hint, commit} beside each record
   uint32_t* bucket;  // bucket id per message (multi-pass only, for k_bucket_bounds)
   uint32_t* bk_off;  // [NBK + 1] written by the one-pass scatter
   uint32_t NBK;
@@ -294,13 +316,16 @@ __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t nti
 }
 
 // Tile loads of k_radix_scatter (coalesced: round r, lane l -> element wave*256 + r*64 + l).
+template <bool X>
 struct ScatTile {
   uint32_t g[RDX_ROUNDS], i[RDX_ROUNDS], o[RDX_ROUNDS];
   uint64_t t[RDX_ROUNDS];  // packed ti
   bool v[RDX_ROUNDS];
+  uint4 x[X ? RDX_ROUNDS : 1];  // X mode: {hint, commit}
 };
+template <bool X>
 __device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_t G, uint32_t base, uint32_t wave,
-                                          uint32_t lane, ScatTile& T) {
+                                          uint32_t lane, ScatTile<X>& T) {
 #pragma unroll
   for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
     const uint32_t i = base + wave * (64 * RDX_ROUNDS) + r * 64 + lane;
@@ -314,6 +339,7 @@ __device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_
       T.i[r] = m.info;
       T.o[r] = m.orig;
       T.t[r] = m.ti;
+      if constexpr (X) T.x[r] = v ? s.recx[i] : make_uint4(0, 0, 0, 0);
     } else {  // the batch: pack Term and Index (a long pair goes to the side table)
       const uint32_t inf = v ? s.info[i] : 0u;
       const uint64_t tm = v ? s.term[i] : 0ull, ix = v ? s.index[i] : 0ull;
@@ -323,7 +349,23 @@ __device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_
         s.side[2 * (size_t)i] = tm;
         s.side[2 * (size_t)i + 1] = ix;
       }
-      T.i[r] = (inf & 0xFFFFu) | (fits ? 0u : REC_LONG);
+      uint32_t ie = (inf & 0x3FFu) | (fits ? 0u : REC_LONG);
+      if constexpr (X) {
+        const uint64_t h = (v && s.hint) ? s.hint[i] : 0ull, c = v ? s.mcommit[i] : 0ull;
+        T.x[r] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)c, (uint32_t)(c >> 32));
+        // a MsgApp's entries: how many, and whether all carry m.Term (the
+        // batch's entry arrays are in arrival order: near-contiguous per wave)
+        if (v && (inf & 0xFu) == HB_MSG_APP && s.eoff && s.eterm) {
+          const uint64_t e0 = s.eoff[i], e1 = i + 1 < n ? s.eoff[i + 1] : s.n_ent;
+          const uint64_t ne = e1 - e0;
+          bool uni = ne <= REC_UNI_MAX;
+#pragma unroll
+          for (uint32_t k = 0; k < REC_UNI_MAX; ++k)  // (bounded: the round loop stays unrolled)
+            if (uni && k < ne) uni = s.eterm[e0 + k] == tm;
+          if (uni) ie |= REC_UNI | ((uint32_t)ne << REC_NE_SHIFT);
+        }
+      }
+      T.i[r] = ie;
       T.o[r] = v ? i : 0u;
       T.t[r] = ti;
     }
@@ -337,7 +379,7 @@ __device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_
 #define HB_SCAT_TPW 2
 #endif
 constexpr uint32_t SCAT_TPW = HB_SCAT_TPW;
-template <bool FINAL>
+template <bool FINAL, bool X>
 __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, RadixDst d, FinalDst f, uint32_t G,
                                                               uint32_t shift, uint32_t dbits, uint32_t ntiles, const uint32_t* off,
                                                               const uint32_t* totals, uint32_t* n_valid) {
@@ -346,15 +388,20 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
   __shared__ uint32_t s_wcnt[RDX_WAVES][RDX_BINS];
   __shared__ uint32_t s_dstart[RDX_BINS + 1];
   __shared__ uint32_t sh4[4];
-  __shared__ uint32_t st_group[RDX_TILE];
-  __shared__ uint32_t st_info[RDX_TILE];
-  __shared__ uint32_t st_orig[RDX_TILE];
-  __shared__ uint64_t st_ti[RDX_TILE];
+  // the tile staged in digit order: group / info / arrival (3 x 4 B) and ti (8 B)
+  // per message; X mode then stages the extensions {hint, commit} (16 B) in the
+  // same 40 KB once the records are written (two workgroups still fit a CU)
+  __shared__ uint64_t st_buf[RDX_TILE * 5 / 2];
+  uint32_t* const st_group = reinterpret_cast<uint32_t*>(st_buf);
+  uint32_t* const st_info = st_group + RDX_TILE;
+  uint32_t* const st_orig = st_info + RDX_TILE;
+  uint64_t* const st_ti = st_buf + 3 * RDX_TILE / 2;
+  uint4* const st_x = reinterpret_cast<uint4*>(st_buf);
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint32_t nb = 1u << dbits;  // the pass's digits (totals / off rows hold nb)
   const uint32_t n = src_n(s);
   const uint32_t tile0 = blockIdx.x * SCAT_TPW;
-  ScatTile cur, nxt;
+  ScatTile<X> cur, nxt;
   scat_load(s, n, G, tile0 * RDX_TILE, wave, lane, cur);
   {
     const uint32_t t = tid < nb ? totals[tid] : 0u;
@@ -417,10 +464,12 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
       if (tid == 0) s_dstart[RDX_BINS] = all;
     }
     __syncthreads();
+    uint32_t sp[RDX_ROUNDS];  // staging position of this thread's messages
 #pragma unroll
     for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+      sp[r] = s_dstart[vd[r]] + s_wcnt[wave][vd[r]] + vr[r];
       if (cur.v[r]) {
-        const uint32_t p = s_dstart[vd[r]] + s_wcnt[wave][vd[r]] + vr[r];
+        const uint32_t p = sp[r];
         st_group[p] = cur.g[r];
         st_info[p] = cur.i[r];
         st_orig[p] = cur.o[r];
@@ -429,6 +478,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
     }
     __syncthreads();
     const uint32_t valid = s_dstart[RDX_BINS];
+    uint32_t wo[RDX_ROUNDS];  // output position of staging position r * RDX_THREADS + tid
 #pragma unroll
     for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
       const uint32_t p = r * RDX_THREADS + tid;
@@ -436,9 +486,10 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
         const uint32_t g = st_group[p];
         const uint32_t dg = rdx_digit(g, shift, dbits);
         const uint32_t o = s_off[dg] + (p - s_dstart[dg]);
+        wo[r] = o;
         if (FINAL) {
           MsgRec m;
-          m.info = (st_info[p] & (0xFFFFu | REC_LONG)) | ((g & (PART - 1)) << 16) |
+          m.info = (st_info[p] & REC_KEEP) | ((g & (PART - 1)) << 16) |
                    (((g >> PART_LOG) & ((1u << f.sis_log) - 1)) << 24);
           m.orig = st_orig[p];
           m.ti = st_ti[p];
@@ -452,6 +503,18 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
           m.ti = st_ti[p];
           d.rec[o] = m;
         }
+      }
+    }
+    if constexpr (X) {  // the extensions, through the same staging
+      __syncthreads();
+#pragma unroll
+      for (uint32_t r = 0; r < RDX_ROUNDS; ++r)
+        if (cur.v[r]) st_x[sp[r]] = cur.x[r];
+      __syncthreads();
+#pragma unroll
+      for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+        const uint32_t p = r * RDX_THREADS + tid;
+        if (p < valid) (FINAL ? f.recx : d.recx)[wo[r]] = st_x[p];
       }
     }
     __syncthreads();  // the next tile reuses s_off / s_wcnt / s_dstart / the staging
@@ -476,6 +539,7 @@ __global__ void k_bucket_bounds(const uint32_t* bucket, const uint32_t* n_dev, u
 // ============================================================================
 // Phase 2: apply
 // ============================================================================
+#include "hipbatch_follow.h"  // (reads the record layout above)
 struct ApplyArgs {
   DevState S;
   const MsgRec* rec;        // sorted batch: bucket order, arrival order inside a bucket
@@ -512,6 +576,9 @@ struct ApplyArgs {
   uint8_t* cnt;             // [G] messages of the group in this batch (saturated at 255)
   uint4* slot;              // [kmax][G] MsgRec {info, arrival index, ti} (slot_unpack)
   const uint64_t* side;     // [2 n] (term, index) of the REC_LONG records, by arrival index
+  // X mode (follower-side batches): the records' extensions {hint, commit}
+  const uint4* recx;        // beside rec (k_route input)
+  uint4* slotx;             // [kmax][G] beside slot (null: no X mode this step)
 };
 
 // Message slots k_route keeps per group: n - 1 (one MsgAppResp per follower,
@@ -838,13 +905,14 @@ template <int KMAX> struct RouteGeom {
   // workgroups per bucket: 2^(PART_LOG + sis_log - RG_LOG) (sis_log >= RG_LOG - PART_LOG)
 };
 
-template <int KMAX>
+template <int KMAX, bool X>
 __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   using RGm = RouteGeom<KMAX>;
   constexpr uint32_t RG = RGm::RG, NP = RG / PART;
   const uint32_t sl = a.sis_log, W = 1u << (PART_LOG + sl - RGm::RG_LOG);
   __shared__ uint32_t l_cnt[RG];
   __shared__ uint4 l_slot[KMAX][RG];  // the group's first KMAX records as they will be stored
+  __shared__ uint4 l_slotx[X ? KMAX : 1][X ? RG : 1];  // X mode: their extensions
   __shared__ uint32_t l_ptot[NP];
   // blockIdx -> (bucket, w): the W sisters of a bucket share blockIdx % 8 (one XCD)
   const uint32_t x = blockIdx.x, q = x >> 3;
@@ -860,11 +928,13 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   const uint32_t sub_lo = lg0 >> PART_LOG, sub_hi = (lg0 + RG) >> PART_LOG;
   for (uint32_t base = lo; base < hi; base += ROUTE_THREADS * ROUTE_UNROLL) {
     MsgRec m[ROUTE_UNROLL];
+    uint4 mx[X ? ROUTE_UNROLL : 1];
     uint32_t sub[ROUTE_UNROLL];
 #pragma unroll
     for (uint32_t u = 0; u < ROUTE_UNROLL; ++u) {
       const uint32_t p = base + u * ROUTE_THREADS + tid;
       if (p < hi) m[u] = a.rec[p];
+      if constexpr (X) mx[u] = p < hi ? a.recx[p] : make_uint4(0, 0, 0, 0);
       sub[u] = p < hi ? (m[u].info >> 24) & 0xFu : 0xFFu;  // the partition in the bucket
     }
     if (w == 0) {  // the key bytes the general kernel's bucket walk scans (one coalesced store per lane)
@@ -881,8 +951,10 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
       const uint32_t l = own ? (((sub[u] - sub_lo) << PART_LOG) | ((m[u].info >> 16) & (PART - 1))) : RG;
       if (l < RG) {
         const uint32_t r = atomicAdd(&l_cnt[l], 1u);
-        if (r < (uint32_t)KMAX)
+        if (r < (uint32_t)KMAX) {
           l_slot[r][l] = make_uint4(m[u].info, m[u].orig, (uint32_t)m[u].ti, (uint32_t)(m[u].ti >> 32));
+          if constexpr (X) l_slotx[r][l] = mx[X ? u : 0];
+        }
       }
     }
   }
@@ -893,8 +965,12 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
     if (g < G) {
       a.cnt[g] = (uint8_t)(c < 255 ? c : 255);
 #pragma unroll
-      for (uint32_t k = 0; k < (uint32_t)KMAX; ++k)
-        if (k < c) at32(a.slot, k * G + g) = l_slot[k][i];
+      for (uint32_t k = 0; k < (uint32_t)KMAX; ++k) {
+        if (k < c) {
+          at32(a.slot, k * G + g) = l_slot[k][i];
+          if constexpr (X) at32(a.slotx, k * G + g) = l_slotx[k][i];
+        }
+      }
     }
     uint32_t s = c;  // the wave's 64 groups lie in one partition
 #pragma unroll
@@ -929,11 +1005,14 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
 // lead: a leader whose state is loaded (the fast path may step it); leader:
 // the group is a leader (for k_elect's test) — a leader with more messages
 // than slots and no proposal is handed over with its state unloaded.
+// fol (X mode): a follower whose messages all sit in its slots, stepped by
+// FollowLane as far as it takes them (s_h / s_c: m.LogTerm, m.Commit).
 template <int NMAX>
-__device__ __forceinline__ bool fast_step(const ApplyArgs& a, FastLane<NMAX>& L, uint32_t part, uint32_t lane,
-                                          bool live, bool lead, bool leader, uint32_t prop_raw, uint32_t cnt,
+__device__ __forceinline__ bool fast_step(const ApplyArgs& a, FollowLane<NMAX>& L, uint32_t part, uint32_t lane,
+                                          bool live, bool lead, bool leader, bool fol, uint32_t prop_raw, uint32_t cnt,
                                           uint32_t (&s_info)[NMAX - 1], uint32_t (&s_orig)[NMAX - 1],
                                           uint64_t (&s_term)[NMAX - 1], uint64_t (&s_index)[NMAX - 1],
+                                          uint64_t (&s_h)[NMAX - 1], uint64_t (&s_c)[NMAX - 1],
                                           uint64_t moff, uint32_t* l_pfill, uint32_t* l_fill, uint32_t* l_flag,
                                           uint32_t* l_eflag, uint32_t (&vals)[ST_N + 1]) {
   constexpr uint32_t KMAX = NMAX - 1;
@@ -972,21 +1051,25 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FastLane<NMAX>& L,
     for (uint32_t k = (r & 1); k + 1 < KMAX; k += 2) {
       const bool sw = s_orig[k + 1] < s_orig[k];
       const uint32_t i0 = s_info[k], o0 = s_orig[k];
-      const uint64_t t0 = s_term[k], x0 = s_index[k];
+      const uint64_t t0 = s_term[k], x0 = s_index[k], h0 = s_h[k], c0 = s_c[k];
       s_info[k] = sw ? s_info[k + 1] : i0;
       s_orig[k] = sw ? s_orig[k + 1] : o0;
       s_term[k] = sw ? s_term[k + 1] : t0;
       s_index[k] = sw ? s_index[k + 1] : x0;
+      s_h[k] = sw ? s_h[k + 1] : h0;
+      s_c[k] = sw ? s_c[k + 1] : c0;
       s_info[k + 1] = sw ? i0 : s_info[k + 1];
       s_orig[k + 1] = sw ? o0 : s_orig[k + 1];
       s_term[k + 1] = sw ? t0 : s_term[k + 1];
       s_index[k + 1] = sw ? x0 : s_index[k + 1];
+      s_h[k + 1] = sw ? h0 : s_h[k + 1];
+      s_c[k + 1] = sw ? c0 : s_c[k + 1];
     }
   }
   L.E.chunk = a.ev + moff;
   L.E.fill = l_fill;
   uint32_t j = 0;  // messages consumed
-  if (live && !lead && cnt > 0 && !flagged) {
+  if (live && !lead && !fol && cnt > 0 && !flagged) {
     flagged = true;
     resume = 0;
   }
@@ -1017,8 +1100,29 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FastLane<NMAX>& L,
       j++;
     }
   }
+  bool fstepped = false;  // FollowLane stepped a message: its state is stored
+  if (fol) {
+#pragma unroll
+    for (uint32_t k = 0; k < KMAX; ++k) {
+      if (k >= cnt || flagged) break;
+      const uint32_t inf = s_info[k];
+      const uint32_t from = (inf >> 4) & 0xF;
+      if (!L.takes_follow(inf, from, s_term[k], s_index[k], s_h[k], s_c[k])) {
+        flagged = true;
+        resume = j;
+        break;
+      }
+      L.arrival = s_orig[k];
+      L.step_follow(inf, from, s_term[k], s_index[k], s_h[k], s_c[k]);
+      fstepped = true;
+      st_msgs++;
+      j++;
+    }
+  }
 
   if (lead) L.store();
+  if (fstepped) L.store_follow();
+  const bool stored = lead || fstepped;
   if constexpr (NMAX >= 5) {  // k_elect's candidates: an election (or a step-down) is likely
     bool higher = false;
 #pragma unroll
@@ -1027,11 +1131,11 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FastLane<NMAX>& L,
   }
   if (flagged) {
     atomicOr(&l_flag[lane >> 5], 1u << (lane & 31));
-    at32(a.resume, g) = resume | (lead ? 0u : 1u << 30);
-    if (lead) at32(a.commit0, g) = commit0;
+    at32(a.resume, g) = resume | (stored ? 0u : 1u << 30);
+    if (stored) at32(a.commit0, g) = commit0;
   }
   vals[ST_MSGS] = st_msgs;
-  vals[ST_APPRESP] = st_msgs;  // every fast message is a MsgAppResp
+  vals[ST_APPRESP] = lead ? st_msgs : 0u;  // every leader message here is a MsgAppResp
   vals[ST_VOTERESP] = 0;
   vals[ST_DROPPED] = st_drop;
   vals[ST_COMMITS] = (uint32_t)(!flagged && L.committed != commit0);  // commitTo only raises
@@ -1062,7 +1166,7 @@ __device__ __forceinline__ void fast_close(const ApplyArgs& a, uint32_t part, co
     a.el_list[(size_t)xs * a.NB + atomicAdd(&a.el_cnt[xs * CTR_STRIDE], 1u)] = part;
 }
 
-template <int NMAX>
+template <int NMAX, bool X>
 __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 ? HB_FAST5_WAVES : HB_FAST7_WAVES))) k_apply_fast(ApplyArgs a) {
   constexpr uint32_t KMAX = NMAX - 1;  // one MsgAppResp per follower per batch
   __shared__ uint32_t l_fill, l_pfill;
@@ -1080,12 +1184,15 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 
   if (tid < FLAG_WORDS) l_flag[tid] = l_eflag[tid] = 0;
 
   // ---- every load of the lane, one round trip
-  FastLane<NMAX> L;
+  FollowLane<NMAX> L;
   L.S = a.S;
   L.g = g;
   L.mlo = gvalid ? at32(reinterpret_cast<uint32_t*>(a.S.meta), 2 * g) : 0u;
   const uint32_t prop_raw = (a.props && gvalid) ? at32(a.props, g) : 0u;
   const uint32_t cnt = gvalid ? at32(a.cnt, g) : 0u;
+  // The state that depends on nothing is loaded beside meta (one round trip
+  // fewer for every leader; a group with no fast-path work wastes 52 bytes)
+  if (gvalid) L.load_head();
   // A group takes part when its slot is live (n > 0) and not faulted.
   const bool live = gvalid && L.n() != 0 && L.faulted() == 0;
   // Only a leader has fast-path work: any other live group is handed to
@@ -1097,17 +1204,24 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 
   // every group; k_elect / k_apply load it); n >= 5 reads its Term for
   // k_elect's step-down test
   const bool lead = leader && (cnt <= KMAX || prop_raw != 0);
+  // X mode: a follower whose messages all sit in its slots and that has no
+  // dense proposal (stepFollower MsgProp forwards it: the general lane)
+  const bool fol = X && live && L.state() == HB_STATE_FOLLOWER && cnt > 0 && cnt <= KMAX && prop_raw == 0;
   L.dirty = 0;
   L.nev = 0;
-  L.last = L.committed = 0;
-  L.term = 0;
-  if (lead) L.load();
-  else if (NMAX >= 5 && leader) L.term = at32(a.S.term, g);
+  if (lead) {
+    L.load_rest();
+  } else if (fol) {
+    L.load_follow();
+  } else {
+    L.last = L.committed = 0;
+    if (!(NMAX >= 5 && leader)) L.term = 0;
+  }
   uint32_t s_info[KMAX], s_orig[KMAX];
-  uint64_t s_term[KMAX], s_index[KMAX];
-  // a leader's used slots, in the state loads' round trip (both wait for meta
-  // and the count); a group the fast path cannot finish reads none
-  const bool slots = lead && cnt <= KMAX;
+  uint64_t s_term[KMAX], s_index[KMAX], s_h[KMAX], s_c[KMAX];
+  // a leader's (follower's) used slots, in the state loads' round trip (both
+  // wait for meta and the count); a group the fast path cannot finish reads none
+  const bool slots = (lead || fol) && cnt <= KMAX;
   uint4 raw[KMAX];
 #pragma unroll
   for (uint32_t k = 0; k < KMAX; ++k) {
@@ -1117,8 +1231,15 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 
   }
 #pragma unroll
   for (uint32_t k = 0; k < KMAX; ++k) slot_unpack(raw[k], a.side, &s_info[k], &s_orig[k], &s_term[k], &s_index[k]);
+#pragma unroll
+  for (uint32_t k = 0; k < KMAX; ++k) {
+    uint4 x = make_uint4(0, 0, 0, 0);
+    if (X && fol && k < cnt) x = at32(a.slotx, k * a.S.G + g);
+    s_h[k] = (uint64_t)x.x | ((uint64_t)x.y << 32);
+    s_c[k] = (uint64_t)x.z | ((uint64_t)x.w << 32);
+  }
   uint32_t vals[ST_N + 1];
-  (void)fast_step<NMAX>(a, L, part, tid, live, lead, leader, prop_raw, cnt, s_info, s_orig, s_term, s_index,
+  (void)fast_step<NMAX>(a, L, part, tid, live, lead, leader, fol, prop_raw, cnt, s_info, s_orig, s_term, s_index, s_h, s_c,
                         a.ev_off[2 * part + 1], &l_pfill, &l_fill, l_flag, l_eflag, vals);
   reduce_stats(a, l_stats, vals);
   if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
@@ -1564,6 +1685,7 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
 #ifndef HB_LEAD_WAVES
 #define HB_LEAD_WAVES 3
 #endif
+
 #ifndef HB_LEAD7_WAVES  // k_apply_lead<7> (measured on cfg4: 2 waves +3 %, 4 waves -0.6 % with 128 B/lane of scratch)
 #define HB_LEAD7_WAVES 3
 #endif
@@ -1609,6 +1731,8 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   const bool spec = leader && (prop_raw != 0 || (fits && cnt <= (uint32_t)NMAX - 1));
   L.dirty = 0;
   L.nev = 0;
+  // (loading the state beside meta, as k_apply_fast does, measured neutral
+  // on cfg3 and +4.5 % on cfg4, whose lanes are mostly not leaders)
   L.last = L.committed = 0;
   L.term = 0;
   if (spec) L.load();
@@ -2348,6 +2472,8 @@ struct PrepSet {
   uint64_t dstage_cap = 0;
   uint4* slot = nullptr;          // [route_kmax][G]
   uint64_t* side = nullptr;       // [2 max_batch] long records' (term, index)
+  uint4* recx = nullptr;          // X mode: [max_batch] beside rec
+  uint4* slotx = nullptr;         // X mode: [route_kmax][G] beside slot
   uint64_t* ev_off = nullptr;     // [2 NB] event chunk offsets (route writes the M chunks)
   uint32_t* ev_counts = nullptr;  // [2 NB]
   hipEvent_t prepped = nullptr;   // prep stream: this set is ready
@@ -2585,7 +2711,8 @@ uint32_t route_grid(const hb_handle* h) {
 }
 template <int KMAX>
 void launch_route(hb_handle* h, const ApplyArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_route<KMAX>, dim3(route_grid<KMAX>(h)), dim3(ROUTE_THREADS), 0, st, a);
+  if (a.slotx) hipLaunchKernelGGL((k_route<KMAX, true>), dim3(route_grid<KMAX>(h)), dim3(ROUTE_THREADS), 0, st, a);
+  else hipLaunchKernelGGL((k_route<KMAX, false>), dim3(route_grid<KMAX>(h)), dim3(ROUTE_THREADS), 0, st, a);
 }
 
 // XCD-aware grid (see block_part()): whole groups of 8 buckets x 2^sis_log partitions.
@@ -2597,7 +2724,8 @@ void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
   const uint32_t grid = apply_grid(h);
   if (ev) (void)hipEventRecord(ev[2], h->stream);
   if constexpr (NMAX >= 5) hipLaunchKernelGGL(k_apply_lead<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
-  else hipLaunchKernelGGL(k_apply_fast<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
+  else if (a.slotx) hipLaunchKernelGGL((k_apply_fast<NMAX, true>), dim3(grid), dim3(PART), 0, h->stream, a);
+  else hipLaunchKernelGGL((k_apply_fast<NMAX, false>), dim3(grid), dim3(PART), 0, h->stream, a);
   if (ev) (void)hipEventRecord(ev[3], h->stream);
   if constexpr (NMAX >= 5) {  // the general kernel spills at n >= 5: elections go first
     if (!sz_on(h->max_msg_size))
@@ -2701,6 +2829,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
     RadixDst& d = h->tmp[k];
     ALLOC(d.group, mb);
     ALLOC(d.rec, mb);
+    ALLOC(d.recx, mb);
   }
   for (PrepSet& ps : h->set) {
     ALLOC(ps.rec, mb);
@@ -2712,6 +2841,8 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
     ALLOC(ps.cnt, G);
     ALLOC(ps.slot, route_kmax(R) * G);
     ALLOC(ps.side, 2 * mb);
+    ALLOC(ps.recx, mb);
+    ALLOC(ps.slotx, route_kmax(R) * G);
     ALLOC(ps.ev_counts, 2ull * h->NB);
     ALLOC(ps.ev_off, 2ull * h->NB);
   }
@@ -3373,14 +3504,17 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
 
   // ---- phase 1: partition (prep stream) ---------------------------------------
   const uint32_t NB = h->NB;
+  // X mode: a follower-side batch (m.Commit given) carries {hint, commit} with every record
+  const bool xmode = bd_commit != nullptr && b->n > 0;
   if (b->n == 0) {
     HB_CHECK(hipMemsetAsync(ps.bk_off, 0, (h->NBK + 1) * 4ull, ps_st));
     HB_CHECK(hipMemsetAsync(ps.bk_fill, 0, h->NBK * 4ull * CTR_STRIDE, ps_st));
     HB_CHECK(hipMemsetAsync(ps.ctr, 0, CTR_WORDS * 4ull, ps_st));
   } else {
     const uint32_t ntiles = (uint32_t)((b->n + RDX_TILE - 1) / RDX_TILE);
-    RadixSrc src{bd.group, bd.info, bd.term, bd.index, nullptr, nullptr, ps.side, (uint32_t)b->n};
-    const FinalDst fin{ps.rec, ps.bucket, h->passes == 1 ? ps.bk_off : nullptr, h->NBK, h->sis_log};
+    RadixSrc src{bd.group, bd.info, bd.term, bd.index, nullptr, nullptr, ps.side, (uint32_t)b->n,
+                 bd.hint, bd_commit, bd_eoff, bd_eterm, b->n_edesc, nullptr};
+    const FinalDst fin{ps.rec, ps.recx, ps.bucket, h->passes == 1 ? ps.bk_off : nullptr, h->NBK, h->sis_log};
     uint32_t shift = PART_LOG + h->sis_log;
     for (uint32_t p = 0; p < h->passes; ++p) {
       const bool last_pass = p + 1 == h->passes;
@@ -3394,13 +3528,20 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
                          shift, dbits, ntiles, h->hist);
       hipLaunchKernelGGL(k_scan_rows, dim3(1u << dbits), dim3(1024), 0, ps_st, h->hist, ntiles, dbits, h->totals, ps.bk_fill,
                          h->NBK, ps.ctr);
-      if (last_pass)
-        hipLaunchKernelGGL(k_radix_scatter<true>, dim3((ntiles + SCAT_TPW - 1) / SCAT_TPW), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
-                           shift, dbits, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
-      else
-        hipLaunchKernelGGL(k_radix_scatter<false>, dim3((ntiles + SCAT_TPW - 1) / SCAT_TPW), dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G,
-                           shift, dbits, ntiles, (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid);
-      src = RadixSrc{dst.group, nullptr, nullptr, nullptr, dst.rec, h->n_valid, nullptr, (uint32_t)b->n};
+      const dim3 sg((ntiles + SCAT_TPW - 1) / SCAT_TPW);
+#define HB_SCATTER(F, X)                                                                                             \
+  hipLaunchKernelGGL((k_radix_scatter<F, X>), sg, dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G, shift, dbits, ntiles, \
+                     (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid)
+      if (last_pass) {
+        if (xmode) HB_SCATTER(true, true);
+        else HB_SCATTER(true, false);
+      } else {
+        if (xmode) HB_SCATTER(false, true);
+        else HB_SCATTER(false, false);
+      }
+#undef HB_SCATTER
+      src = RadixSrc{dst.group, nullptr, nullptr, nullptr, dst.rec, h->n_valid, nullptr, (uint32_t)b->n,
+                     nullptr, nullptr, nullptr, nullptr, 0, dst.recx};
       shift += dbits;
     }
     if (h->passes > 1)
@@ -3451,6 +3592,8 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.cnt = ps.cnt;
   aa.slot = ps.slot;
   aa.side = ps.side;
+  aa.recx = ps.recx;
+  aa.slotx = xmode ? ps.slotx : nullptr;
   switch (h->nmax) {
     case 3: launch_route<route_kmax(3)>(h, aa, ps_st); break;
     case 5: launch_route<route_kmax(5)>(h, aa, ps_st); break;

@@ -42,6 +42,9 @@ struct FastLane {
   uint32_t pm[NMAX];
   uint32_t dirty;
   uint32_t hv;       // bit s: head[s] holds inflights.buffer[start] of slot s (read lazily)
+  // n = 7 keeps no head copies: the leader lane's 7 x 3 Progress words plus its
+  // 8 route slots otherwise spill (132 B/lane); a head is then read when needed
+  static constexpr bool HEADS = NMAX <= 5;
   uint32_t nev;      // public events emitted (an EVC_BCAST word counts once per slot)
 
   __device__ __forceinline__ uint32_t n() const { return (mlo >> 2) & 7; }
@@ -66,11 +69,23 @@ struct FastLane {
 
   // All state loads of the lane are independent, so they are in flight together.
   __device__ __forceinline__ void load() {
+    load_head();
+    load_rest();
+  }
+  // The loads that depend on nothing the lane reads (k_apply_fast issues them
+  // with meta itself, in its first round trip) ...
+  __device__ __forceinline__ void load_head() {
     term = at32(S.term, g);
     committed = at32(S.commit, g);
     first = at32(S.first, g);
     last = at32(S.last, g);
     tfirst = at32(S.tfirst, g);
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) pm[s] = at32(S.pm, s * S.G + g);
+  }
+  // ... and those that wait for meta (which arrays are kept) and pm (the ring
+  // heads): the second round trip.
+  __device__ __forceinline__ void load_rest() {
     // arrays the meta flags mark as not kept are not read (M_TL / M_SM,
     // hipbatch_kernels.h); these loads issue once meta is in, beside the
     // ring heads, which wait for pm anyway
@@ -80,7 +95,6 @@ struct FastLane {
     for (int s = 0; s < NMAX; ++s) {
       match[s] = ((uint32_t)s == sf) ? last : at32(S.match, s * S.G + g);
       next[s] = ((uint32_t)s == sf) ? last + 1 : at32(S.next, s * S.G + g);
-      pm[s] = at32(S.pm, s * S.G + g);
     }
     if (mlo & (uint32_t)M_RS) {  // a group k_elect left in the reset form: every slot written back
       const uint32_t nn = n();
@@ -101,8 +115,8 @@ struct FastLane {
     // them only on demand — an ack at or past Next - 1 frees the whole window
     // unread — measured 1-3 % slower on cfg2 / cfg3 / cfg5.)
 #pragma unroll
-    for (int s = 0; s < NMAX; ++s) head[s] = pm_count(pm[s]) ? *ring_at(s, pm_start(pm[s])) : 0;
-    hv = (1u << NMAX) - 1;
+    for (int s = 0; s < NMAX; ++s) head[s] = (HEADS && pm_count(pm[s])) ? *ring_at(s, pm_start(pm[s])) : 0;
+    hv = HEADS ? (1u << NMAX) - 1 : 0u;
     dirty = 0;
     if (mlo & (uint32_t)M_RS) {
       mlo &= ~(uint32_t)M_RS;

@@ -56,13 +56,13 @@ struct LeadLane : FastLane<NMAX> {
   // One slot's Progress as scalars (a runtime slot: one select per slot and
   // field, so the transitions below exist once in the code, not once per slot).
   __device__ __forceinline__ Pr get(uint32_t s) const {
-    Pr p{match[0], next[0], head[0], pm[0]};
+    Pr p{match[0], next[0], B::HEADS ? head[0] : 0ull, pm[0]};
 #pragma unroll
     for (int k = 1; k < NMAX; ++k) {
       const bool h = (uint32_t)k == s;
       p.match = h ? match[k] : p.match;
       p.next = h ? next[k] : p.next;
-      p.head = h ? head[k] : p.head;
+      if (B::HEADS) p.head = h ? head[k] : p.head;
       p.pm = h ? pm[k] : p.pm;
     }
     return p;
@@ -75,7 +75,7 @@ struct LeadLane : FastLane<NMAX> {
       if (h && p.pm != pm[k]) dirty |= 1u << (B::D_PM0 + k);
       match[k] = h ? p.match : match[k];
       next[k] = h ? p.next : next[k];
-      head[k] = h ? p.head : head[k];
+      if (B::HEADS) head[k] = h ? p.head : head[k];
       pm[k] = h ? p.pm : pm[k];
     }
   }
@@ -100,7 +100,7 @@ struct LeadLane : FastLane<NMAX> {
     }
     if (!((this->hv >> s) & 1u)) {
       p.head = *ring_at(s, idx);
-      this->hv |= 1u << s;
+      if (B::HEADS) this->hv |= 1u << s;
     }
     uint64_t v = p.head;
     if (to < v) return;
@@ -149,7 +149,7 @@ struct LeadLane : FastLane<NMAX> {
         uint32_t idx = start + cnt;
         if (idx >= S.W) idx -= S.W;
         *ring_at(s, idx) = lastsent;  // inflights.add
-        if (cnt == 0) {
+        if (cnt == 0 && B::HEADS) {
           p.head = lastsent;
           this->hv |= 1u << s;
         }

@@ -365,6 +365,46 @@ def follower_messages(now, term_of, nmsg, seed=5, nonmember=0.05, max_ents=4, de
                 eoff=np.array(eoff, np.uint64), eterm=np.array(eterm or [0], np.uint64)[:len(eterm)], props=None)
 
 
+# ---------------------------------------------------------------------------- follow (the mirror of cfg2)
+def follow_groups(G, n=3, seed=0x5EED0006, last_hi=1 << 20, term_hi=1000, with_runs="flat"):
+    """The follower side's steady state: this node (slot 0) follows every group,
+    whose leader is slot 1 at the group's Term (lead = vote = 1); the log's last
+    entry has the current Term and everything but it is committed.  Progress is
+    what the last reset left (Probe; self Match = lastIndex)."""
+    g, runs = steady_groups(G, n, seed=seed, last_hi=last_hi, term_hi=term_hi, with_runs=with_runs)
+    g["state"] = A.HB_STATE_FOLLOWER
+    g["lead"] = 1
+    g["vote"] = 1
+    g["committed"] = g["last_index"] - np.uint64(1)
+    for s in range(n):
+        g["pr"][:, s]["state"] = A.HB_PR_PROBE
+        g["pr"][:, s]["match"] = g["last_index"] if s == 0 else 0
+        g["pr"][:, s]["next"] = g["last_index"] + np.uint64(1)
+    return g, runs
+
+
+def follow_batch(groups, step, seed=0x5EED0006, ents=1):
+    """One follow step (the mirror of cfg2): every group receives its leader's
+    MsgApp (Index = LogTerm's index = the follower's last, `ents` entries at
+    the Term, Commit = the leader's commit: the follower's last) and a
+    MsgHeartbeat (Commit = the same), in one random permutation of the arrival
+    stream.  Step k continues where step k-1 left every follower (last + k)."""
+    G = len(groups)
+    rng = np.random.default_rng(seed + 104729 * step)
+    grp = np.concatenate([np.arange(G, dtype=np.uint32)] * 2)
+    typ = np.concatenate([np.full(G, A.HB_MSG_APP, np.uint32), np.full(G, A.HB_MSG_HEARTBEAT, np.uint32)])
+    perm = rng.permutation(2 * G)
+    grp, typ = grp[perm], typ[perm]
+    app = typ == A.HB_MSG_APP
+    term = groups["term"][grp].astype(np.uint64)
+    base = groups["last_index"][grp].astype(np.uint64) + np.uint64(step * ents)
+    k = np.where(app, ents, 0).astype(np.uint64)
+    eoff = np.concatenate([[0], np.cumsum(k)[:-1]]).astype(np.uint64)
+    return dict(group=grp, info=(typ | (np.uint32(1) << np.uint32(4))).astype(np.uint32), term=term,
+                index=np.where(app, base, 0).astype(np.uint64), hint=np.where(app, term, 0).astype(np.uint64),
+                commit=base, eoff=eoff, eterm=np.repeat(term[app], ents).astype(np.uint64), props=None)
+
+
 def many_runs_groups(G, n=3, seed=9, runs_lo=18, runs_hi=30, run_len=40):
     """Followers whose logs hold runs_lo..runs_hi term runs of 1..run_len
     entries (the follower side's raftLog.term at any depth); every group's

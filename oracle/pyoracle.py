@@ -610,8 +610,9 @@ class ShardedOracleGroups:
     result equals one OracleGroups over the whole batch: events are mapped
     back to global group ids and global arrival positions, statistics summed.
     Used for the full-size BASELINE configurations, where one core would take
-    minutes.  Supports the leader-side batch fields (group / info / term /
-    index / hint / props)."""
+    minutes.  Supports the batch fields group / info / term / index / hint /
+    props / commit / eoff + eterm (a message's entries re-based per shard), not
+    the entry descriptors of a finite MaxSizePerMsg."""
 
     def __init__(self, groups, runs, max_inflight, max_msg_size=NO_LIMIT, shards=16):
         G = len(groups)
@@ -640,8 +641,13 @@ class ShardedOracleGroups:
         return out
 
     def step(self, b):
-        for k in ("edesc", "eoff", "peoff", "commit", "eterm"):
+        for k in ("edesc", "peoff"):
             assert b.get(k) is None, f"ShardedOracleGroups: batch field {k} not supported"
+        ne = None
+        if b.get("eoff") is not None:  # entries per message (eoff / eterm in arrival order)
+            eoff = np.asarray(b["eoff"], dtype=np.int64)
+            eterm = np.asarray(b["eterm"], dtype=np.uint64)
+            ne = np.diff(np.append(eoff, len(eterm)))
         grp = np.asarray(b["group"], dtype=np.uint32)
         per = self.bounds[0][1] - self.bounds[0][0]
         sid = np.minimum(grp // np.uint32(per), np.uint32(len(self.parts)))  # out-of-range ids: dropped below
@@ -659,9 +665,17 @@ class ShardedOracleGroups:
                 sub["hint"] = np.asarray(b["hint"])[idx]
             if b.get("props") is not None:
                 sub["props"] = np.asarray(b["props"])[lo:hi]
+            if b.get("commit") is not None:
+                sub["commit"] = np.asarray(b["commit"])[idx]
+            if ne is not None:
+                k = ne[idx]
+                sub["eoff"] = np.concatenate([[0], np.cumsum(k)[:-1]]).astype(np.uint64)
+                pos = np.repeat(eoff[idx] - sub["eoff"].astype(np.int64), k) + np.arange(int(k.sum()))
+                sub["eterm"] = eterm[pos]
             ev, st = og.step(sub)
             ev["group"] += np.uint32(lo)
-            arr = np.isin(ev["type"], [abi.HB_EV_PROP_FWD, abi.HB_EV_PROP_DROP, abi.HB_EV_FAULT]) & \
+            # events that name an arrival position: back to the global batch
+            arr = np.isin(ev["type"], [abi.HB_EV_PROP_FWD, abi.HB_EV_PROP_DROP, abi.HB_EV_FAULT, abi.HB_EV_FOLLOW]) & \
                 (ev["x"] != np.uint64(abi.HB_NO_INDEX))
             ev["x"][arr] = idx[ev["x"][arr].astype(np.int64)].astype(np.uint64)
             return ev, st

@@ -84,3 +84,18 @@ def test_cfg3_headline_geometry_full_size():
         _, st, now = pair.step(synth.cfg3_open_batch(now, rng), ctx=f"cfg3 headline {k}", check_inflights=False)
         assert st[abi.HB_STAT_FAULTS] == 0 and st[abi.HB_STAT_APPRESP] > 3 * G_HEAD
     assert _sample_windows(pair, now, np.random.default_rng(8), n) >= 200
+
+
+@pytest.mark.timeout(900)
+def test_follow_workload_full_size():
+    """bench.py --workload follow at its size: 1,048,576 groups x 3 that this
+    node follows, each receiving its leader's MsgApp (one entry) and a
+    MsgHeartbeat per step, through k_apply_fast's follower lane; two steps
+    against the oracle (16 shards): every event, statistic and group record."""
+    g, runs = synth.follow_groups(G_HEAD, 3, seed=0x5EED0006, with_runs="flat")
+    pair = Pair(g, runs, 3, 256, max_batch=2 * G_HEAD, oracle_shards=16)
+    for step in range(2):
+        _, st, now = pair.step(synth.follow_batch(g, step), ctx=f"follow step {step}", check_inflights=False)
+        assert st[abi.HB_STAT_COMMITS] == G_HEAD and st[abi.HB_STAT_ENTRIES] == G_HEAD
+        assert st[abi.HB_STAT_MSGS] == 2 * G_HEAD and st[abi.HB_STAT_FAULTS] == 0
+        assert np.array_equal(now["last_index"], g["last_index"] + np.uint64(step + 1))

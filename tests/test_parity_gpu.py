@@ -367,6 +367,62 @@ def test_follower_replication_stream():
         assert st[abi.HB_STAT_COMMITS] == G and st[abi.HB_STAT_FAULTS] == 0
 
 
+@pytest.mark.parametrize("ents", [1, 3])
+def test_follow_workload_fast_lane(ents):
+    """The follow workload (bench.py --workload follow, the mirror of cfg2):
+    every group's leader sends a MsgApp appending `ents` entries and a
+    MsgHeartbeat; k_apply_fast's follower lane steps both (X-mode route
+    extension: m.LogTerm / m.Commit beside each slot).  Then the same groups
+    under random follower-side traffic (rejects, stale indices, higher terms,
+    votes, snapshots) mixed with the workload, which the lane hands over at the
+    first message it does not take."""
+    G = 5000
+    g, runs = synth.follow_groups(G, 3, seed=101, last_hi=1 << 14, with_runs=True)
+    pair = Pair(g, runs, 3, 256, max_batch=4 * G, term_runs=True)
+    for step in range(3):
+        _, st, now = pair.step(synth.follow_batch(g, step, seed=102, ents=ents), ctx=f"follow {ents} step {step}",
+                               check_inflights=False)
+        assert st[abi.HB_STAT_COMMITS] == G and st[abi.HB_STAT_ENTRIES] == ents * G
+        assert st[abi.HB_STAT_MSGS] == 2 * G and st[abi.HB_STAT_FAULTS] == 0
+        assert np.array_equal(now["last_index"], g["last_index"] + np.uint64((step + 1) * ents))
+    for k in range(3):
+        f = synth.follower_messages(now, pair.og.term, 3000, seed=103 + k)
+        b = synth.follow_batch(now, 0, seed=104 + k, ents=ents)
+        keep = np.random.default_rng(k).random(len(b["group"])) < 0.5
+        for key in ("group", "info", "term", "index", "hint", "commit"):
+            b[key] = b[key][keep]
+        ne = np.where((b["info"] & 0xF) == abi.HB_MSG_APP, ents, 0)
+        b["eoff"] = np.concatenate([[0], np.cumsum(ne)[:-1]]).astype(np.uint64)
+        b["eterm"] = np.repeat(b["term"], ne).astype(np.uint64)
+        _, st, now = pair.step(_merge_follow(b, f, 105 + k), ctx=f"follow mixed {k}", check_inflights=False)
+
+
+def _merge_follow(a, b, seed):
+    """Interleave two follower-side batches (each with entries), arrival order
+    within each kept, entry offsets re-based."""
+    rng = np.random.default_rng(seed)
+    na, nb = len(a["group"]), len(b["group"])
+    pick = np.zeros(na + nb, bool)
+    pick[rng.choice(na + nb, nb, replace=False)] = True
+    out = {}
+    for k in ("group", "info", "term", "index", "hint", "commit"):
+        v = np.empty(na + nb, a[k].dtype)
+        v[~pick], v[pick] = a[k], b[k]
+        out[k] = v
+    ca = np.diff(np.append(a["eoff"], len(a["eterm"]))).astype(np.int64)
+    cb = np.diff(np.append(b["eoff"], len(b["eterm"]))).astype(np.int64)
+    cnt = np.zeros(na + nb, np.int64)
+    cnt[~pick], cnt[pick] = ca, cb
+    out["eoff"] = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint64)
+    src_off = np.zeros(na + nb, np.int64)
+    src_off[~pick], src_off[pick] = a["eoff"].astype(np.int64), b["eoff"].astype(np.int64) + len(a["eterm"])
+    allterm = np.concatenate([a["eterm"], b["eterm"]]).astype(np.uint64)
+    pos = np.repeat(src_off - out["eoff"].astype(np.int64), cnt) + np.arange(int(cnt.sum()))
+    out["eterm"] = allterm[pos]
+    out["props"] = None
+    return out
+
+
 # ---------------------------------------------------------------- the log index at depth
 def test_deep_lag_finite_max_msg_size():
     """etcdserver's MaxSizePerMsg = 1 MiB (etcdserver/raft.go:229) with

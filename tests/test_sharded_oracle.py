@@ -53,3 +53,29 @@ def test_sharded_maps_proposal_arrivals_back():
     assert_events_equal(eb, ea, "fuzz")
     assert np.array_equal(sa, sb)
     assert np.any(np.isin(ea["type"], [abi.HB_EV_PROP_FWD, abi.HB_EV_PROP_DROP]))
+
+
+def test_sharded_oracle_follower_batches_equal_one_oracle():
+    """The sharded oracle re-bases each message's entries per shard and maps
+    the follower side's arrival-indexed events (HB_EV_FOLLOW) back: on the
+    follow workload and on random follower-side traffic it equals one oracle
+    over the whole batch."""
+    from etcd_amd import synth
+    from oracle.pyoracle import OracleGroups, ShardedOracleGroups
+    G = 3000
+    g, runs = synth.follow_groups(G, 3, seed=5, last_hi=1 << 12)
+    one = OracleGroups(g, runs, 256)
+    many = ShardedOracleGroups(g, runs, 256, shards=7)
+    for step in range(2):
+        b = synth.follow_batch(g, step, seed=6, ents=2)
+        e1, s1 = one.step(b)
+        e2, s2 = many.step(b)
+        o1, o2 = np.argsort(e1["group"], kind="stable"), np.argsort(e2["group"], kind="stable")
+        assert np.array_equal(e1[o1], e2[o2]) and np.array_equal(s1, s2)
+        assert s1[abi.HB_STAT_COMMITS] == G and s1[abi.HB_STAT_ENTRIES] == 2 * G
+    f = synth.follower_messages(one.groups(), one.term, 4000, seed=8)
+    e1, s1 = one.step(f)
+    e2, s2 = many.step(f)
+    o1, o2 = np.argsort(e1["group"], kind="stable"), np.argsort(e2["group"], kind="stable")
+    assert np.array_equal(e1[o1], e2[o2]) and np.array_equal(s1, s2)
+    assert np.array_equal(one.groups(), many.groups())
