@@ -898,16 +898,22 @@ constexpr uint32_t ROUTE_UNROLL = HB_ROUTE_UNROLL;  // records in flight per lan
 #ifndef HB_RG2_LOG  // route groups per workgroup for KMAX = 2 (log2): 1024 (4 sisters per 4096-group
 #define HB_RG2_LOG 10  // bucket, 53 KB LDS) measured faster than 2048 (2 sisters, 106 KB)
 #endif
-constexpr uint32_t route_rg_log(uint32_t kmax) { return kmax <= 2 ? HB_RG2_LOG : (kmax <= 4 ? 10 : 9); }
-template <int KMAX> struct RouteGeom {
-  static constexpr uint32_t RG_LOG = route_rg_log(KMAX);
+#ifndef HB_RG8_LOG  // route groups per workgroup for KMAX = 6 / 8 (log2)
+#define HB_RG8_LOG 9
+#endif
+// (X mode stages twice the bytes per slot: at most 512 groups per workgroup for KMAX > 4)
+constexpr uint32_t route_rg_log(uint32_t kmax, bool x = false) {
+  return kmax <= 2 ? HB_RG2_LOG : (kmax <= 4 ? 10 : (x && HB_RG8_LOG > 9 ? 9 : HB_RG8_LOG));
+}
+template <int KMAX, bool X> struct RouteGeom {
+  static constexpr uint32_t RG_LOG = route_rg_log(KMAX, X);
   static constexpr uint32_t RG = 1u << RG_LOG;     // groups per workgroup
   // workgroups per bucket: 2^(PART_LOG + sis_log - RG_LOG) (sis_log >= RG_LOG - PART_LOG)
 };
 
 template <int KMAX, bool X>
 __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
-  using RGm = RouteGeom<KMAX>;
+  using RGm = RouteGeom<KMAX, X>;
   constexpr uint32_t RG = RGm::RG, NP = RG / PART;
   const uint32_t sl = a.sis_log, W = 1u << (PART_LOG + sl - RGm::RG_LOG);
   __shared__ uint32_t l_cnt[RG];
@@ -2706,13 +2712,13 @@ int reserve_log(hb_handle* h, uint32_t count, const uint32_t* groups, const uint
 }
 
 template <int KMAX>
-uint32_t route_grid(const hb_handle* h) {
-  return ((h->NBK + 7) & ~7u) << (PART_LOG + h->sis_log - RouteGeom<KMAX>::RG_LOG);
+uint32_t route_grid(const hb_handle* h, bool x) {
+  return ((h->NBK + 7) & ~7u) << (PART_LOG + h->sis_log - (x ? RouteGeom<KMAX, true>::RG_LOG : RouteGeom<KMAX, false>::RG_LOG));
 }
 template <int KMAX>
 void launch_route(hb_handle* h, const ApplyArgs& a, hipStream_t st) {
-  if (a.slotx) hipLaunchKernelGGL((k_route<KMAX, true>), dim3(route_grid<KMAX>(h)), dim3(ROUTE_THREADS), 0, st, a);
-  else hipLaunchKernelGGL((k_route<KMAX, false>), dim3(route_grid<KMAX>(h)), dim3(ROUTE_THREADS), 0, st, a);
+  if (a.slotx) hipLaunchKernelGGL((k_route<KMAX, true>), dim3(route_grid<KMAX>(h, true)), dim3(ROUTE_THREADS), 0, st, a);
+  else hipLaunchKernelGGL((k_route<KMAX, false>), dim3(route_grid<KMAX>(h, false)), dim3(ROUTE_THREADS), 0, st, a);
 }
 
 // XCD-aware grid (see block_part()): whole groups of 8 buckets x 2^sis_log partitions.
