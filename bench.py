@@ -259,12 +259,13 @@ def pmc_traffic(path, kernel, G, n, apply_us):
     the live measurement within 15 % (same build); otherwise None."""
     import glob
     cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")), reverse=True)
+    names = [kernel] if isinstance(kernel, str) else list(kernel)
     for path in cands:  # the newest profile of this configuration
         try:
             d = json.load(open(path))
-            k = d["kernels"][kernel]
+            k = next(d["kernels"][x] for x in names if x in d["kernels"])
             cfg = d["bench"]["config"]
-        except (OSError, KeyError, ValueError):
+        except (OSError, KeyError, ValueError, StopIteration):
             continue
         if cfg.get("groups_per_gpu") == G and cfg.get("replicas") == n and "traffic_bytes" in k:
             break
@@ -314,7 +315,7 @@ def run_multinode(args):
     L.hbnb_run2.restype = C.c_int
     L.hbnb_run2.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                             C.POINTER(C.c_double)]
-    out = (C.c_double * 24)()
+    out = (C.c_double * 32)()
     bulk = args.mn_mode == "bulk"
     flags = 3 if bulk else 0  # HBNB_BULK | HBNB_PAR_APP
     threads = args.mn_threads if bulk else 1
@@ -337,7 +338,8 @@ def run_multinode(args):
                    f"{threads or 'default (min(16, cores))'}, application persists from the same number of threads"
                    if bulk else "one hbn_step / hbn_propose call per message, one host thread"),
            "split_s_per_step": {"ready": out[3] / args.steps, "step_and_propose": out[4] / args.steps,
-                                "append_and_advance": out[5] / args.steps},
+                                "append_and_advance": out[5] / args.steps,
+                                "of_which_app_persist": out[24] / args.steps},
            "parity_sanity": bool(adv == G * args.steps and out[7] == 0),
            "host_phases_s_per_step": {k: round(out[8 + i] / args.steps, 6) for i, k in enumerate(
                ["load_sync", "log_reserve", "hb_step_call", "event_fetch", "event_replay", "stepped_marks",
@@ -604,7 +606,8 @@ def run_replication(args, world, rank, local):
         # HB_PHASE_APPLY brackets exactly the k_apply_fast launch (HIP events on the launch stream)
         achieved = float(alg / (apply_ms * 1e-3) / 1e9)
         kname = f"k_apply_fast<{3 if n <= 3 else (5 if n <= 5 else 7)}>"
-        traffic, tsrc = pmc_traffic(args.traffic_json, kname, G, n, apply_ms * 1e3)
+        # (rocprofv3 names the template with its X-mode flag since r04)
+        traffic, tsrc = pmc_traffic(args.traffic_json, [kname[:-1] + ", false>", kname], G, n, apply_ms * 1e3)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,

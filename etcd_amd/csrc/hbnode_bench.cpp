@@ -27,7 +27,8 @@ extern "C" {
 // out[0] timed seconds, [1] MsgAppResp stepped, [2] commit advances (groups x rounds),
 // [3] seconds in hbn_ready, [4] seconds in hbn_step/hbn_propose, [5] seconds in
 // storage append + hbn_advance, [6] entries committed seen in Ready, [7] faults,
-// [8 .. 8 + 16) the node's host phase seconds over the timed rounds (hbn_profile).
+// [8 .. 8 + 16) the node's host phase seconds over the timed rounds (hbn_profile),
+// [24] seconds the application spent persisting (hbn_storage_append); out has 32 slots.
 // flags: HBNB_BULK = the round's acks and proposals through hbn_step_many /
 // hbn_propose_many (one call each) instead of one call per message;
 // HBNB_PAR_APP = the application persists a Ready's entries to the groups'
@@ -71,7 +72,8 @@ int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t roun
       rc = hbn_step(mn, ids[g], &m);
     }
   uint64_t faults = 0, committed_entries = 0, advances = 0;
-  double t_ready = 0, t_step = 0, t_adv = 0;
+  double t_ready = 0, t_step = 0, t_adv = 0, t_persist = 0;
+  std::vector<uint64_t> adv;  // the groups to advance (kept across cycles)
   // one Ready cycle: take the Ready, persist its entries, advance
   auto cycle = [&]() -> int {
     const hbn_group_ready* rds = nullptr;
@@ -82,27 +84,33 @@ int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t roun
     t_ready += secs(a, b);
     if (r == HBN_EAGAIN) return 0;
     if (r) return r;
-    std::vector<uint64_t> adv(cnt);
+    if (adv.size() < cnt) adv.resize(cnt);
     // the application's part: persist each group's entries (MemoryStorage.Append)
+    // (counts kept in locals: the threads' result slots share a cache line)
     auto persist = [&](uint64_t lo, uint64_t hi, uint64_t* f, uint64_t* ce, uint64_t* av) -> int {
-      for (uint64_t i = lo; i < hi; ++i) {
+      uint64_t nf = 0, nce = 0, nav = 0;
+      int rc2 = 0;
+      for (uint64_t i = lo; i < hi && !rc2; ++i) {
         const hbn_group_ready& rd = rds[i];
         const uint64_t g = rd.group - 1;
-        *f += rd.fault != 0;
+        nf += rd.fault != 0;
         if (rd.n_entries) {
-          const int e = hbn_storage_append(st[g], rd.entries, rd.n_entries);
-          if (e) return e;
+          rc2 = hbn_storage_append(st[g], rd.entries, rd.n_entries);
           last[g] = rd.entries[rd.n_entries - 1].index;
         }
-        *ce += rd.n_committed;
+        nce += rd.n_committed;
         if (rd.hard_state.commit > commit[g]) {
           commit[g] = rd.hard_state.commit;
-          ++*av;
+          ++nav;
         }
         adv[i] = rd.group;
       }
-      return 0;
+      *f += nf;
+      *ce += nce;
+      *av += nav;
+      return rc2;
     };
+    auto p0 = clk::now();
     if (app_threads > 1 && cnt >= 4096) {
       std::vector<uint64_t> f(app_threads), ce(app_threads), av(app_threads);
       std::vector<int> er(app_threads);
@@ -120,6 +128,7 @@ int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t roun
       r = persist(0, cnt, &faults, &committed_entries, &advances);
       if (r) return r;
     }
+    t_persist += secs(p0, clk::now());
     r = hbn_advance(mn, adv.data(), cnt);
     t_adv += secs(b, clk::now());
     return r;
@@ -145,7 +154,7 @@ int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t roun
       acks = 0;
       advances = 0;
       committed_entries = 0;
-      t_ready = t_step = t_adv = 0;
+      t_ready = t_step = t_adv = t_persist = 0;
       hbn_profile(mn, prof0, 16, nullptr);
     }
     auto a = clk::now();
@@ -189,6 +198,7 @@ int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t roun
   out[5] = t_adv;
   out[6] = (double)committed_entries;
   out[7] = (double)faults;
+  out[24] = t_persist;
   hbn_stop(mn);
   for (auto* s : st) hbn_storage_free(s);
   return rc;

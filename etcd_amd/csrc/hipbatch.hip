@@ -878,8 +878,8 @@ __device__ __forceinline__ void reduce_stats<uint32_t>(const ApplyArgs& a, uint6
 
 // ---------------------------------------------------------------------------
 // k_route<KMAX>: W = BK / RG workgroups per bucket, each owning RG groups
-// (RG x KMAX message slots fit in LDS: RG = 2048 / 1024 / 512 for KMAX =
-// 2 / <= 4 / <= 8).  Each workgroup streams its bucket's records (coalesced; the W
+// (RG x KMAX message slots fit in LDS: RG = 2048 / 1024 for KMAX = 2 / > 2,
+// half that in X mode).  Each workgroup streams its bucket's records (coalesced; the W
 // sisters of a bucket share one XCD's L2), ranks the messages of its groups
 // with one LDS counter per group, stages each group's first KMAX messages in
 // LDS and writes them out lane-major (slot k of group g at slots.*[k][g]) with
@@ -895,15 +895,13 @@ constexpr uint32_t ROUTE_THREADS = 1024;
 #define HB_ROUTE_UNROLL 4
 #endif
 constexpr uint32_t ROUTE_UNROLL = HB_ROUTE_UNROLL;  // records in flight per lane
-#ifndef HB_RG2_LOG  // route groups per workgroup for KMAX = 2 (log2): 1024 (4 sisters per 4096-group
-#define HB_RG2_LOG 10  // bucket, 53 KB LDS) measured faster than 2048 (2 sisters, 106 KB)
-#endif
-#ifndef HB_RG8_LOG  // route groups per workgroup for KMAX = 6 / 8 (log2)
-#define HB_RG8_LOG 9
-#endif
-// (X mode stages twice the bytes per slot: at most 512 groups per workgroup for KMAX > 4)
+// Route groups per workgroup (log2), measured on MI355X with 16-byte records
+// (same-box A/B, r04): KMAX = 2 at 2048 (2 sisters per 4096-group bucket, 72 KB
+// LDS) vs 1024: cfg2 119.2 vs 120.5 us, cfg5 0.995 vs 1.004 ms; KMAX = 6 / 8 at
+// 1024 vs 512 (buckets of at least 1024 groups): cfg4 1.949 vs 2.020 ms, cfg3
+// neutral.  X mode stages twice the bytes per slot, so it keeps half as many.
 constexpr uint32_t route_rg_log(uint32_t kmax, bool x = false) {
-  return kmax <= 2 ? HB_RG2_LOG : (kmax <= 4 ? 10 : (x && HB_RG8_LOG > 9 ? 9 : HB_RG8_LOG));
+  return (kmax <= 2 ? 11u : 10u) - (x ? 1u : 0u);
 }
 template <int KMAX, bool X> struct RouteGeom {
   static constexpr uint32_t RG_LOG = route_rg_log(KMAX, X);

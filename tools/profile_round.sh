@@ -26,6 +26,8 @@ timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_
 echo "write done"
 python3 tools/prof_summary.py "$OUT" --tag "$TAG" --out "$OUT/summary" > "$OUT/summary.log"
 echo "summary done"
-timeout -k 10 300 python3 bench.py $WA --no-cpu-baseline --traffic-json "$OUT/summary/${TAG}_traffic.json" > "$OUT/bench.json" 2> "$OUT/bench.err"
+# the summary goes where it is committed (profiles/), so the line's traffic_source names that file
+cp "$OUT/summary/${TAG}_traffic.json" "$ROOT/profiles/"
+timeout -k 10 300 python3 bench.py $WA ${CPUB:---no-cpu-baseline} --traffic-json "profiles/${TAG}_traffic.json" > "$OUT/bench.json" 2> "$OUT/bench.err"
 echo "bench done"
 tail -1 "$OUT/bench.json"
