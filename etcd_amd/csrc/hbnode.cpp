@@ -330,7 +330,9 @@ struct hbn_storage {
     if (lo > hi) panicf("runtime error: slice bounds out of range");
     const size_t a = lo - offset(), b = hi - offset();
     size_t k = 0;
-    if (b > a) {
+    if (max_size == HB_NO_LIMIT) {  // limitSize keeps everything
+      k = b - a;
+    } else if (b > a) {
       uint64_t size = ent_size(ents[a]);
       for (k = 1; a + k < b; ++k) {
         size += ent_size(ents[a + k]);
@@ -478,7 +480,8 @@ struct Log {
         panicf("entries[" + std::to_string(lo) + ":" + std::to_string(h) + ") from storage is out of bound");
       if (rc == HBN_EUNAVAILABLE)
         panicf("entries[" + std::to_string(lo) + ":" + std::to_string(h) + ") is unavailable from storage");
-      for (size_t i = 0; i < k; ++i) f(st->ents[a + i]);
+      auto it = st->ents.cbegin() + a;
+      for (size_t i = 0; i < k; ++i, ++it) f(*it);
     }
     if (hi > offset) {
       const uint64_t a = std::max(lo, offset);
@@ -715,6 +718,10 @@ class Pool {
   template <class F>
   void run(F&& f, unsigned use = 0) {
     const unsigned k = use && use < n_ ? use : n_;
+    if (k == 1) {  // the calling thread alone
+      f(0u);
+      return;
+    }
     std::vector<std::exception_ptr> err(k);
     auto body = [&](unsigned t) {
       try {
@@ -728,7 +735,7 @@ class Pool {
       left_.store(k - 1);
       for (unsigned t = 1; t < k; ++t) post(t, ++w_[t].seq);
       body(0);
-      if (!spin([&] { return left_.load(std::memory_order_acquire) == 0; })) {
+      if (left_.load() != 0) {
         std::unique_lock<std::mutex> lk(mu_);
         waiting_.store(true);
         done_.wait(lk, [&] { return left_.load() == 0; });
@@ -744,11 +751,12 @@ class Pool {
 
  private:
   static constexpr uint64_t STOP = ~0ull;
-  // Only the workers a phase uses are woken, and they (and the caller
-  // waiting for them) poll for ~20 us before blocking: a Ready cycle's phases
-  // come in quick succession, and a futex wake-up per phase costs more than a
-  // small phase's work.  Workers left idle stay blocked, so polling never
-  // takes more cores than the last phase used.
+  // Only the workers a phase uses are woken (one futex each); nobody polls.
+  // Polling for ~20-50 us between phases (r03, and again r04 with per-worker
+  // wake-ups) made the 1k-group MultiNode 3-5x slower on the GPU box — every
+  // phase, single-threaded ones included, slowed down next to the polling
+  // threads under the box's 16-CPU quota — so small phases run on the calling
+  // thread alone (ways()) and workers block between phases.
   struct alignas(64) Worker {
     std::atomic<uint64_t> post{0};  // the job sequence number posted to this worker (STOP: exit)
     std::atomic<bool> sleeping{false};
@@ -756,15 +764,6 @@ class Pool {
     std::condition_variable cv;
     uint64_t seq = 0;  // (caller side) the last number posted
   };
-  template <class P>
-  static bool spin(P&& ready) {
-    auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t i = 1;; ++i) {
-      if (ready()) return true;
-      __builtin_ia32_pause();
-      if ((i & 63) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(20)) return ready();
-    }
-  }
   void post(unsigned t, uint64_t v) {
     Worker& w = w_[t];
     w.post.store(v);  // (seq_cst, against the worker's sleeping flag)
@@ -777,7 +776,7 @@ class Pool {
     Worker& w = w_[t];
     uint64_t seen = 0;
     for (;;) {
-      if (!spin([&] { return w.post.load(std::memory_order_acquire) != seen; })) {
+      if (w.post.load() == seen) {
         std::unique_lock<std::mutex> lk(w.mu);
         w.sleeping.store(true);
         w.cv.wait(lk, [&] { return w.post.load() != seen; });
@@ -828,7 +827,6 @@ struct alignas(64) Lists {
 struct alignas(64) Arena {
   std::vector<hbn_group_ready> out;
   std::vector<hbn_entry> ents;
-  std::vector<uint64_t> ent_off;  // byte offset of each ents[i].data in bytes
   std::vector<hbn_message> msgs;
   std::vector<uint8_t> bytes;
   std::vector<uint64_t> off;  // per out: entries, committed, messages offsets
@@ -836,7 +834,6 @@ struct alignas(64) Arena {
   void clear() {
     out.clear();
     ents.clear();
-    ent_off.clear();
     msgs.clear();
     bytes.clear();
     off.clear();
@@ -1098,11 +1095,12 @@ void materialize(Group& g) {
   }
 }
 
-Msg base_msg(const hbn_node* n, const Group& g, uint32_t type, uint64_t to) {
-  Msg m;
+// a new message at the end of g's r.msgs (raft.send, raft/raft.go:227-236)
+Msg& base_msg(const hbn_node* n, Group& g, uint32_t type, uint64_t to) {
+  Msg& m = g.msgs.emplace_back();
   m.type = type;
   m.to = to;
-  m.from = n->id;   // raft.send (raft/raft.go:227-236)
+  m.from = n->id;
   m.term = g.term;
   return m;
 }
@@ -1150,13 +1148,13 @@ void follower_resp(hbn_node* n, Group& g, const hb_event& e) {
   const uint64_t to = e.to < g.peers.size() ? g.peers[e.to] : g.cur_from;  // HB_REF_OTHER: the sender
   const uint32_t type = kind == HB_RESP_APP ? HB_MSG_APP_RESP
                                             : (kind == HB_RESP_HEARTBEAT ? HB_MSG_HEARTBEAT_RESP : HB_MSG_VOTE_RESP);
-  Msg m = base_msg(n, g, type, to);
+  const uint64_t li = g.log.last_index();
+  Msg& m = base_msg(n, g, type, to);
   m.reject = (e.aux & HB_RESP_REJECT) ? 1 : 0;
   if (kind == HB_RESP_APP) {
     m.index = e.x;
-    if (m.reject) m.reject_hint = g.log.last_index();  // handleAppendEntries :661-663
+    if (m.reject) m.reject_hint = li;  // handleAppendEntries :661-663
   }
-  g.msgs.push_back(std::move(m));
 }
 
 void on_event(hbn_node* n, Group& g, const hb_event& e, Lists& L) {
@@ -1218,38 +1216,41 @@ void on_event(hbn_node* n, Group& g, const hb_event& e, Lists& L) {
       break;
     }
     case HB_EV_APP: {  // sendAppend (raft/raft.go:261-281)
-      Msg m = base_msg(n, g, HB_MSG_APP, g.peers.at(e.to));
-      m.index = e.x;
-      m.log_term = (e.aux & 1u) ? g.term : g.log.term(e.x);  // aux 1: the device saw term(Index) == Term
+      const uint64_t to = g.peers.at(e.to);
+      const uint64_t lt = (e.aux & 1u) ? g.term : g.log.term(e.x);  // aux 1: the device saw term(Index) == Term
       // entries(Index+1, maxMsgSize): (Index, last] under noLimit, one entry under 0
       const uint64_t li = g.log.last_index();
+      uint64_t hi;
+      if (e.x + 1 > li) hi = e.x + 1;
+      else if (n->max_msg == 0) hi = e.x + 2;
+      else if (n->max_msg == HB_NO_LIMIT) hi = li + 1;
+      else hi = e.x + 1 + g.log.limit_count_from(e.x + 1, n->max_msg);  // limitSize, as the device cut it
+      Msg& m = base_msg(n, g, HB_MSG_APP, to);
+      m.index = e.x;
+      m.log_term = lt;
       m.owned = false;
       m.ent_lo = e.x + 1;
-      if (e.x + 1 > li) m.ent_hi = e.x + 1;
-      else if (n->max_msg == 0) m.ent_hi = e.x + 2;
-      else if (n->max_msg == HB_NO_LIMIT) m.ent_hi = li + 1;
-      else m.ent_hi = e.x + 1 + g.log.limit_count_from(e.x + 1, n->max_msg);  // limitSize, as the device cut it
+      m.ent_hi = hi;
       m.commit = g.log.committed;
-      g.msgs.push_back(std::move(m));
       break;
     }
     case HB_EV_SNAP: {  // sendAppend, snapshot branch (:246-260)
-      Msg m = base_msg(n, g, HB_MSG_SNAP, g.peers.at(e.to));
-      m.snap = std::make_shared<const Snap>(g.log.snapshot());
-      g.msgs.push_back(std::move(m));
+      const uint64_t to = g.peers.at(e.to);
+      auto snap = std::make_shared<const Snap>(g.log.snapshot());
+      base_msg(n, g, HB_MSG_SNAP, to).snap = std::move(snap);
       break;
     }
     case HB_EV_HEARTBEAT: {  // sendHeartbeat (:285-299)
-      Msg m = base_msg(n, g, HB_MSG_HEARTBEAT, g.peers.at(e.to));
-      m.commit = e.x;
-      g.msgs.push_back(std::move(m));
+      const uint64_t to = g.peers.at(e.to);
+      base_msg(n, g, HB_MSG_HEARTBEAT, to).commit = e.x;
       break;
     }
     case HB_EV_VOTE: {  // campaign (:429-443)
-      Msg m = base_msg(n, g, HB_MSG_VOTE, g.peers.at(e.to));
+      const uint64_t to = g.peers.at(e.to);
+      const uint64_t lt = g.log.term(g.log.last_index());
+      Msg& m = base_msg(n, g, HB_MSG_VOTE, to);
       m.index = e.x;
-      m.log_term = g.log.term(g.log.last_index());
-      g.msgs.push_back(std::move(m));
+      m.log_term = lt;
       break;
     }
     case HB_EV_PROP_FWD: {  // stepFollower MsgProp (:617-624): m.To = r.lead; r.send(m)
@@ -1327,7 +1328,7 @@ void consume_events(hbn_node* n) {
   }
   n->w_off[nc] = run;
   if (run != total) panicf("device event word counts disagree");
-  const unsigned k = n->pool->ways(total, 2048);
+  const unsigned k = n->pool->ways(total, 16384);
   n->pool->run(
       [&](unsigned t) {
         // partitions [p0, p1) of worker t: an equal share of the words
@@ -1523,7 +1524,7 @@ void push_term_runs(hbn_node* n) {
 // (workers over disjoint ranges of the batch's groups).
 void reserve_batch(hbn_node* n) {
   const size_t nb = n->bx.size();
-  const unsigned k = n->pool->ways(nb, 2048);
+  const unsigned k = n->pool->ways(nb, 4096);
   std::vector<std::vector<uint32_t>> rs(k);
   std::vector<std::vector<uint64_t>> rz(k), rt(k);
   n->pool->run(
@@ -1605,7 +1606,7 @@ void flush(hbn_node* n) {
   {
     HBN_PHASE(n, PH_STEPPED);
     const size_t ns = n->stepped.size();
-    const unsigned k = n->pool->ways(ns, 8192);
+    const unsigned k = n->pool->ways(ns, 16384);
     n->pool->run(
         [&](unsigned t) {
           size_t lo, hi;
@@ -1709,7 +1710,7 @@ void bulk_lookup(hbn_node* n, uint64_t count, const uint64_t* gids, BulkRun& br,
   HBN_PHASE(n, PH_BULK_LOOKUP);
   br.gp.assign(count, nullptr);
   br.fast.assign(count, 0);
-  const unsigned k = n->pool->ways(count, 1024);
+  const unsigned k = n->pool->ways(count, 4096);
   n->pool->run(
       [&](unsigned t) {
         size_t lo, hi;
@@ -1729,7 +1730,7 @@ void bulk_lookup(hbn_node* n, uint64_t count, const uint64_t* gids, BulkRun& br,
 // before anything is queued), workers over disjoint ranges.
 template <class Bad>
 bool bulk_any(hbn_node* n, uint64_t count, Bad&& bad) {
-  const unsigned k = n->pool->ways(count, 16384);
+  const unsigned k = n->pool->ways(count, 65536);
   std::vector<uint8_t> hit(k, 0);
   n->pool->run(
       [&](unsigned t) {
@@ -1751,7 +1752,7 @@ bool bulk_any(hbn_node* n, uint64_t count, Bad&& bad) {
 void push_responses(hbn_node* n, const BulkRun& br, const hbn_message* m, size_t a, size_t b) {
   HBN_PHASE(n, PH_BULK_RESP);
   const size_t cnt = b - a;
-  const unsigned k = n->pool->ways(cnt, 1024);
+  const unsigned k = n->pool->ways(cnt, 4096);
   std::vector<size_t> rows(k + 1, 0);  // rows of each worker's range (groups with a device slot)
   n->pool->run(
       [&](unsigned t) {
@@ -1815,7 +1816,7 @@ void push_proposals(hbn_node* n, const BulkRun& br, const uint8_t* const* data, 
                     size_t b) {
   HBN_PHASE(n, PH_BULK_PROP);
   const size_t cnt = b - a, base = n->b_group.size(), e0 = n->b_nent;
-  const unsigned k = n->pool->ways(cnt, 1024);
+  const unsigned k = n->pool->ways(cnt, 4096);
   for (auto* v : {&n->b_term, &n->b_index, &n->b_hint, &n->b_eoff, &n->b_commit, &n->b_from}) v->resize(base + cnt);
   n->b_group.resize(base + cnt);
   n->b_info.resize(base + cnt);
@@ -1964,17 +1965,16 @@ void step_follower(hbn_node* n, Group& g, const hbn_message* m) {
 
 // ---------------------------------------------------------------- Ready
 void refresh_content(std::vector<Group*>& content, Group& g);
+// (e.data holds the payload's offset in A.bytes until patch_arena)
 void arena_entry(Arena& A, const Ent& x) {
-  hbn_entry e;
+  hbn_entry& e = A.ents.emplace_back();
   e.term = x.term;
   e.index = x.index;
   e.type = x.type;
   e.has_data = x.has_data;
-  e.data = nullptr;
   e.data_len = x.data.size();
-  A.ent_off.push_back(A.bytes.size());
+  e.data = reinterpret_cast<const uint8_t*>(A.bytes.size());
   if (!x.data.empty()) A.bytes.insert(A.bytes.end(), x.data.begin(), x.data.end());
-  A.ents.push_back(e);
 }
 
 void clear_arena(hbn_node* n) {
@@ -1988,8 +1988,7 @@ void build_ready(Group& g, Arena& A, Lists& L) {
   g.touched = false;
   refresh_content(L.content, g);
   if (!g.content && g.msgs.empty() && !g.fault) return;
-  hbn_group_ready r;
-  std::memset(&r, 0, sizeof(r));
+  hbn_group_ready& r = A.out.emplace_back();  // (zeroed)
   r.group = g.id;
   Delivered& d = g.dlv;
   d = Delivered{};
@@ -2020,8 +2019,7 @@ void build_ready(Group& g, Arena& A, Lists& L) {
   r.n_committed = A.ents.size() - A.off.back();
   A.off.push_back(A.msgs.size());  // Messages = r.msgs, then cleared (raft/multinode.go:277-281)
   for (Msg& m : g.msgs) {
-    hbn_message x;
-    std::memset(&x, 0, sizeof(x));
+    hbn_message& x = A.msgs.emplace_back();  // (zeroed)
     x.type = m.type;
     x.reject = m.reject;
     x.to = m.to;
@@ -2042,14 +2040,12 @@ void build_ready(Group& g, Arena& A, Lists& L) {
       A.snaps.push_back(*m.snap);
       snap_view(A.snaps.back(), &x.snapshot);
     }
-    A.msgs.push_back(x);
   }
   r.n_messages = g.msgs.size();
   g.msgs.clear();
   r.fault = g.fault;
   g.delivered = true;
   L.delivered.push_back(&g);
-  A.out.push_back(r);
 }
 
 // A large touched list (the network input's order: random over the groups)
@@ -2084,8 +2080,8 @@ void slot_order_touched(hbn_node* n) {
 
 // once no vector of A grows any more: offsets become pointers
 void patch_arena(Arena& A) {
-  for (size_t i = 0; i < A.ents.size(); ++i)
-    if (A.ents[i].data_len) A.ents[i].data = A.bytes.data() + A.ent_off[i];
+  for (hbn_entry& e : A.ents)
+    e.data = e.data_len ? A.bytes.data() + reinterpret_cast<uintptr_t>(e.data) : nullptr;
   for (hbn_message& x : A.msgs)
     x.entries = x.n_entries ? A.ents.data() + reinterpret_cast<uintptr_t>(x.entries) : nullptr;
   for (size_t i = 0; i < A.out.size(); ++i) {
@@ -2839,7 +2835,7 @@ int hbn_ready(hbn_node* n, const hbn_group_ready** out, uint64_t* count) {
     auto build0 = std::chrono::steady_clock::now();
     slot_order_touched(n);
     const size_t nt = n->touched.size();
-    const unsigned k = n->pool->ways(nt, 256);
+    const unsigned k = n->pool->ways(nt, 2048);
     n->pool->run(
         [&](unsigned t) {
           size_t lo, hi;
@@ -2897,7 +2893,7 @@ int hbn_advance(hbn_node* n, const uint64_t* groups, uint64_t count) {
   return guarded([&] {
     flush(n);
     HBN_PHASE(n, PH_ADVANCE);
-    const unsigned k = n->pool->ways(count, 512);
+    const unsigned k = n->pool->ways(count, 2048);
     n->pool->run(
         [&](unsigned t) {
           size_t lo, hi;

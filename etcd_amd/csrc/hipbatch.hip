@@ -321,7 +321,6 @@ struct ScatTile {
   uint32_t g[RDX_ROUNDS], i[RDX_ROUNDS], o[RDX_ROUNDS];
   uint64_t t[RDX_ROUNDS];  // packed ti
   bool v[RDX_ROUNDS];
-  uint4 x[X ? RDX_ROUNDS : 1];  // X mode: {hint, commit}
 };
 template <bool X>
 __device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_t G, uint32_t base, uint32_t wave,
@@ -339,7 +338,6 @@ __device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_
       T.i[r] = m.info;
       T.o[r] = m.orig;
       T.t[r] = m.ti;
-      if constexpr (X) T.x[r] = v ? s.recx[i] : make_uint4(0, 0, 0, 0);
     } else {  // the batch: pack Term and Index (a long pair goes to the side table)
       const uint32_t inf = v ? s.info[i] : 0u;
       const uint64_t tm = v ? s.term[i] : 0ull, ix = v ? s.index[i] : 0ull;
@@ -351,8 +349,6 @@ __device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_
       }
       uint32_t ie = (inf & 0x3FFu) | (fits ? 0u : REC_LONG);
       if constexpr (X) {
-        const uint64_t h = (v && s.hint) ? s.hint[i] : 0ull, c = v ? s.mcommit[i] : 0ull;
-        T.x[r] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)c, (uint32_t)(c >> 32));
         // a MsgApp's entries: how many, and whether all carry m.Term (the
         // batch's entry arrays are in arrival order: near-contiguous per wave)
         if (v && (inf & 0xFu) == HB_MSG_APP && s.eoff && s.eterm) {
@@ -380,7 +376,7 @@ __device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_
 #endif
 constexpr uint32_t SCAT_TPW = HB_SCAT_TPW;
 template <bool FINAL, bool X>
-__global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, RadixDst d, FinalDst f, uint32_t G,
+__global__ void __launch_bounds__(RDX_THREADS) __attribute__((amdgpu_waves_per_eu(8))) k_radix_scatter(RadixSrc s, RadixDst d, FinalDst f, uint32_t G,
                                                               uint32_t shift, uint32_t dbits, uint32_t ntiles, const uint32_t* off,
                                                               const uint32_t* totals, uint32_t* n_valid) {
   __shared__ uint32_t s_base[RDX_BINS];  // digit base in the pass output (exclusive scan of the totals)
@@ -476,6 +472,25 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
         st_ti[p] = cur.t[r];
       }
     }
+    // X mode: the extensions {m.LogTerm / RejectHint, m.Commit} are read now,
+    // not with the tile (16 more VGPRs per tile in flight left one workgroup
+    // per CU), and cross the records' output phase in flight
+    uint4 xv[X ? RDX_ROUNDS : 1];
+    if constexpr (X) {
+#pragma unroll
+      for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+        const uint32_t i = tile * RDX_TILE + wave * (64 * RDX_ROUNDS) + r * 64 + lane;
+        xv[r] = make_uint4(0, 0, 0, 0);
+        if (cur.v[r]) {
+          if (s.rec) {
+            xv[r] = s.recx[i];
+          } else {
+            const uint64_t h = s.hint ? s.hint[i] : 0ull, c = s.mcommit[i];
+            xv[r] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)c, (uint32_t)(c >> 32));
+          }
+        }
+      }
+    }
     __syncthreads();
     const uint32_t valid = s_dstart[RDX_BINS];
     uint32_t wo[RDX_ROUNDS];  // output position of staging position r * RDX_THREADS + tid
@@ -509,7 +524,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_scatter(RadixSrc s, Radix
       __syncthreads();
 #pragma unroll
       for (uint32_t r = 0; r < RDX_ROUNDS; ++r)
-        if (cur.v[r]) st_x[sp[r]] = cur.x[r];
+        if (cur.v[r]) st_x[sp[r]] = xv[r];
       __syncthreads();
 #pragma unroll
       for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
