@@ -807,7 +807,18 @@ inline void split(size_t n, unsigned k, unsigned t, size_t* lo, size_t* hi) {
   *hi = n * (t + 1) / k;
 }
 // set a membership flag; true for the one caller that set it
-inline bool flag_set(bool& f) { return !__atomic_exchange_n(&f, true, __ATOMIC_RELAXED); }
+// (a plain load first: most calls find the flag set already, and a locked
+// exchange per call costs more than the rest of a small phase's per-group work)
+inline bool flag_set(bool& f, bool shared = true) {
+  if (__atomic_load_n(&f, __ATOMIC_RELAXED)) return false;
+  if (!shared) return f = true;  // one worker: no other thread touches the flag
+  return !__atomic_exchange_n(&f, true, __ATOMIC_RELAXED);
+}
+// a counter that several workers may bump (k > 1) or only this one
+inline void bump(uint64_t& x, bool shared) {
+  if (shared) __atomic_fetch_add(&x, 1, __ATOMIC_RELAXED);
+  else ++x;
+}
 
 // membership lists a parallel phase appends to, one per worker (a cache line
 // of its own: the workers push to them on every group)
@@ -1066,14 +1077,14 @@ uint32_t alloc_slot(hbn_node* n) {
 }
 
 // ---------------------------------------------------------------- event replay
-void touch_into(std::vector<Group*>& v, Group& g) {
-  if (flag_set(g.touched)) v.push_back(&g);
+void touch_into(std::vector<Group*>& v, Group& g, bool shared = true) {
+  if (flag_set(g.touched, shared)) v.push_back(&g);
 }
-void touch(hbn_node* n, Group& g) { touch_into(n->touched, g); }
+void touch(hbn_node* n, Group& g) { touch_into(n->touched, g, false); }  // (the API thread alone)
 
-void mark_stepped(std::vector<Group*>& touched, Group& g) {
+void mark_stepped(std::vector<Group*>& touched, Group& g, bool shared = true) {
   g.hs_commit = g.log.committed;  // r.Commit = r.raftLog.committed after Step (raft/raft.go:488)
-  touch_into(touched, g);
+  touch_into(touched, g, shared);
 }
 
 // worker lists merged into the node's, in worker order
@@ -1376,7 +1387,7 @@ void consume_events(hbn_node* n) {
               e.aux = (uint16_t)((w >> 12) & 0xF);
               on_event(n, g, e, L);
             }
-            mark_stepped(L.touched, g);
+            mark_stepped(L.touched, g, k > 1);
           }
         }
       },
@@ -1616,7 +1627,7 @@ void flush(hbn_node* n) {
             if (i + 8 < hi) __builtin_prefetch(n->stepped[i + 8]);
             Group& g = *n->stepped[i];
             g.stepped = false;
-            mark_stepped(touched, g);
+            mark_stepped(touched, g, k > 1);
           }
         },
         k);
@@ -1785,7 +1796,7 @@ void push_responses(hbn_node* n, const BulkRun& br, const hbn_message* m, size_t
           }
           Group& g = *br.gp[i];
           const hbn_message& x = m[i];
-          touch_into(L.touched, g);
+          touch_into(L.touched, g, k > 1);
           if (g.slot == NO_SLOT) continue;  // prs is empty: responses are filtered (raft/multinode.go:235)
           const int s = g.slot_of(x.from);
           n->b_group[r] = g.slot;
@@ -1797,10 +1808,10 @@ void push_responses(hbn_node* n, const BulkRun& br, const hbn_message* m, size_t
           n->b_commit[r] = 0;
           n->b_from[r] = x.from;
           ++r;
-          __atomic_fetch_add(&g.bx, 1, __ATOMIC_RELAXED);
-          if (x.type == HB_MSG_VOTE_RESP) __atomic_fetch_add(&g.bxr, 1, __ATOMIC_RELAXED);
-          if (flag_set(g.in_bx)) L.bx.push_back(&g);
-          if (s >= 0 && flag_set(g.stepped)) L.stepped.push_back(&g);
+          bump(g.bx, k > 1);
+          if (x.type == HB_MSG_VOTE_RESP) bump(g.bxr, k > 1);
+          if (flag_set(g.in_bx, k > 1)) L.bx.push_back(&g);
+          if (s >= 0 && flag_set(g.stepped, k > 1)) L.stepped.push_back(&g);
         }
       },
       k);
@@ -1852,9 +1863,9 @@ void push_proposals(hbn_node* n, const BulkRun& br, const uint8_t* const* data, 
           n->b_commit[r] = 0;
           n->b_from[r] = n->id;
           g.bx += 2;  // the message and its entry
-          if (flag_set(g.touched)) L.touched.push_back(&g);
-          if (flag_set(g.in_bx)) L.bx.push_back(&g);
-          if (flag_set(g.stepped)) L.stepped.push_back(&g);
+          if (flag_set(g.touched, k > 1)) L.touched.push_back(&g);
+          if (flag_set(g.in_bx, k > 1)) L.bx.push_back(&g);
+          if (flag_set(g.stepped, k > 1)) L.stepped.push_back(&g);
         }
       },
       k);
@@ -2910,12 +2921,14 @@ int hbn_advance(hbn_node* n, const uint64_t* groups, uint64_t count) {
             Group* gp = n->groups.find(groups[i]);
             if (!gp) continue;
             Group& g = *gp;
-            if (!__atomic_exchange_n(&g.delivered, false, __ATOMIC_RELAXED)) continue;  // (a group listed twice)
+            if (!__atomic_load_n(&g.delivered, __ATOMIC_RELAXED) ||
+                !__atomic_exchange_n(&g.delivered, false, __ATOMIC_RELAXED))
+              continue;  // (a group listed twice)
             materialize(g);  // messages stepped since the Ready still read the log
             commit_ready(g, g.dlv);
             // the recomputed Ready (raft/multinode.go:290-295) is a candidate again
             refresh_content(L.content, g);
-            touch_into(L.touched, g);
+            touch_into(L.touched, g, k > 1);
           }
         },
         k);

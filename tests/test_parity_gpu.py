@@ -397,6 +397,21 @@ def test_follow_workload_fast_lane(ents):
         _, st, now = pair.step(_merge_follow(b, f, 105 + k), ctx=f"follow mixed {k}", check_inflights=False)
 
 
+def test_follow_workload_long_records():
+    """X mode with wide values: Terms up to 2^50 and log indices up to 2^62
+    (past the 16-byte record's 24 / 40 bits: REC_LONG, the pair in the side
+    table) on the follower lane, three steps, then mixed follower traffic."""
+    G = 3000
+    g, runs = synth.follow_groups(G, 3, seed=131, last_hi=1 << 62, term_hi=1 << 50, with_runs=True)
+    pair = Pair(g, runs, 3, 256, max_batch=4 * G, term_runs=True)
+    for step in range(3):
+        _, st, now = pair.step(synth.follow_batch(g, step, seed=132), ctx=f"follow long step {step}",
+                               check_inflights=False)
+        assert st[abi.HB_STAT_COMMITS] == G and st[abi.HB_STAT_FAULTS] == 0
+    f = synth.follower_messages(now, pair.og.term, 2000, seed=133)
+    _, st, now = pair.step(f, ctx="follow long mixed", check_inflights=False)
+
+
 def _merge_follow(a, b, seed):
     """Interleave two follower-side batches (each with entries), arrival order
     within each kept, entry offsets re-based."""
