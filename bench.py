@@ -311,7 +311,8 @@ def run_multinode(args):
     import ctypes as C
     G = args.groups or 1000
     n = args.replicas or 3
-    L = C.CDLL(os.path.join(ROOT, "etcd_amd", "libhbnode_bench.so"))
+    # (HBNB_DIR: a variant build's directory, for same-box A/Bs of the host library)
+    L = C.CDLL(os.path.join(os.environ.get("HBNB_DIR", os.path.join(ROOT, "etcd_amd")), "libhbnode_bench.so"))
     L.hbnb_run2.restype = C.c_int
     L.hbnb_run2.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                             C.POINTER(C.c_double)]
@@ -823,6 +824,11 @@ def run_e2e(args, world, rank, local, dev, torch, dist):
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:  # the same cfg2 steps on the host's C oracle
+            try:
+                out["cpu_baseline"] = cpu_baseline(n, args.cpu_groups, args.cpu_seconds)
+            except Exception as e:  # report, never fake
+                out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
 
 

@@ -101,8 +101,10 @@ def main():
                               "measured_read_bytes": cal["fetch_bytes"]}
     # the whole step (every kernel hb_step launches, per step; k_route runs once per step)
     step_k = ("k_radix_hist", "k_scan_rows", "k_radix_scatter", "k_bucket_bounds", "k_route", "k_apply", "k_elect",
-              "k_follow", "k_finish")
+              "k_follow", "k_finish", "k_tick")
     steps = sum(s["calls"] for k, s in ks.items() if k.startswith("k_route"))
+    if not steps:  # a Tick line (hb_tick: k_tick + k_finish per tick)
+        steps = sum(s["calls"] for k, s in ks.items() if k.startswith("k_tick"))
     if steps:
         tb = us = 0.0
         missing = []
