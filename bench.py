@@ -1127,8 +1127,7 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     if args.workload in ("cfg3", "cfg4", "tick"):
         # whole-step roofline (several kernels share the step; per-kernel times: profiles/*kernel_stats.csv)
         ach = alg / (ms / args.steps * 1e-3) / args.steps / 1e9 if ms > 0 else 0.0
-        tr, tsrc = step_traffic(args.traffic_json, args.workload, G, n, ms / args.steps) \
-            if args.workload != "tick" else (None, None)
+        tr, tsrc = step_traffic(args.traffic_json, args.workload, G, n, ms / args.steps)
         extra["roofline"] = {"bound": "hbm", "kernel": "hb_step (whole step)" if args.workload != "tick" else
                              "hb_tick (k_tick + finish)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr,

@@ -697,6 +697,15 @@ struct Group {
 // Advance, bulk ingestion — runs on a pool of host threads, each owning a
 // disjoint set of groups; the node's membership lists are appended per thread
 // and merged in thread order.  The calling thread is worker 0.
+#ifndef HBN_GRAIN_REPLAY  // A/B (r04): phase grains for small node sizes
+#define HBN_GRAIN_REPLAY 16384
+#endif
+#ifndef HBN_GRAIN_BUILD
+#define HBN_GRAIN_BUILD 2048
+#endif
+#ifndef HBN_GRAIN_ADVANCE
+#define HBN_GRAIN_ADVANCE 2048
+#endif
 class Pool {
  public:
   explicit Pool(unsigned n) : n_(n ? n : 1), w_(n_) {
@@ -1339,7 +1348,7 @@ void consume_events(hbn_node* n) {
   }
   n->w_off[nc] = run;
   if (run != total) panicf("device event word counts disagree");
-  const unsigned k = n->pool->ways(total, 16384);
+  const unsigned k = n->pool->ways(total, HBN_GRAIN_REPLAY);
   n->pool->run(
       [&](unsigned t) {
         // partitions [p0, p1) of worker t: an equal share of the words
@@ -2846,7 +2855,7 @@ int hbn_ready(hbn_node* n, const hbn_group_ready** out, uint64_t* count) {
     auto build0 = std::chrono::steady_clock::now();
     slot_order_touched(n);
     const size_t nt = n->touched.size();
-    const unsigned k = n->pool->ways(nt, 2048);
+    const unsigned k = n->pool->ways(nt, HBN_GRAIN_BUILD);
     n->pool->run(
         [&](unsigned t) {
           size_t lo, hi;
@@ -2904,7 +2913,7 @@ int hbn_advance(hbn_node* n, const uint64_t* groups, uint64_t count) {
   return guarded([&] {
     flush(n);
     HBN_PHASE(n, PH_ADVANCE);
-    const unsigned k = n->pool->ways(count, 2048);
+    const unsigned k = n->pool->ways(count, HBN_GRAIN_ADVANCE);
     n->pool->run(
         [&](unsigned t) {
           size_t lo, hi;

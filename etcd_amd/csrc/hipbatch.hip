@@ -1592,6 +1592,10 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint32_t l_eflag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
+  // each lane's route slots, read once: the arrival keys come from them and the
+  // messages are then read back in arrival order (reading the keys from HBM and
+  // the slots again fetched every slot line twice: 16-byte slots, 4-byte keys)
+  __shared__ uint4 l_slot[KS][PART];
   const uint32_t tid = threadIdx.x;
   const uint32_t xs = blockIdx.x & 7, stride = gridDim.x >> 3;
   const uint32_t nl = __hip_atomic_load(&a.el_cnt[xs * CTR_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1630,7 +1634,9 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
       uint32_t perm = 0;
 #pragma unroll
       for (uint32_t k = 0; k < KS; ++k) {
-        key[k] = k < cnt ? at32(a.slot, k * a.S.G + g).y : 0xFFFFFFFFu;
+        const uint4 r = k < cnt ? at32(a.slot, k * a.S.G + g) : make_uint4(0, 0xFFFFFFFFu, 0, 0);
+        l_slot[k][tid] = r;
+        key[k] = r.y;
         perm |= k << (4 * k);
       }
 #pragma unroll
@@ -1648,20 +1654,11 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
       }
       const uint32_t skip = resume & 0x3FFFFFFFu;
       uint32_t x = skip;
-      // the next message's loads are in flight while one is stepped
-      uint32_t inf_n = 0;
-      uint64_t term_n = 0;
-      auto ld = [&](uint32_t y, uint32_t& inf, uint64_t& tm) {
-        uint32_t org;
-        uint64_t ix;
-        slot_unpack(at32(a.slot, ((perm >> (4 * y)) & 0xF) * a.S.G + g), a.side, &inf, &org, &tm, &ix);
-      };
-      if (x < cnt) ld(x, inf_n, term_n);
 #pragma nounroll
       for (; x < cnt; ++x) {
-        const uint32_t inf = inf_n;
-        const uint64_t mterm = term_n;
-        if (x + 1 < cnt) ld(x + 1, inf_n, term_n);
+        uint32_t inf, org;  // (from the lane's LDS copy)
+        uint64_t mterm, ix;
+        slot_unpack(l_slot[(perm >> (4 * x)) & 0xF][tid], a.side, &inf, &org, &mterm, &ix);
         const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
         if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
           st_drop++;
@@ -1728,6 +1725,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint32_t l_eflag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
+  __shared__ uint4 l_slot[KS][PART];  // the lane's route slots, read once (as in k_elect)
   const uint32_t part = block_part(a.sis_log);
   if (part >= a.NB) return;  // uniform: grid padding
   const uint32_t tid = threadIdx.x;
@@ -1754,8 +1752,11 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   // on cfg3 and +4.5 % on cfg4, whose lanes are mostly not leaders)
   L.last = L.committed = 0;
   L.term = 0;
-  if (spec) L.load();
   const bool slots = leader && fits;
+#pragma unroll
+  for (uint32_t k = 0; k < KS; ++k)
+    if (slots && k < cnt) l_slot[k][tid] = at32(a.slot, k * a.S.G + g);
+  if (spec) L.load();
   bool loaded = spec, higher = false;
   if (slots && !spec) {  // a busy leader without a proposal: load it unless a higher term steps it down
     const uint64_t t = at32(a.S.term, g);
@@ -1764,7 +1765,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
       if (k < cnt) {
         uint32_t inf, org;
         uint64_t tm, ix;
-        slot_unpack(at32(a.slot, k * a.S.G + g), a.side, &inf, &org, &tm, &ix);
+        slot_unpack(l_slot[k][tid], a.side, &inf, &org, &tm, &ix);
         higher |= tm > t;
       }
     }
@@ -1780,7 +1781,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   const bool keys = slots && loaded;
 #pragma unroll
   for (uint32_t k = 0; k < KS; ++k) {
-    key[k] = (keys && k < cnt) ? at32(a.slot, k * a.S.G + g).y : 0xFFFFFFFFu;
+    key[k] = (keys && k < cnt) ? l_slot[k][tid].y : 0xFFFFFFFFu;
     perm |= k << (4 * k);
   }
   // arrival order of the slots (odd-even transposition, slot numbers as nibbles)
@@ -1826,19 +1827,12 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
       resume = 0;
     } else {
       uint32_t x = 0;
-      // the next message's loads are in flight while one is stepped
-      uint32_t inf_n = 0, orig_n = 0;
-      uint64_t term_n = 0, index_n = 0;
-      auto ld = [&](uint32_t y, uint32_t& inf, uint32_t& org, uint64_t& tm, uint64_t& ix) {
-        slot_unpack(at32(a.slot, ((perm >> (4 * y)) & 0xF) * a.S.G + g), a.side, &inf, &org, &tm, &ix);
-      };
-      ld(0, inf_n, orig_n, term_n, index_n);
 #pragma nounroll
       for (; x < cnt; ++x) {
         if (L.faulted()) break;
-        const uint32_t inf = inf_n, morig = orig_n;
-        const uint64_t mterm = term_n, mindex = index_n;
-        if (x + 1 < cnt) ld(x + 1, inf_n, orig_n, term_n, index_n);
+        uint32_t inf, morig;  // (from the lane's LDS copy: no load to run ahead of)
+        uint64_t mterm, mindex;
+        slot_unpack(l_slot[(perm >> (4 * x)) & 0xF][tid], a.side, &inf, &morig, &mterm, &mindex);
         const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
         const bool reject = (inf >> 8) & 1u;
         if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
