@@ -697,15 +697,6 @@ struct Group {
 // Advance, bulk ingestion — runs on a pool of host threads, each owning a
 // disjoint set of groups; the node's membership lists are appended per thread
 // and merged in thread order.  The calling thread is worker 0.
-#ifndef HBN_GRAIN_REPLAY  // A/B (r04): phase grains for small node sizes
-#define HBN_GRAIN_REPLAY 16384
-#endif
-#ifndef HBN_GRAIN_BUILD
-#define HBN_GRAIN_BUILD 2048
-#endif
-#ifndef HBN_GRAIN_ADVANCE
-#define HBN_GRAIN_ADVANCE 2048
-#endif
 class Pool {
  public:
   explicit Pool(unsigned n) : n_(n ? n : 1), w_(n_) {
@@ -765,7 +756,10 @@ class Pool {
   // wake-ups) made the 1k-group MultiNode 3-5x slower on the GPU box — every
   // phase, single-threaded ones included, slowed down next to the polling
   // threads under the box's 16-CPU quota — so small phases run on the calling
-  // thread alone (ways()) and workers block between phases.
+  // thread alone (ways()) and workers block between phases.  (Blocking
+  // workers on 1k-group phases — grains 256-1024 — measured 0.37 and 1.22 ms
+  // per cycle in two runs on one box against 0.43-0.44 ms single-threaded:
+  // not kept.)
   struct alignas(64) Worker {
     std::atomic<uint64_t> post{0};  // the job sequence number posted to this worker (STOP: exit)
     std::atomic<bool> sleeping{false};
@@ -1348,7 +1342,7 @@ void consume_events(hbn_node* n) {
   }
   n->w_off[nc] = run;
   if (run != total) panicf("device event word counts disagree");
-  const unsigned k = n->pool->ways(total, HBN_GRAIN_REPLAY);
+  const unsigned k = n->pool->ways(total, 16384);
   n->pool->run(
       [&](unsigned t) {
         // partitions [p0, p1) of worker t: an equal share of the words
@@ -2855,7 +2849,7 @@ int hbn_ready(hbn_node* n, const hbn_group_ready** out, uint64_t* count) {
     auto build0 = std::chrono::steady_clock::now();
     slot_order_touched(n);
     const size_t nt = n->touched.size();
-    const unsigned k = n->pool->ways(nt, HBN_GRAIN_BUILD);
+    const unsigned k = n->pool->ways(nt, 2048);
     n->pool->run(
         [&](unsigned t) {
           size_t lo, hi;
@@ -2913,7 +2907,7 @@ int hbn_advance(hbn_node* n, const uint64_t* groups, uint64_t count) {
   return guarded([&] {
     flush(n);
     HBN_PHASE(n, PH_ADVANCE);
-    const unsigned k = n->pool->ways(count, HBN_GRAIN_ADVANCE);
+    const unsigned k = n->pool->ways(count, 2048);
     n->pool->run(
         [&](unsigned t) {
           size_t lo, hi;
