@@ -170,9 +170,10 @@ Snap snap_from(const hbn_snapshot& s) {
 // by a thread-local bump pointer (45 ms for the same 1M), and freed blocks are
 // recycled through a per-thread cache backed by a global list.  Memory is kept
 // for reuse, never returned to the system.
+template <size_t BLOCK_BYTES>
 class BlockPool {
  public:
-  static constexpr size_t BLOCK = 512;
+  static constexpr size_t BLOCK = BLOCK_BYTES;
   static constexpr size_t CHUNK = size_t(2) << 20;
   static void* get() {
     Local& l = local();
@@ -266,7 +267,12 @@ class BlockPool {
   }
 };
 
-// std::allocator, except that the deque's entry blocks come from BlockPool
+// std::allocator, except for entry storage: a storage deque's blocks (512 /
+// sizeof(Ent) entries, libstdc++'s node) and one-entry vectors (a proposal's
+// entries, the unstable tail between Readys) come from the block pools.  A
+// million proposals per cycle are allocated by the ingesting workers and
+// freed by the replaying ones: from malloc, every free returns a chunk to
+// another thread's arena under its lock.
 template <class T>
 struct BlockAlloc {
   using value_type = T;
@@ -274,14 +280,17 @@ struct BlockAlloc {
   BlockAlloc() = default;
   template <class U>
   BlockAlloc(const BlockAlloc<U>&) {}
-  // (libstdc++'s deque node: 512 / sizeof(T) elements)
-  static bool pooled(size_t n) { return std::is_same<T, Ent>::value && sizeof(T) < 512 && n == 512 / sizeof(T); }
+  static constexpr bool ENT = std::is_same<T, Ent>::value;
+  static bool node(size_t n) { return ENT && sizeof(T) < 512 && n == 512 / sizeof(T); }
+  static bool one(size_t n) { return ENT && n == 1 && sizeof(T) <= 64; }
   T* allocate(size_t n) {
-    if (pooled(n)) return static_cast<T*>(BlockPool::get());
+    if (node(n)) return static_cast<T*>(BlockPool<512>::get());
+    if (one(n)) return static_cast<T*>(BlockPool<64>::get());
     return std::allocator<T>().allocate(n);
   }
   void deallocate(T* p, size_t n) {
-    if (pooled(n)) BlockPool::put(p);
+    if (node(n)) BlockPool<512>::put(p);
+    else if (one(n)) BlockPool<64>::put(p);
     else std::allocator<T>().deallocate(p, n);
   }
   template <class U>
@@ -290,6 +299,31 @@ struct BlockAlloc {
   bool operator!=(const BlockAlloc<U>&) const { return false; }
 };
 using EntLog = std::deque<Ent, BlockAlloc<Ent>>;
+
+// std::allocator whose value-less construct() default-initializes: a vector of
+// integers grows without being zeroed (the batch arrays, written in full by
+// the bulk workers right after they are sized)
+template <class T>
+struct RawAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = RawAlloc<U>;
+  };
+  RawAlloc() = default;
+  template <class U>
+  RawAlloc(const RawAlloc<U>&) {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+template <class T>
+using RawVec = std::vector<T, RawAlloc<T>>;
+using EntVec = std::vector<Ent, BlockAlloc<Ent>>;
 
 }  // namespace
 
@@ -367,7 +401,7 @@ namespace {
 // ---------------------------------------------------------------- raftLog (host half)
 struct Log {
   hbn_storage* st = nullptr;
-  std::vector<Ent> unstable;  // unstable.entries, position i + offset
+  EntVec unstable;  // unstable.entries, position i + offset
   uint64_t offset = 0;
   uint64_t committed = 0, applied = 0;
   bool has_usnap = false;     // unstable.snapshot (set by the follower side's restore)
@@ -415,7 +449,7 @@ struct Log {
   // append :89-98 + truncateAndAppend raft/log_unstable.go:100-122 (entries
   // moved in: the leader's proposals and the follower's MsgApp copies are
   // not read again)
-  void append(std::vector<Ent>&& ents) {
+  void append(EntVec&& ents) {
     if (ents.empty()) return;
     const uint64_t after = ents[0].index - 1;
     if (after < committed)
@@ -562,7 +596,7 @@ struct Log {
 struct Msg {
   uint32_t type = 0, reject = 0;
   uint64_t to = 0, from = 0, term = 0, log_term = 0, index = 0, commit = 0, reject_hint = 0;
-  std::vector<Ent> entries;  // owned entries (proposals), or
+  EntVec entries;  // owned entries (proposals), or
   uint64_t ent_lo = 0, ent_hi = 0;  // log range [lo, hi) still to be read (MsgApp), when !owned
   bool owned = true;
   std::shared_ptr<const Snap> snap;  // MsgSnap's snapshot
@@ -579,7 +613,7 @@ struct MsgQueue {
   Msg& back() { return v.back(); }
   void push_back(Msg&& m) { v.push_back(std::move(m)); }
   void pop_front() {
-    v[head].entries = std::vector<Ent>();
+    v[head].entries = EntVec();
     if (++head == v.size()) {
       clear();
     } else if (head >= 64 && 2 * head >= v.size()) {  // a long-lived backlog: reclaim the drained part
@@ -961,19 +995,21 @@ struct hbn_node {
   IdMap groups;
   std::vector<Group*> by_slot;
   std::vector<uint32_t> free_slots;
-  // pending device batch (host SoA, HB_STEP_HOST_PTRS)
-  std::vector<uint32_t> b_group, b_info;
-  std::vector<uint64_t> b_term, b_index, b_hint;
+  // pending device batch (host SoA, HB_STEP_HOST_PTRS; the bulk paths size the
+  // arrays and their workers write every element, so growth does not zero them)
+  RawVec<uint32_t> b_group, b_info;
+  RawVec<uint64_t> b_term, b_index, b_hint;
   // entries of the batch (hb_batch eoff / eterm / edesc): a MsgProp's (descriptors,
   // finite MaxSizePerMsg) and a MsgApp's (terms; payloads kept here for the replay)
   bool sized = false;
-  std::vector<uint32_t> b_edesc;
-  std::vector<uint64_t> b_eoff, b_eterm;
-  std::vector<Ent> b_ents;           // by entry position (MsgProp positions hold placeholders)
+  RawVec<uint32_t> b_edesc;
+  RawVec<uint64_t> b_eoff, b_eterm;
+  std::vector<Ent> b_ents;  // the MsgApp entries' payloads, in batch order
+  RawVec<uint32_t> b_kept;  // per message: its first entry in b_ents (MsgApp only)
   uint64_t b_nent = 0;
   // follower side (hb_batch commit; the sender ids and snapshots stay here)
-  std::vector<uint64_t> b_commit, b_from;
-  std::vector<uint32_t> b_snapi;     // per message: index into b_snaps, or NO_SLOT
+  RawVec<uint64_t> b_commit, b_from;
+  RawVec<uint32_t> b_snapi;  // per message: index into b_snaps, or NO_SLOT
   std::vector<Snap> b_snaps;
   bool b_app = false, b_follow = false;
   std::vector<Group*> reload;        // groups whose restored ConfState differs from their peers
@@ -1132,7 +1168,8 @@ void follower_append(hbn_node* n, Group& g, uint64_t x) {
   const uint64_t ci = g.log.find_conflict(index, n->b_eterm.data() + e0, e1 - e0);
   if (ci == 0) panicf("device appended entries the host log already holds");
   materialize(g);  // pending MsgApps of this group read entries the append may cut
-  std::vector<Ent> ents(n->b_ents.begin() + (e0 + (ci - index - 1)), n->b_ents.begin() + e1);
+  const uint64_t k0 = n->b_kept[x];  // (the message's entries, contiguous in b_ents)
+  EntVec ents(n->b_ents.begin() + (k0 + (ci - index - 1)), n->b_ents.begin() + (k0 + (e1 - e0)));
   g.log.append(std::move(ents));
 }
 
@@ -1206,7 +1243,7 @@ void on_event(hbn_node* n, Group& g, const hb_event& e, Lists& L) {
       break;
     case HB_EV_LAST: {
       const uint64_t li = g.log.last_index();
-      std::vector<Ent> ents;
+      EntVec ents;
       if (e.aux == 1) {
         ents.resize(1);  // becomeLeader's pb.Entry{Data: nil}
       } else {
@@ -1364,6 +1401,14 @@ void consume_events(hbn_node* n) {
               if (ps < n->by_slot.size())
                 if (const char* q = reinterpret_cast<const char*>(n->by_slot[ps]))
                   for (int l = 0; l < 5; ++l) __builtin_prefetch(q + 64 * l);
+            }
+            if (i + 8 < end) {  // ... and, nearer, the buffers it points to
+              const uint32_t ps = p * n->chunk_groups + ((uint32_t)(W[i + 8] >> 16) & 0xFF);
+              if (ps < n->by_slot.size())
+                if (const Group* q = n->by_slot[ps]) {
+                  __builtin_prefetch(q->msgs.data() + q->msgs.size());
+                  if (!q->props.empty()) __builtin_prefetch(q->props.v.data() + q->props.head);
+                }
             }
             const uint64_t w = W[i];
             const uint32_t type = (uint32_t)w & 0xF;
@@ -1647,6 +1692,7 @@ void flush(hbn_node* n) {
   n->b_eoff.clear();
   n->b_eterm.clear();
   n->b_ents.clear();
+  n->b_kept.clear();
   n->b_nent = 0;
   n->b_commit.clear();
   n->b_from.clear();
@@ -1692,6 +1738,7 @@ void push(hbn_node* n, Group& g, uint32_t type, uint64_t from, bool reject, uint
   n->b_commit.push_back(commit);
   n->b_from.push_back(from);
   n->b_snapi.push_back(NO_SLOT);
+  n->b_kept.push_back((uint32_t)n->b_ents.size());
   g.bx++;  // a noop (becomeLeader) at most
   if (type == HB_MSG_HUP || type == HB_MSG_VOTE_RESP || type == HB_MSG_SNAP) g.bxr++;  // a noop's / restore's run
   if (!g.in_bx) {
@@ -1716,14 +1763,14 @@ Group& group_of(hbn_node* n, uint64_t id) {
 // by one through the single-message path, which raises the reference's errors
 // at the right position.
 struct BulkRun {
-  std::vector<Group*> gp;
-  std::vector<uint8_t> fast;
+  RawVec<Group*> gp;      // (every element written by the lookup's workers)
+  RawVec<uint8_t> fast;
 };
 template <class Ok>
 void bulk_lookup(hbn_node* n, uint64_t count, const uint64_t* gids, BulkRun& br, Ok&& ok) {
   HBN_PHASE(n, PH_BULK_LOOKUP);
-  br.gp.assign(count, nullptr);
-  br.fast.assign(count, 0);
+  br.gp.resize(count);
+  br.fast.resize(count);
   const unsigned k = n->pool->ways(count, 4096);
   n->pool->run(
       [&](unsigned t) {
@@ -1732,8 +1779,9 @@ void bulk_lookup(hbn_node* n, uint64_t count, const uint64_t* gids, BulkRun& br,
         for (size_t i = lo; i < hi; ++i) {
           if (i + 16 < hi) __builtin_prefetch(n->groups.probe(gids[i + 16]));
           Group* g = n->groups.find(gids[i]);
-          if (!g) continue;
           br.gp[i] = g;
+          br.fast[i] = 0;
+          if (!g) continue;
           br.fast[i] = !g->fault && ok(i, *g);
         }
       },
@@ -1784,7 +1832,8 @@ void push_responses(hbn_node* n, const BulkRun& br, const hbn_message* m, size_t
   for (auto* v : {&n->b_term, &n->b_index, &n->b_hint, &n->b_eoff, &n->b_commit, &n->b_from}) v->resize(base + add);
   n->b_group.resize(base + add);
   n->b_info.resize(base + add);
-  n->b_snapi.resize(base + add, NO_SLOT);
+  n->b_snapi.resize(base + add);
+  n->b_kept.resize(base + add);  // (read only for MsgApp)
   n->pool->run(
       [&](unsigned t) {
         size_t lo, hi;
@@ -1810,6 +1859,7 @@ void push_responses(hbn_node* n, const BulkRun& br, const hbn_message* m, size_t
           n->b_eoff[r] = n->b_nent;
           n->b_commit[r] = 0;
           n->b_from[r] = x.from;
+          n->b_snapi[r] = NO_SLOT;
           ++r;
           bump(g.bx, k > 1);
           if (x.type == HB_MSG_VOTE_RESP) bump(g.bxr, k > 1);
@@ -1834,12 +1884,18 @@ void push_proposals(hbn_node* n, const BulkRun& br, const uint8_t* const* data, 
   for (auto* v : {&n->b_term, &n->b_index, &n->b_hint, &n->b_eoff, &n->b_commit, &n->b_from}) v->resize(base + cnt);
   n->b_group.resize(base + cnt);
   n->b_info.resize(base + cnt);
-  n->b_snapi.resize(base + cnt, NO_SLOT);
-  n->b_eterm.resize(e0 + cnt, 0);
-  n->b_ents.resize(e0 + cnt);
+  n->b_snapi.resize(base + cnt);
+  n->b_kept.resize(base + cnt);  // (read only for MsgApp)
+  n->b_eterm.resize(e0 + cnt);
   if (n->sized) n->b_edesc.resize(e0 + cnt);
-  std::vector<uint32_t> sl(cnt);
-  for (size_t i = 0; i < cnt; ++i) sl[i] = br.gp[a + i]->slot;
+  RawVec<uint32_t> sl(cnt);  // each group's owner is slot % k
+  n->pool->run(
+      [&](unsigned t) {
+        size_t lo, hi;
+        split(cnt, k, t, &lo, &hi);
+        for (size_t i = lo; i < hi; ++i) sl[i] = br.gp[a + i]->slot;
+      },
+      k);
   n->pool->run(
       [&](unsigned t) {
         Lists& L = n->lists[t];
@@ -1865,6 +1921,8 @@ void push_proposals(hbn_node* n, const BulkRun& br, const uint8_t* const* data, 
           n->b_eoff[r] = e0 + j;
           n->b_commit[r] = 0;
           n->b_from[r] = n->id;
+          n->b_snapi[r] = NO_SLOT;
+          n->b_eterm[e0 + j] = 0;
           g.bx += 2;  // the message and its entry
           if (flag_set(g.touched, k > 1)) L.touched.push_back(&g);
           if (flag_set(g.in_bx, k > 1)) L.bx.push_back(&g);
@@ -1923,7 +1981,6 @@ void push_entry(hbn_node* n, const Ent& x, bool keep) {
   if (n->sized) n->b_edesc.push_back(ent_desc(x));
   n->b_eterm.push_back(x.term);
   if (keep) n->b_ents.push_back(x);
-  else n->b_ents.emplace_back();
   n->b_nent++;
 }
 
@@ -2579,7 +2636,7 @@ int hbn_create_group(hbn_node* n, uint64_t group, const hbn_config* cfg, hbn_sto
       // ConfChangeAddNode entry per peer, committed = len(peers), addNode each.
       if (g.term != 1) g.vote = 0;
       g.term = 1;
-      std::vector<Ent> ents(n_peers);
+      EntVec ents(n_peers);
       for (uint32_t i = 0; i < n_peers; ++i) {
         ents[i].type = HBN_ENTRY_CONF_CHANGE;
         ents[i].term = 1;
@@ -2856,9 +2913,15 @@ int hbn_ready(hbn_node* n, const hbn_group_ready** out, uint64_t* count) {
           split(nt, k, t, &lo, &hi);
           Arena& A = n->arenas[t];
           for (size_t i = lo; i < hi; ++i) {
-            if (i + 4 < hi) {
+            if (i + 4 < hi) {  // the group 4 ahead, then what the group 2 ahead points to
               const char* q = reinterpret_cast<const char*>(n->touched[i + 4]);
               for (int l = 0; l < 9; ++l) __builtin_prefetch(q + 64 * l);
+            }
+            if (i + 2 < hi) {
+              const Group& q = *n->touched[i + 2];
+              __builtin_prefetch(q.msgs.data());
+              __builtin_prefetch(q.log.unstable.data());
+              __builtin_prefetch(q.log.st);
             }
             build_ready(*n->touched[i], A, n->lists[t]);
           }
