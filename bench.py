@@ -608,7 +608,8 @@ def run_replication(args, world, rank, local):
         achieved = float(alg / (apply_ms * 1e-3) / 1e9)
         kname = f"k_apply_fast<{3 if n <= 3 else (5 if n <= 5 else 7)}>"
         # (rocprofv3 names the template with its X-mode flag since r04)
-        traffic, tsrc = pmc_traffic(args.traffic_json, [kname[:-1] + ", false>", kname], G, n, apply_ms * 1e3)
+        traffic, tsrc = pmc_traffic(args.traffic_json, [kname[:-1] + ", false, 2u>", kname[:-1] + ", false>", kname],
+                                    G, n, apply_ms * 1e3)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
@@ -1089,7 +1090,7 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         alg_note = follow_alg_note()
         kname = "k_apply_fast<3> (X mode: FollowLane)"
         ach_k = FOLLOW_GROUP_BYTES * G / (apply_us * 1e-6) / 1e9 if apply_us > 0 else 0.0
-        tr, tsrc = pmc_traffic(args.traffic_json, "k_apply_fast<3, true>", G, n, apply_us)
+        tr, tsrc = pmc_traffic(args.traffic_json, ["k_apply_fast<3, true, 2u>", "k_apply_fast<3, true>"], G, n, apply_us)
         extra = {"commits_per_s": int(st[abi.HB_STAT_COMMITS]) / sec, "entries_per_s": int(st[abi.HB_STAT_ENTRIES]) / sec,
                  "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(ach_k, 1), "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": round(ach_k / HBM_PEAK_GBS, 4), "traffic": tr,

@@ -56,6 +56,7 @@ HB_SLOT_NONE = 0xF
 HB_STEP_HOST_PTRS = 0x1
 HB_STEP_PROFILE = 0x2
 HB_STEP_PROFILE_APPLY = 0x4
+HB_STEP_MSG_PROPS = 0x8
 
 HB_FAULT_NONE = 0
 HB_FAULT_LEADER_CAMPAIGN = 1

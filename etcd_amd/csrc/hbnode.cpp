@@ -1012,6 +1012,7 @@ struct hbn_node {
   RawVec<uint32_t> b_snapi;  // per message: index into b_snaps, or NO_SLOT
   std::vector<Snap> b_snaps;
   bool b_app = false, b_follow = false;
+  bool b_prop = false;  // the batch carries MsgProp rows (hb_step HB_STEP_MSG_PROPS)
   std::vector<Group*> reload;        // groups whose restored ConfState differs from their peers
   std::vector<Group*> pend_sz;  // groups (re)loaded on the device whose entry sizes are still to push
   std::vector<Group*> pend_tr;  // ... and whose older log term runs are still to push
@@ -1659,7 +1660,7 @@ void flush(hbn_node* n) {
   }
   {
     HBN_PHASE(n, PH_HB_STEP);
-    check(hb_step(n->h, &b, HB_STEP_HOST_PTRS));
+    check(hb_step(n->h, &b, HB_STEP_HOST_PTRS | (n->b_prop ? HB_STEP_MSG_PROPS : 0u)));
   }
   consume_events(n);
   {
@@ -1698,7 +1699,7 @@ void flush(hbn_node* n) {
   n->b_from.clear();
   n->b_snapi.clear();
   n->b_snaps.clear();
-  n->b_app = n->b_follow = false;
+  n->b_app = n->b_follow = n->b_prop = false;
   // restored snapshots whose ConfState differs from the peers: r.prs = the
   // ConfState's nodes, every Progress as setProgress made it (raft/raft.go:700-705)
   for (Group* g : n->reload) {
@@ -1729,6 +1730,7 @@ void push(hbn_node* n, Group& g, uint32_t type, uint64_t from, bool reject, uint
     throw Fail{HBN_EUNSUPPORTED};
   }
   if (n->b_group.size() >= n->max_batch) flush(n);
+  if (type == HB_MSG_PROP) n->b_prop = true;
   n->b_group.push_back(g.slot);
   n->b_info.push_back(HB_INFO(type, fs, reject) | (voted ? HB_INFO_VOTED : 0u));
   n->b_term.push_back(term);
@@ -1931,6 +1933,7 @@ void push_proposals(hbn_node* n, const BulkRun& br, const uint8_t* const* data, 
       },
       k);
   n->b_nent = e0 + cnt;
+  n->b_prop = true;
   merge(n->touched, n->lists, &Lists::touched);
   merge(n->bx, n->lists, &Lists::bx);
   merge(n->stepped, n->lists, &Lists::stepped);

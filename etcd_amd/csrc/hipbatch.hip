@@ -608,8 +608,17 @@ struct ApplyArgs {
 #ifndef HB_KS5
 #define HB_KS5 8
 #endif
+// n = 3 keeps up to 3: a leader's two MsgAppResp plus the MsgProp a MultiNode
+// application proposes in the same Ready cycle stay on the fast lane when the
+// batch says it carries MsgProp messages (HB_STEP_MSG_PROPS); otherwise 2 —
+// the third slot costs cfg2 4 % (route at one workgroup per CU, one more slot
+// per lane: 118.4-120.0 vs 123.5-124.6 us in two same-box pairs)
 constexpr uint32_t route_kmax(int nmax) {
-  return nmax <= 3 ? 2u : (nmax <= 5 ? (uint32_t)HB_KS5 : (uint32_t)(nmax - 1 + HB_KS_EXTRA));
+  return nmax <= 3 ? 3u : (nmax <= 5 ? (uint32_t)HB_KS5 : (uint32_t)(nmax - 1 + HB_KS_EXTRA));
+}
+// the slots a step uses (route_kmax is the most any step uses: the allocation)
+inline uint32_t step_kmax(uint32_t nmax, uint32_t flags) {
+  return nmax <= 3 ? ((flags & HB_STEP_MSG_PROPS) ? 3u : 2u) : route_kmax((int)nmax);
 }
 static_assert(route_kmax(3) <= 8 && route_kmax(5) <= 8 && route_kmax(7) <= 8,
               "the slot sorts carry slot numbers as 4-bit nibbles of one uint32_t");
@@ -916,7 +925,7 @@ constexpr uint32_t ROUTE_UNROLL = HB_ROUTE_UNROLL;  // records in flight per lan
 // 1024 vs 512 (buckets of at least 1024 groups): cfg4 1.949 vs 2.020 ms, cfg3
 // neutral.  X mode stages twice the bytes per slot, so it keeps half as many.
 constexpr uint32_t route_rg_log(uint32_t kmax, bool x = false) {
-  return (kmax <= 2 ? 11u : 10u) - (x ? 1u : 0u);
+  return (kmax <= 3 ? 11u : 10u) - (x ? 1u : 0u);
 }
 template <int KMAX, bool X> struct RouteGeom {
   static constexpr uint32_t RG_LOG = route_rg_log(KMAX, X);
@@ -1026,21 +1035,21 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
 // than slots and no proposal is handed over with its state unloaded.
 // fol (X mode): a follower whose messages all sit in its slots, stepped by
 // FollowLane as far as it takes them (s_h / s_c: m.LogTerm, m.Commit).
-template <int NMAX>
+template <int NMAX, uint32_t KS>
 __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FollowLane<NMAX>& L, uint32_t part, uint32_t lane,
                                           bool live, bool lead, bool leader, bool fol, uint32_t prop_raw, uint32_t cnt,
-                                          uint32_t (&s_info)[NMAX - 1], uint32_t (&s_orig)[NMAX - 1],
-                                          uint64_t (&s_term)[NMAX - 1], uint64_t (&s_index)[NMAX - 1],
-                                          uint64_t (&s_h)[NMAX - 1], uint64_t (&s_c)[NMAX - 1],
+                                          uint32_t (&s_info)[KS], uint32_t (&s_orig)[KS],
+                                          uint64_t (&s_term)[KS], uint64_t (&s_index)[KS],
+                                          uint64_t (&s_h)[KS], uint64_t (&s_c)[KS],
                                           uint64_t moff, uint32_t* l_pfill, uint32_t* l_fill, uint32_t* l_flag,
                                           uint32_t* l_eflag, uint32_t (&vals)[ST_N + 1]) {
-  constexpr uint32_t KMAX = NMAX - 1;
+  constexpr uint32_t KMAX = KS;
   const uint32_t g = part * PART + lane;
   const uint64_t last0 = L.last, commit0 = L.committed;
 
   bool flagged = false;
   uint32_t resume = 0;
-  uint32_t st_msgs = 0, st_drop = 0;
+  uint32_t st_msgs = 0, st_drop = 0, st_app = 0;
 
   // ---- the dense proposal: its events go to the partition's P chunk (fixed
   // slot of ev_per_msg x PART words), before any message event of the group.
@@ -1108,6 +1117,18 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FollowLane<NMAX>& 
         j++;
         continue;
       }
+      if (KMAX >= 3 && type == HB_MSG_PROP) {  // a local proposal (Term 0; Index = its entry count): stepLeader MsgProp
+        if (s_term[k] != 0 || s_index[k] > 0xFFFFFFFFull || !L.prop_ok((uint32_t)s_index[k])) {
+          flagged = true;
+          resume = j;
+          break;
+        }
+        L.arrival = s_orig[k];
+        L.prop((uint32_t)s_index[k]);
+        st_msgs++;
+        j++;
+        continue;
+      }
       if (!L.accept_ok(type, from, s_term[k], reject)) {
         flagged = true;
         resume = j;
@@ -1116,6 +1137,7 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FollowLane<NMAX>& 
       L.arrival = s_orig[k];
       L.accept(from, s_index[k]);
       st_msgs++;
+      if (KMAX >= 3) st_app++;
       j++;
     }
   }
@@ -1154,7 +1176,7 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FollowLane<NMAX>& 
     if (stored) at32(a.commit0, g) = commit0;
   }
   vals[ST_MSGS] = st_msgs;
-  vals[ST_APPRESP] = lead ? st_msgs : 0u;  // every leader message here is a MsgAppResp
+  vals[ST_APPRESP] = KMAX >= 3 ? st_app : (lead ? st_msgs : 0u);  // (two slots: every leader message is a MsgAppResp)
   vals[ST_VOTERESP] = 0;
   vals[ST_DROPPED] = st_drop;
   vals[ST_COMMITS] = (uint32_t)(!flagged && L.committed != commit0);  // commitTo only raises
@@ -1185,9 +1207,8 @@ __device__ __forceinline__ void fast_close(const ApplyArgs& a, uint32_t part, co
     a.el_list[(size_t)xs * a.NB + atomicAdd(&a.el_cnt[xs * CTR_STRIDE], 1u)] = part;
 }
 
-template <int NMAX, bool X>
+template <int NMAX, bool X, uint32_t KMAX>  // KMAX: one MsgAppResp per follower per batch (+ a MsgProp)
 __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 ? HB_FAST5_WAVES : HB_FAST7_WAVES))) k_apply_fast(ApplyArgs a) {
-  constexpr uint32_t KMAX = NMAX - 1;  // one MsgAppResp per follower per batch
   __shared__ uint32_t l_fill, l_pfill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint32_t l_eflag[FLAG_WORDS];
@@ -1258,7 +1279,7 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 
     s_c[k] = (uint64_t)x.z | ((uint64_t)x.w << 32);
   }
   uint32_t vals[ST_N + 1];
-  (void)fast_step<NMAX>(a, L, part, tid, live, lead, leader, fol, prop_raw, cnt, s_info, s_orig, s_term, s_index, s_h, s_c,
+  (void)fast_step<NMAX, KMAX>(a, L, part, tid, live, lead, leader, fol, prop_raw, cnt, s_info, s_orig, s_term, s_index, s_h, s_c,
                         a.ev_off[2 * part + 1], &l_pfill, &l_fill, l_flag, l_eflag, vals);
   reduce_stats(a, l_stats, vals);
   if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
@@ -1346,7 +1367,7 @@ __device__ __forceinline__ bool apply_part(const ApplyArgs& a, uint32_t part, Ge
 
   constexpr uint32_t KS = route_kmax(NMAX);
   const uint32_t cnt = flagged ? a.cnt[g] : 0u;
-  const bool by_slot = flagged && cnt <= KS;
+  const bool by_slot = flagged && cnt <= a.kmax;  // (a.kmax <= KS: the step's slot count)
   const bool by_walk = flagged && !by_slot;
   __syncthreads();  // l_fill
   // one message through the lane; false: handed on (k_apply only)
@@ -2737,8 +2758,13 @@ void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
   const uint32_t grid = apply_grid(h);
   if (ev) (void)hipEventRecord(ev[2], h->stream);
   if constexpr (NMAX >= 5) hipLaunchKernelGGL(k_apply_lead<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
-  else if (a.slotx) hipLaunchKernelGGL((k_apply_fast<NMAX, true>), dim3(grid), dim3(PART), 0, h->stream, a);
-  else hipLaunchKernelGGL((k_apply_fast<NMAX, false>), dim3(grid), dim3(PART), 0, h->stream, a);
+  else if (a.kmax == 3) {
+    if (a.slotx) hipLaunchKernelGGL((k_apply_fast<NMAX, true, 3>), dim3(grid), dim3(PART), 0, h->stream, a);
+    else hipLaunchKernelGGL((k_apply_fast<NMAX, false, 3>), dim3(grid), dim3(PART), 0, h->stream, a);
+  } else {
+    if (a.slotx) hipLaunchKernelGGL((k_apply_fast<NMAX, true, 2>), dim3(grid), dim3(PART), 0, h->stream, a);
+    else hipLaunchKernelGGL((k_apply_fast<NMAX, false, 2>), dim3(grid), dim3(PART), 0, h->stream, a);
+  }
   if (ev) (void)hipEventRecord(ev[3], h->stream);
   if constexpr (NMAX >= 5) {  // the general kernel spills at n >= 5: elections go first
     if (!sz_on(h->max_msg_size))
@@ -3601,14 +3627,17 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.pflag = h->pflag;
   aa.resume = h->resume;
   aa.commit0 = h->commit0;
-  aa.kmax = route_kmax(h->nmax);
+  aa.kmax = step_kmax(h->nmax, flags);
   aa.cnt = ps.cnt;
   aa.slot = ps.slot;
   aa.side = ps.side;
   aa.recx = ps.recx;
   aa.slotx = xmode ? ps.slotx : nullptr;
   switch (h->nmax) {
-    case 3: launch_route<route_kmax(3)>(h, aa, ps_st); break;
+    case 3:
+      if (aa.kmax == 3) launch_route<3>(h, aa, ps_st);
+      else launch_route<2>(h, aa, ps_st);
+      break;
     case 5: launch_route<route_kmax(5)>(h, aa, ps_st); break;
     default: launch_route<route_kmax(7)>(h, aa, ps_st); break;
   }

@@ -358,7 +358,8 @@ struct FastLane {
   // ---- MsgProp with k entries on a leader (prop_ok)
   __device__ __forceinline__ void prop(uint32_t k) {
     const uint64_t old = last;
-    if (sz_on(S.max_msg_size)) sz_append(S, g, old, k, term, S.edesc + S.peoff[g]);  // dense proposal entries
+    if (sz_on(S.max_msg_size))  // the entries' descriptors: the dense proposal's, or the MsgProp message's
+      sz_append(S, g, old, k, term, S.edesc + (arrival == 0xFFFFFFFFu ? S.peoff[g] : S.eoff[arrival]));
     last += k;
     if (tfirst == HB_NO_INDEX) {
       tfirst = old + 1;

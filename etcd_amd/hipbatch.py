@@ -226,10 +226,11 @@ class Engine:
 
     # ---- hot path --------------------------------------------------------------
     def step(self, group, info, term, index, hint=None, props=None, host=None, profile=False, edesc=None,
-             eoff=None, peoff=None, commit=None, eterm=None):
+             eoff=None, peoff=None, commit=None, eterm=None, msg_props=False):
         """Step one batch.  Arrays are numpy (host) or torch tensors (host or cuda).
         profile: False, True (every phase) or "apply" (only HB_PHASE_APPLY).
-        edesc / eoff / peoff: entry descriptors (finite max_msg_size, include/hipbatch.h)."""
+        edesc / eoff / peoff: entry descriptors (finite max_msg_size, include/hipbatch.h).
+        msg_props: the batch carries MsgProp messages (HB_STEP_MSG_PROPS)."""
         b = abi.hb_batch()
         b.n = len(group)
         b.group, b.info, b.term, b.index = _ptr(group), _ptr(info), _ptr(term), _ptr(index)
@@ -240,7 +241,7 @@ class Engine:
         if host is None:
             host = not (hasattr(group, "is_cuda") and group.is_cuda)
         prof = {True: abi.HB_STEP_PROFILE, "apply": abi.HB_STEP_PROFILE_APPLY}.get(profile, 0)
-        flags = (abi.HB_STEP_HOST_PTRS if host else 0) | prof
+        flags = (abi.HB_STEP_HOST_PTRS if host else 0) | prof | (abi.HB_STEP_MSG_PROPS if msg_props else 0)
         self._keep = (group, info, term, index, hint, props, edesc, eoff, peoff, commit, eterm)
         _check("hb_step", lib().hb_step(self.h, C.byref(b), flags))
 
@@ -284,7 +285,8 @@ class Engine:
     def step_batch(self, batch, **kw):
         return self.step(batch["group"], batch["info"], batch["term"], batch["index"],
                          batch.get("hint"), batch.get("props"), edesc=batch.get("edesc"), eoff=batch.get("eoff"),
-                         peoff=batch.get("peoff"), commit=batch.get("commit"), eterm=batch.get("eterm"), **kw)
+                         peoff=batch.get("peoff"), commit=batch.get("commit"), eterm=batch.get("eterm"),
+                         msg_props=bool(batch.get("msg_props", False)), **kw)
 
     def events(self):
         """Dense events of the last step (host copy, synchronizes)."""

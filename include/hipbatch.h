@@ -156,6 +156,9 @@ typedef struct hb_batch {
                                     with one copy, so the arrays may be reused once hb_step returns) */
 #define HB_STEP_PROFILE   0x2u   /* record per-phase HIP events (hb_phase_ms)   */
 #define HB_STEP_PROFILE_APPLY 0x4u  /* only the HB_PHASE_APPLY events (two, on the apply stream) */
+#define HB_STEP_MSG_PROPS 0x8u   /* the batch carries MsgProp messages (no dense props): groups of
+                                    3 keep a third route slot, so a leader's two MsgAppResp and its
+                                    proposal stay on the fast path (a hint: results are the same) */
 
 /* ---- per-group state (host view, array-of-structures) --------------------
  * Device keeps this as SoA.  Field meanings follow the reference:

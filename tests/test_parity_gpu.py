@@ -317,6 +317,55 @@ def test_cfg2_finite_max_msg_size():
         assert st[abi.HB_STAT_FAULTS] == 0
 
 
+def _multinode_leader_batch(g, rng, last, ents):
+    """A MultiNode leader-side cycle at n = 3: both followers ack the last
+    index, then the application proposes (a MsgProp message of `ents[g]`
+    entries, Term 0); all groups' messages interleaved in one random arrival
+    order, each group's own in that order (ack, ack, proposal)."""
+    G = len(g)
+    grp = np.repeat(np.arange(G), 3)[rng.permutation(3 * G)].astype(np.uint32)
+    kind = np.zeros(3 * G, np.int64)  # the group's 0th, 1st, 2nd message in arrival order
+    seen = np.zeros(G, np.int64)
+    for i, x in enumerate(grp):
+        kind[i] = seen[x]
+        seen[x] += 1
+    t = np.where(kind == 2, abi.HB_MSG_PROP, abi.HB_MSG_APP_RESP).astype(np.uint32)
+    slot = np.where(kind == 2, 0, kind + 1).astype(np.uint32)
+    info = (t | (slot << np.uint32(4))).astype(np.uint32)
+    term = np.where(kind == 2, 0, g["term"][grp].astype(np.int64)).astype(np.uint64)
+    index = np.where(kind == 2, ents[grp], last[grp]).astype(np.uint64)
+    return dict(group=grp, info=info, term=term, index=index, hint=None, props=None, msg_props=True)
+
+
+@pytest.mark.parametrize("sized", [False, True])
+def test_msgprop_messages_on_fast_lane(sized):
+    """HB_STEP_MSG_PROPS (n = 3, a third route slot): a leader's two acks and
+    the application's MsgProp of 1-3 entries, as a MultiNode cycle sends them,
+    stay on the fast lane (stepLeader MsgProp -> appendEntry -> maybeCommit ->
+    bcastAppend, raft/raft.go:500-513), with a finite MaxSizePerMsg taking the
+    message's entry descriptors; then the same groups under fuzzed traffic of
+    every type with the flag set."""
+    G, n = 3000, 3
+    g, runs = synth.steady_groups(G, n, seed=141, last_hi=1 << 12)
+    kw = dict(max_msg_size=256, sizes=synth.window_sizes(g, runs, seed=142, frac_full=1.0)) if sized else {}
+    pair = Pair(g, runs, n, 256, max_batch=4 * G, **kw)
+    rng = np.random.default_rng(143)
+    last = g["last_index"].astype(np.int64).copy()
+    for step in range(3):
+        ents = rng.integers(1, 4, G).astype(np.int64)
+        b = _multinode_leader_batch(g, rng, last, ents)
+        if sized:
+            b = synth.attach_entry_descs(b, G, seed=144 + step, max_len=300)
+        _, st, now = pair.step(b, ctx=f"msgprop fast lane step {step}")
+        assert st[abi.HB_STAT_FAULTS] == 0 and st[abi.HB_STAT_ENTRIES] == int(ents.sum())
+        last = last + ents
+    b = synth.random_batch(now, 6000, seed=145, props=False)
+    b["msg_props"] = True
+    if sized:
+        b = synth.attach_entry_descs(b, G, seed=146)
+    pair.step(b, ctx="msgprop fuzz")
+
+
 # ---------------------------------------------------------------- follower side (SURVEY.md 8(f) rank 4)
 @pytest.mark.parametrize("seed,nmax,W", [(71, 3, 8), (72, 5, 16), (73, 7, 8), (74, 3, 256)])
 def test_fuzz_follower_side(seed, nmax, W):

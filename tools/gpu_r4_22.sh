@@ -1,0 +1,10 @@
+#!/bin/bash
+# runtime slot count (HB_STEP_MSG_PROPS): the suite, the MultiNode lines, then cfg2 / cfg5 / follow A/B
+# against the two-slot engine (k2) — the headline paths do not set the flag
+cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out/r4
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
+  > gpurun_out/r4/gpu_tests.log 2>&1 || { tail -60 gpurun_out/r4/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/r4/gpu_tests.log
+SKIP_TESTS=1 bash tools/gpu_r4_mn.sh || exit 1
+bash tools/ab.sh "cfg2 cfg5 follow" k2 full || exit 1
+bash tools/ab.sh "cfg2" k2 full || exit 1
