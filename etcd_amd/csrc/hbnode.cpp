@@ -1249,9 +1249,8 @@ void on_event(hbn_node* n, Group& g, const hb_event& e, Lists& L) {
         ents.resize(1);  // becomeLeader's pb.Entry{Data: nil}
       } else {
         if (g.props.empty()) panicf("device appended entries without a pending proposal");
-        Msg m = std::move(g.props.front());
+        ents = std::move(g.props.front().entries);
         g.props.pop_front();
-        ents = std::move(m.entries);
         for (Ent& x : ents) {  // stepLeader MsgProp (raft/raft.go:500-513)
           if (x.type == HBN_ENTRY_CONF_CHANGE) {
             if (g.pending_conf) x = Ent{};
@@ -1395,15 +1394,16 @@ void consume_events(hbn_node* n) {
         }
         Lists& L = n->lists[t];
         const uint64_t* W = n->w_words;
+        const bool ahead = total >= 65536;  // (a small node's groups sit in cache already)
         for (uint32_t p = p0; p < p1; ++p) {
           for (uint64_t i = n->w_off[2 * p], end = n->w_off[2 * p + 2]; i < end; ++i) {
-            if (i + 16 < end) {  // the group of a word ahead: its hot lines (flags .. log head)
+            if (ahead && i + 16 < end) {  // the group of a word ahead: its hot lines (flags .. log head)
               const uint32_t ps = p * n->chunk_groups + ((uint32_t)(W[i + 16] >> 16) & 0xFF);
               if (ps < n->by_slot.size())
                 if (const char* q = reinterpret_cast<const char*>(n->by_slot[ps]))
                   for (int l = 0; l < 5; ++l) __builtin_prefetch(q + 64 * l);
             }
-            if (i + 8 < end) {  // ... and, nearer, the buffers it points to
+            if (ahead && i + 8 < end) {  // ... and, nearer, the buffers it points to
               const uint32_t ps = p * n->chunk_groups + ((uint32_t)(W[i + 8] >> 16) & 0xFF);
               if (ps < n->by_slot.size())
                 if (const Group* q = n->by_slot[ps]) {
@@ -2915,12 +2915,13 @@ int hbn_ready(hbn_node* n, const hbn_group_ready** out, uint64_t* count) {
           size_t lo, hi;
           split(nt, k, t, &lo, &hi);
           Arena& A = n->arenas[t];
+          const bool ahead = nt >= 65536;  // (a small node's groups sit in cache already)
           for (size_t i = lo; i < hi; ++i) {
-            if (i + 4 < hi) {  // the group 4 ahead, then what the group 2 ahead points to
+            if (ahead && i + 4 < hi) {  // the group 4 ahead, then what the group 2 ahead points to
               const char* q = reinterpret_cast<const char*>(n->touched[i + 4]);
               for (int l = 0; l < 9; ++l) __builtin_prefetch(q + 64 * l);
             }
-            if (i + 2 < hi) {
+            if (ahead && i + 2 < hi) {
               const Group& q = *n->touched[i + 2];
               __builtin_prefetch(q.msgs.data());
               __builtin_prefetch(q.log.unstable.data());
