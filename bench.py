@@ -1057,11 +1057,14 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     elif args.workload == "tick":
         metric, unit, val = "group ticks/sec (MultiNode.Tick over 1M groups x 3)", "group-ticks/s", \
             world * G * args.steps / sec
-        # per group: meta 8 + tcfg 4 + elapsed 4 R + 4 W; a due MsgBeat / MsgHup steps the
-        # group (state ~100 B, SURVEY.md 8(d) per-group figures) and its events (8 B words)
-        alg = (G * 20 * args.steps + int(st[abi.HB_STAT_MSGS]) * 100 + int(st[abi.HB_STAT_EVENTS]) * 8) / world
-        alg_note = ("per tick: 20 B per group (meta, tcfg, elapsed r/w) + 100 B per stepped MsgBeat / MsgHup "
-                    "+ 8 B per event word")
+        # per group: meta 8 + tcfg 4 + elapsed 4 R + 4 W; a leader's MsgBeat reads committed and
+        # each peer's Match and pm (8 + 12 B per peer: bcastHeartbeat); a MsgHup steps the whole
+        # group (state ~100 B, SURVEY.md 8(d) per-group figures); events are 8 B words
+        beats = world * (G // 2 + G % 2) * args.steps  # every leader beats on every tick (HeartbeatTick 1)
+        hups = max(int(st[abi.HB_STAT_MSGS]) - beats, 0)
+        alg = (G * 20 * args.steps + beats * (8 + 12 * (n - 1)) + hups * 100 + int(st[abi.HB_STAT_EVENTS]) * 8) / world
+        alg_note = ("per tick: 20 B per group (meta, tcfg, elapsed r/w) + 8 + 12 B per peer per MsgBeat "
+                    "(committed, Match, pm) + 100 B per MsgHup + 8 B per event word")
         extra = {"msgs_stepped_per_s": int(st[abi.HB_STAT_MSGS]) / sec, "events_per_s": int(st[abi.HB_STAT_EVENTS]) / sec,
                  "campaigns": int(st[abi.HB_STAT_MSGS]) - world * (G // 2 + G % 2) * args.steps}
         ok = int(st[abi.HB_STAT_FAULTS]) == 0

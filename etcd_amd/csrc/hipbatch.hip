@@ -626,27 +626,6 @@ static_assert(route_kmax(3) <= 8 && route_kmax(5) <= 8 && route_kmax(7) <= 8,
 // stats slots reduced per workgroup
 enum { ST_MSGS, ST_APPRESP, ST_VOTERESP, ST_DROPPED, ST_COMMITS, ST_WON, ST_LOST, ST_FAULTS, ST_ENTRIES, ST_N };
 
-// Diagnostic build only (-DHB_X_STAMPS): per-workgroup phase timestamps of
-// k_apply_fast (tid 0, s_memtime cycles + s_memrealtime at start/end).
-#ifdef HB_X_STAMPS
-__device__ uint64_t g_stamps[1 << 20];
-#define XSTAMP(k)                                                                          \
-  do {                                                                                     \
-    if (threadIdx.x == 0) g_stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#define XSTAMP_RT(k)                                                                       \
-  do {                                                                                     \
-    if (threadIdx.x == 0) g_stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define XSTAMP(k) \
-  do {            \
-  } while (0)
-#define XSTAMP_RT(k) \
-  do {               \
-  } while (0)
-#endif
-
 #ifndef HB_FAST_WAVES
 #define HB_FAST_WAVES 4
 #endif
@@ -1924,8 +1903,9 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_follow(ApplyArgs a) {
 // k_tick: one MultiNode.Tick (raft/multinode.go:264-275) — every live group
 // runs tickHeartbeat (leader) or tickElection (raft/raft.go:362-382), the
 // draw of isElectionTimeout (:765-771) read from the node's r.rand stream at
-// the group's own position; a due MsgBeat / MsgHup is stepped at once by the
-// general state machine.  Events go to the partition's P chunk (at most one
+// the group's own position; a leader's due MsgBeat sends its heartbeats from
+// Match / pm alone, a due MsgHup is stepped at once by the general state
+// machine.  Events go to the partition's P chunk (at most one
 // step per group, so the chunk's ev_per_msg x PART words bound them).
 // ---------------------------------------------------------------------------
 template <int NMAX>
@@ -1988,7 +1968,30 @@ __global__ void __launch_bounds__(PART, 2) k_tick(ApplyArgs a) {
     a.S.elapsed[g] = el;
   }
   uint64_t last0 = 0, commit0 = 0;
-  if (type != 0xFF) {
+  if (type == HB_MSG_BEAT && !(L.meta & M_RS)) {
+    // stepLeader MsgBeat -> bcastHeartbeat (raft/raft.go:495-498, :290-300):
+    // a MsgHeartbeat to every peer in slot order at min(Match, committed), each
+    // Progress resumed.  Only those fields are read and only a cleared pause bit
+    // is written (Lane::step would load the whole group, ring heads included,
+    // and write every peer's Progress back unchanged).  The self slot, whose
+    // arrays may be stale under M_SM, is skipped.
+    const uint64_t committed = a.S.commit[g];
+    const uint32_t nn = L.n(), sf = L.self();
+    uint64_t mt[NMAX];
+    uint32_t pmv[NMAX];
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) {
+      const bool on = (uint32_t)s < nn && (uint32_t)s != sf;
+      mt[s] = on ? a.S.match[(size_t)s * a.S.G + g] : 0ull;
+      pmv[s] = on ? a.S.pm[(size_t)s * a.S.G + g] : 0u;
+    }
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) {
+      if ((uint32_t)s >= nn || (uint32_t)s == sf) continue;
+      L.ev(HB_EV_HEARTBEAT, s, 0, umin64(mt[s], committed));
+      if (pmv[s] & PM_PAUSED) a.S.pm[(size_t)s * a.S.G + g] = pmv[s] & ~PM_PAUSED;
+    }
+  } else if (type != 0xFF) {  // MsgHup (or a reset-form leader's MsgBeat): the general state machine
     L.load_all();
     last0 = L.last;
     commit0 = L.committed;
@@ -3844,12 +3847,6 @@ int hb_alloc_pinned(size_t bytes, void** out) {
   if (!out) return HB_EINVAL;
   return hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? HB_OK : HB_ENOMEM;
 }
-
-#ifdef HB_X_STAMPS
-int hb_x_stamps(uint64_t* out, uint32_t n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)n * 8) == hipSuccess ? HB_OK : HB_EDEVICE;
-}
-#endif
 
 int hb_free_pinned(void* p) { return hipHostFree(p) == hipSuccess ? HB_OK : HB_EDEVICE; }
 

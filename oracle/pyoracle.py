@@ -682,6 +682,23 @@ class ShardedOracleGroups:
         res = self._map(run)
         return np.concatenate([r[0] for r in res]), sum((r[1] for r in res), drop_stats)
 
+    def tick(self, draws, ev_cap=None):
+        """One MultiNode.Tick over every shard (each group reads the shared
+        r.rand stream at its own position, so the shards are independent)."""
+        def run(i, og):
+            ev, st = og.tick(draws)
+            ev["group"] += np.uint32(self.bounds[i][0])
+            return ev, st
+        res = self._map(run)
+        return np.concatenate([r[0] for r in res]), sum((r[1] for r in res), np.zeros(abi.HB_STAT_COUNT, np.uint64))
+
+    def load_timers(self, timers):
+        for (lo, hi), og in zip(self.bounds, self.parts):
+            og.load_timers(timers[lo:hi])
+
+    def timers(self):
+        return np.concatenate(self._map(lambda i, og: og.timers()))
+
     def groups(self):
         return np.concatenate(self._map(lambda i, og: og.groups()))
 

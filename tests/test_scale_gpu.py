@@ -43,6 +43,28 @@ def test_cfg5_shard_8m_groups():
 
 
 @pytest.mark.timeout(900)
+def test_tick_line_at_1m_groups():
+    """The tick line's workload at full size: 1,048,576 groups x 3, half leading
+    (HeartbeatTick 1: a MsgBeat every tick, k_tick's heartbeat path) and half
+    following with ElectionTick 10 (draws; MsgHup campaigns through the general
+    state machine), four ticks against the sharded oracle."""
+    G = 1 << 20
+    g, runs = synth.steady_groups(G, 3, seed=81, with_runs="flat")
+    g["state"][1::2] = abi.HB_STATE_FOLLOWER
+    g["lead"][1::2] = 1
+    pair = Pair(g, runs, 3, 8, max_batch=16, oracle_shards=16)
+    t = synth.random_timers(G, seed=82, et_hi=10, ht_hi=1, pos_hi=0)
+    t["election_tick"] = 10
+    pair.set_timers(t, np.random.default_rng(83).integers(0, 1 << 63, 64, dtype=np.uint64))
+    camp = 0
+    for k in range(4):
+        _, st, _ = pair.tick(ctx=f"tick 1M {k}")
+        assert st[abi.HB_STAT_FAULTS] == 0
+        camp += int(st[abi.HB_STAT_MSGS]) - G // 2
+    assert camp > 0  # some followers campaigned
+
+
+@pytest.mark.timeout(900)
 def test_cfg4_storm_over_1m_groups():
     """The bench's repeatable cfg4 storm at 1.1M groups x 7 (W = 8): step-down,
     MsgHup and 6 MsgVoteResp per group through the two-pass partition,

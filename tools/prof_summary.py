@@ -104,7 +104,7 @@ def main():
               "k_follow", "k_finish", "k_tick")
     steps = sum(s["calls"] for k, s in ks.items() if k.startswith("k_route"))
     if not steps:  # a Tick line (hb_tick: k_tick + k_finish per tick)
-        steps = sum(s["calls"] for k, s in ks.items() if k.startswith("k_tick"))
+        steps = sum(s["calls"] for k, s in ks.items() if k.startswith("k_tick<"))
     if steps:
         tb = us = 0.0
         missing = []
