@@ -8,7 +8,7 @@ import ctypes as C
 
 import numpy as np
 
-HB_ABI_VERSION = 4
+HB_ABI_VERSION = 5
 
 HB_OK = 0
 HB_EINVAL = -1
@@ -183,6 +183,8 @@ class hb_group(C.Structure):
         ("votes_resp", C.c_uint32),
         ("votes_grant", C.c_uint32),
         ("fault", C.c_uint32),
+        ("commit_zero", C.c_uint32),
+        ("pad", C.c_uint32),
         ("pr", hb_progress * HB_MAX_REPLICAS),
     ]
 
@@ -234,7 +236,7 @@ GROUP_DTYPE = np.dtype([
     ("term", "<u8"), ("committed", "<u8"), ("first_index", "<u8"), ("last_index", "<u8"),
     ("term_first", "<u8"), ("term_last", "<u8"), ("snap_index", "<u8"),
     ("state", "<u4"), ("n", "<u4"), ("self_slot", "<u4"), ("lead", "<u4"), ("vote", "<u4"),
-    ("votes_resp", "<u4"), ("votes_grant", "<u4"), ("fault", "<u4"),
+    ("votes_resp", "<u4"), ("votes_grant", "<u4"), ("fault", "<u4"), ("commit_zero", "<u4"), ("pad", "<u4"),
     ("pr", PROGRESS_DTYPE, (HB_MAX_REPLICAS,)),
 ])
 TIMER_DTYPE = np.dtype([("elapsed", "<u4"), ("rand_pos", "<u4"), ("election_tick", "<u2"),

@@ -1097,6 +1097,9 @@ hb_group make_record(const hbn_node* n, const Group& g, const std::vector<hb_pro
   r.self_slot = ss >= 0 ? (uint32_t)ss : HB_SLOT_NONE;
   r.lead = ref_of(g, n->id, g.lead);
   r.vote = ref_of(g, n->id, g.vote);
+  // r.Commit (HardState.Commit) is committed, or 0 until the first Step of a
+  // group created with an empty HardState (raft/raft.go:466,488,759)
+  r.commit_zero = (g.hs_commit == 0 && g.log.committed != 0) ? 1u : 0u;
   for (size_t s = 0; s < prs.size(); ++s) r.pr[s] = prs[s];
   return r;
 }

@@ -1038,7 +1038,7 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FollowLane<NMAX>& 
   L.E.fill = l_pfill;
   const uint32_t prop_k = live ? prop_raw : 0u;
   if (prop_k) {
-    if (L.prop_ok(prop_k)) {
+    if (lead && L.prop_ok(prop_k)) {
       L.arrival = 0xFFFFFFFFu;
       L.prop(prop_k);
     } else {
@@ -1124,7 +1124,7 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FollowLane<NMAX>& 
   if (fol) {
 #pragma unroll
     for (uint32_t k = 0; k < KMAX; ++k) {
-      if (k >= cnt || flagged) break;
+      if (k >= cnt || flagged || L.faulted()) break;
       const uint32_t inf = s_info[k];
       const uint32_t from = (inf >> 4) & 0xF;
       if (!L.takes_follow(inf, from, s_term[k], s_index[k], s_h[k], s_c[k])) {
@@ -1218,14 +1218,17 @@ __global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 
   // k_apply whole, without loading its state here (resume bit 30: commit0 =
   // its committed as k_apply loads it).
   const bool leader = live && L.state() == HB_STATE_LEADER;
+  // a group that has not stepped since an empty HardState (r.Commit = 0, M_NC)
+  // is the general lane's: its first Step sets r.Commit
+  const bool nc = (L.mlo & (uint32_t)M_NC) != 0;
   // a leader the fast path cannot finish (more messages than slots) and
   // without a dense proposal is handed over whole, its state unloaded (cfg4:
   // every group; k_elect / k_apply load it); n >= 5 reads its Term for
   // k_elect's step-down test
-  const bool lead = leader && (cnt <= KMAX || prop_raw != 0);
+  const bool lead = leader && !nc && (cnt <= KMAX || prop_raw != 0);
   // X mode: a follower whose messages all sit in its slots and that has no
   // dense proposal (stepFollower MsgProp forwards it: the general lane)
-  const bool fol = X && live && L.state() == HB_STATE_FOLLOWER && cnt > 0 && cnt <= KMAX && prop_raw == 0;
+  const bool fol = X && live && !nc && L.state() == HB_STATE_FOLLOWER && cnt > 0 && cnt <= KMAX && prop_raw == 0;
   L.dirty = 0;
   L.nev = 0;
   if (lead) {
@@ -1619,7 +1622,7 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
     const uint32_t cnt = flagged ? a.cnt[g] : 0u;
     const uint32_t resume = flagged ? a.resume[g] : 0u;
     // (flagged groups are live and not faulted; a pending dense proposal goes to k_apply)
-    const bool mine = flagged && cnt <= KS && (resume >> 31) == 0 && L.self() < L.n();
+    const bool mine = flagged && cnt <= KS && (resume >> 31) == 0 && L.self() < L.n() && !(L.meta & M_NC);
     uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0;
     bool done = false;
     uint64_t last0 = 0, commit0 = 0;
@@ -1744,15 +1747,17 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   const bool live = gvalid && L.n() != 0 && L.faulted() == 0;
   const bool leader = live && L.state() == HB_STATE_LEADER;
   const bool fits = cnt <= KS;  // every message of the group is in its slots
+  // r.Commit = 0 (M_NC): the general lane steps the group's first message
+  const bool nc = (L.mlo & (uint32_t)M_NC) != 0;
   // a leader with a proposal or at most one message per follower loads at once
-  const bool spec = leader && (prop_raw != 0 || (fits && cnt <= (uint32_t)NMAX - 1));
+  const bool spec = leader && !nc && (prop_raw != 0 || (fits && cnt <= (uint32_t)NMAX - 1));
   L.dirty = 0;
   L.nev = 0;
   // (loading the state beside meta, as k_apply_fast does, measured neutral
   // on cfg3 and +4.5 % on cfg4, whose lanes are mostly not leaders)
   L.last = L.committed = 0;
   L.term = 0;
-  const bool slots = leader && fits;
+  const bool slots = leader && !nc && fits;
 #pragma unroll
   for (uint32_t k = 0; k < KS; ++k)
     if (slots && k < cnt) l_slot[k][tid] = at32(a.slot, k * a.S.G + g);
@@ -1968,7 +1973,7 @@ __global__ void __launch_bounds__(PART, 2) k_tick(ApplyArgs a) {
     a.S.elapsed[g] = el;
   }
   uint64_t last0 = 0, commit0 = 0;
-  if (type == HB_MSG_BEAT && !(L.meta & M_RS)) {
+  if (type == HB_MSG_BEAT && !(L.meta & (M_RS | M_NC))) {
     // stepLeader MsgBeat -> bcastHeartbeat (raft/raft.go:495-498, :290-300):
     // a MsgHeartbeat to every peer in slot order at min(Match, committed), each
     // Progress resumed.  Only those fields are read and only a cleared pause bit
@@ -1991,7 +1996,7 @@ __global__ void __launch_bounds__(PART, 2) k_tick(ApplyArgs a) {
       L.ev(HB_EV_HEARTBEAT, s, 0, umin64(mt[s], committed));
       if (pmv[s] & PM_PAUSED) a.S.pm[(size_t)s * a.S.G + g] = pmv[s] & ~PM_PAUSED;
     }
-  } else if (type != 0xFF) {  // MsgHup (or a reset-form leader's MsgBeat): the general state machine
+  } else if (type != 0xFF) {  // MsgHup (or the MsgBeat of a reset-form / M_NC leader): the general state machine
     L.load_all();
     last0 = L.last;
     commit0 = L.committed;
@@ -2220,6 +2225,7 @@ __global__ void k_load(DevState S, uint32_t first, uint32_t count, const hb_grou
   if (r.term_last == r.last_index) m |= M_TL;
   if (r.self_slot < r.n && r.pr[r.self_slot].match == r.last_index && r.pr[r.self_slot].next == r.last_index + 1)
     m |= M_SM;
+  if (r.commit_zero && r.committed != 0) m |= M_NC;  // r.Commit = 0 until the group's first Step
   S.meta[g] = m;
   S.elapsed[g] = 0;  // newRaft: fresh r.rand, becomeFollower -> reset
   S.rpos[g] = 0;
@@ -2260,6 +2266,7 @@ __global__ void k_gather(DevState S, uint32_t first, uint32_t count, hb_group* d
   r.fault = m_fault(m);
   r.votes_resp = m_resp(m);
   r.votes_grant = m_grant(m);
+  r.commit_zero = (m & M_NC) ? 1u : 0u;
   for (uint32_t s = 0; s < S.nmax && s < r.n; ++s) {
     const size_t o = (size_t)s * S.G + g;
     uint32_t p = S.pm[o];

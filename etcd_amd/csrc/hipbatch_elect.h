@@ -54,8 +54,8 @@ struct ElectLane {
   __device__ __forceinline__ void set_lead(uint32_t v) { set_field(9, 0xF, v); }
   __device__ __forceinline__ void set_vote(uint32_t v) { set_field(13, 0xF, v); }
   __device__ __forceinline__ void set_votes(uint32_t resp, uint32_t grant) {
-    set_field(24, 0xFF, resp);
-    set_field(32, 0xFF, grant);
+    set_field(M_RESP_SHIFT, 0xFF, resp);
+    set_field(M_GRANT_SHIFT, 0xFF, grant);
   }
   __device__ __forceinline__ void ev(uint32_t type, uint32_t to, uint32_t aux, uint64_t x) {
     emit_ev(E, g & (PART - 1), type, to, aux, x);

@@ -8,14 +8,15 @@
 // follower-side case; FollowLane is its specialization for the common one, run
 // by k_apply_fast in the same pass and the same registers as the leader lane:
 //
-//   * a follower (not M_RS) receiving, at its own Term, from a member:
+//   * a follower (not M_RS, not M_NC) receiving, at its own Term, from a member:
 //   * MsgHeartbeat with m.Commit <= lastIndex
 //       r.elapsed = 0, r.lead = m.From, commitTo(m.Commit), MsgHeartbeatResp
 //   * MsgApp whose Index is below committed (MsgAppResp{Index: committed}),
 //     whose (Index, LogTerm) does not match the log (a reject, RejectHint
 //     read by the host from its log), or that appends at the log's end
 //     (Index == lastIndex, matching) entries that all carry m.Term (REC_UNI,
-//     counted by the partition's first pass) with no size ring to extend:
+//     counted by the partition's first pass) with no size ring to extend, and
+//     whose commitTo(min(m.Commit, lastnewi)) stays within the log:
 //       maybeAppend without a conflict scan, commitTo(min(m.Commit, lastnewi)),
 //       MsgAppResp{Index: lastnewi}
 //   * any message below its Term (dropped by the Step gate, raft/raft.go:480)
@@ -86,7 +87,11 @@ struct FollowLane : FastLane<NMAX> {
     if (t != lterm) return true;  // the reject
     // no entries: nothing to scan or append; entries: appended at the log's end
     const uint64_t ne = rec_ne(info);
-    return (info & REC_UNI) && (ne == 0 || (index == last && !sz_on(S.max_msg_size)));
+    if (!(info & REC_UNI) || !(ne == 0 || (index == last && !sz_on(S.max_msg_size)))) return false;
+    // commitTo(min(m.Commit, lastnewi)) within the log: an empty MsgApp past the
+    // log's end matches LogTerm 0 (raftLog.term is 0 there) and can commit past
+    // lastIndex, the reference's panic (raft/log.go:175-176) — the general lane's
+    return ne != 0 || umin64(mcommit, index) <= last;
   }
   __device__ __forceinline__ void set_lead(uint32_t from) {
     if (lead() == from) return;
@@ -94,9 +99,14 @@ struct FollowLane : FastLane<NMAX> {
     dirty |= D_META;
     B::ev(HB_EV_STATE, 0, 0, soft());
   }
-  // commitTo raft/log.go:172-180 (takes() keeps `to` within the log)
+  // commitTo raft/log.go:172-180 (takes() keeps `to` within the log; a
+  // screening gap still faults as the general lane does, not silently)
   __device__ __forceinline__ void commit_to(uint64_t to) {
     if (committed < to) {
+      if (last < to) {
+        B::fault(HB_FAULT_COMMIT_RANGE);
+        return;
+      }
       committed = to;
       dirty |= D_COMMIT;
       B::ev(HB_EV_COMMIT, 0, 0, to);
@@ -113,7 +123,8 @@ struct FollowLane : FastLane<NMAX> {
     set_lead(from);      // r.lead = m.From
     if (type == HB_MSG_HEARTBEAT) {  // handleHeartbeat :666-669
       commit_to(mcommit);
-      resp(from, HB_RESP_HEARTBEAT, 0);
+      if (B::faulted()) B::ev(HB_EV_FAULT, 0, B::faulted(), B::arrival_x());
+      else resp(from, HB_RESP_HEARTBEAT, 0);
       return;
     }
     // handleAppendEntries :651-665
@@ -140,7 +151,8 @@ struct FollowLane : FastLane<NMAX> {
       B::ev(HB_EV_FOLLOW, 0, HB_FOLLOW_APPEND, B::arrival_x());
     }
     commit_to(mcommit < lastnewi ? mcommit : lastnewi);
-    resp(from, HB_RESP_APP, lastnewi);
+    if (B::faulted()) B::ev(HB_EV_FAULT, 0, B::faulted(), B::arrival_x());
+    else resp(from, HB_RESP_APP, lastnewi);
   }
   __device__ __forceinline__ void store_follow() {
     // M_TL: the tlast array is kept only while tlast != last

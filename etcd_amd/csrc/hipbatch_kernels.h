@@ -31,18 +31,23 @@ constexpr uint32_t CHUNK = 4 * PART;         // messages staged in LDS per round
 
 // ---- packed group meta (u64) ------------------------------------------------
 //  [0:2) state  [2:5) n  [5:9) self slot  [9:13) lead ref  [13:17) vote ref
-//  [17:21) fault  [21] M_TL  [22] M_SM  [24:32) votes responded  [32:40) votes granted
+//  [17:21) fault  [21] M_TL  [22] M_SM  [23] M_RS  [24] M_NC
+//  [32:40) votes granted  [40:48) votes responded
+//  (the flags every lane tests sit in the low word, which the fast lanes load
+//  and store alone; the vote tally, read only by the election lanes, is above)
 //  M_TL: tlast == last — the tlast array is then not kept (a leader's current-
 //  term run always ends at its last entry).  M_SM: the self slot's Match ==
 //  last and Next == last + 1 — its match / next arrays are then not kept (a
 //  leader's own progress after every append).  The steady-state fast path
 //  neither reads nor writes those 48 bytes per group; every other reader
 //  materializes them from `last`.
+constexpr int M_GRANT_SHIFT = 32;
+constexpr int M_RESP_SHIFT = 40;
 __host__ __device__ inline uint64_t meta_make(uint32_t state, uint32_t n, uint32_t self, uint32_t lead,
                                               uint32_t vote, uint32_t fault, uint32_t resp, uint32_t grant) {
   return (uint64_t)(state & 3) | ((uint64_t)(n & 7) << 2) | ((uint64_t)(self & 0xF) << 5) |
          ((uint64_t)(lead & 0xF) << 9) | ((uint64_t)(vote & 0xF) << 13) | ((uint64_t)(fault & 0xF) << 17) |
-         ((uint64_t)(resp & 0xFF) << 24) | ((uint64_t)(grant & 0xFF) << 32);
+         ((uint64_t)(resp & 0xFF) << M_RESP_SHIFT) | ((uint64_t)(grant & 0xFF) << M_GRANT_SHIFT);
 }
 constexpr uint64_t M_TL = 1ull << 21;
 constexpr uint64_t M_SM = 1ull << 22;
@@ -55,14 +60,22 @@ constexpr uint64_t M_SM = 1ull << 22;
 // lastIndex loads its Progress first).  Readers materialize it (rs_progress),
 // writers of Progress clear it.
 constexpr uint64_t M_RS = 1ull << 23;
+// M_NC: r.Commit (HardState.Commit) is 0 while raftLog.committed is not — a
+// group created with an empty HardState that has not stepped a message yet
+// (hb_group.commit_zero).  The reference sets r.Commit = committed at the end
+// of every Step past the term gate (raft/raft.go:466,488), and only
+// handleAppendEntries reads it (`m.Index < r.Commit`, :652).  Only the general
+// lane (Lane::step) steps such a group: every specialised lane hands it over,
+// and Lane::step clears the flag once the message passes the gate.
+constexpr uint64_t M_NC = 1ull << 24;
 __host__ __device__ inline uint32_t m_state(uint64_t m) { return (uint32_t)(m & 3); }
 __host__ __device__ inline uint32_t m_n(uint64_t m) { return (uint32_t)((m >> 2) & 7); }
 __host__ __device__ inline uint32_t m_self(uint64_t m) { return (uint32_t)((m >> 5) & 0xF); }
 __host__ __device__ inline uint32_t m_lead(uint64_t m) { return (uint32_t)((m >> 9) & 0xF); }
 __host__ __device__ inline uint32_t m_vote(uint64_t m) { return (uint32_t)((m >> 13) & 0xF); }
 __host__ __device__ inline uint32_t m_fault(uint64_t m) { return (uint32_t)((m >> 17) & 0xF); }
-__host__ __device__ inline uint32_t m_resp(uint64_t m) { return (uint32_t)((m >> 24) & 0xFF); }
-__host__ __device__ inline uint32_t m_grant(uint64_t m) { return (uint32_t)((m >> 32) & 0xFF); }
+__host__ __device__ inline uint32_t m_resp(uint64_t m) { return (uint32_t)((m >> M_RESP_SHIFT) & 0xFF); }
+__host__ __device__ inline uint32_t m_grant(uint64_t m) { return (uint32_t)((m >> M_GRANT_SHIFT) & 0xFF); }
 
 // ---- packed progress meta (u32) ----------------------------------------------
 //  [0:2) ProgressState  [2] Paused  [3:13) inflights.start  [13:24) inflights.count
@@ -396,6 +409,7 @@ struct Lane {
   uint32_t won, lost;
   uint32_t nev;  // events emitted
   bool prog;     // match / next / pm / head hold the group's progress (loaded or reset)
+  bool rc_zero;  // r.Commit was 0 when the message being stepped arrived (M_NC)
   bool voted;    // the message's HB_INFO_VOTED bit (follower side)
 
   // ---------------------------------------------------------------- meta
@@ -417,8 +431,8 @@ struct Lane {
   __device__ __forceinline__ void set_lead(uint32_t v) { set_field(9, 0xF, v); }
   __device__ __forceinline__ void set_vote(uint32_t v) { set_field(13, 0xF, v); }
   __device__ __forceinline__ void set_votes(uint32_t resp, uint32_t grant) {
-    set_field(24, 0xFF, resp);
-    set_field(32, 0xFF, grant);
+    set_field(M_RESP_SHIFT, 0xFF, resp);
+    set_field(M_GRANT_SHIFT, 0xFF, grant);
   }
 
   __device__ __forceinline__ uint64_t arrival_x() const {
@@ -839,7 +853,8 @@ struct Lane {
       e0 = S.eoff[arrival];
       ne = (arrival + 1 < S.bn ? S.eoff[arrival + 1] : S.n_ent) - e0;
     }
-    if (index < committed) {  // r.Commit (== committed at a Step boundary)
+    // r.Commit: committed at a Step boundary, or 0 before the group's first Step (M_NC)
+    if (!rc_zero && index < committed) {
       resp(fref, HB_RESP_APP, committed);
       return;
     }
@@ -1015,6 +1030,9 @@ struct Lane {
         else ld1 = HB_REF_OTHER;
       }
     }
+    // past the gate: this Step ends with r.Commit = committed (raft/raft.go:466,488)
+    rc_zero = (meta & M_NC) != 0;
+    if (rc_zero) set_field(24, 1, 0);
     if constexpr (FOLLOW) {  // the events up to the next marker belong to this message
       if (is_follower_type(type)) ev(HB_EV_FOLLOW, 0, HB_FOLLOW_STEP, arrival_x());
     }

@@ -115,8 +115,10 @@ def cfg2_local_batch(groups, slots, frm, step):
 
 
 # ---------------------------------------------------------------------------- fuzz
-def random_groups(G, nmax=3, seed=1, W=8, state_mix=(0.6, 0.2, 0.2)):
-    """Diverse, internally consistent group states for fuzz parity.
+def random_groups(G, nmax=3, seed=1, W=8, state_mix=(0.6, 0.2, 0.2), commit_zero_p=0.0):
+    """Diverse, internally consistent group states for fuzz parity;
+    `commit_zero_p`: the share of groups whose r.Commit is still 0 (created
+    with an empty HardState and not stepped since, hb_group.commit_zero).
 
     Returns (groups, runs, inflights{(g, slot): values})."""
     rng = np.random.default_rng(seed)
@@ -192,6 +194,8 @@ def random_groups(G, nmax=3, seed=1, W=8, state_mix=(0.6, 0.2, 0.2)):
                     vals = np.sort(rng.choice(np.arange(m + 1, nx), size=cnt, replace=False)).astype(np.uint64)
                     ins[(i, s)] = vals
                 p["ins_count"] = cnt
+    if commit_zero_p > 0:  # (drawn after the groups: the streams above are unchanged)
+        g["commit_zero"] = ((rng.random(G) < commit_zero_p) & (g["committed"] > 0)).astype(np.uint32)
     return g, runs, ins
 
 
@@ -300,15 +304,18 @@ def older_runs(groups, runs, keep=None):
     return out
 
 
-def follower_messages(now, term_of, nmsg, seed=5, nonmember=0.05, max_ents=4, deep=0.0):
+def follower_messages(now, term_of, nmsg, seed=5, nonmember=0.05, max_ents=4, deep=0.0, past_end=0.0):
     """Random follower-side messages (MsgApp with entries / MsgHeartbeat /
     MsgSnap / MsgVote) against the groups' current state `now`; term_of(g, i)
     gives a group's log term (the oracle's).  Mostly well-formed (matching
     LogTerms, entries continuing the log at the message's term), with stale,
     conflicting, rejected and out-of-range cases mixed in; every entry and
     snapshot term is one a leader could send (non-decreasing, <= the group's
-    term after the gate), so the log keeps the reference's term order.  Returns the batch
-    arrays plus commit / eterm / eoff."""
+    term after the gate), so the log keeps the reference's term order.
+    `past_end`: the share of MsgApps that are empty LogTerm-0 probes past the
+    log's end (raftLog.term is 0 there, so they match) whose m.Commit lies
+    beyond lastIndex — commitTo's out-of-range panic (raft/log.go:175-176).
+    Returns the batch arrays plus commit / eterm / eoff."""
     rng = np.random.default_rng(seed)
     G = len(now)
     grp, info, term, index, hint, commit, eoff, eterm = [], [], [], [], [], [], [], []
@@ -344,6 +351,9 @@ def follower_messages(now, term_of, nmsg, seed=5, nonmember=0.05, max_ents=4, de
                     et = min(et + 1, mte)
                 ents.append(et)
             c = max(0, com + int(rng.integers(-2, 6)))
+            if past_end > 0 and rng.random() < past_end:  # (a draw only when asked: default streams unchanged)
+                x, h, ents = last + 1 + int(rng.integers(0, 3)), 0, []
+                c = last + 1 + int(rng.integers(0, 3))
         elif t == A.HB_MSG_HEARTBEAT:
             c = max(0, com + int(rng.integers(-1, 3)))
         elif t == A.HB_MSG_SNAP:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define HB_ABI_VERSION 4
+#define HB_ABI_VERSION 5
 
 /* ---- error codes -------------------------------------------------------- */
 #define HB_OK          0
@@ -164,7 +164,7 @@ typedef struct hb_batch {
  * Device keeps this as SoA.  Field meanings follow the reference:
  *   term/vote/commit : pb.HardState (raft/raft.go:126; vote is a node ref)
  *   lead, state      : SoftState (raft/node.go:40-43)
- *   committed        : raftLog.committed (== HardState.Commit between Steps)
+ *   committed        : raftLog.committed
  *   first_index      : raftLog.firstIndex()   (raft/log.go:150-159)
  *   last_index       : raftLog.lastIndex()    (raft/log.go:161-170)
  *   term_first..term_last : the maximal run of indices i in
@@ -176,6 +176,20 @@ typedef struct hb_batch {
  *                      r.id when r.id is not in prs.
  *   fault            : non-zero once the group hit a reference panic; the
  *                      device ignores the group until it is reloaded.
+ *   commit_zero      : r.Commit (= HardState.Commit) is 0 although committed
+ *                      is not.  The reference sets r.Commit = raftLog.committed
+ *                      only in loadState and at the end of every Step that
+ *                      passes the term gate (raft/raft.go:466,488,759), so a
+ *                      group created with an empty HardState keeps r.Commit = 0
+ *                      until its first Step: a bootstrapped MultiNode group
+ *                      (committed = len(peers), raft/multinode.go:197-211) or
+ *                      one restored from a snapshot (committed = firstIndex - 1,
+ *                      raft/log.go:60).  handleAppendEntries tests m.Index <
+ *                      r.Commit (raft/raft.go:652), not committed.  These are
+ *                      the only values r.Commit takes (r.Commit == committed,
+ *                      or 0 before the first Step); 0 = r.Commit == committed.
+ *                      The device clears it when the group steps a message
+ *                      past the term gate.
  */
 typedef struct hb_progress {
   uint64_t match;
@@ -203,6 +217,8 @@ typedef struct hb_group {
   uint32_t votes_resp;
   uint32_t votes_grant;
   uint32_t fault;             /* HB_FAULT_* */
+  uint32_t commit_zero;       /* r.Commit == 0 != committed (no Step since an empty HardState) */
+  uint32_t pad;
   hb_progress pr[HB_MAX_REPLICAS];
 } hb_group;
 

@@ -1076,7 +1076,10 @@ int orc_raft_from_group(orc_raft* r, const hb_group* g, const orc_run* runs, int
   r->election_timeout = 10;
   r->heartbeat_timeout = 1;
   r->term = g->term;
-  r->commit = g->committed;
+  /* r.Commit: committed, or 0 before the first Step of a group created with an
+     empty HardState (newRaft raft/raft.go:157-209 leaves it 0; loadState :759
+     and every Step past the term gate :466,488 set it) */
+  r->commit = g->commit_zero ? 0 : g->committed;
   r->vote = slot_id(g, g->vote);
   r->lead = slot_id(g, g->lead);
   r->state = (int)g->state;
@@ -1144,6 +1147,7 @@ void orc_raft_to_group(const orc_raft* r, hb_group* g) {
     if (r->vote_vals[i]) g->votes_grant |= 1u << bit;
   }
   g->fault = (uint32_t)r->fault;
+  g->commit_zero = (r->commit == 0 && r->log.committed != 0) ? 1u : 0u;
   for (int i = 0; i < r->n && i < HB_MAX_REPLICAS; i++) {
     const orc_progress* pr = &r->prs[i];
     g->pr[i].match = pr->match;

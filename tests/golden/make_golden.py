@@ -63,6 +63,11 @@ def cases():
     tr = synth.older_runs(g, runs)
     yield "follower_n3", 3, 8, g, runs, ins, _follower_batches(g, runs, ins, 8, tr, [0x601D0E, 0x601D1E]), \
         {"term_runs": tr}
+    # r.Commit = 0 before a group's first Step (hb_group.commit_zero) beside r.Commit == committed
+    g, runs, ins = synth.random_groups(160, 5, seed=0x601D0F, W=8, commit_zero_p=0.5)
+    tr = synth.older_runs(g, runs)
+    yield "commitzero_n5", 5, 8, g, runs, ins, _follower_batches(g, runs, ins, 8, tr, [0x601D2E, 0x601D3E]), \
+        {"term_runs": tr}
 
 
 def oracle_for(groups, runs, W, ins, extra):

@@ -43,7 +43,7 @@ def _compile_layout():
 int main(void) {
   printf("hb_progress %zu\nhb_group %zu\nhb_event %zu\nhb_batch %zu\nhb_timer %zu\n", sizeof(hb_progress),
          sizeof(hb_group), sizeof(hb_event), sizeof(hb_batch), sizeof(hb_timer));
-  P(hb_group, term) P(hb_group, snap_index) P(hb_group, state) P(hb_group, fault) P(hb_group, pr)
+  P(hb_group, term) P(hb_group, snap_index) P(hb_group, state) P(hb_group, fault) P(hb_group, commit_zero) P(hb_group, pr)
   P(hb_progress, pending_snapshot) P(hb_progress, ins_count)
   P(hb_event, x) P(hb_event, group) P(hb_event, type) P(hb_event, to) P(hb_event, aux)
   P(hb_batch, n) P(hb_batch, props)

@@ -87,6 +87,50 @@ def test_handle_msg_app(m, windex, wcommit, wreject):
     mn.Stop()
 
 
+def test_first_msgapp_of_bootstrapped_group_reads_rcommit_zero():
+    """A MultiNode group created with peers [1, 2, 3] (raft/multinode.go:197-211)
+    has committed = 3 but r.Commit = 0 until its first Step (raft/raft.go:488).
+    Its first MsgApp{Index 1, LogTerm 1} is below committed but not below
+    r.Commit, so handleAppendEntries (:651-665) runs maybeAppend and acks Index 1
+    (not 3); the Step then sets r.Commit = 3, and the same MsgApp again is
+    answered MsgAppResp{Index: r.Commit = 3} (:652-653)."""
+    mn = StartMultiNode(1, capacity=8)
+    s = MemoryStorage()
+    mn.CreateGroup(1, Config(10, 1), s, peers=[1, 2, 3])
+    rds = mn.Ready()  # the bootstrap entries
+    s.Append(rds[1].Entries)
+    mn.Advance(rds)
+    mn.Step(1, Message(Type=APP, From=2, To=1, Term=2, Index=1, LogTerm=1, Commit=3))
+    rd = one_ready(mn, s)
+    assert rd.Messages == [Message(Type=APPRESP, To=2, From=1, Term=2, Index=1)]
+    assert rd.HardState == HardState(Term=2, Vote=0, Commit=3)
+    assert [e.Index for e in rd.CommittedEntries] == [1, 2, 3]
+    mn.Step(1, Message(Type=APP, From=2, To=1, Term=2, Index=1, LogTerm=1, Commit=3))
+    rd = one_ready(mn, s)
+    assert rd.Messages == [Message(Type=APPRESP, To=2, From=1, Term=2, Index=3)]
+    mn.Stop()
+
+
+def test_first_msgapp_after_snapshot_with_empty_hardstate():
+    """A group restored from a snapshot at index 10 with an empty HardState:
+    committed = firstIndex - 1 = 10 (raft/log.go:60), r.Commit = 0.  Its first
+    MsgApp{Index 5, LogTerm 1} is not below r.Commit, so maybeAppend runs;
+    raftLog.term(5) is 0 below the dummy index (raft/log.go:198-203), the terms
+    differ, and the reference rejects with RejectHint = lastIndex = 10."""
+    st = MemoryStorage()
+    st.ApplySnapshot(Snapshot(Index=10, Term=1, Nodes=[1, 2, 3]))
+    mn = StartMultiNode(1, capacity=8)
+    mn.CreateGroup(1, Config(10, 1), st)
+    rds = mn.Ready()
+    if rds:
+        mn.Advance(rds)
+    mn.Step(1, Message(Type=APP, From=2, To=1, Term=2, Index=5, LogTerm=1, Commit=10))
+    rd = one_ready(mn, st)
+    assert rd.Messages == [Message(Type=APPRESP, To=2, From=1, Term=2, Index=5, Reject=True, RejectHint=10)]
+    assert rd.HardState == HardState(Term=2, Vote=0, Commit=10)
+    mn.Stop()
+
+
 @pytest.mark.parametrize("mcommit,wcommit", [(3, 3), (1, 2)])  # raft/raft_test.go:852-882 TestHandleHeartbeat
 def test_handle_heartbeat(mcommit, wcommit):
     mn, _ = follower([(1, 1), (2, 2), (3, 3)], term=2, commit=2)

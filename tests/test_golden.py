@@ -48,7 +48,7 @@ def unflat(d, key, width):
 def test_fixtures_present():
     names = {os.path.basename(p) for p in FIXTURES}
     assert {"cfg2_n3.npz", "cfg2_n5.npz", "storm_n7.npz", "fuzz_n5.npz", "sized_n3.npz",
-            "follower_n3.npz"} <= names
+            "follower_n3.npz", "commitzero_n5.npz"} <= names
 
 
 @pytest.mark.parametrize("path", FIXTURES, ids=lambda p: os.path.basename(p)[:-4])

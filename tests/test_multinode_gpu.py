@@ -222,12 +222,15 @@ def test_random_multinode_vs_oracle(seed, n):
     for gid in gids:
         s = MemoryStorage()
         mn.CreateGroup(gid, Config(election=3, heartbeat=1), s, peers=peers)
-        o = Raft(1, peers, ents=[(i, 1) for i in range(1, n + 1)], hard=(1, 0, n), max_inflight=8,
+        # the bootstrap of raft/multinode.go:197-211: becomeFollower(1, None), one
+        # entry per peer at term 1, committed = len(peers) — and r.Commit
+        # (HardState.Commit) still 0 until the group's first Step (raft/raft.go:488)
+        o = Raft(1, peers, ents=[(i, 1) for i in range(1, n + 1)], max_inflight=8,
                  election=3, heartbeat=1, draws=draws)
+        o.r.Term = 1
+        o.r.log.committed = n
+        assert o.Commit == 0
         st[gid] = dict(s=s, o=o, data={}, applied=0, prev_hard=(1, 0, 0), prev_soft=(0, 0), seq=0)
-    for gid in gids:  # one Step first, so HardState.Commit (r.Commit) tracks committed from here on
-        mn.Campaign(gid)
-        st[gid]["o"].Step(Msg(abi.HB_MSG_HUP))
     for rnd in range(ROUNDS):
         for gid in gids:
             d, o = st[gid], st[gid]["o"]
@@ -290,7 +293,7 @@ def test_random_multinode_vs_oracle(seed, n):
                 d["dead"] = True
                 continue
             om = _orc_msgs(o)
-            hard = (o.Term, o.Vote, o.committed)
+            hard = (o.Term, o.Vote, o.Commit)  # r.HardState: r.Commit, not raftLog.committed
             soft = (o.lead, o.state)
             unstable_lo = d["s"].LastIndex() + 1
             committed_lo = max(d["applied"] + 1, d["s"].FirstIndex())

@@ -936,3 +936,38 @@ def test_follower_term_lookup_at_any_depth():
         r2.Step(Msg(APP, From=2, To=1, Term=25, LogTerm=t + 1, Index=idx, Commit=0))
         ms = r2.readMessages()
         assert r2.fault == 0 and [(m.Index, bool(m.Reject)) for m in ms] == [(idx, True)], idx
+
+
+def test_rcommit_zero_before_first_step():
+    """r.Commit (HardState.Commit) is set only by loadState and at the end of a
+    Step past the term gate (raft/raft.go:466,488,759); handleAppendEntries
+    compares m.Index with it, not with raftLog.committed (:652).
+    (a) A MultiNode group bootstrapped with peers [1, 2, 3] (raft/multinode.go:
+    197-211: Term 1, committed 3, r.Commit 0): MsgApp{Index 1, LogTerm 1} is
+    acked at Index 1 by maybeAppend; after that Step r.Commit = 3 and the same
+    MsgApp is answered with Index 3.  (b) A group restored from a snapshot at
+    10 with an empty HardState (committed = firstIndex - 1 = 10, raft/log.go:60):
+    MsgApp{Index 5, LogTerm 1} meets term(5) = 0 below the dummy index
+    (raft/log.go:198-203) and is rejected with RejectHint 10."""
+    r = Raft(1, [1, 2, 3], ents=[(1, 1), (2, 1), (3, 1)])
+    r.r.Term = 1
+    r.r.log.committed = 3
+    assert r.Commit == 0
+    r.Step(Msg(APP, From=2, To=1, Term=2, LogTerm=1, Index=1, Commit=3))
+    ms = r.readMessages()
+    assert [(m.Type, m.To, m.Index, bool(m.Reject)) for m in ms] == [(abi.HB_MSG_APP_RESP, 2, 1, False)]
+    assert r.Commit == 3 and r.committed == 3
+    r.Step(Msg(APP, From=2, To=1, Term=2, LogTerm=1, Index=1, Commit=3))
+    assert [(m.Index, bool(m.Reject)) for m in r.readMessages()] == [(3, False)]
+    r = Raft(1, [1, 2, 3], snapshot=(10, 1))
+    assert r.committed == 10 and r.Commit == 0
+    r.Step(Msg(APP, From=2, To=1, Term=2, LogTerm=1, Index=5, Commit=10))
+    ms = r.readMessages()
+    assert [(m.Type, m.Index, bool(m.Reject), m.RejectHint) for m in ms] == [(abi.HB_MSG_APP_RESP, 5, True, 10)]
+    assert r.Commit == 10
+    # a lower-term message is ignored before the gate: r.Commit keeps its value
+    r = Raft(1, [1, 2, 3], ents=[(1, 1), (2, 1), (3, 1)])
+    r.r.Term = 3
+    r.r.log.committed = 3
+    r.Step(Msg(APP, From=2, To=1, Term=2, LogTerm=1, Index=1, Commit=3))
+    assert r.readMessages() == [] and r.Commit == 0

@@ -567,3 +567,97 @@ def test_log_index_precondition_faults():
     b2 = synth.follower_messages(pair2.og.groups(), pair2.og.term, 1500, seed=99, deep=1.0)
     _, st2, ora2 = pair2.step(b2, ctx="no runs")
     assert (ora2["fault"] == abi.HB_FAULT_TERM_WINDOW).sum() > 50
+
+
+# ---------------------------------------------------------------------------------------
+# r.Commit before a group's first Step (hb_group.commit_zero, raft/raft.go:466,488,652)
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("seed,nmax,W", [(31, 3, 8), (32, 5, 8), (33, 7, 16)])
+def test_fuzz_commit_zero(seed, nmax, W):
+    """Groups whose r.Commit is still 0 (created with an empty HardState and not
+    stepped since) next to groups whose r.Commit == committed, stepped with every
+    leader- and follower-side message type: handleAppendEntries compares m.Index
+    with r.Commit, so a MsgApp below committed is answered with MsgAppResp{Index:
+    r.Commit} only once the group has stepped.  Every specialised lane hands such
+    a group to the general one; events, statistics and records (commit_zero
+    included) equal the oracle's after every step."""
+    g, runs, ins = synth.random_groups(1500, nmax, seed=seed, W=W, commit_zero_p=0.5)
+    assert g["commit_zero"].sum() > 300
+    pair = Pair(g, runs, nmax, W, ins=ins, max_batch=1 << 15, term_runs=True)
+    pair.set_timers(synth.random_timers(len(g), seed=seed), DRAWS)
+    now = pair.og.groups()
+    z0 = int(now["commit_zero"].sum())
+    for k in range(3):
+        f = synth.follower_messages(now, pair.og.term, 3000, seed=seed + 13 * k, deep=0.3)
+        b = synth.merge_batches(synth.random_batch(g, 1500, seed=seed + 7 * k), f, seed=seed + k)
+        _, st, now = pair.step(b, ctx=f"commit_zero fuzz {seed} step {k}")
+    assert 0 < int(now["commit_zero"].sum()) < z0  # some groups stepped since, some not yet
+
+
+def test_fast_lanes_hand_over_commit_zero_groups():
+    """The steady-state streams (cfg2 leaders on the fast lane, follow on the
+    follower lane) over groups half of which still have r.Commit = 0: those are
+    stepped by the general lane, whose first Step clears the flag; a follower
+    receiving a MsgApp below committed answers with r.Commit (0 -> maybeAppend's
+    match, or committed once stepped)."""
+    g, runs = synth.steady_groups(4096, 3, seed=41, last_hi=1 << 12)
+    g["commit_zero"] = (np.arange(4096) % 2).astype(np.uint32)
+    pair = Pair(g, runs, 3, 256, max_batch=1 << 15)
+    _, st, now = pair.step(synth.cfg2_batch(g, 0, seed=42), ctx="cfg2 commit_zero")
+    assert st[abi.HB_STAT_COMMITS] == 4096 and not now["commit_zero"].any()
+    f, fruns = synth.follow_groups(4096, 3, seed=43, last_hi=1 << 12)
+    f["commit_zero"] = (np.arange(4096) % 2).astype(np.uint32)
+    pair = Pair(f, fruns, 3, 256, max_batch=1 << 15, term_runs=True)
+    b = synth.follow_batch(f, 0, seed=44)
+    _, st, now = pair.step(b, ctx="follow commit_zero")
+    assert not now["commit_zero"].any()
+    # an empty MsgApp below committed: r.Commit = 0 takes maybeAppend's match
+    # (MsgAppResp{Index: m.Index}); r.Commit = committed answers with it
+    f["commit_zero"] = (np.arange(4096) % 2).astype(np.uint32)
+    pair = Pair(f, fruns, 3, 256, max_batch=1 << 15, term_runs=True)
+    grp = np.nonzero(f["committed"] >= 2)[0].astype(np.uint32)
+    n = len(grp)
+    com = f["committed"][grp].astype(np.uint64)
+    x = com - np.uint64(1)
+    lt = np.array([pair.og.term(int(g), int(i)) for g, i in zip(grp, x)], np.uint64)
+    b = dict(group=grp, info=np.full(n, abi.HB_MSG_APP | (1 << 4), np.uint32), term=f["term"][grp].astype(np.uint64),
+             index=x, hint=lt, commit=com, eoff=np.zeros(n, np.uint64), eterm=np.zeros(0, np.uint64), props=None)
+    ev, st, now = pair.step(b, ctx="below committed")
+    resp = ev[ev["type"] == abi.HB_EV_RESP]
+    want = np.where(grp % 2 == 1, x, com)
+    assert np.array_equal(resp["x"][np.argsort(resp["group"], kind="stable")], want)
+
+
+@pytest.mark.parametrize("seed", [51, 52])
+def test_follower_lane_commit_past_log_end(seed):
+    """An empty MsgApp past the log's end with LogTerm 0 matches (raftLog.term
+    is 0 beyond lastIndex) and commitTo(min(m.Commit, m.Index)) may exceed
+    lastIndex: the reference panics (raft/log.go:175-176).  The follower fast
+    lane must not take it; the general lane reports HB_FAULT_COMMIT_RANGE, as
+    the oracle does.  Directed groups plus a fuzz that mixes such probes into
+    the X-mode follow stream."""
+    f, fruns = synth.follow_groups(2048, 3, seed=seed, last_hi=1 << 12)
+    pair = Pair(f, fruns, 3, 256, max_batch=1 << 15, term_runs=True)
+    G = 2048
+    grp = np.arange(G, dtype=np.uint32)
+    last = f["last_index"].astype(np.uint64)
+    k = grp % 4
+    # k = 0: commit past the end (panic); 1: commit within the log (ack of Index); 2, 3: the normal MsgApp
+    index = np.where(k < 2, last + np.uint64(1) + (grp % 3).astype(np.uint64), last)
+    commit = np.where(k == 0, index + np.uint64(1), np.where(k == 1, last, last))
+    hint = np.where(k < 2, 0, f["term"]).astype(np.uint64)
+    b = dict(group=grp, info=np.full(G, abi.HB_MSG_APP | (1 << 4), np.uint32), term=f["term"].astype(np.uint64),
+             index=index.astype(np.uint64), hint=hint, commit=commit.astype(np.uint64),
+             eoff=np.zeros(G, np.uint64), eterm=np.zeros(0, np.uint64), props=None)
+    ev, st, now = pair.step(b, ctx="past-end probes")
+    assert (now["fault"][k == 0] == abi.HB_FAULT_COMMIT_RANGE).all()
+    assert (now["fault"][k != 0] == 0).all()
+    assert st[abi.HB_STAT_FAULTS] == int((k == 0).sum())
+    # fuzz: the follower-side generator with past-end probes, over fresh followers
+    f2, fruns2 = synth.follow_groups(3000, 3, seed=seed + 100, last_hi=1 << 10)
+    pair2 = Pair(f2, fruns2, 3, 256, max_batch=1 << 15, term_runs=True)
+    now = pair2.og.groups()
+    for j in range(3):
+        b = synth.follower_messages(now, pair2.og.term, 4000, seed=seed * 10 + j, past_end=0.2)
+        _, st, now = pair2.step(b, ctx=f"past-end fuzz {seed} step {j}")
+    assert (now["fault"] == abi.HB_FAULT_COMMIT_RANGE).sum() > 20
