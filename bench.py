@@ -220,6 +220,29 @@ def cpu_baseline_follow(n, groups=200_000, W=256, budget_s=10.0, max_steps=40):
                       f"one core"}
 
 
+def cpu_baseline_mixed(n, groups=200_000, W=256, budget_s=10.0, max_steps=40):
+    """The C oracle on a bounded sample of the mixed workload (a node leading
+    1/3 of its groups, following 2/3: stepLeader + stepFollower), one core."""
+    from etcd_amd import abi, synth
+    from oracle.pyoracle import OracleGroups
+    g, runs = synth.mixed_groups(groups, n, seed=0x5EED0007, with_runs="flat")
+    og = OracleGroups(g, runs, W)
+    msgs = commits = 0
+    spent = 0.0
+    steps = 0
+    while spent < budget_s and steps < max_steps:
+        b, _ = synth.mixed_batch(g, steps)
+        t0 = time.perf_counter()
+        _, st = og.step(b)
+        spent += time.perf_counter() - t0
+        msgs += int(st[abi.HB_STAT_MSGS])
+        commits += int(st[abi.HB_STAT_COMMITS])
+        steps += 1
+    return {"value": msgs / spent, "unit": "msgs/s", "cores": 1, "kind": "port", "commits_per_s": commits / spent,
+            "sample": f"oracle/raft_oracle.c (C restatement, not the Go reference), {groups} groups x {n} (1/3 led, "
+                      f"2/3 followed), {steps} mixed steps, {msgs} messages in {spent:.2f} s, one core"}
+
+
 def cpu_baseline_wire(n, groups=100_000, W=256, budget_s=10.0, max_steps=20):
     """The C oracle decoding the cfg2 wire records (orc_decode_batch, the
     reference's Unmarshal restated) and stepping them, one core."""
@@ -252,7 +275,7 @@ def cpu_baseline_wire(n, groups=100_000, W=256, budget_s=10.0, max_steps=20):
                       f"x {n}, {steps} cfg2 steps from wire records, {acks} MsgAppResp in {spent:.2f} s, one core"}
 
 
-def pmc_traffic(path, kernel, G, n, apply_us):
+def pmc_traffic(path, kernel, G, n, apply_us, workload=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (FETCH_SIZE x 2 + WRITE_SIZE, tools/prof_summary.py).  Used only when the
     profile was taken on the same workload and its average duration agrees with
@@ -267,7 +290,8 @@ def pmc_traffic(path, kernel, G, n, apply_us):
             cfg = d["bench"]["config"]
         except (OSError, KeyError, ValueError, StopIteration):
             continue
-        if cfg.get("groups_per_gpu") == G and cfg.get("replicas") == n and "traffic_bytes" in k:
+        if cfg.get("groups_per_gpu") == G and cfg.get("replicas") == n and "traffic_bytes" in k and \
+                (workload is None or cfg.get("workload", "").startswith(workload + ":")):
             break
     else:
         return None, None
@@ -392,7 +416,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["cfg2", "cfg5", "e2e", "cfg3", "cfg4", "tick", "wire", "multinode", "follow"],
+    ap.add_argument("--workload", choices=["cfg2", "cfg5", "e2e", "cfg3", "cfg4", "tick", "wire", "multinode", "follow",
+                                           "mixed"],
                     default="cfg2",
                     help="cfg2 (headline: 1M groups x 3 per GPU), cfg5 (8M groups x 3 per GPU = BASELINE.json "
                          "configs[4] at 8 GPUs), e2e = cfg2 with the batch in host memory and the events copied "
@@ -400,8 +425,10 @@ def main():
                          "tick = MultiNode.Tick over the cfg2 groups (SURVEY.md 8(f) rank 1), "
                          "wire = cfg2 from raftpb wire records: hb_decode + hb_step (8(f) rank 3), "
                          "multinode = the MultiNode API end to end (Step/Propose/Ready/Advance, 8(f) rank 2), "
-                         "follow = the follower side of cfg2: 1M followed groups x 3, each receiving its "
-                         "leader's MsgApp (1 entry) and MsgHeartbeat per step (8(f) rank 4)")
+                         "follow = the follower side of cfg2: 1M followed groups x 3 (--replicas 5: x 5), each "
+                         "receiving its leader's MsgApp (1 entry) and MsgHeartbeat per step (8(f) rank 4), "
+                         "mixed = a node's Ready cycle: 1M groups x 3, 1/3 led (the cfg2 step) and 2/3 followed "
+                         "(the follow step) in one batch")
     ap.add_argument("--groups", type=int, default=None,
                     help="groups per GPU (cfg2/cfg3/e2e: 1M, cfg5: 8M, cfg4: 4M)")
     ap.add_argument("--replicas", type=int, default=None, help="cfg2/cfg5: 3, cfg3: 5, cfg4: 7")
@@ -457,36 +484,32 @@ def routed_batch(G_per_gpu, world, rank, n):
     map of the global group-id space [0, world x G_per_gpu) (splitmix64(id) %
     world), this rank's groups (steady state, seeded per rank), and ONE global
     arrival stream (every follower of every group acks, same order on every
-    rank) routed to this rank with ShardMap.route_local — owner hash + select
-    + global id -> local slot, timed on its own.  Term / Index come from the
-    local group state."""
+    rank) routed by the host router of libhbnode (include/hbroute.h: one pass,
+    16 host threads, every rank's stream positions and local slots in arrival
+    order), timed on its own.  Term / Index come from the local group state."""
     from etcd_amd import synth
-    from etcd_amd.shard import ShardMap
+    from etcd_amd.shard import NativeRouter
     G_total = G_per_gpu * world
-    sm = ShardMap(np.arange(G_total, dtype=np.uint64), world, rank)
-    G = len(sm)
-    table = sm.dense_slots(G_total)
+    t0 = time.perf_counter()
+    router = NativeRouter(np.arange(G_total, dtype=np.uint64), world)
+    build_s = time.perf_counter() - t0
+    G = len(router.local_ids(rank))
     groups, _ = synth.steady_groups(G, n, seed=0x5EED0002 + rank, with_runs=False)
     gid, frm = synth.global_ack_stream(G_total, n)
-    route_s = 0.0
-    parts_s, parts_f = [], []
-    CH = 1 << 23
-    for c0 in range(0, len(gid), CH):
-        t0 = time.perf_counter()
-        idx, slots = sm.route_local(gid[c0:c0 + CH], table)
-        f = frm[c0:c0 + CH][idx]
-        route_s += time.perf_counter() - t0
-        parts_s.append(slots)
-        parts_f.append(f)
+    t0 = time.perf_counter()
+    out, unknown = router.route(gid)  # every rank's share in one pass (what a node's router does once)
+    route_s = time.perf_counter() - t0
+    pos, slots = out[rank]
+    frm_l = frm[pos]
     n_global = len(gid)
-    del gid, frm, table
-    slots, frm_l = np.concatenate(parts_s), np.concatenate(parts_f)
+    del gid, frm, out
     batch = synth.cfg2_local_batch(groups, slots, frm_l, 0)
-    route = {"global_msgs_scanned": n_global, "local_msgs": int(len(slots)), "seconds": round(route_s, 4),
-             "msgs_scanned_per_s": n_global / route_s if route_s > 0 else None, "cores": 1,
-             "note": "host routing of the global arrival stream to this rank (etcd_amd/shard.py route_local: "
-                     "splitmix64 owner hash, select, id -> local slot), numpy on one core, outside the timed "
-                     "region" + ("" if world > 1 else "; one GPU: every message is local, no hash")}
+    route = {"global_msgs_routed": n_global, "ranks_served": world, "local_msgs": int(len(slots)),
+             "seconds": round(route_s, 4), "msgs_routed_per_s": n_global / route_s if route_s > 0 else None,
+             "threads": router.threads, "unknown_groups": unknown, "router_build_s": round(build_s, 3),
+             "note": "host owner routing of the node's whole arrival stream to every rank in one pass "
+                     "(libhbnode hbn_route: splitmix64 owner + id -> local slot, arrival order kept), outside the "
+                     "timed region; a node runs it once for all its GPUs"}
     return groups, batch, G_total, route
 
 
@@ -583,6 +606,13 @@ def run_replication(args, world, rank, local):
     if world > 1:
         dist.all_reduce(route_t, op=dist.ReduceOp.MAX)
     route["seconds_max_over_ranks"] = float(route_t.item())
+    step_s = ms / args.steps / 1e3
+    if step_s > 0 and route["seconds"] > 0:
+        # the bound a deployment meets: one host router feeds every GPU of the node
+        route["route_s_over_device_step"] = round(route["seconds_max_over_ranks"] / step_s, 2)
+        route["bound"] = (f"the router moves {route['global_msgs_routed'] / route['seconds']:.3g} msgs/s on "
+                          f"{route['threads']} host threads; the node's {world} GPU(s) step "
+                          f"{route['global_msgs_routed'] / step_s:.3g} msgs/s")
 
     phase = {}
     roof = None
@@ -839,7 +869,7 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     from etcd_amd.hipbatch import Engine
     n, W, G = args.replicas, args.inflight, args.groups
     seed = {"cfg3": 0x5EED0003, "cfg4": 0x5EED0004, "tick": 0x5EED0002, "wire": 0x5EED0002,
-            "follow": 0x5EED0006}[args.workload] + rank
+            "follow": 0x5EED0006, "mixed": 0x5EED0007}[args.workload] + rank
     stream = torch.cuda.current_stream(dev)
     total = args.warmup + args.steps
     st_acc = np.zeros(abi.HB_STAT_COUNT, np.uint64)
@@ -874,9 +904,17 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         ms_local = e0.elapsed_time(e1)
         st_acc = stats.cpu().numpy().astype(np.uint64)
         timing = "K steps back to back, inputs resident in HBM"
-    elif args.workload == "follow":
-        g, _ = synth.follow_groups(G, n, seed=seed, with_runs=False)
-        b = synth.follow_batch(g, 0, seed=seed)
+    elif args.workload in ("follow", "mixed"):
+        n_led = 0
+        if args.workload == "follow":
+            g, _ = synth.follow_groups(G, n, seed=seed, with_runs=False)
+            b = synth.follow_batch(g, 0, seed=seed)
+            inc = {"index": ((b["info"] & 0xF) == abi.HB_MSG_APP).astype(np.uint64),
+                   "commit": np.ones(len(b["group"]), np.uint64)}
+        else:
+            g, _ = synth.mixed_groups(G, n, seed=seed, with_runs=False)
+            b, inc = synth.mixed_batch(g, 0, seed=seed)
+            n_led = int((g["state"] == abi.HB_STATE_LEADER).sum())
         nmsg = len(b["group"])
         eng = Engine(G, max_replicas=n, max_inflight=W, max_batch=nmsg, device=local, stream=stream)
         eng.load_groups(g)
@@ -886,15 +924,16 @@ def run_aux(args, world, rank, local, dev, torch, dist):
             return torch.from_numpy(np.ascontiguousarray(a).view(np.int32 if a.dtype == np.uint32 else np.int64)).to(dev)
         d_group, d_info, d_term, d_hint, d_eoff, d_eterm = (dv(b[k]) for k in ("group", "info", "term", "hint",
                                                                             "eoff", "eterm"))
-        app = dv(((b["info"] & 0xF) == abi.HB_MSG_APP).astype(np.uint64))
+        d_props = dv(b["props"]) if b.get("props") is not None else None
+        i_inc, c_inc = dv(inc["index"]), dv(inc["commit"])
         i0, c0 = dv(b["index"]), dv(b["commit"])
-        # step k continues the stream: the follower's log is k entries longer (resident before timing)
-        d_index = [i0 + app * k for k in range(total)]
-        d_commit = [c0 + k for k in range(total)]
+        # step k continues the stream: every log is k entries longer (resident before timing)
+        d_index = [i0 + i_inc * k for k in range(total)]
+        d_commit = [c0 + c_inc * k for k in range(total)]
         stats = torch.zeros(abi.HB_STAT_COUNT, dtype=torch.int64, device=dev)
 
         def one(k, prof=False):
-            eng.step(d_group, d_info, d_term, d_index[k], d_hint, None, host=False, eoff=d_eoff, commit=d_commit[k],
+            eng.step(d_group, d_info, d_term, d_index[k], d_hint, d_props, host=False, eoff=d_eoff, commit=d_commit[k],
                      eterm=d_eterm, profile=prof)
         for k in range(args.warmup):
             one(k)
@@ -1086,24 +1125,43 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         ok = int(st[abi.HB_STAT_VOTERESP]) == world * G * (n - 1) * args.steps and int(st[abi.HB_STAT_FAULTS]) == 0
         wl = f"cfg4: {G} raft groups x {n} per GPU, election storm (step-down, MsgHup, {n - 1} MsgVoteResp per group)"
         data = "synthetic (seeded cfg4 storm replayed at +4 terms per step)"
-    elif args.workload == "follow":
-        metric, unit, val = "follower-side messages stepped/sec (MsgApp + MsgHeartbeat, follow workload)", "msgs/s", \
-            int(st[abi.HB_STAT_MSGS]) / sec
-        alg = FOLLOW_GROUP_BYTES * G * args.steps  # per rank
-        alg_note = follow_alg_note()
-        kname = "k_apply_fast<3> (X mode: FollowLane)"
-        ach_k = FOLLOW_GROUP_BYTES * G / (apply_us * 1e-6) / 1e9 if apply_us > 0 else 0.0
-        tr, tsrc = pmc_traffic(args.traffic_json, ["k_apply_fast<3, true, 2u>", "k_apply_fast<3, true>"], G, n, apply_us)
+    elif args.workload in ("follow", "mixed"):
+        n_fol = G - n_led
+        launch_alg = FOLLOW_GROUP_BYTES * n_fol + alg_bytes_per_group(n) * n_led  # per rank, per step
+        alg = launch_alg * args.steps
+        if n == 3:
+            kname = "k_apply_fast<3> (X mode: FastLane + FollowLane)"
+            knames = ["k_apply_fast<3, true, 2u>", "k_apply_fast<3, true>"]
+        else:
+            kname = f"k_apply_lead<{n}> (X mode: LeadLane + FollowLane)"
+            knames = [f"k_apply_lead<{n}, true>", f"k_apply_lead<{n}>"]
+        ach_k = launch_alg / (apply_us * 1e-6) / 1e9 if apply_us > 0 else 0.0
+        tr, tsrc = pmc_traffic(args.traffic_json, knames, G, n, apply_us, workload=args.workload)
         extra = {"commits_per_s": int(st[abi.HB_STAT_COMMITS]) / sec, "entries_per_s": int(st[abi.HB_STAT_ENTRIES]) / sec,
                  "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(ach_k, 1), "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": round(ach_k / HBM_PEAK_GBS, 4), "traffic": tr,
                               "traffic_source": tsrc, "launch_us_timed": round(apply_us, 2),
-                              "alg_bytes_per_launch": FOLLOW_GROUP_BYTES * G, "alg_bytes_note": alg_note,
+                              "alg_bytes_per_launch": launch_alg,
+                              "alg_bytes_note": follow_alg_note() + (
+                                  f"; a led group {alg_bytes_per_group(n)} B (the cfg2 step: proposal + {n - 1} "
+                                  f"MsgAppResp, SURVEY.md 8(d))" if n_led else ""),
                               "step_frac": round(alg / args.steps / (ms / args.steps * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+        msgs_per_step = 2 * n_fol + (n - 1) * n_led
         ok = int(st[abi.HB_STAT_COMMITS]) == world * G * args.steps and \
-            int(st[abi.HB_STAT_MSGS]) == 2 * world * G * args.steps and int(st[abi.HB_STAT_FAULTS]) == 0
-        wl = f"follow: {G} raft groups x {n} per GPU that this node follows, MsgApp (1 entry) + MsgHeartbeat each"
-        data = "synthetic (seeded follow stream: every group's leader appends one entry and heartbeats per step)"
+            int(st[abi.HB_STAT_MSGS]) == world * msgs_per_step * args.steps and int(st[abi.HB_STAT_FAULTS]) == 0
+        if args.workload == "follow":
+            metric, unit, val = "follower-side messages stepped/sec (MsgApp + MsgHeartbeat, follow workload)", \
+                "msgs/s", int(st[abi.HB_STAT_MSGS]) / sec
+            wl = f"follow: {G} raft groups x {n} per GPU that this node follows, MsgApp (1 entry) + MsgHeartbeat each"
+            data = "synthetic (seeded follow stream: every group's leader appends one entry and heartbeats per step)"
+        else:
+            metric, unit, val = ("messages stepped/sec on a MultiNode node that leads 1/3 of its groups and follows "
+                                 "2/3 (MsgAppResp + MsgApp + MsgHeartbeat in one batch)"), "msgs/s", \
+                int(st[abi.HB_STAT_MSGS]) / sec
+            extra["msgappresp_per_s"] = int(st[abi.HB_STAT_APPRESP]) / sec
+            wl = (f"mixed: {G} raft groups x {n} per GPU, {n_led} led (proposal + {n - 1} MsgAppResp each) and "
+                  f"{n_fol} followed (MsgApp with 1 entry + MsgHeartbeat each) in one batch")
+            data = "synthetic (seeded mixed stream: a node's Ready cycle over the groups it leads and follows)"
     else:
         metric, unit, val = "MsgAppResp applied/sec (cfg3 lagging followers)", "MsgAppResp/s", \
             int(st[abi.HB_STAT_APPRESP]) / sec
@@ -1152,7 +1210,7 @@ def run_aux(args, world, rank, local, dev, torch, dist):
             try:
                 out["cpu_baseline"] = {"cfg4": cpu_baseline_cfg4, "cfg3": cpu_baseline_cfg3,
                                        "tick": cpu_baseline_tick, "wire": cpu_baseline_wire,
-                                       "follow": cpu_baseline_follow}[args.workload](n, W=W)
+                                       "follow": cpu_baseline_follow, "mixed": cpu_baseline_mixed}[args.workload](n, W=W)
             except Exception as e:  # report, never fake
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out))

@@ -1721,14 +1721,21 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
 // first reads only its Term and its slots' terms: with a higher term among
 // them it is handed over unloaded.
 // ---------------------------------------------------------------------------
-template <int NMAX>
+// X mode (follower-side batches): a follower whose messages all sit in its
+// first FOLLOW_SLOTS route slots is stepped by FollowLane in the same pass
+// (the follower side of a node with n >= 5 replicas: about (n-1)/n of its
+// groups), the slots' {m.LogTerm, m.Commit} extensions staged beside them.
+constexpr uint32_t FOLLOW_SLOTS = 4;
+template <int NMAX, bool X>
 __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAVES) k_apply_lead(ApplyArgs a) {
   constexpr uint32_t KS = route_kmax(NMAX);
+  constexpr uint32_t FS = X ? FOLLOW_SLOTS : 1u;
   __shared__ uint32_t l_fill, l_pfill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint32_t l_eflag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
   __shared__ uint4 l_slot[KS][PART];  // the lane's route slots, read once (as in k_elect)
+  __shared__ uint4 l_slotx[FS][PART];  // X mode: a follower's slot extensions
   const uint32_t part = block_part(a.sis_log);
   if (part >= a.NB) return;  // uniform: grid padding
   const uint32_t tid = threadIdx.x;
@@ -1738,7 +1745,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   if (tid <= ST_N) l_stats[tid] = 0;
   if (tid < FLAG_WORDS) l_flag[tid] = l_eflag[tid] = 0;
 
-  LeadLane<NMAX> L;
+  FollowLane<NMAX, LeadLane<NMAX>> L;
   L.S = a.S;
   L.g = g;
   L.mlo = gvalid ? reinterpret_cast<const uint32_t*>(a.S.meta)[2 * (size_t)g] : 0u;
@@ -1751,17 +1758,29 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   const bool nc = (L.mlo & (uint32_t)M_NC) != 0;
   // a leader with a proposal or at most one message per follower loads at once
   const bool spec = leader && !nc && (prop_raw != 0 || (fits && cnt <= (uint32_t)NMAX - 1));
+  // X mode: a follower whose messages all sit in its first FS slots, without a
+  // dense proposal (stepFollower forwards it: the general lane)
+  const bool fol = X && live && !nc && L.state() == HB_STATE_FOLLOWER && cnt > 0 && cnt <= FS && prop_raw == 0;
   L.dirty = 0;
   L.nev = 0;
   // (loading the state beside meta, as k_apply_fast does, measured neutral
   // on cfg3 and +4.5 % on cfg4, whose lanes are mostly not leaders)
   L.last = L.committed = 0;
   L.term = 0;
-  const bool slots = leader && !nc && fits;
+  const bool slots = (leader && !nc && fits) || fol;
 #pragma unroll
   for (uint32_t k = 0; k < KS; ++k)
     if (slots && k < cnt) l_slot[k][tid] = at32(a.slot, k * a.S.G + g);
+  if constexpr (X) {
+#pragma unroll
+    for (uint32_t k = 0; k < FS; ++k)
+      if (fol && k < cnt) l_slotx[k][tid] = at32(a.slotx, k * a.S.G + g);
+  }
   if (spec) L.load();
+  if (fol) {
+    L.load_head();
+    L.load_follow();
+  }
   bool loaded = spec, higher = false;
   if (slots && !spec) {  // a busy leader without a proposal: load it unless a higher term steps it down
     const uint64_t t = at32(a.S.term, g);
@@ -1783,7 +1802,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   // storm's leaders go to k_elect without them)
   uint32_t key[KS];
   uint32_t perm = 0;
-  const bool keys = slots && loaded;
+  const bool keys = (slots && loaded) || fol;
 #pragma unroll
   for (uint32_t k = 0; k < KS; ++k) {
     key[k] = (keys && k < cnt) ? l_slot[k][tid].y : 0xFFFFFFFFu;
@@ -1826,7 +1845,29 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   // ---- the slot messages in arrival order (M chunk reserved by k_route)
   L.E.chunk = a.ev + a.ev_off[2 * part + 1];
   L.E.fill = &l_fill;
-  if (live && cnt > 0 && !flagged && !L.faulted()) {
+  bool fstepped = false;  // FollowLane stepped a message: its state is stored
+  if (X && fol) {
+#pragma nounroll
+    for (uint32_t x = 0; x < cnt; ++x) {
+      if (L.faulted()) break;
+      const uint32_t ks = (perm >> (4 * x)) & 0xF;
+      uint32_t inf, morig;
+      uint64_t mterm, mindex;
+      slot_unpack(l_slot[ks][tid], a.side, &inf, &morig, &mterm, &mindex);
+      const uint4 ext = l_slotx[ks < FS ? ks : 0][tid];
+      const uint64_t lt = (uint64_t)ext.x | ((uint64_t)ext.y << 32), mc = (uint64_t)ext.z | ((uint64_t)ext.w << 32);
+      const uint32_t from = (inf >> 4) & 0xF;
+      if (!L.takes_follow(inf, from, mterm, mindex, lt, mc)) {
+        flagged = true;
+        resume = x;
+        break;
+      }
+      L.arrival = morig;
+      L.step_follow(inf, from, mterm, mindex, lt, mc);
+      fstepped = true;
+      st_msgs++;
+    }
+  } else if (live && cnt > 0 && !flagged && !L.faulted()) {
     if (!loaded || !fits) {  // all to k_apply (or k_elect)
       flagged = true;
       resume = 0;
@@ -1860,12 +1901,14 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
     }
   }
   if (loaded) L.store();
+  if (fstepped) L.store_follow();
+  const bool stored = loaded || fstepped;
   // k_elect's candidates (n >= 5): no leader, or a leader a higher term steps down
   if (NMAX >= 5 && flagged && (!leader || higher)) atomicOr(&l_eflag[tid >> 5], 1u << (tid & 31));
   if (flagged) {
     atomicOr(&l_flag[tid >> 5], 1u << (tid & 31));
-    a.resume[g] = resume | (loaded ? 0u : 1u << 30);
-    if (loaded) a.commit0[g] = commit0;
+    a.resume[g] = resume | (stored ? 0u : 1u << 30);
+    if (stored) a.commit0[g] = commit0;
   }
   const uint32_t vals[ST_N + 1] = {st_msgs,
                                    st_app,
@@ -2767,7 +2810,10 @@ template <int NMAX>
 void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
   const uint32_t grid = apply_grid(h);
   if (ev) (void)hipEventRecord(ev[2], h->stream);
-  if constexpr (NMAX >= 5) hipLaunchKernelGGL(k_apply_lead<NMAX>, dim3(grid), dim3(PART), 0, h->stream, a);
+  if constexpr (NMAX >= 5) {
+    if (a.slotx) hipLaunchKernelGGL((k_apply_lead<NMAX, true>), dim3(grid), dim3(PART), 0, h->stream, a);
+    else hipLaunchKernelGGL((k_apply_lead<NMAX, false>), dim3(grid), dim3(PART), 0, h->stream, a);
+  }
   else if (a.kmax == 3) {
     if (a.slotx) hipLaunchKernelGGL((k_apply_fast<NMAX, true, 3>), dim3(grid), dim3(PART), 0, h->stream, a);
     else hipLaunchKernelGGL((k_apply_fast<NMAX, false, 3>), dim3(grid), dim3(PART), 0, h->stream, a);

@@ -6,7 +6,8 @@
 // (raft/raft.go:616-669 stepFollower, handleAppendEntries, handleHeartbeat;
 // raft/log.go:72-88 maybeAppend).  k_follow (Lane<NMAX, true>) steps every
 // follower-side case; FollowLane is its specialization for the common one, run
-// by k_apply_fast in the same pass and the same registers as the leader lane:
+// by k_apply_fast (n = 3) and k_apply_lead (n >= 5) in the same pass as the
+// leader lane:
 //
 //   * a follower (not M_RS, not M_NC) receiving, at its own Term, from a member:
 //   * MsgHeartbeat with m.Commit <= lastIndex
@@ -34,9 +35,11 @@
 
 namespace hb {
 
-template <int NMAX>
-struct FollowLane : FastLane<NMAX> {
-  using B = FastLane<NMAX>;
+// Base: FastLane (k_apply_fast, n = 3) or LeadLane (k_apply_lead, n >= 5),
+// whose lanes step a partition's leaders and followers side by side.
+template <int NMAX, class Base = FastLane<NMAX>>
+struct FollowLane : Base {
+  using B = Base;
   using B::S;
   using B::g;
   using B::arrival;

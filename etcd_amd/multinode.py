@@ -215,6 +215,14 @@ def lib():
             "hbn_advance": (C.c_int, [vp, P(u64), u64]),
             "hbn_status": (C.c_int, [vp, u64, P(hbn_group_status)]),
             "hbn_engine": (vp, [vp]),
+            # include/hbroute.h: owner routing across a node's GPUs (etcd_amd/shard.py NativeRouter)
+            "hbn_owner": (u32, [u64, u32]),
+            "hbn_router_create": (C.c_int, [vp, u64, u32, u32, P(vp)]),
+            "hbn_router_destroy": (C.c_int, [vp]),
+            "hbn_router_local_count": (u64, [vp, u32]),
+            "hbn_router_local_ids": (C.c_int, [vp, u32, vp]),
+            "hbn_route": (C.c_int, [vp, vp, u64, vp, P(u64)]),
+            "hbn_route_take": (C.c_int, [vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

@@ -7,6 +7,8 @@ hash; each GPU owns a dense local slot space.  The only collective is one
 all-reduce of the per-step statistics (RCCL over xGMI on GPUs, gloo in CPU
 tests).
 """
+import os
+
 import numpy as np
 
 from .synth import splitmix64
@@ -72,3 +74,56 @@ def reduce_stats(stats_tensor, dist=None):
     if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(stats_tensor)
     return stats_tensor
+
+
+class NativeRouter:
+    """The owner routing of libhbnode.so (include/hbroute.h): one pass over an
+    arrival-ordered stream on host threads, every rank's (stream positions,
+    local slots) at once, order kept.  Same shard map as ShardMap (owner =
+    splitmix64(id) % world, local slot = position among the rank's ids)."""
+
+    def __init__(self, group_ids, world, threads=0):
+        import ctypes as C
+        from .multinode import lib
+        self._L = L = lib()
+        self._C = C
+        ids = np.ascontiguousarray(group_ids, dtype=np.uint64)
+        self.world = world
+        self.threads = threads or min(16, os.cpu_count() or 1)
+        self._h = C.c_void_p()
+        rc = L.hbn_router_create(ids.ctypes.data_as(C.c_void_p), len(ids), world, self.threads, C.byref(self._h))
+        if rc != 0:
+            raise ValueError(f"hbn_router_create: {rc}")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.hbn_router_destroy(self._h)
+            self._h = None
+
+    def local_ids(self, rank):
+        C = self._C
+        n = self._L.hbn_router_local_count(self._h, rank)
+        out = np.zeros(n, np.uint64)
+        self._L.hbn_router_local_ids(self._h, rank, out.ctypes.data_as(C.c_void_p))
+        return out
+
+    def route(self, gids, ranks=None):
+        """{rank: (positions u64, local slots u32)} for `ranks` (default all),
+        plus the count of messages for unknown groups."""
+        C = self._C
+        gids = np.ascontiguousarray(gids, dtype=np.uint64)
+        W = self.world
+        counts = np.zeros(W, np.uint64)
+        unk = C.c_uint64()
+        rc = self._L.hbn_route(self._h, gids.ctypes.data_as(C.c_void_p), len(gids), counts.ctypes.data_as(C.c_void_p),
+                               C.byref(unk))
+        if rc != 0:
+            raise ValueError(f"hbn_route: {rc}")
+        ranks = range(W) if ranks is None else ranks
+        out = {k: (np.empty(int(counts[k]), np.uint64), np.empty(int(counts[k]), np.uint32)) for k in ranks}
+        pos = (C.c_void_p * W)(*[out[k][0].ctypes.data if k in out else None for k in range(W)])
+        slot = (C.c_void_p * W)(*[out[k][1].ctypes.data if k in out else None for k in range(W)])
+        rc = self._L.hbn_route_take(self._h, pos, slot)
+        if rc != 0:
+            raise ValueError(f"hbn_route_take: {rc}")
+        return out, int(unk.value)

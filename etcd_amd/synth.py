@@ -415,6 +415,68 @@ def follow_batch(groups, step, seed=0x5EED0006, ents=1):
                 commit=base, eoff=eoff, eterm=np.repeat(term[app], ents).astype(np.uint64), props=None)
 
 
+# ---------------------------------------------------------------------------- mixed (a node's real Ready cycle)
+def mixed_groups(G, n=3, seed=0x5EED0007, lead_every=3, last_hi=1 << 20, term_hi=1000, with_runs="flat"):
+    """A MultiNode node's groups (raft/multinode.go:233-237): this node (slot 0)
+    leads every `lead_every`-th group (g % lead_every == 0, the cfg2 leader
+    state: followers Replicate, every Match = committed = lastIndex) and
+    follows the rest, whose leader is slot 1 (the follow state: the last entry
+    has the Term, everything but it is committed, Progress as the last reset
+    left it)."""
+    g, runs = steady_groups(G, n, seed=seed, last_hi=last_hi, term_hi=term_hi, with_runs=with_runs)
+    f = (np.arange(G) % lead_every) != 0
+    g["state"][f] = A.HB_STATE_FOLLOWER
+    g["lead"][f] = 1
+    g["vote"][f] = 1
+    g["committed"][f] = g["last_index"][f] - np.uint64(1)
+    for s in range(n):
+        pr = g["pr"][:, s]
+        pr["state"][f] = A.HB_PR_PROBE
+        pr["match"][f] = g["last_index"][f] if s == 0 else 0
+        pr["next"][f] = g["last_index"][f] + np.uint64(1)
+    return g, runs
+
+
+def mixed_batch(groups, step=0, seed=0x5EED0007):
+    """One Ready cycle of the mixed node, in one batch (X mode: it carries
+    m.Commit): every led group takes a proposal (dense props) and its n - 1
+    followers' MsgAppResp for it (the cfg2 step); every followed group takes
+    its leader's MsgApp (one entry at the Term, Index = LogTerm's index = the
+    follower's last, Commit = the leader's commit) and MsgHeartbeat (the follow
+    step); all in one random permutation of the arrival stream.  Step k
+    continues where step k-1 left every group.  Returns the batch and the
+    per-step increments of index / commit (inputs stay resident in a bench)."""
+    G = len(groups)
+    n = int(groups["n"][0])
+    rng = np.random.default_rng(seed + 7919 * step)
+    led = np.nonzero(groups["state"] == A.HB_STATE_LEADER)[0].astype(np.uint32)
+    fol = np.nonzero(groups["state"] == A.HB_STATE_FOLLOWER)[0].astype(np.uint32)
+    nf = n - 1
+    g_ack = np.repeat(led, nf)
+    s_ack = np.tile(np.arange(1, n, dtype=np.uint32), len(led))
+    grp = np.concatenate([g_ack, fol, fol])
+    typ = np.concatenate([np.full(len(g_ack), A.HB_MSG_APP_RESP, np.uint32), np.full(len(fol), A.HB_MSG_APP, np.uint32),
+                          np.full(len(fol), A.HB_MSG_HEARTBEAT, np.uint32)])
+    frm = np.concatenate([s_ack, np.ones(2 * len(fol), np.uint32)])
+    perm = rng.permutation(len(grp))
+    grp, typ, frm = grp[perm], typ[perm], frm[perm]
+    ack, app, beat = typ == A.HB_MSG_APP_RESP, typ == A.HB_MSG_APP, typ == A.HB_MSG_HEARTBEAT
+    last = groups["last_index"][grp].astype(np.uint64)
+    term = groups["term"][grp].astype(np.uint64)
+    k = np.uint64(step)
+    index = np.where(ack, last + k + np.uint64(1), np.where(app, last + k, 0)).astype(np.uint64)
+    commit = np.where(ack, 0, last + k).astype(np.uint64)
+    hint = np.where(app, term, 0).astype(np.uint64)
+    ne = app.astype(np.uint64)
+    eoff = np.concatenate([[0], np.cumsum(ne)[:-1]]).astype(np.uint64)
+    props = np.zeros(G, np.uint32)
+    props[led] = 1
+    b = dict(group=grp.astype(np.uint32), info=(typ | (frm << np.uint32(4))).astype(np.uint32), term=term, index=index,
+             hint=hint, commit=commit, eoff=eoff, eterm=term[app].copy(), props=props)
+    inc = dict(index=(ack | app).astype(np.uint64), commit=(app | beat).astype(np.uint64))
+    return b, inc
+
+
 def many_runs_groups(G, n=3, seed=9, runs_lo=18, runs_hi=30, run_len=40):
     """Followers whose logs hold runs_lo..runs_hi term runs of 1..run_len
     entries (the follower side's raftLog.term at any depth); every group's

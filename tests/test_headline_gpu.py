@@ -99,3 +99,33 @@ def test_follow_workload_full_size():
         assert st[abi.HB_STAT_COMMITS] == G_HEAD and st[abi.HB_STAT_ENTRIES] == G_HEAD
         assert st[abi.HB_STAT_MSGS] == 2 * G_HEAD and st[abi.HB_STAT_FAULTS] == 0
         assert np.array_equal(now["last_index"], g["last_index"] + np.uint64(step + 1))
+
+
+@pytest.mark.timeout(900)
+def test_mixed_workload_full_size():
+    """bench.py --workload mixed at its size: 1,048,576 groups x 3, this node
+    leading 1/3 (a proposal + both followers' MsgAppResp) and following 2/3 (its
+    leader's MsgApp with one entry + MsgHeartbeat), all in ONE X-mode batch
+    (raft/multinode.go:233-237: one Ready cycle steps both roles); two steps
+    against the oracle (16 shards): every event, statistic and group record."""
+    g, runs = synth.mixed_groups(G_HEAD, 3, seed=0x5EED0007, with_runs="flat")
+    n_led = int((g["state"] == abi.HB_STATE_LEADER).sum())
+    pair = Pair(g, runs, 3, 256, max_batch=2 * G_HEAD, oracle_shards=16)
+    for step in range(2):
+        b, _ = synth.mixed_batch(g, step, seed=0x5EED0007)
+        _, st, now = pair.step(b, ctx=f"mixed step {step}", check_inflights=False)
+        assert st[abi.HB_STAT_COMMITS] == G_HEAD and st[abi.HB_STAT_ENTRIES] == G_HEAD
+        assert st[abi.HB_STAT_APPRESP] == 2 * n_led and st[abi.HB_STAT_FAULTS] == 0
+        assert np.array_equal(now["last_index"], g["last_index"] + np.uint64(step + 1))
+
+
+@pytest.mark.timeout(900)
+def test_follow_workload_n5_full_size():
+    """bench.py --workload follow --replicas 5 at its size: 1,048,576 followed
+    groups x 5, MsgApp + MsgHeartbeat each per step, against the oracle."""
+    g, runs = synth.follow_groups(G_HEAD, 5, seed=0x5EED0006, with_runs="flat")
+    pair = Pair(g, runs, 5, 256, max_batch=2 * G_HEAD, oracle_shards=16)
+    for step in range(2):
+        _, st, now = pair.step(synth.follow_batch(g, step), ctx=f"follow n5 step {step}", check_inflights=False)
+        assert st[abi.HB_STAT_COMMITS] == G_HEAD and st[abi.HB_STAT_MSGS] == 2 * G_HEAD
+        assert st[abi.HB_STAT_FAULTS] == 0

@@ -16,7 +16,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SUITES = ["tests/test_storage.py", "tests/test_oracle_kat.py", "tests/test_wire.py", "tests/test_tick.py",
-          "tests/test_workloads.py"]
+          "tests/test_workloads.py", "tests/test_route.py"]
 
 
 def _runtime(name):
