@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "hipbatch_kernels.h"
@@ -1726,16 +1727,31 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
 // (the follower side of a node with n >= 5 replicas: about (n-1)/n of its
 // groups), the slots' {m.LogTerm, m.Commit} extensions staged beside them.
 constexpr uint32_t FOLLOW_SLOTS = 4;
+// Leaders' Match / Next in LDS (LeadLaneL) or in registers (LeadLane), per n
+#ifndef HB_LEAD_LDS5
+#define HB_LEAD_LDS5 1
+#endif
+#ifndef HB_LEAD_LDS7
+#define HB_LEAD_LDS7 1
+#endif
+template <int NMAX> struct LeadOf {
+  static constexpr bool LDS = NMAX <= 5 ? HB_LEAD_LDS5 : HB_LEAD_LDS7;
+  using T = typename std::conditional<LDS, LeadLaneL<NMAX>, LeadLane<NMAX>>::type;
+};
 template <int NMAX, bool X>
 __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAVES) k_apply_lead(ApplyArgs a) {
   constexpr uint32_t KS = route_kmax(NMAX);
   constexpr uint32_t FS = X ? FOLLOW_SLOTS : 1u;
+  constexpr bool LDS = LeadOf<NMAX>::LDS;
   __shared__ uint32_t l_fill, l_pfill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint32_t l_eflag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
   __shared__ uint4 l_slot[KS][PART];  // the lane's route slots, read once (as in k_elect)
-  __shared__ uint4 l_slotx[FS][PART];  // X mode: a follower's slot extensions
+  // per lane, one 16-byte word per slot: a leader's {Match, Next} (LeadLaneL) or,
+  // X mode, a follower's slot extensions {m.LogTerm, m.Commit} — a lane is one or the other
+  constexpr uint32_t LW = LDS ? (NMAX > FS ? NMAX : FS) : (X ? FS : 1u);
+  __shared__ uint4 l_lane[LW][(LDS || X) ? PART : 1];
   const uint32_t part = block_part(a.sis_log);
   if (part >= a.NB) return;  // uniform: grid padding
   const uint32_t tid = threadIdx.x;
@@ -1745,9 +1761,10 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   if (tid <= ST_N) l_stats[tid] = 0;
   if (tid < FLAG_WORDS) l_flag[tid] = l_eflag[tid] = 0;
 
-  FollowLane<NMAX, LeadLane<NMAX>> L;
+  FollowLane<NMAX, typename LeadOf<NMAX>::T> L;
   L.S = a.S;
   L.g = g;
+  if constexpr (LDS) L.lp = &l_lane[0][tid];
   L.mlo = gvalid ? reinterpret_cast<const uint32_t*>(a.S.meta)[2 * (size_t)g] : 0u;
   const uint32_t prop_raw = (a.props && gvalid) ? a.props[g] : 0u;
   const uint32_t cnt = gvalid ? a.cnt[g] : 0u;
@@ -1774,7 +1791,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   if constexpr (X) {
 #pragma unroll
     for (uint32_t k = 0; k < FS; ++k)
-      if (fol && k < cnt) l_slotx[k][tid] = at32(a.slotx, k * a.S.G + g);
+      if (fol && k < cnt) l_lane[k][tid] = at32(a.slotx, k * a.S.G + g);
   }
   if (spec) L.load();
   if (fol) {
@@ -1854,7 +1871,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
       uint32_t inf, morig;
       uint64_t mterm, mindex;
       slot_unpack(l_slot[ks][tid], a.side, &inf, &morig, &mterm, &mindex);
-      const uint4 ext = l_slotx[ks < FS ? ks : 0][tid];
+      const uint4 ext = l_lane[ks < FS ? ks : 0][(LDS || X) ? tid : 0];
       const uint64_t lt = (uint64_t)ext.x | ((uint64_t)ext.y << 32), mc = (uint64_t)ext.z | ((uint64_t)ext.w << 32);
       const uint32_t from = (inf >> 4) & 0xF;
       if (!L.takes_follow(inf, from, mterm, mindex, lt, mc)) {
