@@ -630,12 +630,6 @@ enum { ST_MSGS, ST_APPRESP, ST_VOTERESP, ST_DROPPED, ST_COMMITS, ST_WON, ST_LOST
 #ifndef HB_FAST_WAVES
 #define HB_FAST_WAVES 4
 #endif
-#ifndef HB_FAST5_WAVES  // k_apply_fast<5>
-#define HB_FAST5_WAVES 2
-#endif
-#ifndef HB_FAST7_WAVES  // k_apply_fast<7>
-#define HB_FAST7_WAVES 2
-#endif
 constexpr uint32_t FLAG_WORDS = PART / 32;  // per-partition bitmask of groups handed to k_apply
 constexpr uint32_t KPL = 64;                // bucket key bytes scanned per lane per segment
 constexpr uint32_t SEG = PART * KPL;        // positions per key-scan segment
@@ -1187,8 +1181,10 @@ __device__ __forceinline__ void fast_close(const ApplyArgs& a, uint32_t part, co
     a.el_list[(size_t)xs * a.NB + atomicAdd(&a.el_cnt[xs * CTR_STRIDE], 1u)] = part;
 }
 
+// (n = 3 only: n >= 5 runs k_apply_lead)
 template <int NMAX, bool X, uint32_t KMAX>  // KMAX: one MsgAppResp per follower per batch (+ a MsgProp)
-__global__ void __launch_bounds__(PART, (NMAX <= 3 ? HB_FAST_WAVES : (NMAX <= 5 ? HB_FAST5_WAVES : HB_FAST7_WAVES))) k_apply_fast(ApplyArgs a) {
+__global__ void __launch_bounds__(PART, HB_FAST_WAVES) k_apply_fast(ApplyArgs a) {
+  static_assert(NMAX <= 3, "n >= 5 leaders and followers step in k_apply_lead");
   __shared__ uint32_t l_fill, l_pfill;
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint32_t l_eflag[FLAG_WORDS];
@@ -1799,7 +1795,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
     L.load_follow();
   }
   bool loaded = spec, higher = false;
-  if (slots && !spec) {  // a busy leader without a proposal: load it unless a higher term steps it down
+  if (slots && !spec && !fol) {  // a busy leader without a proposal: load it unless a higher term steps it down
     const uint64_t t = at32(a.S.term, g);
 #pragma unroll
     for (uint32_t k = 0; k < KS; ++k) {

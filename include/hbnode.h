@@ -147,6 +147,12 @@ const char* hbn_last_error(void);
 int hbn_storage_new(hbn_storage** out);                       /* NewMemoryStorage :75-80 */
 /* &MemoryStorage{ents: ents} as the reference's tests build it (ents[0] is the dummy). */
 int hbn_storage_new_with_entries(const hbn_entry* ents, uint64_t n, hbn_storage** out);
+/* Memory: the entries of every storage (and of every node's unstable log) live
+ * in 512- and 64-byte blocks from process-wide block pools (1 GiB MAP_NORESERVE
+ * regions carved into 2 MiB chunks).  A freed block returns to the pool's free
+ * lists, not to the system: hbn_storage_free / hbn_stop / Compact make the
+ * memory reusable by later storages in the same process, while the process
+ * keeps its peak entry memory mapped for its lifetime. */
 int hbn_storage_free(hbn_storage* s);
 int hbn_storage_initial_state(hbn_storage* s, hbn_hard_state* hs, uint64_t* nodes, uint32_t cap, uint32_t* n_nodes);
 int hbn_storage_set_hard_state(hbn_storage* s, const hbn_hard_state* hs);

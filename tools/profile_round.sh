@@ -14,7 +14,9 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT"
 STEPS=${STEPS:-20}
-WA="--workload ${WL:-cfg2}"
+# WL=<workload>[:<replicas>] (e.g. follow:5)
+SPEC=${WL:-cfg2}; W0=${SPEC%%:*}
+WA="--workload $W0"; [ "$SPEC" != "$W0" ] && WA="$WA --replicas ${SPEC#*:}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
     python3 bench.py $WA --steps "$STEPS" --warmup 5 --no-cpu-baseline > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
 echo "trace done"
