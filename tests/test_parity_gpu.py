@@ -606,7 +606,7 @@ def test_fast_lanes_hand_over_commit_zero_groups():
     pair = Pair(g, runs, 3, 256, max_batch=1 << 15)
     _, st, now = pair.step(synth.cfg2_batch(g, 0, seed=42), ctx="cfg2 commit_zero")
     assert st[abi.HB_STAT_COMMITS] == 4096 and not now["commit_zero"].any()
-    f, fruns = synth.follow_groups(4096, 3, seed=43, last_hi=1 << 12)
+    f, fruns = synth.follow_groups(4096, 3, seed=43, last_hi=1 << 12, with_runs=True)
     f["commit_zero"] = (np.arange(4096) % 2).astype(np.uint32)
     pair = Pair(f, fruns, 3, 256, max_batch=1 << 15, term_runs=True)
     b = synth.follow_batch(f, 0, seed=44)
@@ -637,7 +637,7 @@ def test_follower_lane_commit_past_log_end(seed):
     lane must not take it; the general lane reports HB_FAULT_COMMIT_RANGE, as
     the oracle does.  Directed groups plus a fuzz that mixes such probes into
     the X-mode follow stream."""
-    f, fruns = synth.follow_groups(2048, 3, seed=seed, last_hi=1 << 12)
+    f, fruns = synth.follow_groups(2048, 3, seed=seed, last_hi=1 << 12, with_runs=True)
     pair = Pair(f, fruns, 3, 256, max_batch=1 << 15, term_runs=True)
     G = 2048
     grp = np.arange(G, dtype=np.uint32)
@@ -655,7 +655,7 @@ def test_follower_lane_commit_past_log_end(seed):
     assert (now["fault"][k != 0] == 0).all()
     assert st[abi.HB_STAT_FAULTS] == int((k == 0).sum())
     # fuzz: the follower-side generator with past-end probes, over fresh followers
-    f2, fruns2 = synth.follow_groups(3000, 3, seed=seed + 100, last_hi=1 << 10)
+    f2, fruns2 = synth.follow_groups(3000, 3, seed=seed + 100, last_hi=1 << 10, with_runs=True)
     pair2 = Pair(f2, fruns2, 3, 256, max_batch=1 << 15, term_runs=True)
     now = pair2.og.groups()
     for j in range(3):
