@@ -83,6 +83,8 @@ class NativeRouter:
     splitmix64(id) % world, local slot = position among the rank's ids)."""
 
     def __init__(self, group_ids, world, threads=0):
+        # (a process that also uses the GPU through torch imports torch first, so
+        # that libhbnode's engine library binds to torch's HIP runtime)
         import ctypes as C
         from .multinode import lib
         self._L = L = lib()
