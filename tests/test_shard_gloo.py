@@ -48,10 +48,16 @@ def _worker(rank, world, port, out):
         sm = ShardMap(ids, world, rank)
         local = sm.local_ids.astype(np.int64)
         og = OracleGroups(g[local], [runs[i] for i in local], 256)
-        # route the arrival-ordered batch: this rank's messages, order kept
-        idx = sm.route(b["group"].astype(np.uint64))[rank]
+        # route the arrival-ordered batch: this rank's messages, order kept — by the
+        # host router of libhbnode (include/hbroute.h), checked against ShardMap
+        from etcd_amd.shard import NativeRouter
+        routed, unknown = NativeRouter(ids, world).route(b["group"].astype(np.uint64), ranks=[rank])
+        idx, slots = routed[rank]
+        idx = idx.astype(np.int64)
+        assert unknown == 0 and np.array_equal(idx, sm.route(b["group"].astype(np.uint64))[rank])
         lb = {k: (v[idx] if (v is not None and k != "props") else v) for k, v in b.items()}
-        lb["group"] = sm.local_slot(b["group"][idx].astype(np.uint64)).astype(np.uint32)
+        lb["group"] = slots
+        assert np.array_equal(slots, sm.local_slot(b["group"][idx].astype(np.uint64)).astype(np.uint32))
         lb["props"] = b["props"][local]
         _, st = og.step(lb)
         t = torch.from_numpy(st.astype(np.int64))
