@@ -75,11 +75,19 @@ struct FastLane {
   // The loads that depend on nothing the lane reads (k_apply_fast issues them
   // with meta itself, in its first round trip) ...
   __device__ __forceinline__ void load_head() {
+    load_state_head();
+    load_pm();
+  }
+  // (the per-group fields, which every role steps with, and the packed
+  // Progress states, which only a leader reads)
+  __device__ __forceinline__ void load_state_head() {
     term = at32(S.term, g);
     committed = at32(S.commit, g);
     first = at32(S.first, g);
     last = at32(S.last, g);
     tfirst = at32(S.tfirst, g);
+  }
+  __device__ __forceinline__ void load_pm() {
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) pm[s] = at32(S.pm, s * S.G + g);
   }

@@ -52,6 +52,12 @@ struct LeadLane : FastLane<NMAX> {
     return type == HB_MSG_APP_RESP || type == HB_MSG_HEARTBEAT_RESP || type == HB_MSG_UNREACHABLE ||
            type == HB_MSG_SNAP_STATUS || type == HB_MSG_VOTE_RESP;
   }
+  // head: the per-group fields were loaded already (load_state_head)
+  __device__ __forceinline__ void load(bool head = false) {
+    if (!head) B::load_state_head();
+    B::load_pm();
+    B::load_rest();
+  }
 
   // One slot's Progress as scalars (a runtime slot: one select per slot and
   // field, so the transitions below exist once in the code, not once per slot).
@@ -364,9 +370,11 @@ struct LeadLaneL : FastLane<NMAX> {
            type == HB_MSG_SNAP_STATUS || type == HB_MSG_VOTE_RESP;
   }
 
-  // FastLane::load_rest with Match / Next into LDS (ring heads not cached)
-  __device__ __forceinline__ void load() {
-    B::load_head();
+  // FastLane::load_rest with Match / Next into LDS (ring heads not cached);
+  // head: the per-group fields were loaded already (load_state_head)
+  __device__ __forceinline__ void load(bool head = false) {
+    if (!head) B::load_state_head();
+    B::load_pm();
 #pragma unroll
     for (int s = 0; s < NMAX; ++s) pm[s] = B::pm[s];
     this->tlast = (this->mlo & (uint32_t)M_TL) ? last : at32(S.tlast, g);
@@ -581,15 +589,43 @@ struct LeadLaneL : FastLane<NMAX> {
       this->ev(HB_EV_SNAP, s, 0, x);
     }
   }
-  __device__ __forceinline__ void bcast() {
-    const uint32_t nn = this->n(), sf = this->self();
+  // The sends to the slots of `mask` in slot order — bcastAppend (every peer
+  // but self) or one sendAppend — at compile-time slots: every decision first
+  // (each slot's {Match, Next} at a constant LDS offset, its state word a
+  // constant register), then the events in slot order (a send emits nothing
+  // itself, so deferring them keeps the order).  A fault stops the slots after
+  // it, as the rolled loop did.
+  __device__ __forceinline__ void sends(uint32_t mask) {
+    uint32_t kind[NMAX];
+    uint64_t xs[NMAX];
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) {
+      kind[s] = B::SEND_NONE;
+      xs[s] = 0;
+      if (((mask >> s) & 1u) && !faulted()) {
+        Pr p = get((uint32_t)s);
+        const Pr p0 = p;
+        kind[s] = send_decide((uint32_t)s, p, &xs[s]);
+        put((uint32_t)s, p, p0);
+      }
+    }
     run_mask = 0;
-#pragma nounroll
-    for (uint32_t s = 0; s < nn; ++s) {
-      if (faulted()) break;
-      if (s != sf) send(s);
+#pragma unroll
+    for (int s = 0; s < NMAX; ++s) {
+      if (kind[s] == B::SEND_APP) {
+        if (run_mask && xs[s] != run_x) run_flush();
+        run_mask |= 1u << s;
+        run_x = xs[s];
+      } else if (kind[s] == B::SEND_SNAP) {
+        run_flush();
+        this->ev(HB_EV_SNAP, s, 0, xs[s]);
+      }
     }
     run_flush();
+  }
+  __device__ __forceinline__ void bcast() {
+    const uint32_t nn = this->n(), sf = this->self();
+    sends(((1u << nn) - 1) & ~(1u << sf));
   }
 
   // MsgProp with k entries on a leader: stepLeader raft/raft.go:500-513 ->
@@ -690,15 +726,14 @@ struct LeadLaneL : FastLane<NMAX> {
       }
     }  // MsgVoteResp: a leader ignores it
     put(from, p, p0);
-    if (updated) {  // maybeCommit -> bcastAppend, else a paused follower gets sendAppend
-      if (maybe_commit()) bcast();
-      else if (old_paused) send_one = true;
+    // maybeCommit -> bcastAppend, else a paused follower gets sendAppend: one
+    // send pass either way
+    uint32_t mask = send_one ? 1u << from : 0u;
+    if (updated) {
+      if (maybe_commit()) mask = ((1u << this->n()) - 1) & ~(1u << this->self());
+      else if (old_paused) mask = 1u << from;
     }
-    if (send_one && !faulted()) {
-      run_mask = 0;
-      send(from);
-      run_flush();
-    }
+    if (mask && !faulted()) sends(mask);
     if (faulted()) this->ev(HB_EV_FAULT, 0, faulted(), this->arrival_x());
   }
 };
