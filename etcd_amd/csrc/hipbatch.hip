@@ -1182,14 +1182,6 @@ __device__ __forceinline__ void fast_close(const ApplyArgs& a, uint32_t part, co
 }
 
 // (n = 3 only: n >= 5 runs k_apply_lead)
-//
-// X mode (a MultiNode node's batch: it leads some of a partition's groups and
-// follows the others): the leader and follower lanes run different code, and a
-// wave holding both runs both, one after the other.  So a partition whose
-// waves mix the two roles re-deals its groups to the threads, leaders first,
-// then followers, then the rest (stable): the loads of meta's round trip are
-// exchanged through LDS (no reload), and each thread then steps the group it
-// was dealt (events, flags and stores name the group, not the thread).
 template <int NMAX, bool X, uint32_t KMAX>  // KMAX: one MsgAppResp per follower per batch (+ a MsgProp)
 __global__ void __launch_bounds__(PART, HB_FAST_WAVES) k_apply_fast(ApplyArgs a) {
   static_assert(NMAX <= 3, "n >= 5 leaders and followers step in k_apply_lead");
@@ -1197,20 +1189,12 @@ __global__ void __launch_bounds__(PART, HB_FAST_WAVES) k_apply_fast(ApplyArgs a)
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint32_t l_eflag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
-  // X mode: the role deal (class counts per wave, the dealt group of each
-  // thread, and meta's round trip of every group for the exchange)
-  constexpr uint32_t XP = X ? PART : 1u;
-  __shared__ uint32_t l_wc[X ? PART / 64 : 1][4];
-  __shared__ uint32_t l_src[XP];
-  __shared__ uint64_t l_x64[5][XP];
-  __shared__ uint32_t l_x32[NMAX + 3][XP];
 
   const uint32_t part = block_part(a.sis_log);
   if (part >= a.NB) return;  // uniform: grid padding
   const uint32_t tid = threadIdx.x;
-  uint32_t lane = tid;  // the group this thread steps: part * PART + lane
-  uint32_t g = part * PART + tid;
-  bool gvalid = g < a.S.G;
+  const uint32_t g = part * PART + tid;
+  const bool gvalid = g < a.S.G;
   if (tid == 0) l_fill = l_pfill = 0;
   if (tid <= ST_N) l_stats[tid] = 0;
   if (tid < FLAG_WORDS) l_flag[tid] = l_eflag[tid] = 0;
@@ -1220,81 +1204,27 @@ __global__ void __launch_bounds__(PART, HB_FAST_WAVES) k_apply_fast(ApplyArgs a)
   L.S = a.S;
   L.g = g;
   L.mlo = gvalid ? at32(reinterpret_cast<uint32_t*>(a.S.meta), 2 * g) : 0u;
-  uint32_t prop_raw = (a.props && gvalid) ? at32(a.props, g) : 0u;
-  uint32_t cnt = gvalid ? at32(a.cnt, g) : 0u;
+  const uint32_t prop_raw = (a.props && gvalid) ? at32(a.props, g) : 0u;
+  const uint32_t cnt = gvalid ? at32(a.cnt, g) : 0u;
   // The state that depends on nothing is loaded beside meta (one round trip
   // fewer for every leader; a group with no fast-path work wastes 52 bytes)
   if (gvalid) L.load_head();
-  // the roles, from meta's round trip:
   // A group takes part when its slot is live (n > 0) and not faulted.
+  const bool live = gvalid && L.n() != 0 && L.faulted() == 0;
   // Only a leader has fast-path work: any other live group is handed to
   // k_apply whole, without loading its state here (resume bit 30: commit0 =
   // its committed as k_apply loads it).
-  // A group that has not stepped since an empty HardState (r.Commit = 0, M_NC)
-  // is the general lane's: its first Step sets r.Commit.
-  // A leader the fast path cannot finish (more messages than slots) and
+  const bool leader = live && L.state() == HB_STATE_LEADER;
+  // a group that has not stepped since an empty HardState (r.Commit = 0, M_NC)
+  // is the general lane's: its first Step sets r.Commit
+  const bool nc = (L.mlo & (uint32_t)M_NC) != 0;
+  // a leader the fast path cannot finish (more messages than slots) and
   // without a dense proposal is handed over whole, its state unloaded (cfg4:
-  // every group; k_elect / k_apply load it).
+  // every group; k_elect / k_apply load it)
+  const bool lead = leader && !nc && (cnt <= KMAX || prop_raw != 0);
   // X mode: a follower whose messages all sit in its slots and that has no
-  // dense proposal (stepFollower MsgProp forwards it: the general lane).
-  bool live, leader, lead, fol;
-  auto roles = [&]() {
-    live = gvalid && L.n() != 0 && L.faulted() == 0;
-    leader = live && L.state() == HB_STATE_LEADER;
-    const bool nc = (L.mlo & (uint32_t)M_NC) != 0;
-    lead = leader && !nc && (cnt <= KMAX || prop_raw != 0);
-    fol = X && live && !nc && L.state() == HB_STATE_FOLLOWER && cnt > 0 && cnt <= KMAX && prop_raw == 0;
-  };
-  roles();
-  if constexpr (X) {
-    const uint32_t cls = lead ? 0u : (fol ? 1u : 2u);
-    const uint64_t bl = __ballot(cls == 0), bf = __ballot(cls == 1);
-    const bool mixed = (bl != 0 && bl != ~0ull) || (bf != 0 && bf != ~0ull);
-    if (__syncthreads_or(mixed)) {  // uniform: some wave of the partition holds two roles
-      const uint32_t wave = tid >> 6, wl = tid & 63;
-      const uint64_t mine = cls == 0 ? bl : (cls == 1 ? bf : ~(bl | bf));
-      if (wl == 0) {
-        l_wc[wave][0] = (uint32_t)__popcll(bl);
-        l_wc[wave][1] = (uint32_t)__popcll(bf);
-        l_wc[wave][2] = 64u - (uint32_t)__popcll(bl | bf);
-      }
-      l_x64[0][tid] = L.term;
-      l_x64[1][tid] = L.committed;
-      l_x64[2][tid] = L.first;
-      l_x64[3][tid] = L.last;
-      l_x64[4][tid] = L.tfirst;
-#pragma unroll
-      for (int s = 0; s < NMAX; ++s) l_x32[s][tid] = L.pm[s];
-      l_x32[NMAX][tid] = L.mlo;
-      l_x32[NMAX + 1][tid] = prop_raw;
-      l_x32[NMAX + 2][tid] = cnt;
-      __syncthreads();
-      uint32_t pos = 0;  // classes in order, waves in order, lanes in order: a stable deal
-#pragma unroll
-      for (uint32_t c = 0; c < 3; ++c)
-#pragma unroll
-        for (uint32_t w = 0; w < PART / 64; ++w)
-          pos += (c < cls || (c == cls && w < wave)) ? l_wc[w][c] : 0u;
-      pos += mbcnt64(mine);
-      l_src[pos] = tid;
-      __syncthreads();
-      lane = l_src[tid];
-      g = part * PART + lane;
-      gvalid = g < a.S.G;
-      L.g = g;
-      L.term = l_x64[0][lane];
-      L.committed = l_x64[1][lane];
-      L.first = l_x64[2][lane];
-      L.last = l_x64[3][lane];
-      L.tfirst = l_x64[4][lane];
-#pragma unroll
-      for (int s = 0; s < NMAX; ++s) L.pm[s] = l_x32[s][lane];
-      L.mlo = l_x32[NMAX][lane];
-      prop_raw = l_x32[NMAX + 1][lane];
-      cnt = l_x32[NMAX + 2][lane];
-      roles();
-    }
-  }
+  // dense proposal (stepFollower MsgProp forwards it: the general lane)
+  const bool fol = X && live && !nc && L.state() == HB_STATE_FOLLOWER && cnt > 0 && cnt <= KMAX && prop_raw == 0;
   L.dirty = 0;
   L.nev = 0;
   if (lead) {
@@ -1327,7 +1257,7 @@ __global__ void __launch_bounds__(PART, HB_FAST_WAVES) k_apply_fast(ApplyArgs a)
     s_c[k] = (uint64_t)x.z | ((uint64_t)x.w << 32);
   }
   uint32_t vals[ST_N + 1];
-  (void)fast_step<NMAX, KMAX>(a, L, part, lane, live, lead, leader, fol, prop_raw, cnt, s_info, s_orig, s_term, s_index, s_h,
+  (void)fast_step<NMAX, KMAX>(a, L, part, tid, live, lead, leader, fol, prop_raw, cnt, s_info, s_orig, s_term, s_index, s_h,
                         s_c, a.ev_off[2 * part + 1], &l_pfill, &l_fill, l_flag, l_eflag, vals);
   reduce_stats(a, l_stats, vals);
   if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
