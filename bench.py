@@ -1065,6 +1065,10 @@ def run_aux(args, world, rank, local, dev, torch, dist):
             d = [torch.from_numpy(b[f].view(np.int32 if b[f].dtype == np.uint32 else np.int64)).to(dev)
                  for f in ("group", "info", "term", "index", "hint", "props")]
             torch.cuda.synchronize()
+            # a device-side wait (~1 ms) ahead of e0: the step's launches queue behind it, so the
+            # timed region is the device step, not the host's launch latency from an idle GPU
+            # (the other lines hide it by running their steps back to back)
+            torch.cuda._sleep(2_000_000)
             e0.record(stream)
             eng.step(*d, host=False)
             e1.record(stream)
@@ -1072,7 +1076,8 @@ def run_aux(args, world, rank, local, dev, torch, dist):
             if k >= args.warmup:
                 ms_local += e0.elapsed_time(e1)
                 st_acc += eng.stats()
-        timing = "sum of per-step HIP event times (stream generation from the engine state between steps excluded)"
+        timing = ("sum of per-step HIP event times, each step's launches queued behind a device-side wait "
+                  "(stream generation from the engine state between steps excluded)")
     ms_t = torch.tensor([ms_local], dtype=torch.float64, device=dev)
     st_t = torch.from_numpy(st_acc.view(np.int64).copy()).to(dev)
     if world > 1:
