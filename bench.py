@@ -342,7 +342,7 @@ def run_multinode(args):
                             C.POINTER(C.c_double)]
     out = (C.c_double * 32)()
     bulk = args.mn_mode == "bulk"
-    flags = 3 if bulk else 0  # HBNB_BULK | HBNB_PAR_APP
+    flags = (3 if bulk else 0) | (0 if args.mn_no_pin else 4)  # HBNB_BULK | HBNB_PAR_APP, HBNB_PIN
     threads = args.mn_threads if bulk else 1
     t0 = time.perf_counter()
     rc = L.hbnb_run2(int(os.environ.get("LOCAL_RANK", "0")), G, n, args.warmup, args.steps, flags, threads, out)
@@ -361,7 +361,8 @@ def run_multinode(args):
            "commits_per_s": adv / secs,
            "api": ("hbn_step_many + hbn_propose_many, host threads "
                    f"{threads or 'default (min(16, cores))'}, application persists from the same number of threads"
-                   if bulk else "one hbn_step / hbn_propose call per message, one host thread"),
+                   if bulk else "one hbn_step / hbn_propose call per message, one host thread") +
+                  ("" if args.mn_no_pin else "; the application's Ready-loop thread pinned to its CPU"),
            "split_s_per_step": {"ready": out[3] / args.steps, "step_and_propose": out[4] / args.steps,
                                 "append_and_advance": out[5] / args.steps,
                                 "of_which_app_persist": out[24] / args.steps},
@@ -447,6 +448,8 @@ def main():
     ap.add_argument("--mn-mode", choices=["bulk", "percall"], default="bulk",
                     help="multinode: bulk = hbn_step_many / hbn_propose_many + host threads (default), "
                          "percall = one API call per message on one thread (the r01/r02 path, for A/B)")
+    ap.add_argument("--mn-no-pin", action="store_true",
+                    help="multinode: leave the application's Ready-loop thread unpinned")
     ap.add_argument("--mn-threads", type=int, default=0, help="multinode bulk: host threads (0 = library default)")
     ap.add_argument("--traffic-json", default=None,
                     help="profiles/<tag>_traffic.json from tools/profile_round.sh (default: newest in profiles/)")

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <random>
+#include <sched.h>
 #include <thread>
 #include <vector>
 
@@ -36,6 +37,9 @@ extern "C" {
 // node's host threads too (hbn_set_threads; 0 = the library default).
 #define HBNB_BULK 1u
 #define HBNB_PAR_APP 2u
+// HBNB_PIN: the application pins its Ready-loop thread to the CPU it starts on
+// (before hbn_start, whose small-phase worker then shares that CPU's L3)
+#define HBNB_PIN 4u
 int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t rounds, uint32_t flags,
               uint32_t threads, double* out);
 int hbnb_run(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t rounds, double* out) {
@@ -45,6 +49,21 @@ int hbnb_run(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t round
 int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t rounds, uint32_t flags,
               uint32_t threads, double* out) {
   if (G == 0 || n < 2 || n > HB_MAX_REPLICAS || !out) return HB_EINVAL;
+  cpu_set_t old_mask;
+  const bool pinned = (flags & HBNB_PIN) && sched_getaffinity(0, sizeof(old_mask), &old_mask) == 0;
+  if (pinned) {
+    cpu_set_t one;
+    CPU_ZERO(&one);
+    CPU_SET(sched_getcpu(), &one);
+    (void)sched_setaffinity(0, sizeof(one), &one);
+  }
+  struct Unpin {
+    bool on;
+    cpu_set_t* m;
+    ~Unpin() {
+      if (on) (void)sched_setaffinity(0, sizeof(*m), m);
+    }
+  } unpin{pinned, &old_mask};
   hbn_node* mn = nullptr;
   const uint64_t max_batch = (uint64_t)G * n + 16;
   int rc = hbn_start(device, 1, G, n, 256, HB_NO_LIMIT, max_batch, &mn);
@@ -116,7 +135,10 @@ int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t roun
       std::vector<int> er(app_threads);
       std::vector<std::thread> th;
       for (uint32_t t = 0; t < app_threads; ++t)
-        th.emplace_back([&, t] { er[t] = persist(cnt * t / app_threads, cnt * (t + 1) / app_threads, &f[t], &ce[t], &av[t]); });
+        th.emplace_back([&, t] {
+          if (pinned) (void)sched_setaffinity(0, sizeof(old_mask), &old_mask);  // (not the loop thread's CPU)
+          er[t] = persist(cnt * t / app_threads, cnt * (t + 1) / app_threads, &f[t], &ce[t], &av[t]);
+        });
       for (auto& x : th) x.join();
       for (uint32_t t = 0; t < app_threads; ++t) {
         if (er[t]) return er[t];

@@ -376,10 +376,13 @@ __device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_
 #define HB_SCAT_TPW 2
 #endif
 constexpr uint32_t SCAT_TPW = HB_SCAT_TPW;
-template <bool FINAL, bool X>
-__global__ void __launch_bounds__(RDX_THREADS) __attribute__((amdgpu_waves_per_eu(8))) k_radix_scatter(RadixSrc s, RadixDst d, FinalDst f, uint32_t G,
-                                                              uint32_t shift, uint32_t dbits, uint32_t ntiles, const uint32_t* off,
-                                                              const uint32_t* totals, uint32_t* n_valid) {
+// The scatter of TPW consecutive tiles from tile0 (`first`: the workgroup that
+// writes n_valid and the one-pass bucket bounds); `off` / `totals` may be LDS.
+template <bool FINAL, bool X, uint32_t TPW>
+__device__ __forceinline__ void scatter_tiles(const RadixSrc& s, const RadixDst& d, const FinalDst& f, uint32_t G,
+                                              uint32_t shift, uint32_t dbits, uint32_t ntiles, uint32_t tile0,
+                                              const uint32_t* off, const uint32_t* totals, uint32_t* n_valid,
+                                              bool first) {
   __shared__ uint32_t s_base[RDX_BINS];  // digit base in the pass output (exclusive scan of the totals)
   __shared__ uint32_t s_off[RDX_BINS];
   __shared__ uint32_t s_wcnt[RDX_WAVES][RDX_BINS];
@@ -397,7 +400,6 @@ __global__ void __launch_bounds__(RDX_THREADS) __attribute__((amdgpu_waves_per_e
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const uint32_t nb = 1u << dbits;  // the pass's digits (totals / off rows hold nb)
   const uint32_t n = src_n(s);
-  const uint32_t tile0 = blockIdx.x * SCAT_TPW;
   ScatTile<X> cur, nxt;
   scat_load(s, n, G, tile0 * RDX_TILE, wave, lane, cur);
   {
@@ -405,7 +407,7 @@ __global__ void __launch_bounds__(RDX_THREADS) __attribute__((amdgpu_waves_per_e
     uint32_t all;
     const uint32_t excl = excl_scan256(t, sh4, &all);
     if (tid < RDX_BINS) s_base[tid] = excl;
-    if (blockIdx.x == 0) {
+    if (first) {
       if (FINAL && f.bk_off && tid <= f.NBK && tid < RDX_BINS) f.bk_off[tid] = excl;
       if (tid == 0) {
         *n_valid = all;
@@ -414,7 +416,7 @@ __global__ void __launch_bounds__(RDX_THREADS) __attribute__((amdgpu_waves_per_e
     }
   }
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (uint32_t j = 0; j < SCAT_TPW; ++j) {
+  for (uint32_t j = 0; j < TPW; ++j) {
     const uint32_t tile = tile0 + j;
     if (tile >= ntiles) break;  // uniform
     // this tile's digit starts in the output; per-wave digit counters cleared
@@ -426,7 +428,7 @@ __global__ void __launch_bounds__(RDX_THREADS) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (uint32_t r = 0; r < RDX_ROUNDS; ++r) vd[r] = rdx_digit(cur.g[r], shift, dbits);
     // the next tile's loads go out now
-    if (j + 1 < SCAT_TPW && tile + 1 < ntiles) scat_load(s, n, G, (tile + 1) * RDX_TILE, wave, lane, nxt);
+    if (j + 1 < TPW && tile + 1 < ntiles) scat_load(s, n, G, (tile + 1) * RDX_TILE, wave, lane, nxt);
     // stable rank inside the wave: rounds in order, lanes in order
 #pragma unroll
     for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
@@ -536,6 +538,48 @@ __global__ void __launch_bounds__(RDX_THREADS) __attribute__((amdgpu_waves_per_e
     __syncthreads();  // the next tile reuses s_off / s_wcnt / s_dstart / the staging
     cur = nxt;
   }
+}
+template <bool FINAL, bool X>
+__global__ void __launch_bounds__(RDX_THREADS) __attribute__((amdgpu_waves_per_eu(8))) k_radix_scatter(RadixSrc s, RadixDst d, FinalDst f, uint32_t G,
+                                                              uint32_t shift, uint32_t dbits, uint32_t ntiles, const uint32_t* off,
+                                                              const uint32_t* totals, uint32_t* n_valid) {
+  scatter_tiles<FINAL, X, SCAT_TPW>(s, d, f, G, shift, dbits, ntiles, blockIdx.x * SCAT_TPW, off, totals, n_valid,
+                                    blockIdx.x == 0);
+}
+
+// A small one-pass batch (at most SMALL_TILES tiles: a MultiNode node's Ready
+// cycle over a few thousand groups) in ONE workgroup: the tile histograms and
+// their column scan in LDS, then the same scatter — k_radix_hist +
+// k_scan_rows + k_radix_scatter in one launch, the same output.
+constexpr uint32_t SMALL_TILES = 8;
+template <bool X>
+__global__ void __launch_bounds__(RDX_THREADS) k_radix_small(RadixSrc s, FinalDst f, uint32_t G, uint32_t shift,
+                                                            uint32_t ntiles, uint32_t* bk_fill, uint32_t NBK,
+                                                            uint32_t* ctr, uint32_t* n_valid) {
+  __shared__ uint32_t s_hist[SMALL_TILES * RDX_BINS];  // [tile][digit]: counts, then exclusive prefixes
+  __shared__ uint32_t s_tot[RDX_BINS];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < SMALL_TILES * RDX_BINS; i += RDX_THREADS) s_hist[i] = 0;
+  for (uint32_t i = tid; i < NBK; i += RDX_THREADS) bk_fill[i * CTR_STRIDE] = 0;  // (k_scan_rows' clears)
+  for (uint32_t i = tid; i < CTR_WORDS; i += RDX_THREADS) ctr[i] = 0;
+  __syncthreads();
+  const uint32_t n = src_n(s);
+  for (uint32_t i = tid; i < n; i += RDX_THREADS) {
+    const uint32_t g = s.group[i];
+    if (g < G) atomicAdd(&s_hist[(i / RDX_TILE) * RDX_BINS + rdx_digit(g, shift, RDX_BITS)], 1u);
+  }
+  __syncthreads();
+  if (tid < RDX_BINS) {
+    uint32_t run = 0;
+    for (uint32_t t = 0; t < ntiles; ++t) {
+      const uint32_t c = s_hist[t * RDX_BINS + tid];
+      s_hist[t * RDX_BINS + tid] = run;
+      run += c;
+    }
+    s_tot[tid] = run;
+  }
+  __syncthreads();
+  scatter_tiles<true, X, SMALL_TILES>(s, RadixDst{}, f, G, shift, RDX_BITS, ntiles, 0, s_hist, s_tot, n_valid, true);
 }
 
 // bk_off[b] = first position of bucket b in the sorted batch (b <= NBK); the
@@ -2554,6 +2598,34 @@ __global__ void __launch_bounds__(256) k_gather_words(const uint64_t* base, cons
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) o[i] = src[i];
 }
 
+// Both in one workgroup when the chunks are few (a small node: 2 chunks per
+// 256 groups): chunk offsets scanned in LDS, then a wave per chunk copies.
+constexpr uint32_t WORDS_SMALL = 1024;
+__global__ void __launch_bounds__(1024) k_words_small(const uint32_t* counts, uint32_t n, const uint64_t* base,
+                                                      const uint64_t* offs, uint64_t* out, uint64_t cap,
+                                                      uint32_t* h_counts, uint64_t* h_total) {
+  __shared__ uint32_t sh16[16];
+  __shared__ uint64_t s_dst[WORDS_SMALL];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t c = tid < n ? counts[tid] : 0u;
+  uint32_t tot;
+  const uint32_t run = block_excl_scan(c, sh16, &tot);  // total words < 2^32
+  if (tid < n) {
+    s_dst[tid] = run;
+    h_counts[tid] = c;
+  }
+  if (tid == 0) *h_total = tot;
+  __syncthreads();
+  if (tot > cap) return;  // the caller's buffer is too small: counts and total only
+  const uint32_t wave = tid >> 6, lane = tid & 63;
+  for (uint32_t k = wave; k < n; k += 16) {
+    const uint32_t m = counts[k];
+    const uint64_t* src = base + offs[k];
+    uint64_t* o = out + s_dst[k];
+    for (uint32_t i = lane; i < m; i += 64) o[i] = src[i];
+  }
+}
+
 // ============================================================================
 // host side
 // ============================================================================
@@ -2654,6 +2726,10 @@ struct hb_handle {
   uint32_t NBK = 0;               // buckets
   uint32_t sis_log = SIS_LOG_MAX;  // partitions per bucket (log2)
   uint32_t passes = 1;
+  // small steps (a few thousand messages, hb_step / hb_events_to_host): one
+  // launch for the partition and one for the event words; HB_SMALL_STEP=0
+  // turns that off (same output: the A/B and the parity tests compare both)
+  bool no_small = false;
   uint32_t bk_bits = 1;            // bits of a bucket id
   // host-pointer staging
   uint32_t* s_group = nullptr;
@@ -2883,6 +2959,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   h->max_msg_size = max_msg_size;
   h->max_batch = max_batch;
   h->NB = (capacity + PART - 1) / PART;
+  if (const char* e = getenv("HB_SMALL_STEP")) h->no_small = e[0] == '0';
   const size_t G = capacity, R = h->nmax;
   DevState& s = h->st;
   s.G = capacity;
@@ -3623,7 +3700,15 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
                  bd.hint, bd_commit, bd_eoff, bd_eterm, b->n_edesc, nullptr};
     const FinalDst fin{ps.rec, ps.recx, ps.bucket, h->passes == 1 ? ps.bk_off : nullptr, h->NBK, h->sis_log};
     uint32_t shift = PART_LOG + h->sis_log;
-    for (uint32_t p = 0; p < h->passes; ++p) {
+    if (h->passes == 1 && ntiles <= SMALL_TILES && !h->no_small) {  // one launch for the whole partition
+      if (xmode)
+        hipLaunchKernelGGL(k_radix_small<true>, dim3(1), dim3(RDX_THREADS), 0, ps_st, src, fin, h->G, shift, ntiles,
+                           ps.bk_fill, h->NBK, ps.ctr, h->n_valid);
+      else
+        hipLaunchKernelGGL(k_radix_small<false>, dim3(1), dim3(RDX_THREADS), 0, ps_st, src, fin, h->G, shift, ntiles,
+                           ps.bk_fill, h->NBK, ps.ctr, h->n_valid);
+    }
+    for (uint32_t p = 0; p < h->passes && !(h->passes == 1 && ntiles <= SMALL_TILES && !h->no_small); ++p) {
       const bool last_pass = p + 1 == h->passes;
       const RadixDst& dst = h->tmp[p & 1];
       // two passes split the bucket id's bits evenly (the first takes the low
@@ -3797,6 +3882,12 @@ int hb_events_to_host(hb_handle* h, uint64_t* words, uint64_t cap, uint32_t* cou
     h->evw_cap = nc + 1ull;
   }
   const PrepSet& ps = h->set[h->cur];
+  if (nc <= WORDS_SMALL && !h->no_small) {
+    hipLaunchKernelGGL(k_words_small, dim3(1), dim3(1024), 0, h->stream, (const uint32_t*)ps.ev_counts, nc,
+                       (const uint64_t*)h->ev, (const uint64_t*)ps.ev_off, static_cast<uint64_t*>(dw), cap,
+                       static_cast<uint32_t*>(dc), static_cast<uint64_t*>(dt));
+    return hipGetLastError() == hipSuccess ? HB_OK : HB_EDEVICE;
+  }
   hipLaunchKernelGGL(k_scan_words, dim3(1), dim3(1024), 0, h->stream, (const uint32_t*)ps.ev_counts, nc, h->evw,
                      static_cast<uint32_t*>(dc), static_cast<uint64_t*>(dt));
   hipLaunchKernelGGL(k_gather_words, dim3(nc), dim3(256), 0, h->stream, (const uint64_t*)h->ev,

@@ -224,7 +224,10 @@ int hbn_propose_many(hbn_node* n, uint64_t count, const uint64_t* groups, const 
 /* Host threads for the per-group work of a Ready cycle (event replay, Ready
  * assembly, Advance, bulk ingestion); groups are independent, each worker owns
  * a disjoint set.  Default min(16, cores), or the HBN_THREADS environment
- * variable.  The calling thread is one of them. */
+ * variable.  The calling thread is one of them.  Phases below a few thousand
+ * groups run on the caller alone, except the event replay and the Ready
+ * assembly, which take up to HBN_SMALL_WAYS workers (default 2; 1 = the caller
+ * alone) from 512 touched groups / 2048 event words on. */
 int hbn_set_threads(hbn_node* n, uint32_t threads);
 /* Seconds the node's host side spent per phase since hbn_start (diagnostics;
  * out[0..min(cap, *count)), order: load sync, log-index reserve, hb_step call,
