@@ -547,6 +547,71 @@ __global__ void __launch_bounds__(RDX_THREADS) __attribute__((amdgpu_waves_per_e
                                     blockIdx.x == 0);
 }
 
+// One bucket (a node of at most 4,096 groups): the partition is the identity
+// on the kept messages, so the final records are the batch's in arrival order
+// minus the messages beyond capacity — a stable compaction (ballot prefixes
+// per wave, one block scan per tile), no ranking or staging.  Same output as
+// k_radix_small / the tiled kernels.
+template <bool X>
+__global__ void __launch_bounds__(RDX_THREADS) k_pack_one(RadixSrc s, FinalDst f, uint32_t G, uint32_t ntiles,
+                                                         uint32_t* bk_fill, uint32_t NBK, uint32_t* ctr,
+                                                         uint32_t* n_valid) {
+  __shared__ uint32_t s_w[RDX_WAVES];
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (uint32_t i = tid; i < NBK; i += RDX_THREADS) bk_fill[i * CTR_STRIDE] = 0;  // (k_scan_rows' clears)
+  for (uint32_t i = tid; i < CTR_WORDS; i += RDX_THREADS) ctr[i] = 0;
+  const uint32_t n = src_n(s);
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t base = 0;
+  ScatTile<X> cur, nxt;
+  scat_load(s, n, G, 0, wave, lane, cur);
+  for (uint32_t tile = 0; tile < ntiles; ++tile) {
+    if (tile + 1 < ntiles) scat_load(s, n, G, (tile + 1) * RDX_TILE, wave, lane, nxt);
+    // element wave * 64 R + r * 64 + lane: prefixes in (wave, r, lane) order = arrival order
+    uint32_t rank[RDX_ROUNDS], wc = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+      const uint64_t b = __ballot(cur.v[r]);
+      rank[r] = wc + (uint32_t)__popcll(b & lt);
+      wc += (uint32_t)__popcll(b);
+    }
+    if (lane == 0) s_w[wave] = wc;
+    __syncthreads();
+    uint32_t before = base, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < RDX_WAVES; ++w) {
+      const uint32_t c = s_w[w];
+      before += w < wave ? c : 0u;
+      all += c;
+    }
+    __syncthreads();  // (s_w is rewritten by the next tile)
+#pragma unroll
+    for (uint32_t r = 0; r < RDX_ROUNDS; ++r) {
+      if (!cur.v[r]) continue;
+      const uint32_t o = before + rank[r], g = cur.g[r];
+      MsgRec m;
+      m.info = (cur.i[r] & REC_KEEP) | ((g & (PART - 1)) << 16) | (((g >> PART_LOG) & ((1u << f.sis_log) - 1)) << 24);
+      m.orig = cur.o[r];
+      m.ti = cur.t[r];
+      f.rec[o] = m;
+      if constexpr (X) {
+        const uint32_t i = cur.o[r];
+        const uint64_t h = s.hint ? s.hint[i] : 0ull, c = s.mcommit[i];
+        f.recx[o] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)c, (uint32_t)(c >> 32));
+      }
+    }
+    base += all;
+    cur = nxt;
+  }
+  if (tid == 0) {
+    *n_valid = base;
+    if (f.bk_off) {
+      f.bk_off[0] = 0;
+      f.bk_off[1] = base;
+    }
+  }
+}
+
 // A small one-pass batch (at most SMALL_TILES tiles: a MultiNode node's Ready
 // cycle over a few thousand groups) in ONE workgroup: the tile histograms and
 // their column scan in LDS, then the same scatter — k_radix_hist +
@@ -3700,7 +3765,14 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
                  bd.hint, bd_commit, bd_eoff, bd_eterm, b->n_edesc, nullptr};
     const FinalDst fin{ps.rec, ps.recx, ps.bucket, h->passes == 1 ? ps.bk_off : nullptr, h->NBK, h->sis_log};
     uint32_t shift = PART_LOG + h->sis_log;
-    if (h->passes == 1 && ntiles <= SMALL_TILES && !h->no_small) {  // one launch for the whole partition
+    if (h->passes == 1 && h->NBK == 1 && ntiles <= SMALL_TILES && !h->no_small) {  // one bucket: a compaction
+      if (xmode)
+        hipLaunchKernelGGL(k_pack_one<true>, dim3(1), dim3(RDX_THREADS), 0, ps_st, src, fin, h->G, ntiles, ps.bk_fill,
+                           h->NBK, ps.ctr, h->n_valid);
+      else
+        hipLaunchKernelGGL(k_pack_one<false>, dim3(1), dim3(RDX_THREADS), 0, ps_st, src, fin, h->G, ntiles, ps.bk_fill,
+                           h->NBK, ps.ctr, h->n_valid);
+    } else if (h->passes == 1 && ntiles <= SMALL_TILES && !h->no_small) {  // one launch for the whole partition
       if (xmode)
         hipLaunchKernelGGL(k_radix_small<true>, dim3(1), dim3(RDX_THREADS), 0, ps_st, src, fin, h->G, shift, ntiles,
                            ps.bk_fill, h->NBK, ps.ctr, h->n_valid);

@@ -1,5 +1,6 @@
 """Small steps (a MultiNode node's Ready cycle over a few thousand groups):
-the one-workgroup partition (`k_radix_small`: histogram, column scan and
+the one-workgroup partitions (`k_pack_one` for a single 4,096-group bucket: a
+stable compaction; `k_radix_small` otherwise: histogram, column scan and
 scatter of at most 8 tiles of 2048 messages in one launch) and the
 one-workgroup event-word compaction (`k_words_small`) against the tiled
 kernels they stand in for (`HB_SMALL_STEP=0` at hb_create) and the oracle:
@@ -41,23 +42,26 @@ def _same(a, b, batch, ctx):
 
 
 # 1 tile, exactly 1 / 8 tiles, one message past 1 and past 8 (9 tiles: the tiled path on both)
+# (1,800 groups: one bucket, k_pack_one; 20,000: five buckets, k_radix_small)
 @pytest.mark.parametrize("nmsg", [1, 2047, 2048, 2049, 16384, 16385])
 @pytest.mark.parametrize("nmax", [3, 5, 7])
-def test_small_partition_matches_tiled(monkeypatch, nmsg, nmax):
-    g, runs, ins = synth.random_groups(1800, nmax, seed=nmsg + nmax, W=8)
+@pytest.mark.parametrize("G", [1800, 20000])
+def test_small_partition_matches_tiled(monkeypatch, G, nmsg, nmax):
+    g, runs, ins = synth.random_groups(G, nmax, seed=nmsg + nmax, W=8)
     a, b = _pairs(monkeypatch, lambda: Pair(g, runs, nmax, 8, ins=ins, max_batch=1 << 15))
     for k in range(2):
         batch = synth.random_batch(g, nmsg, seed=31 * nmsg + k)
         if k == 1 and nmsg > 40:  # messages of groups beyond capacity: dropped by the partition
             batch["group"] = batch["group"].copy()
-            batch["group"][::37] = 5000
+            batch["group"][::37] = G + 3000
         _same(a, b, batch, f"n={nmax} nmsg={nmsg} step {k}")
 
 
 @pytest.mark.parametrize("nmax", [3, 5])
-def test_small_partition_follower_side(monkeypatch, nmax):
-    """X mode (m.Commit with every record: the extensions through the same staging)."""
-    g, runs, ins = synth.random_groups(1500, nmax, seed=90 + nmax, W=8)
+@pytest.mark.parametrize("G", [1500, 9000])
+def test_small_partition_follower_side(monkeypatch, G, nmax):
+    """X mode (m.Commit with every record: the extensions beside the records)."""
+    g, runs, ins = synth.random_groups(G, nmax, seed=90 + nmax, W=8)
     a, b = _pairs(monkeypatch, lambda: Pair(g, runs, nmax, 8, ins=ins, max_batch=1 << 15, term_runs=True))
     for p in (a, b):
         p.set_timers(synth.random_timers(len(g), seed=5), DRAWS)

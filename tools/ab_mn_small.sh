@@ -1,16 +1,11 @@
 #!/bin/bash
-# MultiNode A/B: bulk ingestion over the small-phase partners (HBN_SMALL_BULK); 1M groups with the
-# application thread pinned or not, and the other workers on the caller's NUMA node (HBN_PIN_NODE)
-cd ${GRAFT_REPO_ROOT:-$(pwd)} && mkdir -p gpurun_out/abmn12
+# MultiNode 1k-group A/B: small-step device path on / off (HB_SMALL_STEP), after the small-step tests
+cd ${GRAFT_REPO_ROOT:-$(pwd)} && mkdir -p gpurun_out/abmn13
+timeout -k 10 400 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_small_step_gpu.py > gpurun_out/abmn13/tests.log 2>&1 || { tail -30 gpurun_out/abmn13/tests.log; exit 1; }
+tail -1 gpurun_out/abmn13/tests.log
 for rep in 1 2 3; do
-for v in "0" "512"; do
-  A=""; [ $v != 0 ] && A="HBN_SMALL_BULK=$v"
-  env $A timeout -k 10 120 python3 bench.py --workload multinode --groups 1000 --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/abmn12/mn_${v}_$rep.json 2>&1 || exit 1
-  python3 -c "import json;d=json.loads(open('gpurun_out/abmn12/mn_${v}_$rep.json').read().strip().splitlines()[-1]);h=d['host_phases_s_per_step'];print('bulk $v rep=$rep', round(d['value']/1e6,3),'M', round(d['ms_per_step']*1e3,1),'us', {k:round(v*1e6) for k,v in h.items() if v>2e-6})"
+for v in 0 1; do
+  HB_SMALL_STEP=$v timeout -k 10 120 python3 bench.py --workload multinode --groups 1000 --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/abmn13/mn_${v}_$rep.json 2>&1 || exit 1
+  python3 -c "import json;d=json.loads(open('gpurun_out/abmn13/mn_${v}_$rep.json').read().strip().splitlines()[-1]);h=d['host_phases_s_per_step'];print('small $v rep=$rep', round(d['value']/1e6,3),'M', round(d['ms_per_step']*1e3,1),'us', {k:round(v*1e6) for k,v in h.items() if v>2e-6})"
 done; done
-for v in "0 pin" "0 nopin" "1 pin" "1 nopin"; do
-  set -- $v
-  P=""; [ $2 = nopin ] && P="--mn-no-pin"
-  HBN_PIN_NODE=$1 timeout -k 10 400 python3 bench.py --workload multinode --groups 1048576 --steps 4 --warmup 2 --no-cpu-baseline $P > gpurun_out/abmn12/mn1m_$1_$2.json 2> gpurun_out/abmn12/mn1m_$1_$2.err || exit 1
-  python3 -c "import json;d=json.loads(open('gpurun_out/abmn12/mn1m_$1_$2.json').read().strip().splitlines()[-1]);h=d['host_phases_s_per_step'];print('1M $v', round(d['value']/1e6,3),'M', round(d['ms_per_step'],1),'ms', {k:round(v*1e3,1) for k,v in h.items() if v>2e-4}, {k:round(v*1e3,1) for k,v in d['split_s_per_step'].items()})"
-done
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/abmn13/trace -- ./tools/mnprof/mnprof 1000 300 3 4 > gpurun_out/abmn13/trace_run.txt 2>&1
