@@ -181,12 +181,26 @@ int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t roun
     }
     auto a = clk::now();
     if (flags & HBNB_BULK) {  // the round's network input and proposals, one call each
-      for (size_t i = 0; i < order.size(); ++i) {
-        const uint64_t g = order[i] / (n - 1);
-        bg[i] = ids[g];
-        bm[i] = m;
-        bm[i].from = 2 + order[i] % (n - 1);
-        bm[i].index = last[g];
+      auto fill = [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+          const uint64_t g = order[i] / (n - 1);
+          bg[i] = ids[g];
+          bm[i] = m;
+          bm[i].from = 2 + order[i] % (n - 1);
+          bm[i].index = last[g];
+        }
+      };
+      const size_t no = order.size();
+      if (app_threads > 1 && no >= 65536) {  // (the application builds a large round's messages on its threads)
+        std::vector<std::thread> th;
+        for (uint32_t t = 0; t < app_threads; ++t)
+          th.emplace_back([&, t] {
+            if (pinned) (void)sched_setaffinity(0, sizeof(old_mask), &old_mask);
+            fill(no * t / app_threads, no * (t + 1) / app_threads);
+          });
+        for (auto& x : th) x.join();
+      } else {
+        fill(0, no);
       }
       uint64_t done = 0;
       rc = hbn_step_many(mn, order.size(), bg.data(), bm.data(), &done);
