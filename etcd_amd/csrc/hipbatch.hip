@@ -998,6 +998,17 @@ __device__ __forceinline__ void reduce_stats<uint32_t>(const ApplyArgs& a, uint6
 // bucket's region (one atomic per partition).  No raft logic runs here.
 // ---------------------------------------------------------------------------
 constexpr uint32_t ROUTE_THREADS = 1024;
+// HB_ROUTE_SORTED=1: the route writes a group's slots in arrival order when
+// they hold all its messages (a sort of the <= KMAX arrival indices per group
+// in the write-out), so k_apply_lead reads slot x for message x straight from
+// HBM instead of staging all slots in LDS to sort them (32 KB per workgroup at
+// n = 5: 4 waves/SIMD instead of 3 with HB_LEAD_WAVES=4).  Measured (r05,
+// same box): cfg3 0.457-0.460 vs 0.461-0.463 ms, follow n = 5 lane 66.4 vs
+// 71.7 us but its step 0.193 vs 0.190 ms and cfg4 1.912 vs 1.871 ms (the
+// route's sort): off.
+#ifndef HB_ROUTE_SORTED
+#define HB_ROUTE_SORTED 0
+#endif
 #ifndef HB_ROUTE_UNROLL
 #define HB_ROUTE_UNROLL 4
 #endif
@@ -1075,11 +1086,35 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
     const uint32_t c = l_cnt[i], g = gbase + i;
     if (g < G) {
       a.cnt[g] = (uint8_t)(c < 255 ? c : 255);
+      // arrival order of a group whose messages all fit (odd-even transposition
+      // over the arrival indices, slot numbers riding along as nibbles)
+      uint32_t perm = 0, key[KMAX];
+#pragma unroll
+      for (uint32_t k = 0; k < (uint32_t)KMAX; ++k) {
+        perm |= k << (4 * k);
+        key[k] = (HB_ROUTE_SORTED && k < c && c <= (uint32_t)KMAX) ? l_slot[k][i].y : 0xFFFFFFFFu;
+      }
+      if (HB_ROUTE_SORTED && c > 1 && c <= (uint32_t)KMAX) {
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)KMAX; ++r) {
+#pragma unroll
+          for (uint32_t k = (r & 1); k + 1 < (uint32_t)KMAX; k += 2) {
+            const uint32_t k0 = key[k], k1 = key[k + 1];
+            const bool sw = k1 < k0;
+            key[k] = sw ? k1 : k0;
+            key[k + 1] = sw ? k0 : k1;
+            const uint32_t p0 = (perm >> (4 * k)) & 0xF, p1 = (perm >> (4 * (k + 1))) & 0xF;
+            const uint32_t swp = (perm & ~(0xFFu << (4 * k))) | (p1 << (4 * k)) | (p0 << (4 * (k + 1)));
+            perm = sw ? swp : perm;
+          }
+        }
+      }
 #pragma unroll
       for (uint32_t k = 0; k < (uint32_t)KMAX; ++k) {
         if (k < c) {
-          at32(a.slot, k * G + g) = l_slot[k][i];
-          if constexpr (X) at32(a.slotx, k * G + g) = l_slotx[k][i];
+          const uint32_t src = (perm >> (4 * k)) & 0xF;
+          at32(a.slot, k * G + g) = l_slot[src][i];
+          if constexpr (X) at32(a.slotx, k * G + g) = l_slotx[src][i];
         }
       }
     }
@@ -1807,7 +1842,7 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
 }
 
 #ifndef HB_LEAD_WAVES
-#define HB_LEAD_WAVES 3
+#define HB_LEAD_WAVES 3  // (n = 5: 125 VGPRs, 53 KB of LDS: 3 workgroups per CU)
 #endif
 
 #ifndef HB_LEAD7_WAVES  // k_apply_lead<7> (measured on cfg4: 2 waves +3 %, 4 waves -0.6 % with 128 B/lane of scratch)
@@ -1851,7 +1886,9 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   __shared__ uint32_t l_flag[FLAG_WORDS];
   __shared__ uint32_t l_eflag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
-  __shared__ uint4 l_slot[KS][PART];  // the lane's route slots, read once (as in k_elect)
+  // the lane's route slots, read once (as in k_elect) — unless the route wrote
+  // them in arrival order (HB_ROUTE_SORTED): then slot x is read for message x
+  __shared__ uint4 l_slot[HB_ROUTE_SORTED ? 1 : KS][HB_ROUTE_SORTED ? 1 : PART];
   // per lane, one 16-byte word per slot: a leader's {Match, Next} (LeadLaneL) or,
   // X mode, a follower's slot extensions {m.LogTerm, m.Commit} — a lane is one or the other
   constexpr uint32_t LW = LDS ? (NMAX > FS ? NMAX : FS) : (X ? FS : 1u);
@@ -1861,6 +1898,10 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   const uint32_t tid = threadIdx.x;
   const uint32_t g = part * PART + tid;
   const bool gvalid = g < a.S.G;
+  auto slot_at = [&](uint32_t k) -> uint4 {
+    if constexpr (HB_ROUTE_SORTED) return at32(a.slot, k * a.S.G + g);
+    else return l_slot[k][threadIdx.x];
+  };
   if (tid == 0) l_fill = l_pfill = 0;
   if (tid <= ST_N) l_stats[tid] = 0;
   if (tid < FLAG_WORDS) l_flag[tid] = l_eflag[tid] = 0;
@@ -1892,9 +1933,11 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   // (without X, loading the state beside meta, as k_apply_fast does, measured
   // neutral on cfg3 and +4.5 % on cfg4, whose lanes are mostly not leaders)
   const bool slots = (leader && !nc && fits) || fol;
+  if constexpr (!HB_ROUTE_SORTED) {
 #pragma unroll
-  for (uint32_t k = 0; k < KS; ++k)
-    if (slots && k < cnt) l_slot[k][tid] = at32(a.slot, k * a.S.G + g);
+    for (uint32_t k = 0; k < KS; ++k)
+      if (slots && k < cnt) l_slot[k][tid] = at32(a.slot, k * a.S.G + g);
+  }
   if constexpr (X) {
 #pragma unroll
     for (uint32_t k = 0; k < FS; ++k)
@@ -1910,7 +1953,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
       if (k < cnt) {
         uint32_t inf, org;
         uint64_t tm, ix;
-        slot_unpack(l_slot[k][tid], a.side, &inf, &org, &tm, &ix);
+        slot_unpack(slot_at(k), a.side, &inf, &org, &tm, &ix);
         higher |= tm > t;
       }
     }
@@ -1926,12 +1969,12 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   const bool keys = (slots && loaded) || fol;
 #pragma unroll
   for (uint32_t k = 0; k < KS; ++k) {
-    key[k] = (keys && k < cnt) ? l_slot[k][tid].y : 0xFFFFFFFFu;
+    key[k] = (!HB_ROUTE_SORTED && keys && k < cnt) ? l_slot[HB_ROUTE_SORTED ? 0 : k][tid].y : 0xFFFFFFFFu;
     perm |= k << (4 * k);
   }
   // arrival order of the slots (odd-even transposition, slot numbers as nibbles)
 #pragma unroll
-  for (uint32_t r = 0; r < KS; ++r) {
+  for (uint32_t r = 0; r < (HB_ROUTE_SORTED ? 0u : KS); ++r) {
 #pragma unroll
     for (uint32_t k = (r & 1); k + 1 < KS; k += 2) {
       const uint32_t k0 = key[k], k1 = key[k + 1];
@@ -1974,7 +2017,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
       const uint32_t ks = (perm >> (4 * x)) & 0xF;
       uint32_t inf, morig;
       uint64_t mterm, mindex;
-      slot_unpack(l_slot[ks][tid], a.side, &inf, &morig, &mterm, &mindex);
+      slot_unpack(slot_at(ks), a.side, &inf, &morig, &mterm, &mindex);
       const uint4 ext = l_lane[ks < FS ? ks : 0][(LDS || X) ? tid : 0];
       const uint64_t lt = (uint64_t)ext.x | ((uint64_t)ext.y << 32), mc = (uint64_t)ext.z | ((uint64_t)ext.w << 32);
       const uint32_t from = (inf >> 4) & 0xF;
@@ -1994,12 +2037,15 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
       resume = 0;
     } else {
       uint32_t x = 0;
+      uint4 nx = slot_at(perm & 0xF);  // (sorted slots: the next one's load runs ahead of this step)
 #pragma nounroll
       for (; x < cnt; ++x) {
         if (L.faulted()) break;
-        uint32_t inf, morig;  // (from the lane's LDS copy: no load to run ahead of)
+        uint32_t inf, morig;
         uint64_t mterm, mindex;
-        slot_unpack(l_slot[(perm >> (4 * x)) & 0xF][tid], a.side, &inf, &morig, &mterm, &mindex);
+        const uint4 cur = nx;
+        if (x + 1 < cnt) nx = slot_at((perm >> (4 * (x + 1))) & 0xF);
+        slot_unpack(cur, a.side, &inf, &morig, &mterm, &mindex);
         const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
         const bool reject = (inf >> 8) & 1u;
         if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
