@@ -1841,6 +1841,12 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
   }
 }
 
+#ifndef HB_LEAD_XSTAGE
+#define HB_LEAD_XSTAGE 1
+#endif
+#ifndef HB_LEAD_XWAVES  // k_apply_lead<5> in X mode (LDS: 4 staged slots + the lane rows = 36 KB)
+#define HB_LEAD_XWAVES 4
+#endif
 #ifndef HB_LEAD_WAVES
 #define HB_LEAD_WAVES 3  // (n = 5: 125 VGPRs, 53 KB of LDS: 3 workgroups per CU)
 #endif
@@ -1878,7 +1884,8 @@ template <int NMAX> struct LeadOf {
   using T = typename std::conditional<LDS, LeadLaneL<NMAX>, LeadLane<NMAX>>::type;
 };
 template <int NMAX, bool X>
-__global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAVES) k_apply_lead(ApplyArgs a) {
+__global__ void __launch_bounds__(PART, NMAX <= 5 ? (X && HB_LEAD_XSTAGE ? HB_LEAD_XWAVES : HB_LEAD_WAVES)
+                                                 : HB_LEAD7_WAVES) k_apply_lead(ApplyArgs a) {
   constexpr uint32_t KS = route_kmax(NMAX);
   constexpr uint32_t FS = X ? FOLLOW_SLOTS : 1u;
   constexpr bool LDS = LeadOf<NMAX>::LDS;
@@ -1887,8 +1894,11 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   __shared__ uint32_t l_eflag[FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
   // the lane's route slots, read once (as in k_elect) — unless the route wrote
-  // them in arrival order (HB_ROUTE_SORTED): then slot x is read for message x
-  __shared__ uint4 l_slot[HB_ROUTE_SORTED ? 1 : KS][HB_ROUTE_SORTED ? 1 : PART];
+  // them in arrival order (HB_ROUTE_SORTED): then slot x is read for message x.
+  // X mode stages only the first FS (a follower's; a leader reads the rest from
+  // HBM), so that the kernel fits 4 workgroups per CU (HB_LEAD_XSTAGE)
+  constexpr uint32_t SR = HB_ROUTE_SORTED ? 0u : ((X && HB_LEAD_XSTAGE) ? FS : KS);
+  __shared__ uint4 l_slot[SR ? SR : 1][SR ? PART : 1];
   // per lane, one 16-byte word per slot: a leader's {Match, Next} (LeadLaneL) or,
   // X mode, a follower's slot extensions {m.LogTerm, m.Commit} — a lane is one or the other
   constexpr uint32_t LW = LDS ? (NMAX > FS ? NMAX : FS) : (X ? FS : 1u);
@@ -1899,7 +1909,8 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   const uint32_t g = part * PART + tid;
   const bool gvalid = g < a.S.G;
   auto slot_at = [&](uint32_t k) -> uint4 {
-    if constexpr (HB_ROUTE_SORTED) return at32(a.slot, k * a.S.G + g);
+    if constexpr (SR == 0) return at32(a.slot, k * a.S.G + g);
+    else if constexpr (SR < KS) return k < SR ? l_slot[k < SR ? k : 0][threadIdx.x] : at32(a.slot, k * a.S.G + g);
     else return l_slot[k][threadIdx.x];
   };
   if (tid == 0) l_fill = l_pfill = 0;
@@ -1933,9 +1944,9 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   // (without X, loading the state beside meta, as k_apply_fast does, measured
   // neutral on cfg3 and +4.5 % on cfg4, whose lanes are mostly not leaders)
   const bool slots = (leader && !nc && fits) || fol;
-  if constexpr (!HB_ROUTE_SORTED) {
+  if constexpr (SR > 0) {
 #pragma unroll
-    for (uint32_t k = 0; k < KS; ++k)
+    for (uint32_t k = 0; k < SR; ++k)
       if (slots && k < cnt) l_slot[k][tid] = at32(a.slot, k * a.S.G + g);
   }
   if constexpr (X) {
@@ -1969,7 +1980,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? HB_LEAD_WAVES : HB_LEAD7_WAV
   const bool keys = (slots && loaded) || fol;
 #pragma unroll
   for (uint32_t k = 0; k < KS; ++k) {
-    key[k] = (!HB_ROUTE_SORTED && keys && k < cnt) ? l_slot[HB_ROUTE_SORTED ? 0 : k][tid].y : 0xFFFFFFFFu;
+    key[k] = (!HB_ROUTE_SORTED && keys && k < cnt) ? slot_at(k).y : 0xFFFFFFFFu;
     perm |= k << (4 * k);
   }
   // arrival order of the slots (odd-even transposition, slot numbers as nibbles)
