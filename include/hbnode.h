@@ -225,9 +225,14 @@ int hbn_propose_many(hbn_node* n, uint64_t count, const uint64_t* groups, const 
  * assembly, Advance, bulk ingestion); groups are independent, each worker owns
  * a disjoint set.  Default min(16, cores), or the HBN_THREADS environment
  * variable.  The calling thread is one of them.  Phases below a few thousand
- * groups run on the caller alone, except the event replay and the Ready
- * assembly, which take up to HBN_SMALL_WAYS workers (default 2; 1 = the caller
- * alone) from 512 touched groups / 2048 event words on. */
+ * groups run on the caller alone, except the event replay, the Ready assembly,
+ * Advance and bulk ingestion, which take up to HBN_SMALL_WAYS workers (default
+ * 4; 1 = the caller alone) from 512 groups / messages (2,048 event words) on.
+ * Those partner workers are pinned, one physical core each, to the L3 domain
+ * (CCD) of the thread that starts the node or sets its threads (HBN_PIN_L3=0:
+ * not pinned), are woken when hbn_ready launches the device step and spin for
+ * up to HBN_SPIN_US microseconds (default 150) after a job before blocking;
+ * the other workers may run on any CPU of the container's cpuset. */
 int hbn_set_threads(hbn_node* n, uint32_t threads);
 /* Seconds the node's host side spent per phase since hbn_start (diagnostics;
  * out[0..min(cap, *count)), order: load sync, log-index reserve, hb_step call,

@@ -361,7 +361,11 @@ typedef struct hb_handle hb_handle;
  * Device memory: per group ~100 B + nmax x (28 + 8 max_inflight) B of state,
  * 16 B + a 128-byte term-run ring, and for a finite max_msg_size 16 B + a
  * 128-byte size ring (rings grow with hb_reserve_log: 8 B per log entry,
- * 16 B per term run). */
+ * 16 B per term run).
+ * A step of at most 16,384 messages on a handle of at most 1M groups
+ * partitions in one workgroup (one launch), and hb_events_to_host compacts at
+ * most 1,024 chunks in one; HB_SMALL_STEP=0 in the environment at hb_create
+ * keeps the tiled kernels for such steps (the same results). */
 int  hb_create(int device, uint32_t capacity, uint32_t max_replicas,
                uint32_t max_inflight, uint64_t max_msg_size, uint64_t max_batch,
                hb_handle** out);
