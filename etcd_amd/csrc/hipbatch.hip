@@ -998,6 +998,14 @@ __device__ __forceinline__ void reduce_stats<uint32_t>(const ApplyArgs& a, uint6
 // bucket's region (one atomic per partition).  No raft logic runs here.
 // ---------------------------------------------------------------------------
 constexpr uint32_t ROUTE_THREADS = 1024;
+// cnt[g]: the group's message count (saturated at 127) | CNT_HIGHER when some
+// message of the group carries a Term above the group's (n >= 5 routes of
+// batches without dense proposals: k_apply_lead then hands a busy leader — an
+// election storm's — over without reading its slots or state; cfg4 1.914 ->
+// 1.83 ms.  With dense proposals the check cost cfg3 1.3 % for nothing: a
+// leader there proposes, and one without the flag is loaded and stepped up to
+// the higher term, as before)
+constexpr uint32_t CNT_MASK = 0x7F, CNT_HIGHER = 0x80;
 // HB_ROUTE_SORTED=1: the route writes a group's slots in arrival order when
 // they hold all its messages (a sort of the <= KMAX arrival indices per group
 // in the write-out), so k_apply_lead reads slot x for message x straight from
@@ -1036,17 +1044,28 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   __shared__ uint4 l_slot[KMAX][RG];  // the group's first KMAX records as they will be stored
   __shared__ uint4 l_slotx[X ? KMAX : 1][X ? RG : 1];  // X mode: their extensions
   __shared__ uint32_t l_ptot[NP];
+  constexpr bool HI = KMAX >= 5;  // (CNT_HIGHER)
+  __shared__ uint64_t l_term[HI ? RG : 1];
+  __shared__ uint8_t l_hi[HI ? RG : 1];
   // blockIdx -> (bucket, w): the W sisters of a bucket share blockIdx % 8 (one XCD)
   const uint32_t x = blockIdx.x, q = x >> 3;
   const uint32_t bk = ((q / W) << 3) | (x & 7), w = q % W;
   if (bk >= a.NBK) return;  // uniform: grid padding
   const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) l_cnt[i] = 0;
+  const uint32_t G = a.S.G;
+  const uint32_t lg0 = w * RG;  // first group (in the bucket) of this workgroup
+  const bool hi_on = HI && !a.props_on;  // (uniform)
+  for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) {
+    l_cnt[i] = 0;
+    if (hi_on) {
+      const uint32_t g = (bk << (PART_LOG + sl)) + lg0 + i;
+      l_term[i] = g < G ? a.S.term[g] : ~0ull;
+      l_hi[i] = 0;
+    }
+  }
   if (tid < NP) l_ptot[tid] = 0;
   __syncthreads();
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
-  const uint32_t G = a.S.G;
-  const uint32_t lg0 = w * RG;  // first group (in the bucket) of this workgroup
   const uint32_t sub_lo = lg0 >> PART_LOG, sub_hi = (lg0 + RG) >> PART_LOG;
   for (uint32_t base = lo; base < hi; base += ROUTE_THREADS * ROUTE_UNROLL) {
     MsgRec m[ROUTE_UNROLL];
@@ -1072,6 +1091,11 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
       const bool own = p < hi && sub[u] >= sub_lo && sub[u] < sub_hi;
       const uint32_t l = own ? (((sub[u] - sub_lo) << PART_LOG) | ((m[u].info >> 16) & (PART - 1))) : RG;
       if (l < RG) {
+        if (hi_on) {
+          uint64_t tm, ix;
+          rec_unpack(m[u].info, m[u].orig, m[u].ti, a.side, &tm, &ix);
+          if (tm > l_term[l]) l_hi[l] = 1;  // (every writer stores 1)
+        }
         const uint32_t r = atomicAdd(&l_cnt[l], 1u);
         if (r < (uint32_t)KMAX) {
           l_slot[r][l] = make_uint4(m[u].info, m[u].orig, (uint32_t)m[u].ti, (uint32_t)(m[u].ti >> 32));
@@ -1085,7 +1109,7 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) {
     const uint32_t c = l_cnt[i], g = gbase + i;
     if (g < G) {
-      a.cnt[g] = (uint8_t)(c < 255 ? c : 255);
+      a.cnt[g] = (uint8_t)((c < CNT_MASK ? c : CNT_MASK) | ((hi_on && l_hi[HI ? i : 0]) ? CNT_HIGHER : 0u));
       // arrival order of a group whose messages all fit (odd-even transposition
       // over the arrival indices, slot numbers riding along as nibbles)
       uint32_t perm = 0, key[KMAX];
@@ -1349,7 +1373,7 @@ __global__ void __launch_bounds__(PART, HB_FAST_WAVES) k_apply_fast(ApplyArgs a)
   L.g = g;
   L.mlo = gvalid ? at32(reinterpret_cast<uint32_t*>(a.S.meta), 2 * g) : 0u;
   const uint32_t prop_raw = (a.props && gvalid) ? at32(a.props, g) : 0u;
-  const uint32_t cnt = gvalid ? at32(a.cnt, g) : 0u;
+  const uint32_t cnt = gvalid ? at32(a.cnt, g) & CNT_MASK : 0u;
   // The state that depends on nothing is loaded beside meta (one round trip
   // fewer for every leader; a group with no fast-path work wastes 52 bytes)
   if (gvalid) L.load_head();
@@ -1488,7 +1512,7 @@ __device__ __forceinline__ bool apply_part(const ApplyArgs& a, uint32_t part, Ge
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
 
   constexpr uint32_t KS = route_kmax(NMAX);
-  const uint32_t cnt = flagged ? a.cnt[g] : 0u;
+  const uint32_t cnt = flagged ? a.cnt[g] & CNT_MASK : 0u;
   const bool by_slot = flagged && cnt <= a.kmax;  // (a.kmax <= KS: the step's slot count)
   const bool by_walk = flagged && !by_slot;
   __syncthreads();  // l_fill
@@ -1759,7 +1783,7 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
     L.E.fill = &l_fill;
     L.g = g;
     L.meta = flagged ? a.S.meta[g] : 0ull;
-    const uint32_t cnt = flagged ? a.cnt[g] : 0u;
+    const uint32_t cnt = flagged ? a.cnt[g] & CNT_MASK : 0u;
     const uint32_t resume = flagged ? a.resume[g] : 0u;
     // (flagged groups are live and not faulted; a pending dense proposal goes to k_apply)
     const bool mine = flagged && cnt <= KS && (resume >> 31) == 0 && L.self() < L.n() && !(L.meta & M_NC);
@@ -1923,7 +1947,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? (X && HB_LEAD_XSTAGE ? HB_LE
   if constexpr (LDS) L.lp = &l_lane[0][tid];
   L.mlo = gvalid ? reinterpret_cast<const uint32_t*>(a.S.meta)[2 * (size_t)g] : 0u;
   const uint32_t prop_raw = (a.props && gvalid) ? a.props[g] : 0u;
-  const uint32_t cnt = gvalid ? a.cnt[g] : 0u;
+  const uint32_t craw = gvalid ? a.cnt[g] : 0u, cnt = craw & CNT_MASK;
   // X mode (a MultiNode node's batch: it leads some groups and follows most):
   // the per-group fields every role steps with come in meta's round trip
   L.last = L.committed = 0;
@@ -1943,7 +1967,10 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? (X && HB_LEAD_XSTAGE ? HB_LE
   L.nev = 0;
   // (without X, loading the state beside meta, as k_apply_fast does, measured
   // neutral on cfg3 and +4.5 % on cfg4, whose lanes are mostly not leaders)
-  const bool slots = (leader && !nc && fits) || fol;
+  // (a busy leader with a higher-term message — the route's CNT_HIGHER — is
+  // handed over without reading its slots or its state)
+  const bool busy_hi = leader && !nc && fits && !spec && (craw & CNT_HIGHER) != 0;
+  const bool slots = (leader && !nc && fits && !busy_hi) || fol;
   if constexpr (SR > 0) {
 #pragma unroll
     for (uint32_t k = 0; k < SR; ++k)
@@ -1956,22 +1983,10 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? (X && HB_LEAD_XSTAGE ? HB_LE
   }
   if (spec) L.load(X);
   if (fol) L.load_follow();  // (a follower reads no Progress)
-  bool loaded = spec, higher = false;
-  if (slots && !spec && !fol) {  // a busy leader without a proposal: load it unless a higher term steps it down
-    const uint64_t t = X ? L.term : at32(a.S.term, g);
-#pragma unroll
-    for (uint32_t k = 0; k < KS; ++k) {
-      if (k < cnt) {
-        uint32_t inf, org;
-        uint64_t tm, ix;
-        slot_unpack(slot_at(k), a.side, &inf, &org, &tm, &ix);
-        higher |= tm > t;
-      }
-    }
-    if (!higher) {
-      L.load(X);
-      loaded = true;
-    }
+  bool loaded = spec, higher = busy_hi;
+  if (slots && !spec && !fol) {  // a busy leader without a proposal and no higher term: load it
+    L.load(X);
+    loaded = true;
   }
   // the slots' arrival indices, only for a group this kernel steps (an election
   // storm's leaders go to k_elect without them)
