@@ -1000,7 +1000,7 @@ __device__ __forceinline__ void reduce_stats<uint32_t>(const ApplyArgs& a, uint6
 constexpr uint32_t ROUTE_THREADS = 1024;
 // cnt[g]: the group's message count (saturated at 127) | CNT_HIGHER when some
 // message of the group carries a Term above the group's (n >= 5 routes of
-// batches without dense proposals: k_apply_lead then hands a busy leader — an
+// leader-side batches without dense proposals: k_apply_lead then hands a busy leader — an
 // election storm's — over without reading its slots or state; cfg4 1.914 ->
 // 1.83 ms.  With dense proposals the check cost cfg3 1.3 % for nothing: a
 // leader there proposes, and one without the flag is loaded and stepped up to
@@ -1054,7 +1054,7 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   const uint32_t tid = threadIdx.x;
   const uint32_t G = a.S.G;
   const uint32_t lg0 = w * RG;  // first group (in the bucket) of this workgroup
-  const bool hi_on = HI && !a.props_on;  // (uniform)
+  const bool hi_on = HI && !X && !a.props_on;  // (uniform; a follower-side batch's route measured +12 us with it)
   for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) {
     l_cnt[i] = 0;
     if (hi_on) {
