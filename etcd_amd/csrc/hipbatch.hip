@@ -1045,8 +1045,6 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   __shared__ uint4 l_slotx[X ? KMAX : 1][X ? RG : 1];  // X mode: their extensions
   __shared__ uint32_t l_ptot[NP];
   constexpr bool HI = KMAX >= 5;  // (CNT_HIGHER)
-  __shared__ uint64_t l_term[HI ? RG : 1];
-  __shared__ uint8_t l_hi[HI ? RG : 1];
   // blockIdx -> (bucket, w): the W sisters of a bucket share blockIdx % 8 (one XCD)
   const uint32_t x = blockIdx.x, q = x >> 3;
   const uint32_t bk = ((q / W) << 3) | (x & 7), w = q % W;
@@ -1054,15 +1052,9 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   const uint32_t tid = threadIdx.x;
   const uint32_t G = a.S.G;
   const uint32_t lg0 = w * RG;  // first group (in the bucket) of this workgroup
-  const bool hi_on = HI && !X && !a.props_on;  // (uniform; a follower-side batch's route measured +12 us with it)
-  for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) {
-    l_cnt[i] = 0;
-    if (hi_on) {
-      const uint32_t g = (bk << (PART_LOG + sl)) + lg0 + i;
-      l_term[i] = g < G ? a.S.term[g] : ~0ull;
-      l_hi[i] = 0;
-    }
-  }
+  // (uniform; a follower-side batch's route measured +12 us with it)
+  const bool hi_on = HI && !X && !a.props_on;
+  for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) l_cnt[i] = 0;
   if (tid < NP) l_ptot[tid] = 0;
   __syncthreads();
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
@@ -1091,11 +1083,6 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
       const bool own = p < hi && sub[u] >= sub_lo && sub[u] < sub_hi;
       const uint32_t l = own ? (((sub[u] - sub_lo) << PART_LOG) | ((m[u].info >> 16) & (PART - 1))) : RG;
       if (l < RG) {
-        if (hi_on) {
-          uint64_t tm, ix;
-          rec_unpack(m[u].info, m[u].orig, m[u].ti, a.side, &tm, &ix);
-          if (tm > l_term[l]) l_hi[l] = 1;  // (every writer stores 1)
-        }
         const uint32_t r = atomicAdd(&l_cnt[l], 1u);
         if (r < (uint32_t)KMAX) {
           l_slot[r][l] = make_uint4(m[u].info, m[u].orig, (uint32_t)m[u].ti, (uint32_t)(m[u].ti >> 32));
@@ -1109,7 +1096,21 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) {
     const uint32_t c = l_cnt[i], g = gbase + i;
     if (g < G) {
-      a.cnt[g] = (uint8_t)((c < CNT_MASK ? c : CNT_MASK) | ((hi_on && l_hi[HI ? i : 0]) ? CNT_HIGHER : 0u));
+      // a group whose messages all sit in its slots: any Term above its own?
+      bool hib = false;
+      if (hi_on && c <= (uint32_t)KMAX) {
+        const uint64_t t = a.S.term[g];
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)KMAX; ++k) {
+          if (k < c) {
+            const uint4 r = l_slot[k][i];
+            uint64_t tm, ix;
+            rec_unpack(r.x, r.y, (uint64_t)r.z | ((uint64_t)r.w << 32), a.side, &tm, &ix);
+            hib |= tm > t;
+          }
+        }
+      }
+      a.cnt[g] = (uint8_t)((c < CNT_MASK ? c : CNT_MASK) | (hib ? CNT_HIGHER : 0u));
       // arrival order of a group whose messages all fit (odd-even transposition
       // over the arrival indices, slot numbers riding along as nibbles)
       uint32_t perm = 0, key[KMAX];
