@@ -729,6 +729,11 @@ struct Group {
 };
 
 // ---------------------------------------------------------------- host threads
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#endif
+}
 // CPUs of a sysfs cpu list ("0-7,128-135")
 inline void parse_cpu_list(const char* path, cpu_set_t* set) {
   CPU_ZERO(set);
@@ -924,7 +929,7 @@ class Pool {
         const auto t0 = std::chrono::steady_clock::now();
         const auto lim = std::chrono::microseconds(spin_us_);
         while (w.post.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() - t0 < lim)
-          __builtin_ia32_pause();
+          cpu_relax();
       }
       if (w.post.load() == seen) {
         std::unique_lock<std::mutex> lk(w.mu);
