@@ -3048,16 +3048,21 @@ void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
     else hipLaunchKernelGGL((k_apply_fast<NMAX, false, 2>), dim3(grid), dim3(PART), 0, h->stream, a);
   }
   if (ev) (void)hipEventRecord(ev[3], h->stream);
+  // the list kernels loop over their XCD slot's list, so a small handle (a
+  // MultiNode node of a few thousand groups: 4 partitions under a 128-entry
+  // virtual grid) launches one workgroup per list entry it can have, at least 8
+  const uint32_t lists = std::max(8u, (h->NB + 7) & ~7u);
   if constexpr (NMAX >= 5) {  // the general kernel spills at n >= 5: elections go first
     if (!sz_on(h->max_msg_size))
-      hipLaunchKernelGGL(k_elect<NMAX>, dim3(ELECT_GRID ? std::min(grid, ELECT_GRID) : grid), dim3(PART), 0,
-                         h->stream, a);
+      hipLaunchKernelGGL(k_elect<NMAX>, dim3(std::min(lists, ELECT_GRID ? std::min(grid, ELECT_GRID) : grid)),
+                         dim3(PART), 0, h->stream, a);
   }
   if constexpr (NMAX <= 3) {  // chained follower pass; the last workgroup runs the finish
-    const uint32_t gg = GEN_GRID3 ? std::min(grid, GEN_GRID3) : grid;
+    const uint32_t gg = std::min(lists, GEN_GRID3 ? std::min(grid, GEN_GRID3) : grid);
     hipLaunchKernelGGL(k_apply<NMAX>, dim3(gg), dim3(PART), 0, h->stream, a);
   } else {
-    hipLaunchKernelGGL(k_apply<NMAX>, dim3(GEN_GRID ? std::min(grid, GEN_GRID) : grid), dim3(PART), 0, h->stream, a);
+    hipLaunchKernelGGL(k_apply<NMAX>, dim3(std::min(lists, GEN_GRID ? std::min(grid, GEN_GRID) : grid)), dim3(PART), 0,
+                       h->stream, a);
     // k_follow's last workgroup also runs the step's finish (k_finish)
     hipLaunchKernelGGL(k_follow<NMAX>, dim3(FOLLOW_GRID), dim3(PART), 0, h->stream, a);
   }
