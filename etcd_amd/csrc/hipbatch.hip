@@ -2868,6 +2868,7 @@ struct hb_handle {
   // launch for the partition and one for the event words; HB_SMALL_STEP=0
   // turns that off (same output: the A/B and the parity tests compare both)
   bool no_small = false;
+  uint32_t agrid = 0;  // the apply kernels' grid (apply_grid_for)
   uint32_t bk_bits = 1;            // bits of a bucket id
   // host-pointer staging
   uint32_t* s_group = nullptr;
@@ -3028,8 +3029,19 @@ void launch_route(hb_handle* h, const ApplyArgs& a, hipStream_t st) {
   else hipLaunchKernelGGL((k_route<KMAX, false>), dim3(route_grid<KMAX>(h, false)), dim3(ROUTE_THREADS), 0, st, a);
 }
 
-// XCD-aware grid (see block_part()): whole groups of 8 buckets x 2^sis_log partitions.
-uint32_t apply_grid(const hb_handle* h) { return ((h->NBK + 7) & ~7u) << h->sis_log; }
+// XCD-aware grid (see block_part()): whole groups of 8 buckets x 2^sis_log
+// partitions, cut after the last block that maps to a real partition (a small
+// handle's 4 partitions sit at blocks 0, 8, 16, 24 of a 128-block grid).
+uint32_t apply_grid_for(uint32_t NBK, uint32_t sl, uint32_t NB) {
+  const uint32_t full = ((NBK + 7) & ~7u) << sl;
+  uint32_t need = 0;
+  for (uint32_t x = 0; x < full; ++x) {
+    const uint32_t r = x & 7, q = x >> 3;  // part_of() on the host
+    if ((((((q >> sl) << 3) | r) << sl) | (q & ((1u << sl) - 1))) < NB) need = x + 1;
+  }
+  return (need + 7) & ~7u;
+}
+uint32_t apply_grid(const hb_handle* h) { return h->agrid; }
 
 // The apply kernels; ev = this step's phase events (HB_STEP_PROFILE) or null.
 template <int NMAX>
@@ -3148,6 +3160,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   h->NBK = nbk_for(h->sis_log);
   h->passes = passes_for(h->sis_log);
   h->bk_bits = std::max<uint32_t>(ceil_log2(h->NBK), 1);
+  h->agrid = apply_grid_for(h->NBK, h->sis_log, h->NB);
   const size_t tiles_max = (mb + RDX_TILE - 1) / RDX_TILE;
   ALLOC(h->hist, (size_t)RDX_BINS * tiles_max);
   ALLOC(h->n_valid, 4);
