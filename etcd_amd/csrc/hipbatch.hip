@@ -248,7 +248,7 @@ __device__ __forceinline__ uint32_t excl_scan256(uint32_t v, uint32_t* sh4, uint
 #endif
 constexpr uint32_t HIST_TPB = HB_HIST_TPB;
 __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t G, uint32_t shift, uint32_t dbits,
-                                                           uint32_t ntiles, uint32_t* hist) {
+                                                           uint32_t ntiles, uint32_t* hist, uint32_t dm) {
   __shared__ uint32_t cnt[HIST_TPB][RDX_BINS];
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < HIST_TPB * RDX_BINS; i += RDX_THREADS) (&cnt[0][0])[i] = 0;
@@ -270,27 +270,36 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t
       if (gv[t][r] < G) atomicAdd(&cnt[t][rdx_digit(gv[t][r], shift, dbits)], 1u);
   __syncthreads();
   for (uint32_t i = tid; i < (HIST_TPB << dbits); i += RDX_THREADS) {  // the pass's digits only
-    const uint32_t t = i >> dbits, dg = i & ((1u << dbits) - 1);
-    if (t0 + t < ntiles) hist[((size_t)(t0 + t) << dbits) + dg] = cnt[t][dg];  // [tile][digit]
+    if (dm) {  // [digit][tile]
+      const uint32_t t = i % HIST_TPB, dg = i / HIST_TPB;
+      if (t0 + t < ntiles) hist[(size_t)dg * ntiles + (t0 + t)] = cnt[t][dg];
+    } else {  // [tile][digit]
+      const uint32_t t = i >> dbits, dg = i & ((1u << dbits) - 1);
+      if (t0 + t < ntiles) hist[((size_t)(t0 + t) << dbits) + dg] = cnt[t][dg];
+    }
   }
 }
 
-// Column scan: workgroup d turns column d of hist (tile counts, [ntiles][nb]
-// rows) into exclusive per-tile prefixes and writes the column total to
-// totals[d]; the digits of one 128-byte line of every row are scanned by
-// workgroups of one XCD, so each line is fetched into one L2 once.  It also clears the per-bucket event-chunk cursors for
-// the coming apply.
+// Digit scan: workgroup d turns digit d's counts of every tile into exclusive
+// per-tile prefixes and writes their total to totals[d].  Two-pass handles keep
+// the counts digit-major ([nb][ntiles], dm: a streaming read per workgroup;
+// tile-major rows made each workgroup read one word per row: cfg4 1.793 ->
+// 1.765 ms, cfg5 0.982 -> 0.968 ms); a one-pass handle keeps them tile-major
+// ([ntiles][nb]: the scatter reads its tile's row in one line; digit-major
+// measured cfg2 +2 us), with the digits of one 128-byte line of every row
+// scanned by workgroups of one XCD.  It also clears the per-bucket event-chunk
+// cursors for the coming apply.
 #ifndef HB_SCAN_PER
 #define HB_SCAN_PER 16
 #endif
 constexpr uint32_t SCAN_PER = HB_SCAN_PER;
 __global__ void __launch_bounds__(1024) k_scan_rows(uint32_t* hist, uint32_t ntiles, uint32_t dbits, uint32_t* totals,
-                                                    uint32_t* bk_fill, uint32_t NBK, uint32_t* ctr) {
+                                                    uint32_t* bk_fill, uint32_t NBK, uint32_t* ctr, uint32_t dm) {
   __shared__ uint32_t sh16[16];
   const uint32_t nb = 1u << dbits;
-  const uint32_t d = nb >= 8 ? (blockIdx.x & 7) * (nb / 8) + (blockIdx.x >> 3) : blockIdx.x;
-  uint32_t* col = hist + d;
-  const uint32_t CS = dbits;
+  const uint32_t d = dm ? blockIdx.x : (nb >= 8 ? (blockIdx.x & 7) * (nb / 8) + (blockIdx.x >> 3) : blockIdx.x);
+  uint32_t* col = dm ? hist + (size_t)d * ntiles : hist + d;
+  const uint32_t CS = dm ? 0u : dbits;  // element i of the digit's counts at col[i << CS]
   for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < NBK; i += gridDim.x * 1024) bk_fill[i * CTR_STRIDE] = 0;
   if (blockIdx.x == 0)
     for (uint32_t i = threadIdx.x; i < CTR_WORDS; i += blockDim.x) ctr[i] = 0;
@@ -378,11 +387,12 @@ __device__ __forceinline__ void scat_load(const RadixSrc& s, uint32_t n, uint32_
 constexpr uint32_t SCAT_TPW = HB_SCAT_TPW;
 // The scatter of TPW consecutive tiles from tile0 (`first`: the workgroup that
 // writes n_valid and the one-pass bucket bounds); `off` / `totals` may be LDS.
+// off[dg * ds + tile * ts]: a tile's exclusive prefix of digit dg.
 template <bool FINAL, bool X, uint32_t TPW>
 __device__ __forceinline__ void scatter_tiles(const RadixSrc& s, const RadixDst& d, const FinalDst& f, uint32_t G,
                                               uint32_t shift, uint32_t dbits, uint32_t ntiles, uint32_t tile0,
-                                              const uint32_t* off, const uint32_t* totals, uint32_t* n_valid,
-                                              bool first) {
+                                              const uint32_t* off, uint32_t ds, uint32_t ts, const uint32_t* totals,
+                                              uint32_t* n_valid, bool first) {
   __shared__ uint32_t s_base[RDX_BINS];  // digit base in the pass output (exclusive scan of the totals)
   __shared__ uint32_t s_off[RDX_BINS];
   __shared__ uint32_t s_wcnt[RDX_WAVES][RDX_BINS];
@@ -420,7 +430,7 @@ __device__ __forceinline__ void scatter_tiles(const RadixSrc& s, const RadixDst&
     const uint32_t tile = tile0 + j;
     if (tile >= ntiles) break;  // uniform
     // this tile's digit starts in the output; per-wave digit counters cleared
-    if (tid < nb) s_off[tid] = s_base[tid] + off[((size_t)tile << dbits) + tid];
+    if (tid < nb) s_off[tid] = s_base[tid] + off[(size_t)tid * ds + (size_t)tile * ts];
 #pragma unroll
     for (uint32_t k = 0; k < RDX_WAVES * RDX_BINS / RDX_THREADS; ++k) (&s_wcnt[0][0])[tid + k * RDX_THREADS] = 0;
     __syncthreads();
@@ -542,8 +552,8 @@ __device__ __forceinline__ void scatter_tiles(const RadixSrc& s, const RadixDst&
 template <bool FINAL, bool X>
 __global__ void __launch_bounds__(RDX_THREADS) __attribute__((amdgpu_waves_per_eu(8))) k_radix_scatter(RadixSrc s, RadixDst d, FinalDst f, uint32_t G,
                                                               uint32_t shift, uint32_t dbits, uint32_t ntiles, const uint32_t* off,
-                                                              const uint32_t* totals, uint32_t* n_valid) {
-  scatter_tiles<FINAL, X, SCAT_TPW>(s, d, f, G, shift, dbits, ntiles, blockIdx.x * SCAT_TPW, off, totals, n_valid,
+                                                              uint32_t ds, uint32_t ts, const uint32_t* totals, uint32_t* n_valid) {
+  scatter_tiles<FINAL, X, SCAT_TPW>(s, d, f, G, shift, dbits, ntiles, blockIdx.x * SCAT_TPW, off, ds, ts, totals, n_valid,
                                     blockIdx.x == 0);
 }
 
@@ -644,7 +654,8 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_small(RadixSrc s, FinalDs
     s_tot[tid] = run;
   }
   __syncthreads();
-  scatter_tiles<true, X, SMALL_TILES>(s, RadixDst{}, f, G, shift, RDX_BITS, ntiles, 0, s_hist, s_tot, n_valid, true);
+  scatter_tiles<true, X, SMALL_TILES>(s, RadixDst{}, f, G, shift, RDX_BITS, ntiles, 0, s_hist, 1u, RDX_BINS, s_tot,
+                                      n_valid, true);
 }
 
 // bk_off[b] = first position of bucket b in the sorted batch (b <= NBK); the
@@ -3879,14 +3890,16 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
       // passes, where 8 + 2 wrote 8-message runs (partial lines) in the first
       const uint32_t b0 = h->bk_bits / 2;
       const uint32_t dbits = h->passes == 1 ? RDX_BITS : p == 0 ? b0 : h->bk_bits - b0;
+      const uint32_t dm = h->passes > 1;  // digit-major tile counts (k_scan_rows)
       hipLaunchKernelGGL(k_radix_hist, dim3((ntiles + HIST_TPB - 1) / HIST_TPB), dim3(RDX_THREADS), 0, ps_st, src, h->G,
-                         shift, dbits, ntiles, h->hist);
+                         shift, dbits, ntiles, h->hist, dm);
       hipLaunchKernelGGL(k_scan_rows, dim3(1u << dbits), dim3(1024), 0, ps_st, h->hist, ntiles, dbits, h->totals, ps.bk_fill,
-                         h->NBK, ps.ctr);
+                         h->NBK, ps.ctr, dm);
       const dim3 sg((ntiles + SCAT_TPW - 1) / SCAT_TPW);
 #define HB_SCATTER(F, X)                                                                                             \
   hipLaunchKernelGGL((k_radix_scatter<F, X>), sg, dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G, shift, dbits, ntiles, \
-                     (const uint32_t*)h->hist, (const uint32_t*)h->totals, h->n_valid)
+                     (const uint32_t*)h->hist, dm ? ntiles : 1u, dm ? 1u : (1u << dbits), (const uint32_t*)h->totals,    \
+                     h->n_valid)
       if (last_pass) {
         if (xmode) HB_SCATTER(true, true);
         else HB_SCATTER(true, false);
