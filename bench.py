@@ -523,9 +523,8 @@ def run_replication(args, world, rank, local):
     """cfg2 (headline) / cfg5: steady-state replication, weak scaling over
     `world` ranks, one GPU each."""
     n = args.replicas
-    # torch first: its HIP runtime is the one libhipbatch (under the router's
-    # libhbnode) binds to; loading the engine library first would bring in a
-    # second copy of the runtime (nothing here touches the GPU yet)
+    # (the engine library under the router's libhbnode binds to torch's HIP
+    # runtime in either import order: etcd_amd/hipbatch.py _bind_one_hip_runtime)
     import torch  # noqa: F401
     t_setup = time.perf_counter()
     groups, batch, G_total, route = routed_batch(args.groups, world, rank, n)

@@ -20,6 +20,7 @@
 // Nothing here steps raft: every Step/Campaign/Propose/Report goes into the
 // device batch, and the host only replays the events the device returns.
 #include "../../include/hbnode.h"
+#include "hbpool.h"
 
 #include <algorithm>
 #include <atomic>
@@ -729,243 +730,10 @@ struct Group {
 };
 
 // ---------------------------------------------------------------- host threads
-inline void cpu_relax() {
-#if defined(__x86_64__) || defined(__i386__)
-  __builtin_ia32_pause();
-#endif
-}
-// CPUs of a sysfs cpu list ("0-7,128-135")
-inline void parse_cpu_list(const char* path, cpu_set_t* set) {
-  CPU_ZERO(set);
-  FILE* f = std::fopen(path, "r");
-  if (!f) return;
-  char buf[1024];
-  const size_t len = std::fread(buf, 1, sizeof(buf) - 1, f);
-  std::fclose(f);
-  buf[len] = 0;
-  for (char* p = buf; *p;) {
-    char* e = nullptr;
-    const long a = std::strtol(p, &e, 10);
-    if (e == p) break;
-    long b = a;
-    p = e;
-    if (*p == '-') b = std::strtol(p + 1, &p, 10);
-    for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET((int)c, set);
-    while (*p == ',' || *p == '\n' || *p == ' ') ++p;
-  }
-}
-// The CPUs a worker may run on: the container's cpuset (not the creating
-// thread's mask, which workers would inherit: an application may have pinned
-// its thread to one CPU).
-inline void allowed_cpus(cpu_set_t* out) {
-  parse_cpu_list("/sys/fs/cgroup/cpuset.cpus.effective", out);
-  if (CPU_COUNT(out) == 0) parse_cpu_list("/sys/devices/system/cpu/online", out);
-}
-// One CPU per physical core sharing the calling thread's L3 (its CCD on
-// EPYC), its own core excluded, in core order; empty when the topology is unknown.
-inline std::vector<int> l3_partner_cores() {
-  std::vector<int> out;
-  const int c = sched_getcpu();
-  if (c < 0) return out;
-  cpu_set_t l3, allowed, seen;
-  char path[128];
-  std::snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", c);
-  parse_cpu_list(path, &l3);
-  allowed_cpus(&allowed);
-  CPU_ZERO(&seen);
-  for (int i = 0; i < CPU_SETSIZE; ++i) {
-    if (!CPU_ISSET(i, &l3) || CPU_ISSET(i, &seen)) continue;
-    cpu_set_t sib;
-    std::snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", i);
-    parse_cpu_list(path, &sib);
-    CPU_SET(i, &sib);
-    CPU_OR(&seen, &seen, &sib);
-    if (!CPU_ISSET(c, &sib) && CPU_ISSET(i, &allowed)) out.push_back(i);
-  }
-  return out;
-}
-
-// Groups are independent (raft/multinode.go:125-131), so the per-group host
-// work of a Ready cycle — replaying the device's events, assembling Ready,
-// Advance, bulk ingestion — runs on a pool of host threads, each owning a
-// disjoint set of groups; the node's membership lists are appended per thread
-// and merged in thread order.  The calling thread is worker 0.
-class Pool {
- public:
-  explicit Pool(unsigned n) : n_(n ? n : 1), w_(n_) {
-    if (const char* e = std::getenv("HBN_SMALL_WAYS")) set_small_ways((unsigned)std::max(1, std::atoi(e)));
-    if (const char* e = std::getenv("HBN_SMALL_ADV")) adv_min_ = (size_t)std::max(1, std::atoi(e));  // (A/B knob)
-    if (const char* e = std::getenv("HBN_SPIN_US")) spin_us_ = (unsigned)std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("HBN_SMALL_BULK")) bulk_min_ = (size_t)std::max(1, std::atoi(e));
-    for (unsigned t = 1; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
-    // The small phases' partners (workers 1 .. small_ways-1) run on the creating
-    // thread's L3 (CCD), one physical core each: the groups they replay and
-    // assemble move between the threads' caches every phase, and across CCDs
-    // each such line costs a remote fetch (measured: 1k-group cycles 2.5-3x
-    // slower whenever the scheduler placed a partner on another CCD).
-    // HBN_PIN_L3=0: no pinning.
-    // Every other worker may run anywhere in the container, whatever the
-    // creating thread's mask is (measured at 1M groups: pinning them to the
-    // creating thread's NUMA node changed nothing).
-    const char* pin = std::getenv("HBN_PIN_L3");
-    const std::vector<int> cores =
-        (!pin || pin[0] != '0') && n_ > 1 ? l3_partner_cores() : std::vector<int>();
-    cpu_set_t any;
-    allowed_cpus(&any);
-    for (unsigned t = 1; t < n_; ++t) {
-      cpu_set_t one;
-      CPU_ZERO(&one);
-      if (t < small_ && !cores.empty()) CPU_SET(cores[(t - 1) % cores.size()], &one);
-      const cpu_set_t& m = CPU_COUNT(&one) ? one : any;
-      if (CPU_COUNT(&m)) (void)pthread_setaffinity_np(th_[t - 1].native_handle(), sizeof(m), &m);
-    }
-  }
-  ~Pool() {
-    for (unsigned t = 1; t < n_; ++t) post(t, STOP);
-    for (auto& t : th_) t.join();
-  }
-  unsigned size() const { return n_; }
-  // workers for `items` units of work of which one worker should take at least `grain`
-  unsigned ways(size_t items, size_t grain) const {
-    const size_t k = items / (grain ? grain : 1);
-    return (unsigned)std::max<size_t>(1, std::min<size_t>(n_, k));
-  }
-  // ... and for the two long phases of a small node's Ready cycle (event replay,
-  // Ready build: ~100 us each at 1k groups), up to small_ways() workers once
-  // `items` reaches `small_min` — one futex wake per extra worker, which the
-  // caller's own share hides
-  unsigned ways_small(size_t items, size_t grain, size_t small_min) const {
-    const unsigned k = ways(items, grain);
-    if (k > 1 || items < small_min) return k;
-    return std::min<unsigned>(n_, small_);
-  }
-  void set_small_ways(unsigned k) { small_ = k ? k : 1; }
-  size_t small_adv() const { return adv_min_; }
-  size_t small_bulk() const { return bulk_min_; }
-  // Wake workers 1..k-1 ahead of a phase (hbn_ready: while the device steps),
-  // so that, spinning for up to spin_us, they take the phase's job at once.
-  void prewake(unsigned k) {
-    if (!spin_us_) return;
-    for (unsigned t = 1; t < k && t < n_; ++t) {
-      Worker& w = w_[t];
-      w.poke.store(true);
-      if (w.sleeping.load()) {
-        std::lock_guard<std::mutex> lk(w.mu);
-        w.cv.notify_one();
-      }
-    }
-  }
-  unsigned small_ways() const { return std::min(n_, small_); }
-  // f(tid) for tid in [0, k) (k = use, at most size()); returns once every
-  // worker finished; the first exception (lowest tid) is rethrown on the
-  // calling thread
-  template <class F>
-  void run(F&& f, unsigned use = 0) {
-    const unsigned k = use && use < n_ ? use : n_;
-    if (k == 1) {  // the calling thread alone
-      f(0u);
-      return;
-    }
-    std::vector<std::exception_ptr> err(k);
-    auto body = [&](unsigned t) {
-      try {
-        f(t);
-      } catch (...) {
-        err[t] = std::current_exception();
-      }
-    };
-    if (k > 1) {
-      job_ = body;
-      left_.store(k - 1);
-      for (unsigned t = 1; t < k; ++t) post(t, ++w_[t].seq);
-      body(0);
-      if (left_.load() != 0) {
-        std::unique_lock<std::mutex> lk(mu_);
-        waiting_.store(true);
-        done_.wait(lk, [&] { return left_.load() == 0; });
-        waiting_.store(false);
-      }
-      job_ = nullptr;
-    } else {
-      body(0);
-    }
-    for (auto& e : err)
-      if (e) std::rethrow_exception(e);
-  }
-
- private:
-  static constexpr uint64_t STOP = ~0ull;
-  // Only the workers a phase uses are woken (one futex each); nobody polls.
-  // Polling for ~20-50 us between phases (r03, and again r04 with per-worker
-  // wake-ups) made the 1k-group MultiNode 3-5x slower on the GPU box — every
-  // phase, single-threaded ones included, slowed down next to the polling
-  // threads under the box's 16-CPU quota — so small phases run on the calling
-  // thread alone (ways()) and workers block between phases.  (Blocking
-  // workers on 1k-group phases — grains 256-1024 — measured 0.37 and 1.22 ms
-  // per cycle in two runs on one box against 0.43-0.44 ms single-threaded:
-  // not kept.)
-  struct alignas(64) Worker {
-    std::atomic<uint64_t> post{0};  // the job sequence number posted to this worker (STOP: exit)
-    std::atomic<bool> sleeping{false};
-    std::atomic<bool> poke{false};  // prewake(): spin for the next job
-    std::mutex mu;
-    std::condition_variable cv;
-    uint64_t seq = 0;  // (caller side) the last number posted
-  };
-  void post(unsigned t, uint64_t v) {
-    Worker& w = w_[t];
-    w.post.store(v);  // (seq_cst, against the worker's sleeping flag)
-    if (w.sleeping.load()) {
-      std::lock_guard<std::mutex> lk(w.mu);
-      w.cv.notify_one();
-    }
-  }
-  void loop(unsigned t) {
-    Worker& w = w_[t];
-    uint64_t seen = 0;
-    bool spin = false;
-    for (;;) {
-      if (spin && spin_us_ && t < small_) {  // (a small-phase partner, after a job or a prewake) spin briefly
-        const auto t0 = std::chrono::steady_clock::now();
-        const auto lim = std::chrono::microseconds(spin_us_);
-        while (w.post.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() - t0 < lim)
-          cpu_relax();
-      }
-      if (w.post.load() == seen) {
-        std::unique_lock<std::mutex> lk(w.mu);
-        w.sleeping.store(true);
-        w.cv.wait(lk, [&] { return w.post.load() != seen || w.poke.load(); });
-        w.sleeping.store(false);
-        if (w.post.load() == seen) {  // poked: spin for the job
-          w.poke.store(false);
-          spin = true;
-          continue;
-        }
-      }
-      w.poke.store(false);
-      spin = true;
-      seen = w.post.load();
-      if (seen == STOP) return;
-      job_(t);
-      if (left_.fetch_sub(1) == 1 && waiting_.load()) {
-        std::lock_guard<std::mutex> lk(mu_);
-        done_.notify_one();
-      }
-    }
-  }
-  unsigned n_;
-  unsigned small_ = 4;
-  unsigned spin_us_ = 150;  // HBN_SPIN_US: the small-phase partners spin this long after a job / prewake
-  size_t adv_min_ = 512;  // Advance: split over the partners from this many groups on
-  size_t bulk_min_ = 512;  // bulk ingestion (HBN_SMALL_BULK): the same, from this many messages
-  std::vector<Worker> w_;
-  std::vector<std::thread> th_;
-  std::mutex mu_;
-  std::condition_variable done_;
-  std::function<void(unsigned)> job_;
-  std::atomic<unsigned> left_{0};
-  std::atomic<bool> waiting_{false};
-};
+// (Pool and its CPU placement: hbpool.h)
+using hbpool::Pool;
+using hbpool::SMALL_CYCLE_MSGS;
+using hbpool::PREWAKE_MIN_MSGS;
 
 // [lo, hi) of n items for worker t of k
 inline void split(size_t n, unsigned k, unsigned t, size_t* lo, size_t* hi) {
@@ -1794,7 +1562,12 @@ void flush(hbn_node* n) {
     HBN_PHASE(n, PH_HB_STEP);
     check(hb_step(n->h, &b, HB_STEP_HOST_PTRS | (n->b_prop ? HB_STEP_MSG_PROPS : 0u)));
   }
-  n->pool->prewake(n->pool->small_ways());  // (the replay's workers wake while the device steps)
+  // A small cycle's replay and Ready build split over the partners: they wake
+  // while the device steps and spin between the cycle's phases.  A cycle of
+  // many messages runs its phases on the whole pool for far longer than a
+  // wake-up, and a tiny one stays on the caller: no spinning for either.
+  n->pool->set_small_cycle(b.n < SMALL_CYCLE_MSGS);
+  if (b.n >= PREWAKE_MIN_MSGS) n->pool->prewake(n->pool->small_ways());
   consume_events(n);
   {
     HBN_PHASE(n, PH_STEPPED);

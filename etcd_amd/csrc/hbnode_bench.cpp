@@ -37,8 +37,9 @@ extern "C" {
 // node's host threads too (hbn_set_threads; 0 = the library default).
 #define HBNB_BULK 1u
 #define HBNB_PAR_APP 2u
-// HBNB_PIN: the application pins its Ready-loop thread to the CPU it starts on
-// (before hbn_start, whose small-phase worker then shares that CPU's L3)
+// HBNB_PIN: the application pins its Ready-loop thread to the CPU it starts on,
+// after hbn_start (whose small-phase partners share that CPU's L3; the
+// threads the library starts inherit the unpinned mask)
 #define HBNB_PIN 4u
 int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t rounds, uint32_t flags,
               uint32_t threads, double* out);
@@ -51,12 +52,7 @@ int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t roun
   if (G == 0 || n < 2 || n > HB_MAX_REPLICAS || !out) return HB_EINVAL;
   cpu_set_t old_mask;
   const bool pinned = (flags & HBNB_PIN) && sched_getaffinity(0, sizeof(old_mask), &old_mask) == 0;
-  if (pinned) {
-    cpu_set_t one;
-    CPU_ZERO(&one);
-    CPU_SET(sched_getcpu(), &one);
-    (void)sched_setaffinity(0, sizeof(one), &one);
-  }
+  const int cpu0 = sched_getcpu();  // the CPU the loop starts on (the node's partners share its L3)
   struct Unpin {
     bool on;
     cpu_set_t* m;
@@ -69,6 +65,14 @@ int hbnb_run2(int device, uint32_t G, uint32_t n, uint32_t warmup, uint32_t roun
   int rc = hbn_start(device, 1, G, n, 256, HB_NO_LIMIT, max_batch, &mn);
   if (rc) return rc;
   if (threads) rc = hbn_set_threads(mn, threads);
+  // pinned only once the node (and its threads) exist: a thread the library
+  // starts inherits the creating thread's mask, which must not be one CPU
+  if (pinned && cpu0 >= 0) {
+    cpu_set_t one;
+    CPU_ZERO(&one);
+    CPU_SET(cpu0, &one);
+    (void)sched_setaffinity(0, sizeof(one), &one);
+  }
   const uint32_t app_threads =
       (flags & HBNB_PAR_APP) ? (threads ? threads : std::min(16u, std::max(1u, std::thread::hardware_concurrency()))) : 1;
   std::vector<hbn_storage*> st(G, nullptr);

@@ -11,6 +11,9 @@
 // open-addressing table (16-byte slots, load <= 1/2).
 #include <algorithm>
 #include <cstring>
+#include <memory>
+#include <new>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -27,6 +30,22 @@ inline uint64_t splitmix64(uint64_t x) {  // etcd_amd/synth.py splitmix64
 }
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+// The exports' bodies run under this: nothing thrown crosses the C boundary
+// (a Go / Python host would std::terminate).  A failed allocation is
+// HB_ENOMEM, as in the rest of libhbnode (hbnode.cpp guarded()).
+template <class F>
+int route_guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return HB_ENOMEM;
+  } catch (const std::system_error&) {  // (thread resources: parallel() runs such a chunk inline)
+    return HB_ENOMEM;
+  } catch (...) {
+    return HB_EINVARIANT;
+  }
+}
 
 }  // namespace
 
@@ -70,25 +89,30 @@ struct hbn_router {
       h = (h + 1) & hmask;
     }
   }
+  // body(t) for t in [0, T): chunk 0 on the calling thread; a chunk whose
+  // thread cannot be started runs inline (the threads started are always joined)
   template <class F>
   void parallel(uint64_t T, F&& body) {
     std::vector<std::thread> th;
-    for (uint64_t t = 1; t < T; ++t) th.emplace_back(body, t);
+    th.reserve(T);
+    std::vector<uint64_t> inl;
+    for (uint64_t t = 1; t < T; ++t) {
+      try {
+        th.emplace_back(body, t);
+      } catch (const std::system_error&) {
+        inl.push_back(t);
+      }
+    }
     body(0);
+    for (uint64_t t : inl) body(t);
     for (auto& x : th) x.join();
   }
 };
 
-extern "C" {
+namespace {
 
-uint32_t hbn_owner(uint64_t group_id, uint32_t world) {
-  return world <= 1 ? 0u : (uint32_t)(splitmix64(group_id) % world);
-}
-
-int hbn_router_create(const uint64_t* ids, uint64_t n, uint32_t world, uint32_t threads, hbn_router** out) {
-  if (!out || world == 0 || world > 255 || (n && !ids)) return HB_EINVAL;
-  *out = nullptr;
-  auto* r = new hbn_router;
+int router_create(const uint64_t* ids, uint64_t n, uint32_t world, uint32_t threads, hbn_router** out) {
+  std::unique_ptr<hbn_router> r(new hbn_router);
   r->world = world;
   r->n = n;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
@@ -106,52 +130,32 @@ int hbn_router_create(const uint64_t* ids, uint64_t n, uint32_t world, uint32_t 
     r->hval.assign(cap, NONE);
     r->hmask = cap - 1;
   }
-  auto fail = [&] {
-    delete r;
-    return HB_EINVAL;
-  };
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t id = ids[i];
     const uint32_t k = hbn_owner(id, world);
-    if (r->ids[k].size() > SLOT_MASK) return fail();  // more than an engine holds
+    if (r->ids[k].size() > SLOT_MASK) return HB_EINVAL;  // more than an engine holds
     const uint32_t v = (k << SLOT_BITS) | (uint32_t)r->ids[k].size();
     if (r->dense) {
-      if (r->loc[id] != NONE) return fail();  // a duplicate id
+      if (r->loc[id] != NONE) return HB_EINVAL;  // a duplicate id
       r->loc[id] = v;
     } else if (id == ~0ull) {
-      if (r->has_max) return fail();
+      if (r->has_max) return HB_EINVAL;
       r->has_max = true;
       r->max_val = v;
     } else {
       uint64_t h = splitmix64(id ^ 0x5bd1e995ull) & r->hmask;
       while (r->hkey[h] != ~0ull && r->hkey[h] != id) h = (h + 1) & r->hmask;
-      if (r->hkey[h] == id) return fail();
+      if (r->hkey[h] == id) return HB_EINVAL;
       r->hkey[h] = id;
       r->hval[h] = v;
     }
     r->ids[k].push_back(id);
   }
-  *out = r;
+  *out = r.release();
   return HB_OK;
 }
 
-int hbn_router_destroy(hbn_router* r) {
-  delete r;
-  return HB_OK;
-}
-
-uint64_t hbn_router_local_count(const hbn_router* r, uint32_t rank) {
-  return (r && rank < r->world) ? r->ids[rank].size() : 0;
-}
-
-int hbn_router_local_ids(const hbn_router* r, uint32_t rank, uint64_t* ids) {
-  if (!r || rank >= r->world || (!ids && !r->ids[rank].empty())) return HB_EINVAL;
-  if (!r->ids[rank].empty()) std::memcpy(ids, r->ids[rank].data(), r->ids[rank].size() * 8);
-  return HB_OK;
-}
-
-int hbn_route(hbn_router* r, const uint64_t* gids, uint64_t n, uint64_t* counts, uint64_t* unknown) {
-  if (!r || !counts || (n && !gids)) return HB_EINVAL;
+int route(hbn_router* r, const uint64_t* gids, uint64_t n, uint64_t* counts, uint64_t* unknown) {
   const uint32_t W = r->world;
   // contiguous chunks of at least 64K messages, one per thread at most
   const uint64_t T = std::max<uint64_t>(1, std::min<uint64_t>(r->threads, (n + 65535) / 65536));
@@ -189,15 +193,15 @@ int hbn_route(hbn_router* r, const uint64_t* gids, uint64_t n, uint64_t* counts,
   return HB_OK;
 }
 
-int hbn_route_take(hbn_router* r, uint64_t* const* pos, uint32_t* const* slot) {
-  if (!r || (!pos && !slot)) return HB_EINVAL;
+int route_take(hbn_router* r, uint64_t* const* pos, uint32_t* const* slot) {
   const uint32_t W = r->world;
   const uint64_t n = r->n_last, T = r->T_last, per = r->per_last;
   // each chunk writes its messages at its offsets: sequential reads of the
   // places, sequential writes per rank
   r->parallel(T, [&](uint64_t t) {
     const uint64_t lo = t * per, hi = std::min(n, lo + per);
-    std::vector<uint64_t> o(r->off.begin() + t * W, r->off.begin() + (t + 1) * W);
+    uint64_t o[256];  // (world <= 255; nothing in a chunk's thread allocates, so nothing throws there)
+    std::copy(r->off.begin() + t * W, r->off.begin() + (t + 1) * W, o);
     const uint32_t* pl = r->place.data();
     for (uint64_t i = lo; i < hi; ++i) {
       const uint32_t v = pl[i];
@@ -209,6 +213,45 @@ int hbn_route_take(hbn_router* r, uint64_t* const* pos, uint32_t* const* slot) {
     }
   });
   return HB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t hbn_owner(uint64_t group_id, uint32_t world) {
+  return world <= 1 ? 0u : (uint32_t)(splitmix64(group_id) % world);
+}
+
+int hbn_router_destroy(hbn_router* r) {
+  delete r;
+  return HB_OK;
+}
+
+uint64_t hbn_router_local_count(const hbn_router* r, uint32_t rank) {
+  return (r && rank < r->world) ? r->ids[rank].size() : 0;
+}
+
+int hbn_router_local_ids(const hbn_router* r, uint32_t rank, uint64_t* ids) {
+  if (!r || rank >= r->world || (!ids && !r->ids[rank].empty())) return HB_EINVAL;
+  if (!r->ids[rank].empty()) std::memcpy(ids, r->ids[rank].data(), r->ids[rank].size() * 8);
+  return HB_OK;
+}
+
+int hbn_router_create(const uint64_t* ids, uint64_t n, uint32_t world, uint32_t threads, hbn_router** out) {
+  if (!out || world == 0 || world > 255 || (n && !ids)) return HB_EINVAL;
+  *out = nullptr;
+  return route_guarded([&] { return router_create(ids, n, world, threads, out); });
+}
+
+int hbn_route(hbn_router* r, const uint64_t* gids, uint64_t n, uint64_t* counts, uint64_t* unknown) {
+  if (!r || !counts || (n && !gids)) return HB_EINVAL;
+  return route_guarded([&] { return route(r, gids, n, counts, unknown); });
+}
+
+int hbn_route_take(hbn_router* r, uint64_t* const* pos, uint32_t* const* slot) {
+  if (!r || (!pos && !slot)) return HB_EINVAL;
+  return route_guarded([&] { return route_take(r, pos, slot); });
 }
 
 }  // extern "C"

@@ -29,6 +29,56 @@ def _strerror(code):
         return "?"
 
 
+class HipRuntimeConflict(RuntimeError):
+    """Two HIP runtimes (libamdhip64) are or would be mapped in this process:
+    the engine's handle would live in one and the caller's streams and tensors
+    in the other (hb_create then fails with HB_EDEVICE)."""
+
+
+def _mapped_hip_runtimes():
+    """The distinct libamdhip64 files mapped into this process (real paths)."""
+    out = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1]
+                if "libamdhip64" in os.path.basename(p):
+                    out.add(os.path.realpath(p))
+    except OSError:
+        pass
+    return out
+
+
+def _bind_one_hip_runtime():
+    """Make the engine bind to the HIP runtime torch uses, whatever the import order.
+
+    libhipbatch.so needs `libamdhip64.so.7` (RUNPATH /opt/rocm).  PyTorch-ROCm
+    ships its own copy, which its libraries load as `libamdhip64.so` from their
+    own directory.  Loaded after torch, the engine binds to torch's copy by
+    soname; loaded first, it would map /opt/rocm's and torch would later map a
+    second runtime beside it (r05: `hb_create failed: -3` in a process that
+    imported the router before torch).  So when no runtime is mapped yet and
+    torch's copy exists, that file is preloaded (RTLD_GLOBAL): the engine binds
+    to it by soname and torch's later load finds the same file already mapped.
+    A process that already holds two runtimes cannot be fixed here: a named
+    error instead of HB_EDEVICE at the first call."""
+    have = _mapped_hip_runtimes()
+    if len(have) > 1:
+        raise HipRuntimeConflict(f"two HIP runtimes already mapped: {sorted(have)}")
+    if have:
+        return
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    for d in (spec.submodule_search_locations or []) if spec else []:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            C.CDLL(p, mode=C.RTLD_GLOBAL)
+            return
+
+
 def lib():
     """Load libhipbatch.so (built by `make -C etcd_amd/csrc`)."""
     global _lib
@@ -37,7 +87,11 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: build it with `make -C etcd_amd/csrc` "
                           "(there is no CPU fallback)")
+    _bind_one_hip_runtime()
     L = C.CDLL(LIB_PATH)
+    have = _mapped_hip_runtimes()
+    if len(have) > 1:
+        raise HipRuntimeConflict(f"loading {LIB_PATH} mapped a second HIP runtime: {sorted(have)}")
     P = C.POINTER
     H = C.c_void_p
     sig = {

@@ -83,8 +83,8 @@ class NativeRouter:
     splitmix64(id) % world, local slot = position among the rank's ids)."""
 
     def __init__(self, group_ids, world, threads=0):
-        # (a process that also uses the GPU through torch imports torch first, so
-        # that libhbnode's engine library binds to torch's HIP runtime)
+        # (hipbatch.lib() binds the engine to torch's HIP runtime whatever the
+        # import order: tests/test_runtime_bind.py)
         import ctypes as C
         from .multinode import lib
         self._L = L = lib()
@@ -94,6 +94,8 @@ class NativeRouter:
         self.threads = threads or min(16, os.cpu_count() or 1)
         self._h = C.c_void_p()
         rc = L.hbn_router_create(ids.ctypes.data_as(C.c_void_p), len(ids), world, self.threads, C.byref(self._h))
+        if rc == -2:  # HB_ENOMEM
+            raise MemoryError("hbn_router_create: out of host memory")
         if rc != 0:
             raise ValueError(f"hbn_router_create: {rc}")
 
@@ -119,6 +121,8 @@ class NativeRouter:
         unk = C.c_uint64()
         rc = self._L.hbn_route(self._h, gids.ctypes.data_as(C.c_void_p), len(gids), counts.ctypes.data_as(C.c_void_p),
                                C.byref(unk))
+        if rc == -2:
+            raise MemoryError("hbn_route: out of host memory")
         if rc != 0:
             raise ValueError(f"hbn_route: {rc}")
         ranks = range(W) if ranks is None else ranks

@@ -33,10 +33,13 @@ uint32_t hbn_owner(uint64_t group_id, uint32_t world);
 /* A router over the node's groups: ids[0 .. n) (distinct), each owned by rank
  * hbn_owner(id, world) at local slot = its position among that rank's ids in
  * the order given (etcd_amd/shard.py ShardMap.local_ids).  A dense id space
- * (every id < 2 n) is looked up in a flat table, any other through an
+ * (every id < 2 n + 1024) is looked up in a flat table, any other through an
  * open-addressing hash.  threads: host threads for hbn_route (0 = min(16,
  * cores)).  Returns HB_EINVAL (-1) on a duplicate id, world 0 or above 255,
- * or a rank owning more than 2^24 groups (an engine's capacity, hb_create). */
+ * or a rank owning more than 2^24 groups (an engine's capacity, hb_create);
+ * HB_ENOMEM (-2) when the tables cannot be allocated.  No router function
+ * lets a C++ exception out: hbn_route / hbn_route_take return HB_ENOMEM when
+ * host memory runs out. */
 int hbn_router_create(const uint64_t* ids, uint64_t n, uint32_t world, uint32_t threads, hbn_router** out);
 int hbn_router_destroy(hbn_router* r);
 /* Groups owned by `rank` (its engine's capacity), and their global ids by slot. */

@@ -95,3 +95,29 @@ def test_route_global_ack_stream_like_the_bench():
         sm = ShardMap(ids, world, k)
         idx, slots = sm.route_local(gid, sm.dense_slots(G_total))
         assert np.array_equal(out[k][0], idx) and np.array_equal(out[k][1], slots)
+
+
+def test_router_out_of_memory_is_an_error_code():
+    """A failed allocation inside the router is HB_ENOMEM (MemoryError here),
+    not a C++ exception through the C ABI (which would abort the host).  The
+    child caps its address space just above what it holds, then asks for a
+    sparse router whose hash table (96 MB) cannot fit."""
+    import subprocess
+    import sys
+    code = (
+        "import resource, numpy as np\n"
+        "from etcd_amd.shard import NativeRouter\n"
+        "from etcd_amd import multinode; multinode.lib()\n"
+        "ids = np.arange(4_000_000, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)\n"
+        "vm = [int(l.split()[1]) for l in open('/proc/self/status') if l.startswith('VmSize:')][0] * 1024\n"
+        "resource.setrlimit(resource.RLIMIT_AS, (vm + (32 << 20), resource.RLIM_INFINITY))\n"
+        "try:\n"
+        "    NativeRouter(ids, 2, threads=1)\n"
+        "    print('created')\n"
+        "except MemoryError:\n"
+        "    print('enomem')\n")
+    if "libasan" in os.environ.get("LD_PRELOAD", ""):
+        pytest.skip("under ASan (tests/test_sanitizers.py) operator new aborts on out-of-memory instead of throwing")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == "enomem"

@@ -42,3 +42,24 @@ def test_host_libraries_under_asan_ubsan():
     out = r.stdout + r.stderr
     bad = [ln for ln in out.splitlines() if "runtime error:" in ln or "AddressSanitizer" in ln]
     assert r.returncode == 0 and not bad, out[-6000:]
+
+
+def test_host_threading_under_tsan():
+    """libhbnode's host threading under ThreadSanitizer: the Pool (hbpool.h:
+    run / prewake / post / STOP, partners spinning or not, small and large
+    cycles, 1-16 workers, two nodes' pools at once) and the router's threaded
+    passes (hbroute.cpp), driven by tests/tsan/pool_tsan.cpp with no GPU.
+    Any race report fails the test."""
+    exe = os.path.join(ROOT, "oracle", "build", "pool_tsan")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    cc = subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=thread", "-pthread", "-o", exe,
+                         os.path.join(ROOT, "tests", "tsan", "pool_tsan.cpp"),
+                         os.path.join(ROOT, "etcd_amd", "csrc", "hbroute.cpp")], capture_output=True, text=True)
+    if cc.returncode != 0 and "tsan" in (cc.stderr or "").lower():
+        pytest.skip("gcc ThreadSanitizer runtime not installed")
+    assert cc.returncode == 0, cc.stderr[-3000:]
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=0:exitcode=66"))
+    out = r.stdout + r.stderr
+    assert "WARNING: ThreadSanitizer" not in out, out[-6000:]
+    assert r.returncode == 0 and "pool_tsan ok" in out, out[-3000:]
