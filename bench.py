@@ -643,12 +643,19 @@ def run_replication(args, world, rank, local):
                               "apply_ms": float(ph2[abi.HB_PHASE_APPLY]),
                               "general_ms": float(ph2[abi.HB_PHASE_GENERAL]),
                               "finish_ms": float(ph2[abi.HB_PHASE_FINISH]), "steps": nph2}}
-        # HB_PHASE_APPLY brackets exactly the k_apply_fast launch (HIP events on the launch stream)
+        # HB_PHASE_APPLY brackets exactly the dominant kernel's launch (HIP events on
+        # its launch stream): k_route_fast where the route runs inside the fast
+        # lane's workgroups (hb_step_kernels), else k_apply_fast
         achieved = float(alg / (apply_ms * 1e-3) / 1e9)
-        kname = f"k_apply_fast<{3 if n <= 3 else (5 if n <= 5 else 7)}>"
-        # (rocprofv3 names the template with its X-mode flag since r04)
-        traffic, tsrc = pmc_traffic(args.traffic_json, [kname[:-1] + ", false, 2u>", kname[:-1] + ", false>", kname],
-                                    G, n, apply_ms * 1e3)
+        fused = bool(eng.step_kernels() & abi.HB_KERN_ROUTE_FAST)
+        if fused:
+            kname = "k_route_fast"
+            knames = [kname]
+        else:
+            kname = f"k_apply_fast<{3 if n <= 3 else (5 if n <= 5 else 7)}>"
+            # (rocprofv3 names the template with its X-mode flag since r04)
+            knames = [kname[:-1] + ", false, 2u>", kname[:-1] + ", false>", kname]
+        traffic, tsrc = pmc_traffic(args.traffic_json, knames, G, n, apply_ms * 1e3)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
@@ -659,7 +666,9 @@ def run_replication(args, world, rank, local):
                 "frac_isolated": round(alg / (float(ph2[abi.HB_PHASE_APPLY]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "alg_bytes_per_launch": alg,
                 "alg_bytes_note": f"SURVEY.md 8(d): {alg_bytes_per_group(n)} B/group = "
-                                  f"{alg_bytes_per_group(n) / (n - 1):.0f} B/MsgAppResp x {G * (n - 1)} MsgAppResp",
+                                  f"{alg_bytes_per_group(n) / (n - 1):.0f} B/MsgAppResp x {G * (n - 1)} MsgAppResp"
+                                  + (" (the message's 24 B are read by this kernel as its 16-byte partitioned "
+                                     "record: the route runs inside it)" if fused else ""),
                 # the whole step (partition + route + apply + finish) against the same bytes
                 "step_frac": round(alg / (ms / args.steps * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 

@@ -123,6 +123,7 @@ HB_PHASE_APPLY = 1
 HB_PHASE_GENERAL = 2
 HB_PHASE_FINISH = 3
 HB_PHASE_COUNT = 4
+HB_KERN_ROUTE_FAST = 1  # hb_step_kernels: k_route_fast ran the route and the fast lane
 
 STAT_NAMES = ["msgs", "appresp", "voteresp", "dropped", "commits", "won", "lost",
               "events", "faults", "entries"]

@@ -1448,6 +1448,178 @@ __global__ void __launch_bounds__(PART, HB_FAST_WAVES) k_apply_fast(ApplyArgs a)
 }
 
 // ---------------------------------------------------------------------------
+// k_route_fast: k_route<2> and k_apply_fast<3> in one workgroup (n = 3,
+// leader-side batches, one-pass geometry).  The route phase stages each of
+// the workgroup's RF_RG groups' first two messages in LDS exactly as k_route
+// does; the fast lane then reads them from there instead of from the slot
+// arrays, so the slots are neither written nor read back (32 + 1 bytes per
+// group, twice).  Only a group the fast lane hands over gets its count and
+// slots written to HBM, where k_apply reads them.  512 lanes and 73 KB of LDS
+// per workgroup: two workgroups per CU, each lane stepping RF_RG / 512 groups
+// in turn (no barrier between them: the partitions' event cursors and
+// hand-over masks stay in LDS until the end).
+// ---------------------------------------------------------------------------
+#ifndef HB_ROUTE_FAST
+#define HB_ROUTE_FAST 1
+#endif
+#ifndef HB_RF_NOUNROLL
+#define HB_RF_NOUNROLL 0
+#endif
+#ifndef HB_RF_UNROLL
+#define HB_RF_UNROLL 4  // records in flight per lane in the route phase
+#endif
+#ifndef HB_RF_THREADS
+#define HB_RF_THREADS 512
+#endif
+#ifndef HB_RF_RG_LOG
+#define HB_RF_RG_LOG 11
+#endif
+#ifndef HB_RF_WAVES
+#define HB_RF_WAVES 4
+#endif
+constexpr uint32_t RF_THREADS = HB_RF_THREADS;
+constexpr uint32_t RF_RG_LOG = HB_RF_RG_LOG, RF_RG = 1u << RF_RG_LOG;  // groups per workgroup (2 per 4096-group bucket)
+constexpr uint32_t RF_NP = RF_RG / PART;                       // partitions per workgroup
+constexpr uint32_t RF_KMAX = 2;
+constexpr uint32_t RF_UNROLL = HB_RF_UNROLL;
+__global__ void __launch_bounds__(RF_THREADS, HB_RF_WAVES) k_route_fast(ApplyArgs a) {
+  constexpr uint32_t KMAX = RF_KMAX;
+  constexpr int NMAX = 3;
+  const uint32_t sl = a.sis_log, W = 1u << (PART_LOG + sl - RF_RG_LOG);
+  __shared__ uint32_t l_cnt[RF_RG];
+  __shared__ uint4 l_slot[KMAX][RF_RG];
+  __shared__ uint32_t l_ptot[RF_NP];
+  __shared__ uint64_t l_moff[RF_NP];
+  __shared__ uint32_t l_fill[RF_NP], l_pfill[RF_NP];
+  __shared__ uint32_t l_flag[RF_NP][FLAG_WORDS];
+  __shared__ uint64_t l_stats[ST_N + 1];
+  const uint32_t x = blockIdx.x, q = x >> 3;
+  const uint32_t bk = ((q / W) << 3) | (x & 7), w = q % W;
+  if (bk >= a.NBK) return;  // uniform: grid padding
+  const uint32_t tid = threadIdx.x;
+  const uint32_t G = a.S.G;
+  const uint32_t lg0 = w * RF_RG;
+  for (uint32_t i = tid; i < RF_RG; i += RF_THREADS) l_cnt[i] = 0;
+  if (tid < RF_NP) {
+    l_ptot[tid] = 0;
+    l_fill[tid] = l_pfill[tid] = 0;
+  }
+  if (tid < RF_NP * FLAG_WORDS) (&l_flag[0][0])[tid] = 0;
+  if (tid <= ST_N) l_stats[tid] = 0;
+  __syncthreads();
+  // ---- route: the bucket's records, the workgroup's groups ranked into LDS (as k_route)
+  const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
+  const uint32_t sub_lo = lg0 >> PART_LOG, sub_hi = (lg0 + RF_RG) >> PART_LOG;
+  for (uint32_t base = lo; base < hi; base += RF_THREADS * RF_UNROLL) {
+    MsgRec m[RF_UNROLL];
+    uint32_t sub[RF_UNROLL];
+#pragma unroll
+    for (uint32_t u = 0; u < RF_UNROLL; ++u) {
+      const uint32_t p = base + u * RF_THREADS + tid;
+      if (p < hi) m[u] = a.rec[p];
+      sub[u] = p < hi ? (m[u].info >> 24) & 0xFu : 0xFFu;
+    }
+    if (w == 0) {  // the key bytes of the general kernel's bucket walk
+#pragma unroll
+      for (uint32_t u = 0; u < RF_UNROLL; ++u) {
+        const uint32_t p = base + u * RF_THREADS + tid;
+        if (p < hi) a.key[p] = (uint8_t)sub[u];
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < RF_UNROLL; ++u) {
+      const uint32_t p = base + u * RF_THREADS + tid;
+      const bool own = p < hi && sub[u] >= sub_lo && sub[u] < sub_hi;
+      const uint32_t l = own ? (((sub[u] - sub_lo) << PART_LOG) | ((m[u].info >> 16) & (PART - 1))) : RF_RG;
+      if (l < RF_RG) {
+        const uint32_t r = atomicAdd(&l_cnt[l], 1u);
+        if (r < KMAX) l_slot[r][l] = make_uint4(m[u].info, m[u].orig, (uint32_t)m[u].ti, (uint32_t)(m[u].ti >> 32));
+      }
+    }
+  }
+  __syncthreads();
+  // ---- each partition's M event chunk in its bucket's region (as k_route)
+  for (uint32_t i = tid; i < RF_RG; i += RF_THREADS) {
+    uint32_t s = l_cnt[i];  // (a wave's 64 groups lie in one partition)
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+    if ((tid & 63) == 0 && s) atomicAdd(&l_ptot[i >> PART_LOG], s);
+  }
+  __syncthreads();
+  const uint32_t part0 = (bk << sl) + w * RF_NP;
+  if (tid < RF_NP) {
+    const uint32_t part = part0 + tid;
+    uint64_t mo = 0;
+    if (part < a.NB) {
+      const uint32_t r = atomicAdd(&a.bk_fill[bk * CTR_STRIDE], a.ev_per_msg * (l_ptot[tid] + PART * a.props_on));
+      mo = (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + lo + ((uint64_t)bk * PART << sl) * a.props_on) + r;
+      a.ev_off[2 * part + 1] = mo;
+    }
+    l_moff[tid] = mo;
+  }
+  __syncthreads();
+  // ---- the fast lane (as k_apply_fast) over the workgroup's groups, RF_RG / RF_THREADS per lane
+  uint32_t acc[ST_N + 1];
+#pragma unroll
+  for (int k = 0; k <= ST_N; ++k) acc[k] = 0;
+#if HB_RF_NOUNROLL
+#pragma nounroll
+#endif
+  for (uint32_t i = tid; i < RF_RG; i += RF_THREADS) {
+    const uint32_t p = i >> PART_LOG, part = part0 + p, lane = i & (PART - 1);
+    const uint32_t g = part * PART + lane;
+    const bool gvalid = part < a.NB && g < G;
+    FollowLane<NMAX> L;
+    L.S = a.S;
+    L.g = g;
+    L.mlo = gvalid ? at32(reinterpret_cast<uint32_t*>(a.S.meta), 2 * g) : 0u;
+    const uint32_t prop_raw = (a.props && gvalid) ? at32(a.props, g) : 0u;
+    const uint32_t c = gvalid ? l_cnt[i] : 0u;
+    const uint32_t cnt = c < CNT_MASK ? c : CNT_MASK;
+    if (gvalid) L.load_head();
+    const bool live = gvalid && L.n() != 0 && L.faulted() == 0;
+    const bool leader = live && L.state() == HB_STATE_LEADER;
+    const bool nc = (L.mlo & (uint32_t)M_NC) != 0;
+    const bool lead = leader && !nc && (cnt <= KMAX || prop_raw != 0);
+    L.dirty = 0;
+    L.nev = 0;
+    if (lead) {
+      L.load_rest();
+    } else {
+      L.last = L.committed = 0;
+      L.term = 0;
+    }
+    uint32_t s_info[KMAX], s_orig[KMAX];
+    uint64_t s_term[KMAX], s_index[KMAX], s_h[KMAX], s_c[KMAX];
+    const bool slots = lead && cnt <= KMAX;
+#pragma unroll
+    for (uint32_t k = 0; k < KMAX; ++k) {
+      const uint4 r = (slots && k < cnt) ? l_slot[k][i] : make_uint4(0, 0, 0, 0);
+      slot_unpack(r, a.side, &s_info[k], &s_orig[k], &s_term[k], &s_index[k]);
+      s_h[k] = s_c[k] = 0;
+    }
+    uint32_t vals[ST_N + 1];
+    const bool flagged = fast_step<NMAX, KMAX>(a, L, part, lane, live, lead, leader, false, prop_raw, cnt, s_info, s_orig,
+                                               s_term, s_index, s_h, s_c, l_moff[p], &l_pfill[p], &l_fill[p], l_flag[p],
+                                               nullptr, vals);
+#pragma unroll
+    for (int k = 0; k <= ST_N; ++k) acc[k] += vals[k];
+    if (flagged) {  // what k_apply reads of a group it takes over: its count and slots
+      a.cnt[g] = (uint8_t)cnt;
+#pragma unroll
+      for (uint32_t k = 0; k < KMAX; ++k)
+        if (k < c) at32(a.slot, k * G + g) = l_slot[k][i];
+    }
+  }
+  reduce_stats(a, l_stats, acc);  // (ends with a barrier: the partitions' fills and flags are final)
+  for (uint32_t j = tid; j < RF_NP * FLAG_WORDS; j += RF_THREADS) {
+    const uint32_t p = j / FLAG_WORDS, part = part0 + p;
+    if (part < a.NB) a.pflag[(size_t)part * FLAG_WORDS + j % FLAG_WORDS] = l_flag[p][j % FLAG_WORDS];
+  }
+  if (tid < RF_NP && part0 + tid < a.NB) fast_close(a, part0 + tid, l_flag[tid], nullptr, l_pfill[tid], l_fill[tid]);
+}
+
+// ---------------------------------------------------------------------------
 // k_apply: the general state machine (Lane::step) for the groups
 // k_apply_fast handed over, from their resume point: every leader / candidate
 // message type; at a group's first follower-side message (MsgApp /
@@ -2879,6 +3051,8 @@ struct hb_handle {
   // launch for the partition and one for the event words; HB_SMALL_STEP=0
   // turns that off (same output: the A/B and the parity tests compare both)
   bool no_small = false;
+  uint32_t kern = 0;  // hb_step_kernels of the last step
+  uint32_t fuse = 1;  // k_route_fast: 0 never, 1 one-pass handles, 2 every geometry (HB_ROUTE_FUSE at hb_create)
   uint32_t agrid = 0;  // the apply kernels' grid (apply_grid_for)
   uint32_t bk_bits = 1;            // bits of a bucket id
   // host-pointer staging
@@ -3055,11 +3229,15 @@ uint32_t apply_grid_for(uint32_t NBK, uint32_t sl, uint32_t NB) {
 uint32_t apply_grid(const hb_handle* h) { return h->agrid; }
 
 // The apply kernels; ev = this step's phase events (HB_STEP_PROFILE) or null.
+// fused: k_route_fast stood in for k_route + k_apply_fast (launched by hb_step)
 template <int NMAX>
-void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full) {
+void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full, bool fused = false) {
   const uint32_t grid = apply_grid(h);
   if (ev) (void)hipEventRecord(ev[2], h->stream);
-  if constexpr (NMAX >= 5) {
+  if (fused) {
+    hipLaunchKernelGGL(k_route_fast, dim3(((h->NBK + 7) & ~7u) << (PART_LOG + h->sis_log - RF_RG_LOG)), dim3(RF_THREADS),
+                       0, h->stream, a);
+  } else if constexpr (NMAX >= 5) {
     if (a.slotx) hipLaunchKernelGGL((k_apply_lead<NMAX, true>), dim3(grid), dim3(PART), 0, h->stream, a);
     else hipLaunchKernelGGL((k_apply_lead<NMAX, false>), dim3(grid), dim3(PART), 0, h->stream, a);
   }
@@ -3126,6 +3304,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   h->max_batch = max_batch;
   h->NB = (capacity + PART - 1) / PART;
   if (const char* e = getenv("HB_SMALL_STEP")) h->no_small = e[0] == '0';
+  if (const char* e = getenv("HB_ROUTE_FUSE")) h->fuse = (uint32_t)atoi(e);
   const size_t G = capacity, R = h->nmax;
   DevState& s = h->st;
   s.G = capacity;
@@ -3675,6 +3854,7 @@ int hb_tick(hb_handle* h, uint32_t flags) {
   h->cur = h->next_set;
   h->next_set ^= 1;
   h->stepped = true;
+  h->kern = 0;
   return HB_OK;
 }
 
@@ -3962,8 +4142,13 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.side = ps.side;
   aa.recx = ps.recx;
   aa.slotx = xmode ? ps.slotx : nullptr;
+  // n = 3, leader-side, one-pass geometry, prep and apply on one stream: the
+  // route runs inside the fast kernel's workgroups (k_route_fast)
+  const bool fused = HB_ROUTE_FAST && h->nmax == 3 && aa.kmax == RF_KMAX && !xmode && !two &&
+                     (h->fuse >= 2 || (h->fuse == 1 && h->passes == 1)) && PART_LOG + h->sis_log >= RF_RG_LOG;
   switch (h->nmax) {
     case 3:
+      if (fused) break;
       if (aa.kmax == 3) launch_route<3>(h, aa, ps_st);
       else launch_route<2>(h, aa, ps_st);
       break;
@@ -3977,7 +4162,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     HB_CHECK(hipStreamWaitEvent(st, ps.prepped, 0));
   }
   switch (h->nmax) {
-    case 3: launch_apply<3>(h, aa, prof_apply ? ev : nullptr, prof); break;
+    case 3: launch_apply<3>(h, aa, prof_apply ? ev : nullptr, prof, fused); break;
     case 5: launch_apply<5>(h, aa, prof_apply ? ev : nullptr, prof); break;
     default: launch_apply<7>(h, aa, prof_apply ? ev : nullptr, prof); break;
   }
@@ -3992,6 +4177,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     h->prof_n++;
   }
   h->stepped = true;
+  h->kern = fused ? HB_KERN_ROUTE_FAST : 0u;
   return HB_OK;
 }
 
@@ -4146,6 +4332,12 @@ int hb_phase_ms(hb_handle* h, float* out, uint32_t* steps) {
       out[i] += ms / (float)(i == HB_PHASE_APPLY ? n : nfull);
     }
   }
+  return HB_OK;
+}
+
+int hb_step_kernels(hb_handle* h, uint32_t* mask) {
+  if (!h || !mask) return HB_EINVAL;
+  *mask = h->kern;
   return HB_OK;
 }
 

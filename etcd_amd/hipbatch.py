@@ -130,6 +130,7 @@ def lib():
         "hb_stats": (C.c_int, [H, C.c_void_p]),
         "hb_phase_ms": (C.c_int, [H, C.c_void_p, P(C.c_uint32)]),
         "hb_phase_reset": (C.c_int, [H]),
+        "hb_step_kernels": (C.c_int, [H, P(C.c_uint32)]),
         "hb_stats_to": (C.c_int, [H, C.c_void_p]),
         "hb_set_stats_accum": (C.c_int, [H, C.c_void_p]),
         "hb_alloc_pinned": (C.c_int, [C.c_size_t, P(C.c_void_p)]),
@@ -442,6 +443,12 @@ class Engine:
 
     def phase_reset(self):
         _check("hb_phase_reset", lib().hb_phase_reset(self.h))
+
+    def step_kernels(self):
+        """hb_step_kernels: HB_KERN_* bits of the kernels the last step launched."""
+        m = C.c_uint32()
+        _check("hb_step_kernels", lib().hb_step_kernels(self.h, C.byref(m)))
+        return int(m.value)
 
     def phase_ms(self):
         """(per-phase average ms, number of profiled steps) since phase_reset()."""

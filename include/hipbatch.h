@@ -578,6 +578,12 @@ int  hb_set_stats_accum(hb_handle* h, uint64_t* dev_accum);
  * hb_phase_reset (the last 256 of them); *steps = how many (synchronizes). */
 int  hb_phase_ms(hb_handle* h, float* out /* [HB_PHASE_COUNT] */, uint32_t* steps);
 int  hb_phase_reset(hb_handle* h);
+/* Which apply kernels the last hb_step launched (for profiles and rooflines):
+ * HB_KERN_ROUTE_FAST = the route and the n = 3 fast lane ran as one kernel
+ * (k_route_fast; HB_PHASE_APPLY then brackets it), else k_route and
+ * k_apply_fast / k_apply_lead separately. */
+#define HB_KERN_ROUTE_FAST 1u
+int  hb_step_kernels(hb_handle* h, uint32_t* mask);
 
 /* ---- pinned host memory for cgo callers (Go must not hand Go memory to C
  * that C retains; raft/hipbatch packs batches into these buffers). -------- */
