@@ -1448,16 +1448,18 @@ __global__ void __launch_bounds__(PART, HB_FAST_WAVES) k_apply_fast(ApplyArgs a)
 }
 
 // ---------------------------------------------------------------------------
-// k_route_fast: k_route<2> and k_apply_fast<3> in one workgroup (n = 3,
-// leader-side batches, one-pass geometry).  The route phase stages each of
-// the workgroup's RF_RG groups' first two messages in LDS exactly as k_route
-// does; the fast lane then reads them from there instead of from the slot
-// arrays, so the slots are neither written nor read back (32 + 1 bytes per
-// group, twice).  Only a group the fast lane hands over gets its count and
-// slots written to HBM, where k_apply reads them.  512 lanes and 73 KB of LDS
-// per workgroup: two workgroups per CU, each lane stepping RF_RG / 512 groups
-// in turn (no barrier between them: the partitions' event cursors and
-// hand-over masks stay in LDS until the end).
+// k_route_fast<KMAX, X>: k_route<KMAX, X> and k_apply_fast<3, X, KMAX> in one
+// workgroup (n = 3, prep and apply on one stream).  The route phase stages
+// each of the workgroup's RG groups' first KMAX messages (and, X mode, their
+// extensions) in LDS exactly as k_route does; the fast lane then reads them
+// from there instead of from the slot arrays, so the slots are neither
+// written nor read back (16 + 16 B per message in X mode, plus the count, each
+// way).  Only a group the fast lane hands over gets its count and slots
+// written to HBM, where k_apply reads them.  512 lanes per workgroup and at
+// most ~73 KB of LDS (RG = 2048 groups for two leader-side slots, fewer when
+// a group keeps more bytes): two workgroups per CU, each lane stepping
+// RG / 512 groups in turn, with no barrier between them (the partitions'
+// event cursors and hand-over masks stay in LDS until the end).
 // ---------------------------------------------------------------------------
 #ifndef HB_ROUTE_FAST
 #define HB_ROUTE_FAST 1
@@ -1472,51 +1474,59 @@ __global__ void __launch_bounds__(PART, HB_FAST_WAVES) k_apply_fast(ApplyArgs a)
 #define HB_RF_THREADS 512
 #endif
 #ifndef HB_RF_RG_LOG
-#define HB_RF_RG_LOG 11
+#define HB_RF_RG_LOG 11  // (two leader-side slots; each doubling of a group's LDS bytes halves it)
 #endif
 #ifndef HB_RF_WAVES
 #define HB_RF_WAVES 4
 #endif
 constexpr uint32_t RF_THREADS = HB_RF_THREADS;
-constexpr uint32_t RF_RG_LOG = HB_RF_RG_LOG, RF_RG = 1u << RF_RG_LOG;  // groups per workgroup (2 per 4096-group bucket)
-constexpr uint32_t RF_NP = RF_RG / PART;                       // partitions per workgroup
-constexpr uint32_t RF_KMAX = 2;
 constexpr uint32_t RF_UNROLL = HB_RF_UNROLL;
+template <uint32_t KMAX, bool X> struct RouteFastGeom {
+  // 16 B per slot, twice in X mode: 2 slots x 2048, 3 x 1024, X 2 x 1024, X 3 x 512 groups
+  static constexpr uint32_t RG_LOG = HB_RF_RG_LOG - (KMAX > 2 ? 1u : 0u) - (X ? 1u : 0u);
+  static constexpr uint32_t RG = 1u << RG_LOG;  // groups per workgroup
+  static constexpr uint32_t NP = RG / PART;     // partitions per workgroup
+};
+template <uint32_t KMAX, bool X>
 __global__ void __launch_bounds__(RF_THREADS, HB_RF_WAVES) k_route_fast(ApplyArgs a) {
-  constexpr uint32_t KMAX = RF_KMAX;
   constexpr int NMAX = 3;
-  const uint32_t sl = a.sis_log, W = 1u << (PART_LOG + sl - RF_RG_LOG);
-  __shared__ uint32_t l_cnt[RF_RG];
-  __shared__ uint4 l_slot[KMAX][RF_RG];
-  __shared__ uint32_t l_ptot[RF_NP];
-  __shared__ uint64_t l_moff[RF_NP];
-  __shared__ uint32_t l_fill[RF_NP], l_pfill[RF_NP];
-  __shared__ uint32_t l_flag[RF_NP][FLAG_WORDS];
+  using GM = RouteFastGeom<KMAX, X>;
+  constexpr uint32_t RG = GM::RG, NP = GM::NP;
+  const uint32_t sl = a.sis_log, W = 1u << (PART_LOG + sl - GM::RG_LOG);
+  __shared__ uint32_t l_cnt[RG];
+  __shared__ uint4 l_slot[KMAX][RG];
+  __shared__ uint4 l_slotx[X ? KMAX : 1][X ? RG : 1];
+  __shared__ uint32_t l_ptot[NP];
+  __shared__ uint64_t l_moff[NP];
+  __shared__ uint32_t l_fill[NP], l_pfill[NP];
+  __shared__ uint32_t l_flag[NP][FLAG_WORDS];
   __shared__ uint64_t l_stats[ST_N + 1];
   const uint32_t x = blockIdx.x, q = x >> 3;
   const uint32_t bk = ((q / W) << 3) | (x & 7), w = q % W;
   if (bk >= a.NBK) return;  // uniform: grid padding
   const uint32_t tid = threadIdx.x;
   const uint32_t G = a.S.G;
-  const uint32_t lg0 = w * RF_RG;
-  for (uint32_t i = tid; i < RF_RG; i += RF_THREADS) l_cnt[i] = 0;
-  if (tid < RF_NP) {
+  const uint32_t lg0 = w * RG;
+  for (uint32_t i = tid; i < RG; i += RF_THREADS) l_cnt[i] = 0;
+  if (tid < NP) {
     l_ptot[tid] = 0;
     l_fill[tid] = l_pfill[tid] = 0;
   }
-  if (tid < RF_NP * FLAG_WORDS) (&l_flag[0][0])[tid] = 0;
+  for (uint32_t i = tid; i < NP * FLAG_WORDS; i += RF_THREADS) (&l_flag[0][0])[i] = 0;
   if (tid <= ST_N) l_stats[tid] = 0;
   __syncthreads();
   // ---- route: the bucket's records, the workgroup's groups ranked into LDS (as k_route)
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
-  const uint32_t sub_lo = lg0 >> PART_LOG, sub_hi = (lg0 + RF_RG) >> PART_LOG;
+  const uint32_t sub_lo = lg0 >> PART_LOG, sub_hi = (lg0 + RG) >> PART_LOG;
   for (uint32_t base = lo; base < hi; base += RF_THREADS * RF_UNROLL) {
     MsgRec m[RF_UNROLL];
+    uint4 mx[X ? RF_UNROLL : 1];
     uint32_t sub[RF_UNROLL];
 #pragma unroll
     for (uint32_t u = 0; u < RF_UNROLL; ++u) {
       const uint32_t p = base + u * RF_THREADS + tid;
       if (p < hi) m[u] = a.rec[p];
+      if constexpr (X) mx[u] = p < hi ? a.recx[p] : make_uint4(0, 0, 0, 0);
       sub[u] = p < hi ? (m[u].info >> 24) & 0xFu : 0xFFu;
     }
     if (w == 0) {  // the key bytes of the general kernel's bucket walk
@@ -1530,24 +1540,27 @@ __global__ void __launch_bounds__(RF_THREADS, HB_RF_WAVES) k_route_fast(ApplyArg
     for (uint32_t u = 0; u < RF_UNROLL; ++u) {
       const uint32_t p = base + u * RF_THREADS + tid;
       const bool own = p < hi && sub[u] >= sub_lo && sub[u] < sub_hi;
-      const uint32_t l = own ? (((sub[u] - sub_lo) << PART_LOG) | ((m[u].info >> 16) & (PART - 1))) : RF_RG;
-      if (l < RF_RG) {
+      const uint32_t l = own ? (((sub[u] - sub_lo) << PART_LOG) | ((m[u].info >> 16) & (PART - 1))) : RG;
+      if (l < RG) {
         const uint32_t r = atomicAdd(&l_cnt[l], 1u);
-        if (r < KMAX) l_slot[r][l] = make_uint4(m[u].info, m[u].orig, (uint32_t)m[u].ti, (uint32_t)(m[u].ti >> 32));
+        if (r < KMAX) {
+          l_slot[r][l] = make_uint4(m[u].info, m[u].orig, (uint32_t)m[u].ti, (uint32_t)(m[u].ti >> 32));
+          if constexpr (X) l_slotx[r][l] = mx[X ? u : 0];
+        }
       }
     }
   }
   __syncthreads();
   // ---- each partition's M event chunk in its bucket's region (as k_route)
-  for (uint32_t i = tid; i < RF_RG; i += RF_THREADS) {
+  for (uint32_t i = tid; i < RG; i += RF_THREADS) {
     uint32_t s = l_cnt[i];  // (a wave's 64 groups lie in one partition)
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
     if ((tid & 63) == 0 && s) atomicAdd(&l_ptot[i >> PART_LOG], s);
   }
   __syncthreads();
-  const uint32_t part0 = (bk << sl) + w * RF_NP;
-  if (tid < RF_NP) {
+  const uint32_t part0 = (bk << sl) + w * NP;
+  if (tid < NP) {
     const uint32_t part = part0 + tid;
     uint64_t mo = 0;
     if (part < a.NB) {
@@ -1558,14 +1571,14 @@ __global__ void __launch_bounds__(RF_THREADS, HB_RF_WAVES) k_route_fast(ApplyArg
     l_moff[tid] = mo;
   }
   __syncthreads();
-  // ---- the fast lane (as k_apply_fast) over the workgroup's groups, RF_RG / RF_THREADS per lane
+  // ---- the fast lane (as k_apply_fast) over the workgroup's groups, RG / RF_THREADS per lane
   uint32_t acc[ST_N + 1];
 #pragma unroll
   for (int k = 0; k <= ST_N; ++k) acc[k] = 0;
 #if HB_RF_NOUNROLL
 #pragma nounroll
 #endif
-  for (uint32_t i = tid; i < RF_RG; i += RF_THREADS) {
+  for (uint32_t i = tid; i < RG; i += RF_THREADS) {
     const uint32_t p = i >> PART_LOG, part = part0 + p, lane = i & (PART - 1);
     const uint32_t g = part * PART + lane;
     const bool gvalid = part < a.NB && g < G;
@@ -1581,25 +1594,33 @@ __global__ void __launch_bounds__(RF_THREADS, HB_RF_WAVES) k_route_fast(ApplyArg
     const bool leader = live && L.state() == HB_STATE_LEADER;
     const bool nc = (L.mlo & (uint32_t)M_NC) != 0;
     const bool lead = leader && !nc && (cnt <= KMAX || prop_raw != 0);
+    const bool fol = X && live && !nc && L.state() == HB_STATE_FOLLOWER && cnt > 0 && cnt <= KMAX && prop_raw == 0;
     L.dirty = 0;
     L.nev = 0;
     if (lead) {
       L.load_rest();
+    } else if (fol) {
+      L.load_follow();
     } else {
       L.last = L.committed = 0;
       L.term = 0;
     }
     uint32_t s_info[KMAX], s_orig[KMAX];
     uint64_t s_term[KMAX], s_index[KMAX], s_h[KMAX], s_c[KMAX];
-    const bool slots = lead && cnt <= KMAX;
+    const bool slots = (lead || fol) && cnt <= KMAX;
 #pragma unroll
     for (uint32_t k = 0; k < KMAX; ++k) {
-      const uint4 r = (slots && k < cnt) ? l_slot[k][i] : make_uint4(0, 0, 0, 0);
-      slot_unpack(r, a.side, &s_info[k], &s_orig[k], &s_term[k], &s_index[k]);
-      s_h[k] = s_c[k] = 0;
+      const bool u = slots && k < cnt;
+      slot_unpack(u ? l_slot[k][i] : make_uint4(0, 0, 0, 0), a.side, &s_info[k], &s_orig[k], &s_term[k], &s_index[k]);
+      uint4 xe = make_uint4(0, 0, 0, 0);
+      if constexpr (X) {
+        if (fol && k < cnt) xe = l_slotx[k][i];
+      }
+      s_h[k] = (uint64_t)xe.x | ((uint64_t)xe.y << 32);
+      s_c[k] = (uint64_t)xe.z | ((uint64_t)xe.w << 32);
     }
     uint32_t vals[ST_N + 1];
-    const bool flagged = fast_step<NMAX, KMAX>(a, L, part, lane, live, lead, leader, false, prop_raw, cnt, s_info, s_orig,
+    const bool flagged = fast_step<NMAX, KMAX>(a, L, part, lane, live, lead, leader, fol, prop_raw, cnt, s_info, s_orig,
                                                s_term, s_index, s_h, s_c, l_moff[p], &l_pfill[p], &l_fill[p], l_flag[p],
                                                nullptr, vals);
 #pragma unroll
@@ -1607,16 +1628,20 @@ __global__ void __launch_bounds__(RF_THREADS, HB_RF_WAVES) k_route_fast(ApplyArg
     if (flagged) {  // what k_apply reads of a group it takes over: its count and slots
       a.cnt[g] = (uint8_t)cnt;
 #pragma unroll
-      for (uint32_t k = 0; k < KMAX; ++k)
-        if (k < c) at32(a.slot, k * G + g) = l_slot[k][i];
+      for (uint32_t k = 0; k < KMAX; ++k) {
+        if (k < c) {
+          at32(a.slot, k * G + g) = l_slot[k][i];
+          if constexpr (X) at32(a.slotx, k * G + g) = l_slotx[k][i];
+        }
+      }
     }
   }
   reduce_stats(a, l_stats, acc);  // (ends with a barrier: the partitions' fills and flags are final)
-  for (uint32_t j = tid; j < RF_NP * FLAG_WORDS; j += RF_THREADS) {
+  for (uint32_t j = tid; j < NP * FLAG_WORDS; j += RF_THREADS) {
     const uint32_t p = j / FLAG_WORDS, part = part0 + p;
     if (part < a.NB) a.pflag[(size_t)part * FLAG_WORDS + j % FLAG_WORDS] = l_flag[p][j % FLAG_WORDS];
   }
-  if (tid < RF_NP && part0 + tid < a.NB) fast_close(a, part0 + tid, l_flag[tid], nullptr, l_pfill[tid], l_fill[tid]);
+  if (tid < NP && part0 + tid < a.NB) fast_close(a, part0 + tid, l_flag[tid], nullptr, l_pfill[tid], l_fill[tid]);
 }
 
 // ---------------------------------------------------------------------------
@@ -3229,14 +3254,33 @@ uint32_t apply_grid_for(uint32_t NBK, uint32_t sl, uint32_t NB) {
 uint32_t apply_grid(const hb_handle* h) { return h->agrid; }
 
 // The apply kernels; ev = this step's phase events (HB_STEP_PROFILE) or null.
+template <uint32_t KMAX, bool X>
+void launch_route_fast_t(hb_handle* h, const ApplyArgs& a) {
+  hipLaunchKernelGGL((k_route_fast<KMAX, X>),
+                     dim3(((h->NBK + 7) & ~7u) << (PART_LOG + h->sis_log - RouteFastGeom<KMAX, X>::RG_LOG)),
+                     dim3(RF_THREADS), 0, h->stream, a);
+}
+void launch_route_fast(hb_handle* h, const ApplyArgs& a) {
+  if (a.kmax == 3) {
+    if (a.slotx) launch_route_fast_t<3, true>(h, a);
+    else launch_route_fast_t<3, false>(h, a);
+  } else {
+    if (a.slotx) launch_route_fast_t<2, true>(h, a);
+    else launch_route_fast_t<2, false>(h, a);
+  }
+}
+// the largest route-fast workgroup (groups, log2) of a step
+inline uint32_t route_fast_rg_log(uint32_t kmax, bool x) {
+  return kmax == 3 ? (x ? RouteFastGeom<3, true>::RG_LOG : RouteFastGeom<3, false>::RG_LOG)
+                   : (x ? RouteFastGeom<2, true>::RG_LOG : RouteFastGeom<2, false>::RG_LOG);
+}
 // fused: k_route_fast stood in for k_route + k_apply_fast (launched by hb_step)
 template <int NMAX>
 void launch_apply(hb_handle* h, const ApplyArgs& a, hipEvent_t* ev, bool full, bool fused = false) {
   const uint32_t grid = apply_grid(h);
   if (ev) (void)hipEventRecord(ev[2], h->stream);
   if (fused) {
-    hipLaunchKernelGGL(k_route_fast, dim3(((h->NBK + 7) & ~7u) << (PART_LOG + h->sis_log - RF_RG_LOG)), dim3(RF_THREADS),
-                       0, h->stream, a);
+    if constexpr (NMAX <= 3) launch_route_fast(h, a);
   } else if constexpr (NMAX >= 5) {
     if (a.slotx) hipLaunchKernelGGL((k_apply_lead<NMAX, true>), dim3(grid), dim3(PART), 0, h->stream, a);
     else hipLaunchKernelGGL((k_apply_lead<NMAX, false>), dim3(grid), dim3(PART), 0, h->stream, a);
@@ -4144,8 +4188,8 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.slotx = xmode ? ps.slotx : nullptr;
   // n = 3, leader-side, one-pass geometry, prep and apply on one stream: the
   // route runs inside the fast kernel's workgroups (k_route_fast)
-  const bool fused = HB_ROUTE_FAST && h->nmax == 3 && aa.kmax == RF_KMAX && !xmode && !two &&
-                     (h->fuse >= 2 || (h->fuse == 1 && h->passes == 1)) && PART_LOG + h->sis_log >= RF_RG_LOG;
+  const bool fused = HB_ROUTE_FAST && h->nmax == 3 && !two && (h->fuse >= 2 || (h->fuse == 1 && h->passes == 1)) &&
+                     PART_LOG + h->sis_log >= route_fast_rg_log(aa.kmax, xmode);
   switch (h->nmax) {
     case 3:
       if (fused) break;
