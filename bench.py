@@ -1067,6 +1067,7 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         rng = np.random.default_rng(seed)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         mix = np.zeros(5, np.int64)  # timed steps: acks, rejects, heartbeat resps, unreachable, groups proposing
+        cfg3_ms, cfg3_n = [0.0, 0.0], [0, 0]  # (queued, idle-GPU) step time sums and counts
         for k in range(total):
             now = eng.get_groups()  # the stream is generated from the engine's state (untimed)
             b = synth.cfg3_open_batch(now, rng)
@@ -1079,19 +1080,28 @@ def run_aux(args, world, rank, local, dev, torch, dist):
             d = [torch.from_numpy(b[f].view(np.int32 if b[f].dtype == np.uint32 else np.int64)).to(dev)
                  for f in ("group", "info", "term", "index", "hint", "props")]
             torch.cuda.synchronize()
-            # a device-side wait (~1 ms) ahead of e0: the step's launches queue behind it, so the
-            # timed region is the device step, not the host's launch latency from an idle GPU
-            # (the other lines hide it by running their steps back to back)
-            torch.cuda._sleep(2_000_000)
+            # Alternate timed steps are taken on two bases: "queued" — a device-side wait
+            # (torch.cuda._sleep, ~1 ms) ahead of e0, so the step's launches queue behind it
+            # and the timed region is the device step (the other lines hide launch latency
+            # by running their steps back to back) — and "idle" — e0 on an idle GPU, so the
+            # host's launch latency is inside (the basis of the r01-r04 cfg3 lines).
+            queued = (k - args.warmup) % 2 == 0
+            if queued:
+                torch.cuda._sleep(2_000_000)
             e0.record(stream)
             eng.step(*d, host=False)
             e1.record(stream)
             torch.cuda.synchronize()
             if k >= args.warmup:
-                ms_local += e0.elapsed_time(e1)
+                t = e0.elapsed_time(e1)
+                cfg3_ms[0 if queued else 1] += t
+                cfg3_n[0 if queued else 1] += 1
                 st_acc += eng.stats()
-        timing = ("sum of per-step HIP event times, each step's launches queued behind a device-side wait "
-                  "(stream generation from the engine state between steps excluded)")
+        # the line's time: the queued basis' mean step, over every timed step
+        ms_local = cfg3_ms[0] / max(cfg3_n[0], 1) * args.steps
+        timing = ("per-step HIP event times, each step's launches queued behind a device-side wait (even timed "
+                  "steps; the odd ones are timed from an idle GPU, launch latency included: ms_per_step_idle_gpu); "
+                  "stream generation from the engine state between steps excluded")
     ms_t = torch.tensor([ms_local], dtype=torch.float64, device=dev)
     st_t = torch.from_numpy(st_acc.view(np.int64).copy()).to(dev)
     if world > 1:
@@ -1205,7 +1215,12 @@ def run_aux(args, world, rank, local, dev, torch, dist):
                      "unreachable": n_unr // args.steps, "msgapp_sent": sends // args.steps // world}
 
         extra = {"msgs_per_s": int(st[abi.HB_STAT_MSGS]) / sec, "commits_per_s": int(st[abi.HB_STAT_COMMITS]) / sec,
-                 "mix_per_step_rank0": extra_mix}
+                 "mix_per_step_rank0": extra_mix,
+                 # both bases side by side (rank 0): the line's value is the queued one
+                 "ms_per_step_queued": cfg3_ms[0] / max(cfg3_n[0], 1),
+                 "ms_per_step_idle_gpu": cfg3_ms[1] / max(cfg3_n[1], 1) if cfg3_n[1] else None,
+                 "value_idle_gpu": (int(st[abi.HB_STAT_APPRESP]) / (cfg3_ms[1] / cfg3_n[1] * args.steps / 1e3)
+                                    if cfg3_n[1] and cfg3_ms[1] > 0 else None)}
         ok = int(st[abi.HB_STAT_FAULTS]) == 0
         wl = f"cfg3: {G} raft groups x {n} per GPU, lagging followers (W={W})"
         data = "synthetic (seeded open-loop cfg3 stream generated from the engine state each step)"

@@ -1459,13 +1459,15 @@ __global__ void __launch_bounds__(PART, HB_FAST_WAVES) k_apply_fast(ApplyArgs a)
 // most ~73 KB of LDS (RG = 2048 groups for two leader-side slots, fewer when
 // a group keeps more bytes): two workgroups per CU, each lane stepping
 // RG / 512 groups in turn, with no barrier between them (the partitions'
-// event cursors and hand-over masks stay in LDS until the end).
+// event cursors and hand-over masks stay in LDS until the end).  Measured on
+// cfg2 (same-box A/Bs) and not kept: 1024-group workgroups of 256 or 512
+// lanes (+6-9 %), 8 or 16 records in flight per lane in the route phase
+// (0 / +1.5 %), the slots staged as four 4-byte planes (neutral), the group
+// loop not unrolled (neutral), the next group's first-round loads issued
+// before this group's second round (+8 %: 128 VGPRs already, it spills).
 // ---------------------------------------------------------------------------
 #ifndef HB_ROUTE_FAST
 #define HB_ROUTE_FAST 1
-#endif
-#ifndef HB_RF_NOUNROLL
-#define HB_RF_NOUNROLL 0
 #endif
 #ifndef HB_RF_UNROLL
 #define HB_RF_UNROLL 4  // records in flight per lane in the route phase
@@ -1575,9 +1577,6 @@ __global__ void __launch_bounds__(RF_THREADS, HB_RF_WAVES) k_route_fast(ApplyArg
   uint32_t acc[ST_N + 1];
 #pragma unroll
   for (int k = 0; k <= ST_N; ++k) acc[k] = 0;
-#if HB_RF_NOUNROLL
-#pragma nounroll
-#endif
   for (uint32_t i = tid; i < RG; i += RF_THREADS) {
     const uint32_t p = i >> PART_LOG, part = part0 + p, lane = i & (PART - 1);
     const uint32_t g = part * PART + lane;
