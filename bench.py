@@ -649,8 +649,8 @@ def run_replication(args, world, rank, local):
         achieved = float(alg / (apply_ms * 1e-3) / 1e9)
         fused = bool(eng.step_kernels() & abi.HB_KERN_ROUTE_FAST)
         if fused:
-            kname = "k_route_fast"
-            knames = [kname]
+            kname = "k_route_fast<2>"
+            knames = ["k_route_fast<2u, false>", "k_route_fast"]
         else:
             kname = f"k_apply_fast<{3 if n <= 3 else (5 if n <= 5 else 7)}>"
             # (rocprofv3 names the template with its X-mode flag since r04)
@@ -970,6 +970,7 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         st_acc = stats.cpu().numpy().astype(np.uint64)
         ph, nph = eng.phase_ms()
         apply_us = float(ph[abi.HB_PHASE_APPLY]) * 1e3
+        fused_x = bool(eng.step_kernels() & abi.HB_KERN_ROUTE_FAST)  # (the apply phase brackets k_route_fast)
         timing = "K steps back to back, inputs resident in HBM"
     elif args.workload == "tick":
         g, _ = synth.steady_groups(G, n, seed=seed, with_runs=False)
@@ -1162,7 +1163,10 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         n_fol = G - n_led
         launch_alg = FOLLOW_GROUP_BYTES * n_fol + alg_bytes_per_group(n) * n_led  # per rank, per step
         alg = launch_alg * args.steps
-        if n == 3:
+        if n == 3 and fused_x:
+            kname = "k_route_fast<2> (X mode: the route, FastLane + FollowLane in one kernel)"
+            knames = ["k_route_fast<2u, true>"]
+        elif n == 3:
             kname = "k_apply_fast<3> (X mode: FastLane + FollowLane)"
             knames = ["k_apply_fast<3, true, 2u>", "k_apply_fast<3, true>"]
         else:
