@@ -2357,6 +2357,9 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_follow(ApplyArgs a) {
 // machine.  Events go to the partition's P chunk (at most one
 // step per group, so the chunk's ev_per_msg x PART words bound them).
 // ---------------------------------------------------------------------------
+#ifndef HB_TICK_ELECT
+#define HB_TICK_ELECT 1  // a tick's campaigns through ElectLane (reset form, M_RS)
+#endif
 template <int NMAX>
 __global__ void __launch_bounds__(PART, 2) k_tick(ApplyArgs a) {
   __shared__ uint32_t l_fill;
@@ -2440,6 +2443,30 @@ __global__ void __launch_bounds__(PART, 2) k_tick(ApplyArgs a) {
       L.ev(HB_EV_HEARTBEAT, s, 0, umin64(mt[s], committed));
       if (pmv[s] & PM_PAUSED) a.S.pm[(size_t)s * a.S.G + g] = pmv[s] & ~PM_PAUSED;
     }
+  } else if (type == HB_MSG_HUP && HB_TICK_ELECT && !sz_on(a.S.max_msg_size) && !(L.meta & M_NC) &&
+             L.self() < L.n()) {
+    // a non-leader's election timeout: campaign through the election lane
+    // (hipbatch_elect.h, as k_elect steps it), which leaves the n Progress
+    // entries in the reset form (M_RS) instead of writing them — ~4 % of the
+    // groups campaign per tick, each writing n x 20 scattered bytes through
+    // the general lane (the tick's 2.3 x traffic over its byte model, r05)
+    ElectLane<NMAX> E;
+    E.S = a.S;
+    E.E = L.E;
+    E.g = g;
+    E.meta = L.meta;
+    E.load();
+    last0 = E.last;
+    commit0 = E.committed;
+    E.step(HB_MSG_HUP, L.self(), 0, false);
+    E.store();
+    L.meta = E.meta;
+    L.last = E.last;
+    L.committed = E.committed;
+    L.won = E.won;
+    L.lost = E.lost;
+    L.nev = E.nev;
+    L.dirty = 0;  // (stored)
   } else if (type != 0xFF) {  // MsgHup (or the MsgBeat of a reset-form / M_NC leader): the general state machine
     L.load_all();
     last0 = L.last;
