@@ -75,7 +75,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh16, 
 // Phase 1: partition the batch into buckets
 //
 // A bucket is 2^sis_log consecutive apply partitions (sis_log <= 4: up to
-// 4096 groups; hb_create picks the smallest that needs no extra pass, down to
+// 4096 groups, 7 at n = 3; hb_create picks the smallest that needs no extra pass, down to
 // one k_route workgroup per bucket).  The batch is sorted by bucket id with a
 // stable LSD radix sort, 8-bit digits: one pass up to 256 buckets, two up to
 // 64K.  A 512-lane workgroup ranks a 2048-message tile stably (ballot
@@ -87,7 +87,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh16, 
 //
 // The final pass writes the apply input: one 16-byte MsgRec per message
 // (info with the group's lane in bits 16-23 and its partition in the bucket
-// in bits 24-27, arrival index, Term and Index packed into one word, below).
+// in bits 24-27 (30-31 and 14 above 16 partitions: rec_sub), arrival index, Term and Index packed into one word, below).
 // k_route reads the records and writes the partition once more as a key byte
 // per message, contiguous, for the general kernel's bucket walk (a separate
 // key array written here took 8-byte runs per digit per tile: partial lines).
@@ -114,6 +114,16 @@ struct BatchDev {
 // hb_create: at most SIS_MAX, fewer when that costs no extra radix pass, so
 // that one k_route workgroup owns a whole bucket and reads it once).
 constexpr uint32_t SIS_LOG_MAX = 4;
+// HB_SIS_LOG_MAX3 > 4: n = 3 handles take buckets of up to 2^7 partitions
+// (32K groups) when that saves a radix pass (8M groups: 256 buckets, one pass
+// instead of two); k_route_fast's 16 sisters then read their bucket from L2,
+// 16 times over.  Measured (cfg5, same box): partition 433 -> 241 us but
+// k_route_fast 485 -> 1032 us (0.92 -> 1.27 ms/step): off.
+#ifndef HB_SIS_LOG_MAX3
+#define HB_SIS_LOG_MAX3 4
+#endif
+constexpr uint32_t SIS_LOG_MAX3 = HB_SIS_LOG_MAX3;
+static_assert(SIS_LOG_MAX3 <= 7, "a record carries its partition in the bucket in 7 bits (rec_sub)");
 // a prep set's counters: k_apply's 8 work-list lengths, k_elect's 8, k_follow's, the finish ticket —
 // each on a 128-byte line of its own (CTR_STRIDE words): the returning atomics of every partition
 // on one line serialise at the memory side (~7 ns each; 16K partitions put 16K on a list)
@@ -137,7 +147,7 @@ constexpr uint32_t RDX_ROUNDS = HB_RDX_ROUNDS;
 constexpr uint32_t RDX_TILE = RDX_THREADS * RDX_ROUNDS;  // 2048
 
 struct MsgRec {      // apply input record (16 B)
-  uint32_t info;     // type | from << 4 | reject << 8 | voted << 9 | lane << 16 | sub << 24 | long << 28
+  uint32_t info;     // type | from << 4 | reject << 8 | voted << 9 | lane << 16 | sub (rec_sub_bits) | long << 28
   uint32_t orig;     // arrival index in the batch
   uint64_t ti;       // Index | Term << 40 (REC_LONG: side[2 orig], side[2 orig + 1])
 };
@@ -152,9 +162,18 @@ constexpr uint32_t REC_LONG = 1u << 28;
 constexpr uint32_t REC_UNI = 1u << 29;
 constexpr uint32_t REC_UNI_MAX = 8;
 constexpr uint32_t REC_NE_SHIFT = 10;
-__device__ __forceinline__ uint32_t rec_ne(uint32_t info) { return (info >> REC_NE_SHIFT) & 0x3Fu; }
+__device__ __forceinline__ uint32_t rec_ne(uint32_t info) { return (info >> REC_NE_SHIFT) & 0xFu; }
+// A final record's partition in its bucket (sub < 2^sis_log, at most 7 bits):
+// bits 0-3 at 24-27, bits 4-5 at 30-31, bit 6 at 14 (the entry count above
+// uses bits 10-13 only: REC_UNI_MAX = 8)
+__device__ __forceinline__ uint32_t rec_sub_bits(uint32_t sub) {
+  return ((sub & 0xFu) << 24) | (((sub >> 4) & 3u) << 30) | (((sub >> 6) & 1u) << 14);
+}
+__device__ __forceinline__ uint32_t rec_sub(uint32_t info) {
+  return ((info >> 24) & 0xFu) | (((info >> 30) & 3u) << 4) | (((info >> 14) & 1u) << 6);
+}
 // the bits of a batch info word a record keeps (lane / partition bits are added by the final pass)
-constexpr uint32_t REC_KEEP = 0xFFFFu | REC_LONG | REC_UNI;
+constexpr uint32_t REC_KEEP = 0x3FFFu | REC_LONG | REC_UNI;
 constexpr uint32_t REC_IDX_BITS = 40;
 constexpr uint64_t REC_IDX_MASK = (1ull << REC_IDX_BITS) - 1;
 // pack (term, index) into ti; false: does not fit (REC_LONG)
@@ -518,7 +537,7 @@ __device__ __forceinline__ void scatter_tiles(const RadixSrc& s, const RadixDst&
         if (FINAL) {
           MsgRec m;
           m.info = (st_info[p] & REC_KEEP) | ((g & (PART - 1)) << 16) |
-                   (((g >> PART_LOG) & ((1u << f.sis_log) - 1)) << 24);
+                   rec_sub_bits((g >> PART_LOG) & ((1u << f.sis_log) - 1));
           m.orig = st_orig[p];
           m.ti = st_ti[p];
           f.rec[o] = m;
@@ -600,7 +619,7 @@ __global__ void __launch_bounds__(RDX_THREADS) k_pack_one(RadixSrc s, FinalDst f
       if (!cur.v[r]) continue;
       const uint32_t o = before + rank[r], g = cur.g[r];
       MsgRec m;
-      m.info = (cur.i[r] & REC_KEEP) | ((g & (PART - 1)) << 16) | (((g >> PART_LOG) & ((1u << f.sis_log) - 1)) << 24);
+      m.info = (cur.i[r] & REC_KEEP) | ((g & (PART - 1)) << 16) | rec_sub_bits((g >> PART_LOG) & ((1u << f.sis_log) - 1));
       m.orig = cur.o[r];
       m.ti = cur.t[r];
       f.rec[o] = m;
@@ -1079,7 +1098,7 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
       const uint32_t p = base + u * ROUTE_THREADS + tid;
       if (p < hi) m[u] = a.rec[p];
       if constexpr (X) mx[u] = p < hi ? a.recx[p] : make_uint4(0, 0, 0, 0);
-      sub[u] = p < hi ? (m[u].info >> 24) & 0xFu : 0xFFu;  // the partition in the bucket
+      sub[u] = p < hi ? rec_sub(m[u].info) : 0xFFu;  // the partition in the bucket
     }
     if (w == 0) {  // the key bytes the general kernel's bucket walk scans (one coalesced store per lane)
 #pragma unroll
@@ -1529,7 +1548,7 @@ __global__ void __launch_bounds__(RF_THREADS, HB_RF_WAVES) k_route_fast(ApplyArg
       const uint32_t p = base + u * RF_THREADS + tid;
       if (p < hi) m[u] = a.rec[p];
       if constexpr (X) mx[u] = p < hi ? a.recx[p] : make_uint4(0, 0, 0, 0);
-      sub[u] = p < hi ? (m[u].info >> 24) & 0xFu : 0xFFu;
+      sub[u] = p < hi ? rec_sub(m[u].info) : 0xFFu;
     }
     if (w == 0) {  // the key bytes of the general kernel's bucket walk
 #pragma unroll
@@ -3414,9 +3433,10 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   auto passes_for = [&](uint32_t sl) {
     return (std::max<uint32_t>(ceil_log2(nbk_for(sl)), 1) + RDX_BITS - 1) / RDX_BITS;
   };
-  h->sis_log = SIS_LOG_MAX;
+  const uint32_t sl_max = h->nmax <= 3 ? SIS_LOG_MAX3 : SIS_LOG_MAX;
+  h->sis_log = sl_max;
   const uint32_t sl_min = route_rg_log(route_kmax(h->nmax)) - PART_LOG;
-  while (h->sis_log > sl_min && passes_for(h->sis_log - 1) == passes_for(SIS_LOG_MAX)) --h->sis_log;
+  while (h->sis_log > sl_min && passes_for(h->sis_log - 1) == passes_for(sl_max)) --h->sis_log;
   h->NBK = nbk_for(h->sis_log);
   h->passes = passes_for(h->sis_log);
   h->bk_bits = std::max<uint32_t>(ceil_log2(h->NBK), 1);
