@@ -2407,8 +2407,12 @@ __global__ void __launch_bounds__(PART, 2) k_tick(ApplyArgs a) {
   L.arrival = 0xFFFFFFFFu;
   uint32_t type = 0xFF;
   bool live = false;
+  // meta's low word (state, n, self, flags) decides a tick; the high word (the
+  // vote tally) is read only by a group that steps or faults (4 B per group)
+  const uint32_t* meta32 = reinterpret_cast<const uint32_t*>(a.S.meta);
+  auto meta_hi = [&]() { L.meta |= (uint64_t)at32(meta32, 2 * g + 1) << 32; };
   if (g < a.S.G) {
-    L.meta = a.S.meta[g];
+    L.meta = at32(meta32, 2 * g);
     live = L.n() != 0 && !L.faulted();
   }
   if (live) {
@@ -2425,6 +2429,7 @@ __global__ void __launch_bounds__(PART, 2) k_tick(ApplyArgs a) {
     } else if (++el >= et) {  // isElectionTimeout: d = elapsed - et >= 0 takes a draw
       const uint32_t pos = a.S.rpos[g];
       if (pos >= a.S.nrnd) {
+        meta_hi();
         L.fault(HB_FAULT_RAND_EXHAUSTED);
         L.dirty |= D_META;
         L.ev(HB_EV_FAULT, 0, HB_FAULT_RAND_EXHAUSTED, HB_NO_INDEX);
@@ -2469,6 +2474,7 @@ __global__ void __launch_bounds__(PART, 2) k_tick(ApplyArgs a) {
     // entries in the reset form (M_RS) instead of writing them — ~4 % of the
     // groups campaign per tick, each writing n x 20 scattered bytes through
     // the general lane (the tick's 2.3 x traffic over its byte model, r05)
+    meta_hi();
     ElectLane<NMAX> E;
     E.S = a.S;
     E.E = L.E;
@@ -2487,6 +2493,7 @@ __global__ void __launch_bounds__(PART, 2) k_tick(ApplyArgs a) {
     L.nev = E.nev;
     L.dirty = 0;  // (stored)
   } else if (type != 0xFF) {  // MsgHup (or the MsgBeat of a reset-form / M_NC leader): the general state machine
+    meta_hi();
     L.load_all();
     last0 = L.last;
     commit0 = L.committed;
