@@ -3444,6 +3444,10 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   h->sis_log = sl_max;
   const uint32_t sl_min = route_rg_log(route_kmax(h->nmax)) - PART_LOG;
   while (h->sis_log > sl_min && passes_for(h->sis_log - 1) == passes_for(sl_max)) --h->sis_log;
+  if (const char* e = getenv("HB_SIS_LOG")) {  // (A/B knob: a fixed bucket size, within the allowed range)
+    const int v = atoi(e);
+    if (v >= (int)sl_min && v <= (int)sl_max) h->sis_log = (uint32_t)v;
+  }
   h->NBK = nbk_for(h->sis_log);
   h->passes = passes_for(h->sis_log);
   h->bk_bits = std::max<uint32_t>(ceil_log2(h->NBK), 1);
