@@ -662,3 +662,37 @@ def test_follower_lane_commit_past_log_end(seed):
         b = synth.follower_messages(now, pair2.og.term, 4000, seed=seed * 10 + j, past_end=0.2)
         _, st, now = pair2.step(b, ctx=f"past-end fuzz {seed} step {j}")
     assert (now["fault"] == abi.HB_FAULT_COMMIT_RANGE).sum() > 20
+
+
+# ---------------------------------------------------------------- k_route_fast (r06) and its unfused form
+@pytest.mark.parametrize("fuse", ["0", "1", "2"])
+def test_route_fast_and_unfused_paths(fuse, monkeypatch):
+    """n = 3 steps run the route inside the fast lane's workgroups
+    (k_route_fast, HB_ROUTE_FUSE=2, the default; 1 = one-pass handles only) or
+    as k_route + k_apply_fast (0).  Each form against the oracle on leader-side
+    steps with two slots (cfg2), three slots (MsgProp batches) and X mode (the
+    follow workload and random follower-side traffic); hb_step_kernels says
+    which form ran.  (Two-pass handles: test_two_pass_partition_over_1m_groups,
+    with the default.)"""
+    monkeypatch.setenv("HB_ROUTE_FUSE", fuse)
+    G = 3000
+    g, runs = synth.steady_groups(G, 3, seed=161, last_hi=1 << 14)
+    pair = Pair(g, runs, 3, 256, max_batch=4 * G)
+    for step in range(2):
+        pair.step(synth.cfg2_batch(g, step, seed=162 + step), ctx=f"fuse {fuse} cfg2 {step}")
+        assert bool(pair.eng.step_kernels() & abi.HB_KERN_ROUTE_FAST) == (fuse != "0")
+    rng = np.random.default_rng(163)
+    last = g["last_index"].astype(np.int64) + 2
+    ents = rng.integers(1, 4, G).astype(np.int64)
+    _, _, now = pair.step(_multinode_leader_batch(g, rng, last, ents), ctx=f"fuse {fuse} msgprop")
+    b = synth.random_batch(now, 6000, seed=164, props=False)
+    b["msg_props"] = True
+    pair.step(b, ctx=f"fuse {fuse} msgprop fuzz")
+    # X mode
+    gf, runsf = synth.follow_groups(G, 3, seed=165, last_hi=1 << 14, with_runs=True)
+    pf = Pair(gf, runsf, 3, 256, max_batch=4 * G, term_runs=True)
+    _, _, nowf = pf.step(synth.follow_batch(gf, 0, seed=166, ents=2), ctx=f"fuse {fuse} follow",
+                         check_inflights=False)
+    f = synth.follower_messages(nowf, pf.og.term, 3000, seed=167)
+    pf.step(synth.merge_batches(synth.random_batch(nowf, 2000, seed=168), f, seed=169),
+            ctx=f"fuse {fuse} follower fuzz", check_inflights=False)
