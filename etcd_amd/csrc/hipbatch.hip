@@ -954,6 +954,33 @@ __device__ __forceinline__ void gather_round(St& sl, const ApplyArgs& a, uint32_
   *cnt = my_cnt;
 }
 
+// The arrival order of a lane's KS route slots as slot numbers in nibbles of
+// one word (nibble x = the slot of the lane's x-th message): key[k] = slot k's
+// arrival index (0xFFFFFFFF for an unused slot, which sorts last); an
+// odd-even transposition network carries the nibbles through its exchanges.
+// (Ranking each slot by counting — KS^2 compares, no exchanges — measured
+// neutral on cfg3 / cfg4.)
+template <uint32_t KS>
+__device__ __forceinline__ uint32_t arrival_perm(uint32_t (&key)[KS]) {
+  uint32_t perm = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < KS; ++k) perm |= k << (4 * k);
+#pragma unroll
+  for (uint32_t r = 0; r < KS; ++r) {
+#pragma unroll
+    for (uint32_t k = (r & 1); k + 1 < KS; k += 2) {
+      const uint32_t k0 = key[k], k1 = key[k + 1];
+      const bool sw = k1 < k0;
+      key[k] = sw ? k1 : k0;
+      key[k + 1] = sw ? k0 : k1;
+      const uint32_t p0 = (perm >> (4 * k)) & 0xF, p1 = (perm >> (4 * (k + 1))) & 0xF;
+      const uint32_t swp = (perm & ~(0xFFu << (4 * k))) | (p1 << (4 * k)) | (p0 << (4 * (k + 1)));
+      perm = sw ? swp : perm;
+    }
+  }
+  return perm;
+}
+
 __device__ __forceinline__ bool is_response(uint32_t type) {  // raft/util.go:53-55
   return type == HB_MSG_APP_RESP || type == HB_MSG_VOTE_RESP || type == HB_MSG_HEARTBEAT_RESP ||
          type == HB_MSG_UNREACHABLE;
@@ -2025,27 +2052,13 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
       commit0 = ((resume >> 30) & 1u) ? L.committed : a.commit0[g];
       // arrival order of the slots (odd-even transposition, slot numbers as nibbles)
       uint32_t key[KS];
-      uint32_t perm = 0;
 #pragma unroll
       for (uint32_t k = 0; k < KS; ++k) {
         const uint4 r = k < cnt ? at32(a.slot, k * a.S.G + g) : make_uint4(0, 0xFFFFFFFFu, 0, 0);
         l_slot[k][tid] = r;
         key[k] = r.y;
-        perm |= k << (4 * k);
       }
-#pragma unroll
-      for (uint32_t r = 0; r < KS; ++r) {
-#pragma unroll
-        for (uint32_t k = (r & 1); k + 1 < KS; k += 2) {
-          const uint32_t k0 = key[k], k1 = key[k + 1];
-          const bool sw = k1 < k0;
-          key[k] = sw ? k1 : k0;
-          key[k + 1] = sw ? k0 : k1;
-          const uint32_t p0 = (perm >> (4 * k)) & 0xF, p1 = (perm >> (4 * (k + 1))) & 0xF;
-          const uint32_t swp = (perm & ~(0xFFu << (4 * k))) | (p1 << (4 * k)) | (p0 << (4 * (k + 1)));
-          perm = sw ? swp : perm;
-        }
-      }
+      const uint32_t perm = arrival_perm<KS>(key);
       const uint32_t skip = resume & 0x3FFFFFFFu;
       uint32_t x = skip;
 #pragma nounroll
@@ -2218,26 +2231,16 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? (X && HB_LEAD_XSTAGE ? HB_LE
   // the slots' arrival indices, only for a group this kernel steps (an election
   // storm's leaders go to k_elect without them)
   uint32_t key[KS];
-  uint32_t perm = 0;
   const bool keys = (slots && loaded) || fol;
 #pragma unroll
-  for (uint32_t k = 0; k < KS; ++k) {
-    key[k] = (!HB_ROUTE_SORTED && keys && k < cnt) ? slot_at(k).y : 0xFFFFFFFFu;
-    perm |= k << (4 * k);
-  }
-  // arrival order of the slots (odd-even transposition, slot numbers as nibbles)
+  for (uint32_t k = 0; k < KS; ++k) key[k] = (!HB_ROUTE_SORTED && keys && k < cnt) ? slot_at(k).y : 0xFFFFFFFFu;
+  // arrival order of the slots (slot numbers as nibbles)
+  uint32_t perm = 0;
+  if (HB_ROUTE_SORTED) {
 #pragma unroll
-  for (uint32_t r = 0; r < (HB_ROUTE_SORTED ? 0u : KS); ++r) {
-#pragma unroll
-    for (uint32_t k = (r & 1); k + 1 < KS; k += 2) {
-      const uint32_t k0 = key[k], k1 = key[k + 1];
-      const bool sw = k1 < k0;
-      key[k] = sw ? k1 : k0;
-      key[k + 1] = sw ? k0 : k1;
-      const uint32_t p0 = (perm >> (4 * k)) & 0xF, p1 = (perm >> (4 * (k + 1))) & 0xF;
-      const uint32_t swp = (perm & ~(0xFFu << (4 * k))) | (p1 << (4 * k)) | (p0 << (4 * (k + 1)));
-      perm = sw ? swp : perm;
-    }
+    for (uint32_t k = 0; k < KS; ++k) perm |= k << (4 * k);
+  } else {
+    perm = arrival_perm<KS>(key);
   }
   const uint64_t last0 = L.last, commit0 = L.committed;
   bool flagged = false;
