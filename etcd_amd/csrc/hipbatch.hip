@@ -770,6 +770,28 @@ enum { ST_MSGS, ST_APPRESP, ST_VOTERESP, ST_DROPPED, ST_COMMITS, ST_WON, ST_LOST
 #define HB_FAST_WAVES 4
 #endif
 constexpr uint32_t FLAG_WORDS = PART / 32;  // per-partition bitmask of groups handed to k_apply
+// Set (or clear) lane `lane`'s bit of a partition flag mask.  `lane & 63` must
+// be the hardware lane and `lane >> 6` the wave's slot in the partition, so a
+// wave owns words 2w and 2w + 1.  With HB_FLAG_BALLOT the wave ballots the
+// predicate and its lowest active lane issues at most two LDS atomics, instead
+// of one per flagged lane all landing on the same word (32-way serialised).
+#ifndef HB_FLAG_BALLOT
+#define HB_FLAG_BALLOT 1
+#endif
+template <bool SET>
+__device__ __forceinline__ void flag_put(uint32_t* words, uint32_t lane, bool on) {
+#if HB_FLAG_BALLOT
+  const uint64_t act = __ballot(1);
+  const uint64_t b = __ballot(on);
+  if (b && (lane & 63) == (uint32_t)__ffsll((long long)act) - 1) {
+    const uint32_t w = (lane >> 6) * 2, lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+    if (lo) SET ? atomicOr(&words[w], lo) : atomicAnd(&words[w], ~lo);
+    if (hi) SET ? atomicOr(&words[w + 1], hi) : atomicAnd(&words[w + 1], ~hi);
+  }
+#else
+  if (on) SET ? atomicOr(&words[lane >> 5], 1u << (lane & 31)) : atomicAnd(&words[lane >> 5], ~(1u << (lane & 31)));
+#endif
+}
 constexpr uint32_t KPL = 64;                // bucket key bytes scanned per lane per segment
 constexpr uint32_t SEG = PART * KPL;        // positions per key-scan segment
 
@@ -1368,10 +1390,10 @@ __device__ __forceinline__ bool fast_step(const ApplyArgs& a, FollowLane<NMAX>& 
     bool higher = false;
 #pragma unroll
     for (uint32_t k = 0; k < KMAX; ++k) higher |= k < cnt && s_term[k] > L.term;
-    if (flagged && (!leader || higher)) atomicOr(&l_eflag[lane >> 5], 1u << (lane & 31));
+    flag_put<true>(l_eflag, lane, flagged && (!leader || higher));
   }
+  flag_put<true>(l_flag, lane, flagged);
   if (flagged) {
-    atomicOr(&l_flag[lane >> 5], 1u << (lane & 31));
     at32(a.resume, g) = resume | (stored ? 0u : 1u << 30);
     if (stored) at32(a.commit0, g) = commit0;
   }
@@ -2081,13 +2103,13 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
         L.store();
         if (x == cnt) {
           done = true;  // the group's batch ends here
-          atomicAnd(&l_flag[tid >> 5], ~(1u << (tid & 31)));
         } else {  // k_apply resumes at message x, loading what was stored
           a.resume[g] = x;
           a.commit0[g] = commit0;
         }
       }
     }
+    flag_put<false>(l_flag, tid, done);
     const uint64_t vals[ST_N + 1] = {st_msgs,
                                      st_app,
                                      st_vote,
@@ -2327,9 +2349,9 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? (X && HB_LEAD_XSTAGE ? HB_LE
   if (fstepped) L.store_follow();
   const bool stored = loaded || fstepped;
   // k_elect's candidates (n >= 5): no leader, or a leader a higher term steps down
-  if (NMAX >= 5 && flagged && (!leader || higher)) atomicOr(&l_eflag[tid >> 5], 1u << (tid & 31));
+  if constexpr (NMAX >= 5) flag_put<true>(l_eflag, tid, flagged && (!leader || higher));
+  flag_put<true>(l_flag, tid, flagged);
   if (flagged) {
-    atomicOr(&l_flag[tid >> 5], 1u << (tid & 31));
     a.resume[g] = resume | (stored ? 0u : 1u << 30);
     if (stored) a.commit0[g] = commit0;
   }
