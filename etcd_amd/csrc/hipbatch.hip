@@ -2025,6 +2025,12 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
 #ifndef HB_ELECT_GRID
 #define HB_ELECT_GRID 0  // as HB_GEN_GRID
 #endif
+#ifndef HB_ELECT_EAGER
+#define HB_ELECT_EAGER 1
+#endif
+#ifndef HB_ELECT_PF
+#define HB_ELECT_PF 1
+#endif
 constexpr uint32_t ELECT_GRID = HB_ELECT_GRID;
 static_assert(ELECT_GRID % 8 == 0, "k_elect strides its XCD-slot lists by gridDim.x / 8");
 
@@ -2042,6 +2048,31 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
   const uint32_t tid = threadIdx.x;
   const uint32_t xs = blockIdx.x & 7, stride = gridDim.x >> 3;
   const uint32_t nl = __hip_atomic_load(&a.el_cnt[xs * CTR_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if HB_ELECT_PF
+  // the partition list two ahead and the next partition's flags and event fill
+  // are fetched during this partition's work (two round trips off each turn)
+  const uint32_t* list = a.el_list + (size_t)xs * a.NB;
+  uint32_t i = blockIdx.x >> 3;
+  uint32_t part = i < nl ? list[i] : 0u;
+  uint32_t nxt = i + stride < nl ? list[i + stride] : 0u;
+  uint32_t pf = 0, pe = 0, pfill = 0;
+  if (i < nl) {
+    if (tid < FLAG_WORDS) {
+      pf = a.pflag[(size_t)part * FLAG_WORDS + tid];
+      pe = a.eflag[(size_t)part * FLAG_WORDS + tid];
+    }
+    if (tid == 0) pfill = a.ev_counts[2 * part + 1];
+  }
+  for (; i < nl; i += stride) {  // uniform
+    const uint32_t g = part * PART + tid;
+    if (tid < FLAG_WORDS) {
+      l_flag[tid] = pf;
+      l_eflag[tid] = pe;
+    }
+    if (tid == 0) l_fill = pfill;  // after k_apply_fast's events
+    if (tid <= ST_N) l_stats[tid] = 0;
+    __syncthreads();
+#else
   for (uint32_t i = blockIdx.x >> 3; i < nl; i += stride) {  // uniform
     const uint32_t part = a.el_list[(size_t)xs * a.NB + i];
     const uint32_t g = part * PART + tid;
@@ -2052,6 +2083,7 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
     if (tid == 0) l_fill = a.ev_counts[2 * part + 1];  // after k_apply_fast's events
     if (tid <= ST_N) l_stats[tid] = 0;
     __syncthreads();
+#endif
     const bool flagged = (l_eflag[tid >> 5] >> (tid & 31)) & 1u;  // (a subset of the k_apply flags)
     ElectLane<NMAX> L;
     L.S = a.S;
@@ -2068,18 +2100,52 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
     uint64_t last0 = 0, commit0 = 0;
     L.won = L.lost = L.nev = 0;
     L.committed = L.last = 0;
-    if (mine) {
+    uint32_t key[KS];  // the slots' arrival keys (0xFFFFFFFF past cnt)
+#if HB_ELECT_EAGER
+    // every load of a flagged lane in the round trip of meta / cnt / resume: the
+    // state, commit0 and all KS slots (those past cnt are masked here)
+    uint64_t c0 = 0;
+    if (flagged) {
       L.load();
+      c0 = a.commit0[g];
+      uint4 sl[KS];
+#pragma unroll
+      for (uint32_t k = 0; k < KS; ++k) sl[k] = at32(a.slot, k * a.S.G + g);
+#pragma unroll
+      for (uint32_t k = 0; k < KS; ++k) {
+        const uint4 r = k < cnt ? sl[k] : make_uint4(0, 0xFFFFFFFFu, 0, 0);
+        l_slot[k][tid] = r;
+        key[k] = r.y;
+      }
+    }
+#endif
+#if HB_ELECT_PF
+    const uint32_t nn = i + 2 * stride < nl ? list[i + 2 * stride] : 0u;
+    if (i + stride < nl) {
+      if (tid < FLAG_WORDS) {
+        pf = a.pflag[(size_t)nxt * FLAG_WORDS + tid];
+        pe = a.eflag[(size_t)nxt * FLAG_WORDS + tid];
+      }
+      if (tid == 0) pfill = a.ev_counts[2 * nxt + 1];
+    }
+#endif
+    if (mine) {
+#if !HB_ELECT_EAGER
+      L.load();
+#endif
       last0 = L.last;
+#if HB_ELECT_EAGER
+      commit0 = ((resume >> 30) & 1u) ? L.committed : c0;
+#else
       commit0 = ((resume >> 30) & 1u) ? L.committed : a.commit0[g];
-      // arrival order of the slots (odd-even transposition, slot numbers as nibbles)
-      uint32_t key[KS];
 #pragma unroll
       for (uint32_t k = 0; k < KS; ++k) {
         const uint4 r = k < cnt ? at32(a.slot, k * a.S.G + g) : make_uint4(0, 0xFFFFFFFFu, 0, 0);
         l_slot[k][tid] = r;
         key[k] = r.y;
       }
+#endif
+      // arrival order of the slots (odd-even transposition, slot numbers as nibbles)
       const uint32_t perm = arrival_perm<KS>(key);
       const uint32_t skip = resume & 0x3FFFFFFFu;
       uint32_t x = skip;
@@ -2124,6 +2190,10 @@ __global__ void __launch_bounds__(PART, HB_ELECT_WAVES) k_elect(ApplyArgs a) {
     if (tid < FLAG_WORDS) a.pflag[(size_t)part * FLAG_WORDS + tid] = l_flag[tid];
     if (tid == 0) a.ev_counts[2 * part + 1] = l_fill;
     __syncthreads();  // the next partition reuses the LDS
+#if HB_ELECT_PF
+    part = nxt;
+    nxt = nn;
+#endif
   }
 }
 
