@@ -734,6 +734,12 @@ struct ApplyArgs {
   // X mode (follower-side batches): the records' extensions {hint, commit}
   const uint4* recx;        // beside rec (k_route input)
   uint4* slotx;             // [kmax][G] beside slot (null: no X mode this step)
+  // storm hand-over (n >= 5, HB_ROUTE_STORM): k_route closes a partition whose
+  // groups with messages are all busy leaders with a higher-term message, as
+  // k_apply_lead would (flags, lists, event chunks), and k_apply_lead skips it
+  uint32_t nmax;            // the handle's replica bound (5 or 7)
+  uint32_t storm;           // 1: this step's route may close partitions (lskip)
+  uint8_t* lskip;           // [NB] 1: the route closed the partition
 };
 
 // Message slots k_route keeps per group: n - 1 (one MsgAppResp per follower,
@@ -1099,6 +1105,9 @@ constexpr uint32_t CNT_MASK = 0x7F, CNT_HIGHER = 0x80;
 #ifndef HB_ROUTE_UNROLL
 #define HB_ROUTE_UNROLL 4
 #endif
+#ifndef HB_ROUTE_STORM
+#define HB_ROUTE_STORM 1
+#endif
 constexpr uint32_t ROUTE_UNROLL = HB_ROUTE_UNROLL;  // records in flight per lane
 // Route groups per workgroup (log2), measured on MI355X with 16-byte records
 // (same-box A/B, r04): KMAX = 2 at 2048 (2 sisters per 4096-group bucket, 72 KB
@@ -1124,6 +1133,11 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   __shared__ uint4 l_slotx[X ? KMAX : 1][X ? RG : 1];  // X mode: their extensions
   __shared__ uint32_t l_ptot[NP];
   constexpr bool HI = KMAX >= 5;  // (CNT_HIGHER)
+  constexpr bool ST = HI && !X && HB_ROUTE_STORM;
+  static_assert(!ST || RG % ROUTE_THREADS == 0, "the storm ballots run at loop level");
+  __shared__ uint32_t l_pf[ST ? RG / 32 : 1];  // groups k_apply_lead would hand over unloaded (pflag words)
+  __shared__ uint32_t l_ef[ST ? RG / 32 : 1];  // ... of them, k_elect's (eflag words)
+  __shared__ uint32_t l_ok[ST ? NP : 1];       // 1: the partition needs no k_apply_lead
   // blockIdx -> (bucket, w): the W sisters of a bucket share blockIdx % 8 (one XCD)
   const uint32_t x = blockIdx.x, q = x >> 3;
   const uint32_t bk = ((q / W) << 3) | (x & 7), w = q % W;
@@ -1133,8 +1147,10 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   const uint32_t lg0 = w * RG;  // first group (in the bucket) of this workgroup
   // (uniform; a follower-side batch's route measured +12 us with it)
   const bool hi_on = HI && !X && !a.props_on;
+  const bool storm = ST && a.storm;  // (the host sets it only without props and X)
   for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) l_cnt[i] = 0;
   if (tid < NP) l_ptot[tid] = 0;
+  if (ST && tid < NP) l_ok[tid] = 1;
   __syncthreads();
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
   const uint32_t sub_lo = lg0 >> PART_LOG, sub_hi = (lg0 + RG) >> PART_LOG;
@@ -1174,9 +1190,11 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   const uint32_t gbase = (bk << (PART_LOG + sl)) + lg0;
   for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) {
     const uint32_t c = l_cnt[i], g = gbase + i;
+    bool hand = false, elect = false, ok = true;  // (storm)
     if (g < G) {
       // a group whose messages all sit in its slots: any Term above its own?
       bool hib = false;
+      const uint32_t mlo = (storm && c > 0) ? at32(reinterpret_cast<const uint32_t*>(a.S.meta), 2 * g) : 0u;
       if (hi_on && c <= (uint32_t)KMAX) {
         const uint64_t t = a.S.term[g];
 #pragma unroll
@@ -1190,6 +1208,19 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
         }
       }
       a.cnt[g] = (uint8_t)((c < CNT_MASK ? c : CNT_MASK) | (hib ? CNT_HIGHER : 0u));
+      if (storm && c > 0) {
+        // what k_apply_lead (no proposals, no X) hands over unloaded at message 0:
+        // a live group that is no leader, a leader whose r.Commit is unknown
+        // (M_NC), and a busy leader (more messages than n - 1, all in its slots)
+        // with a higher-term message (busy_hi); k_elect tries all but M_NC leaders
+        const bool live = m_n(mlo) != 0 && m_fault(mlo) == 0;
+        const bool leader = m_state(mlo) == HB_STATE_LEADER, nc = (mlo & (uint32_t)M_NC) != 0;
+        const bool busy_hi = leader && !nc && c > a.nmax - 1 && c <= (uint32_t)KMAX && hib;
+        hand = live && (!leader || nc || busy_hi);
+        elect = live && (!leader || busy_hi);
+        ok = !live || hand;  // (a leader to step: k_apply_lead runs the partition)
+        if (hand) a.resume[g] = 1u << 30;
+      }
       // arrival order of a group whose messages all fit (odd-even transposition
       // over the arrival indices, slot numbers riding along as nibbles)
       uint32_t perm = 0, key[KMAX];
@@ -1226,6 +1257,18 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
     if ((tid & 63) == 0 && s) atomicAdd(&l_ptot[i >> PART_LOG], s);
+    if constexpr (ST) {
+      if (storm) {
+        const uint64_t b = __ballot(hand), e = __ballot(elect), bad = __ballot(!ok);
+        if ((tid & 63) == 0) {
+          l_pf[i >> 5] = (uint32_t)b;
+          l_pf[(i >> 5) + 1] = (uint32_t)(b >> 32);
+          l_ef[i >> 5] = (uint32_t)e;
+          l_ef[(i >> 5) + 1] = (uint32_t)(e >> 32);
+          if (bad) atomicAnd(&l_ok[i >> PART_LOG], 0u);
+        }
+      }
+    }
   }
   __syncthreads();
   if (tid < NP) {
@@ -1234,6 +1277,37 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
       const uint32_t r = atomicAdd(&a.bk_fill[bk * CTR_STRIDE], a.ev_per_msg * (l_ptot[tid] + PART * a.props_on));
       a.ev_off[2 * part + 1] =
           (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + lo + ((uint64_t)bk * PART << sl) * a.props_on) + r;
+    }
+  }
+  if constexpr (ST) {
+    if (storm) {  // close the partitions k_apply_lead would only hand over (its fast_close)
+      if (tid < NP * FLAG_WORDS) {
+        const uint32_t p = tid / FLAG_WORDS, j = tid % FLAG_WORDS, part = (bk << sl) + w * NP + p;
+        if (part < a.NB && l_ok[p]) {
+          a.pflag[(size_t)part * FLAG_WORDS + j] = l_pf[p * FLAG_WORDS + j];
+          a.eflag[(size_t)part * FLAG_WORDS + j] = l_ef[p * FLAG_WORDS + j];
+        }
+      }
+      if (tid < NP) {
+        const uint32_t part = (bk << sl) + w * NP + tid;
+        if (part < a.NB) {
+          a.lskip[part] = (uint8_t)l_ok[tid];
+          if (l_ok[tid]) {
+            a.ev_off[2 * part] = (uint64_t)part * PART * a.ev_per_msg;
+            a.ev_counts[2 * part] = 0;
+            a.ev_counts[2 * part + 1] = 0;
+            uint32_t any = 0, eany = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < FLAG_WORDS; ++j) {
+              any |= l_pf[tid * FLAG_WORDS + j];
+              eany |= l_ef[tid * FLAG_WORDS + j];
+            }
+            const uint32_t xs = blockIdx.x & 7;  // (= the bucket's XCD slot, as k_apply_lead's)
+            if (any) a.ap_list[(size_t)xs * a.NB + atomicAdd(&a.ap_cnt[xs * CTR_STRIDE], 1u)] = part;
+            if (eany) a.el_list[(size_t)xs * a.NB + atomicAdd(&a.el_cnt[xs * CTR_STRIDE], 1u)] = part;
+          }
+        }
+      }
     }
   }
 }
@@ -2261,6 +2335,7 @@ __global__ void __launch_bounds__(PART, NMAX <= 5 ? (X && HB_LEAD_XSTAGE ? HB_LE
   __shared__ uint4 l_lane[LW][(LDS || X) ? PART : 1];
   const uint32_t part = block_part(a.sis_log);
   if (part >= a.NB) return;  // uniform: grid padding
+  if (!X && a.storm && a.lskip[part]) return;  // uniform: the route closed it (storm hand-over)
   const uint32_t tid = threadIdx.x;
   const uint32_t g = part * PART + tid;
   const bool gvalid = g < a.S.G;
@@ -3225,6 +3300,7 @@ struct hb_handle {
   bool no_small = false;
   uint32_t kern = 0;  // hb_step_kernels of the last step
   uint32_t fuse = 2;  // k_route_fast: 0 never, 1 one-pass handles, 2 every geometry (HB_ROUTE_FUSE at hb_create)
+  uint32_t storm = 1;  // n >= 5: the route's storm hand-over (HB_STORM=0 at hb_create: off)
   uint32_t agrid = 0;  // the apply kernels' grid (apply_grid_for)
   uint32_t bk_bits = 1;            // bits of a bucket id
   // host-pointer staging
@@ -3258,6 +3334,7 @@ struct hb_handle {
   uint32_t* ap_list = nullptr;    // [8][NB]
   uint32_t* fl_list = nullptr;    // [NB]
   uint32_t* eflag = nullptr;      // [NB][PART/32] k_elect's groups (n >= 5)
+  uint8_t* lskip = nullptr;       // [NB] partitions the route closed (n >= 5 storm hand-over)
   uint32_t* el_list = nullptr;    // [8][NB]
   uint32_t* done = nullptr;       // k_apply workgroups finished this step
   uint32_t* resume = nullptr;     // [G]
@@ -3496,6 +3573,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   h->NB = (capacity + PART - 1) / PART;
   if (const char* e = getenv("HB_SMALL_STEP")) h->no_small = e[0] == '0';
   if (const char* e = getenv("HB_ROUTE_FUSE")) h->fuse = (uint32_t)atoi(e);
+  if (const char* e = getenv("HB_STORM")) h->storm = e[0] != '0';
   const size_t G = capacity, R = h->nmax;
   DevState& s = h->st;
   s.G = capacity;
@@ -3592,6 +3670,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->fl_list, h->NB);
   if (h->nmax >= 5) {
     ALLOC(h->eflag, (size_t)h->NB * FLAG_WORDS);
+    ALLOC(h->lskip, (size_t)h->NB);
     ALLOC(h->el_list, 8ull * h->NB);
   }
   ALLOC(h->resume, G);
@@ -4294,7 +4373,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   }
 
   // ---- phase 2: route each partition's messages to its lanes (prep stream) ----
-  ApplyArgs aa;
+  ApplyArgs aa{};
   aa.S = h->st;
   aa.S.edesc = bd_edesc;
   aa.S.eoff = bd_eoff;
@@ -4338,6 +4417,11 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.side = ps.side;
   aa.recx = ps.recx;
   aa.slotx = xmode ? ps.slotx : nullptr;
+  aa.nmax = h->nmax;
+  aa.lskip = h->lskip;
+  // the route's storm hand-over writes the handle's flags and lists: only when
+  // the apply of the previous step is not running beside it (one stream)
+  aa.storm = (HB_ROUTE_STORM && h->nmax >= 5 && !two && !xmode && !bd.props && h->storm) ? 1u : 0u;
   // n = 3, prep and apply on one stream: the route runs inside the fast
   // kernel's workgroups (k_route_fast; two-pass handles too: cfg5 0.998 ->
   // 0.931 ms/step same box)

@@ -176,16 +176,33 @@ def test_pipelined_steps_with_input_stream():
     assert_groups_equal(eng.get_groups(), og.groups(), "pipelined")
 
 
-def test_cfg4_storm_repeatable_stream():
+@pytest.mark.parametrize("n", [5, 7])
+def test_cfg4_storm_repeatable_stream(n):
     """The bench's repeatable cfg4 storm: step-down, campaign, n-1 votes, replayed
-    at +4 terms per step on the state the previous storm left."""
+    at +4 terms per step on the state the previous storm left.  Every partition
+    holds only groups k_apply_lead would hand over unloaded, so the route closes
+    them (storm hand-over, k_route); the last step adds one leader to step in
+    partition 3 (a MsgHeartbeatResp at its own term), so k_apply_lead runs that
+    partition and the route closes the others."""
     G = 2500
-    g, runs = synth.election_groups(G, 7, seed=21)
-    pair = Pair(g, runs, 7, 64, max_batch=8 * G)
+    g, runs = synth.election_groups(G, n, seed=21)
+    pair = Pair(g, runs, n, 64, max_batch=8 * G)
     b = synth.cfg4_storm_batch(g, seed=22)
     for k in range(3):
         _, st, _ = pair.step(dict(b, term=synth.storm_terms(b["term"], k)), ctx=f"storm {k}")
-        assert st[abi.HB_STAT_VOTERESP] == G * 6 and st[abi.HB_STAT_WON] > 0
+        assert st[abi.HB_STAT_VOTERESP] == G * (n - 1) and st[abi.HB_STAT_WON] > 0
+    now = pair.og.groups()
+    lead = np.flatnonzero((now["state"] == abi.HB_STATE_LEADER) & (np.arange(G) // 256 == 3))
+    assert len(lead)
+    x = int(lead[0])
+    keep = b["group"] != x
+    b3 = {k: (v[keep] if isinstance(v, np.ndarray) else v) for k, v in b.items()}
+    b3["term"] = synth.storm_terms(b3["term"], 3)
+    b3["group"] = np.append(b3["group"], np.uint32(x))
+    b3["info"] = np.append(b3["info"], np.uint32(abi.HB_MSG_HEARTBEAT_RESP | (1 << 4)))
+    b3["term"] = np.append(b3["term"], np.uint64(now["term"][x]))
+    b3["index"] = np.append(b3["index"], np.uint64(0))
+    pair.step(b3, ctx="storm 3 + a leader")
 
 
 @pytest.mark.parametrize("W", [8, 256])
