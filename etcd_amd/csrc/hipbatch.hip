@@ -738,7 +738,7 @@ struct ApplyArgs {
   // groups with messages are all busy leaders with a higher-term message, as
   // k_apply_lead would (flags, lists, event chunks), and k_apply_lead skips it
   uint32_t nmax;            // the handle's replica bound (5 or 7)
-  uint32_t storm;           // 1: this step's route may close partitions (lskip)
+  uint32_t storm;           // 1: this step's route may close partitions (lskip), 2: and run k_elect's lane there
   uint8_t* lskip;           // [NB] 1: the route closed the partition
 };
 
@@ -1123,7 +1123,9 @@ template <int KMAX, bool X> struct RouteGeom {
   // workgroups per bucket: 2^(PART_LOG + sis_log - RG_LOG) (sis_log >= RG_LOG - PART_LOG)
 };
 
-template <int KMAX, bool X>
+// EN > 0 (n = EN, storm mode 2): the election lane runs in the route's
+// workgroup over the partitions it closes, from the LDS slots (§3.2)
+template <int KMAX, bool X, int EN = 0>
 __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   using RGm = RouteGeom<KMAX, X>;
   constexpr uint32_t RG = RGm::RG, NP = RG / PART;
@@ -1138,6 +1140,11 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   __shared__ uint32_t l_pf[ST ? RG / 32 : 1];  // groups k_apply_lead would hand over unloaded (pflag words)
   __shared__ uint32_t l_ef[ST ? RG / 32 : 1];  // ... of them, k_elect's (eflag words)
   __shared__ uint32_t l_ok[ST ? NP : 1];       // 1: the partition needs no k_apply_lead
+  constexpr bool EL = ST && EN > 0;
+  static_assert(!EL || (RG == ROUTE_THREADS && !HB_ROUTE_SORTED), "EL: one group per lane, slots as routed");
+  __shared__ uint64_t l_moff[EL ? NP : 1];      // EL: the partitions' M chunks
+  __shared__ uint32_t l_efill[EL ? NP : 1];     // ... and their fill
+  __shared__ uint64_t l_stats[EL ? ST_N + 1 : 1];
   // blockIdx -> (bucket, w): the W sisters of a bucket share blockIdx % 8 (one XCD)
   const uint32_t x = blockIdx.x, q = x >> 3;
   const uint32_t bk = ((q / W) << 3) | (x & 7), w = q % W;
@@ -1151,6 +1158,8 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) l_cnt[i] = 0;
   if (tid < NP) l_ptot[tid] = 0;
   if (ST && tid < NP) l_ok[tid] = 1;
+  if (EL && tid < NP) l_efill[tid] = 0;
+  if (EL && tid <= ST_N) l_stats[tid] = 0;
   __syncthreads();
   const uint32_t lo = a.bk_off[bk], hi = a.bk_off[bk + 1];
   const uint32_t sub_lo = lg0 >> PART_LOG, sub_hi = (lg0 + RG) >> PART_LOG;
@@ -1188,13 +1197,20 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
   }
   __syncthreads();
   const uint32_t gbase = (bk << (PART_LOG + sl)) + lg0;
+  const bool el = EL && storm;            // slots written after the election lane (EL)
+  uint32_t e_c = 0;                       // (EL: the lane's group, i = tid)
+  bool e_hand = false, e_elect = false;
+  uint64_t e_meta = 0;
   for (uint32_t i = tid; i < RG; i += ROUTE_THREADS) {
     const uint32_t c = l_cnt[i], g = gbase + i;
     bool hand = false, elect = false, ok = true;  // (storm)
     if (g < G) {
       // a group whose messages all sit in its slots: any Term above its own?
       bool hib = false;
-      const uint32_t mlo = (storm && c > 0) ? at32(reinterpret_cast<const uint32_t*>(a.S.meta), 2 * g) : 0u;
+      uint64_t meta = 0;
+      if (storm && c > 0)
+        meta = EL ? a.S.meta[g] : (uint64_t)at32(reinterpret_cast<const uint32_t*>(a.S.meta), 2 * g);
+      const uint32_t mlo = (uint32_t)meta;
       if (hi_on && c <= (uint32_t)KMAX) {
         const uint64_t t = a.S.term[g];
 #pragma unroll
@@ -1221,6 +1237,12 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
         ok = !live || hand;  // (a leader to step: k_apply_lead runs the partition)
         if (hand) a.resume[g] = 1u << 30;
       }
+      if constexpr (EL) {
+        e_c = c;
+        e_hand = hand;
+        e_elect = elect;
+        e_meta = meta;
+      }
       // arrival order of a group whose messages all fit (odd-even transposition
       // over the arrival indices, slot numbers riding along as nibbles)
       uint32_t perm = 0, key[KMAX];
@@ -1246,7 +1268,7 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
       }
 #pragma unroll
       for (uint32_t k = 0; k < (uint32_t)KMAX; ++k) {
-        if (k < c) {
+        if (k < c && !el) {
           const uint32_t src = (perm >> (4 * k)) & 0xF;
           at32(a.slot, k * G + g) = l_slot[src][i];
           if constexpr (X) at32(a.slotx, k * G + g) = l_slotx[src][i];
@@ -1275,8 +1297,79 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
     const uint32_t part = (bk << sl) + w * NP + tid;
     if (part < a.NB) {
       const uint32_t r = atomicAdd(&a.bk_fill[bk * CTR_STRIDE], a.ev_per_msg * (l_ptot[tid] + PART * a.props_on));
-      a.ev_off[2 * part + 1] =
+      const uint64_t mo =
           (uint64_t)a.ev_per_msg * ((uint64_t)a.NB * PART + lo + ((uint64_t)bk * PART << sl) * a.props_on) + r;
+      a.ev_off[2 * part + 1] = mo;
+      if constexpr (EL) l_moff[tid] = mo;
+    }
+  }
+  if constexpr (EL) {
+    if (el) {  // ---- the election lane over the closed partitions (k_elect's work, slots from LDS)
+      __syncthreads();  // l_moff
+      const uint32_t p = __builtin_amdgcn_readfirstlane(tid >> PART_LOG);
+      const uint32_t g = gbase + tid;
+      const bool closed = l_ok[p] != 0;  // (uniform per wave)
+      bool done = false;
+      uint32_t st_msgs = 0, st_app = 0, st_vote = 0, st_drop = 0, st_commit = 0;
+      ElectLane<EN> L;
+      L.won = L.lost = L.nev = 0;
+      L.committed = L.last = 0;
+      uint64_t last0 = 0;
+      if (closed) {
+        L.S = a.S;
+        L.E.chunk = a.ev + l_moff[p];
+        L.E.fill = &l_efill[p];
+        L.g = g;
+        L.meta = e_meta;
+        // k_elect's own groups: no leader, or a busy leader with a higher-term message (resume 0, not loaded)
+        const bool mine = e_elect && e_c <= (uint32_t)KMAX && L.self() < L.n() && !(L.meta & M_NC);
+        if (mine) {
+          L.load();
+          last0 = L.last;
+          const uint64_t commit0 = L.committed;
+          uint32_t key[KMAX];
+#pragma unroll
+          for (uint32_t k = 0; k < (uint32_t)KMAX; ++k) key[k] = k < e_c ? l_slot[k][tid].y : 0xFFFFFFFFu;
+          const uint32_t perm = arrival_perm<(uint32_t)KMAX>(key);
+          uint32_t x = 0;
+#pragma nounroll
+          for (; x < e_c; ++x) {
+            uint32_t inf, org;
+            uint64_t mterm, ix;
+            slot_unpack(l_slot[(perm >> (4 * x)) & 0xF][tid], a.side, &inf, &org, &mterm, &ix);
+            const uint32_t type = inf & 0xF, from = (inf >> 4) & 0xF;
+            if (from >= L.n() && is_response(type)) {  // raft/multinode.go:235
+              st_drop++;
+              continue;
+            }
+            if (!L.takes(type, from, mterm)) break;
+            L.step(type, from, mterm, (inf >> 8) & 1u);
+            st_msgs++;
+            st_app += type == HB_MSG_APP_RESP;
+            st_vote += type == HB_MSG_VOTE_RESP;
+          }
+          if (x > 0) {
+            L.store();
+            if (x == e_c) {
+              done = true;  // the group's batch ends here
+            } else {        // k_apply resumes at message x, loading what was stored
+              a.resume[g] = x;
+              a.commit0[g] = commit0;
+            }
+          }
+          st_commit = done && L.committed != commit0;
+        }
+        flag_put<false>(&l_pf[p * FLAG_WORDS], tid & (PART - 1), done);
+      }
+      // the slots k_apply (or k_apply_lead / k_elect of an open partition) reads
+      if (g < G && e_c > 0 && (!closed || (e_hand && !done))) {
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)KMAX; ++k)
+          if (k < e_c) at32(a.slot, k * G + g) = l_slot[k][tid];
+      }
+      const uint32_t vals[ST_N + 1] = {st_msgs, st_app, st_vote, st_drop, st_commit, L.won, L.lost, 0,
+                                       (uint32_t)(L.last - last0), L.nev};
+      reduce_stats(a, l_stats, vals);  // (ends with a barrier: l_pf and l_efill are final)
     }
   }
   if constexpr (ST) {
@@ -1285,7 +1378,7 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
         const uint32_t p = tid / FLAG_WORDS, j = tid % FLAG_WORDS, part = (bk << sl) + w * NP + p;
         if (part < a.NB && l_ok[p]) {
           a.pflag[(size_t)part * FLAG_WORDS + j] = l_pf[p * FLAG_WORDS + j];
-          a.eflag[(size_t)part * FLAG_WORDS + j] = l_ef[p * FLAG_WORDS + j];
+          if (!el) a.eflag[(size_t)part * FLAG_WORDS + j] = l_ef[p * FLAG_WORDS + j];
         }
       }
       if (tid < NP) {
@@ -1295,7 +1388,7 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
           if (l_ok[tid]) {
             a.ev_off[2 * part] = (uint64_t)part * PART * a.ev_per_msg;
             a.ev_counts[2 * part] = 0;
-            a.ev_counts[2 * part + 1] = 0;
+            a.ev_counts[2 * part + 1] = EL ? l_efill[EL ? tid : 0] : 0u;
             uint32_t any = 0, eany = 0;
 #pragma unroll
             for (uint32_t j = 0; j < FLAG_WORDS; ++j) {
@@ -1304,7 +1397,7 @@ __global__ void __launch_bounds__(ROUTE_THREADS) k_route(ApplyArgs a) {
             }
             const uint32_t xs = blockIdx.x & 7;  // (= the bucket's XCD slot, as k_apply_lead's)
             if (any) a.ap_list[(size_t)xs * a.NB + atomicAdd(&a.ap_cnt[xs * CTR_STRIDE], 1u)] = part;
-            if (eany) a.el_list[(size_t)xs * a.NB + atomicAdd(&a.el_cnt[xs * CTR_STRIDE], 1u)] = part;
+            if (eany && !el) a.el_list[(size_t)xs * a.NB + atomicAdd(&a.el_cnt[xs * CTR_STRIDE], 1u)] = part;
           }
         }
       }
@@ -3300,7 +3393,7 @@ struct hb_handle {
   bool no_small = false;
   uint32_t kern = 0;  // hb_step_kernels of the last step
   uint32_t fuse = 2;  // k_route_fast: 0 never, 1 one-pass handles, 2 every geometry (HB_ROUTE_FUSE at hb_create)
-  uint32_t storm = 1;  // n >= 5: the route's storm hand-over (HB_STORM=0 at hb_create: off)
+  uint32_t storm = 2;  // n >= 5: the route's storm hand-over, 2: with the election lane (HB_STORM=0/1/2 at hb_create)
   uint32_t agrid = 0;  // the apply kernels' grid (apply_grid_for)
   uint32_t bk_bits = 1;            // bits of a bucket id
   // host-pointer staging
@@ -3459,6 +3552,15 @@ uint32_t route_grid(const hb_handle* h, bool x) {
 }
 template <int KMAX>
 void launch_route(hb_handle* h, const ApplyArgs& a, hipStream_t st) {
+  if constexpr (KMAX >= 5) {
+    if (!a.slotx && a.storm >= 2) {  // the storm hand-over with the election lane in the route
+      if (h->nmax <= 5)
+        hipLaunchKernelGGL((k_route<KMAX, false, 5>), dim3(route_grid<KMAX>(h, false)), dim3(ROUTE_THREADS), 0, st, a);
+      else
+        hipLaunchKernelGGL((k_route<KMAX, false, 7>), dim3(route_grid<KMAX>(h, false)), dim3(ROUTE_THREADS), 0, st, a);
+      return;
+    }
+  }
   if (a.slotx) hipLaunchKernelGGL((k_route<KMAX, true>), dim3(route_grid<KMAX>(h, true)), dim3(ROUTE_THREADS), 0, st, a);
   else hipLaunchKernelGGL((k_route<KMAX, false>), dim3(route_grid<KMAX>(h, false)), dim3(ROUTE_THREADS), 0, st, a);
 }
@@ -3573,7 +3675,7 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   h->NB = (capacity + PART - 1) / PART;
   if (const char* e = getenv("HB_SMALL_STEP")) h->no_small = e[0] == '0';
   if (const char* e = getenv("HB_ROUTE_FUSE")) h->fuse = (uint32_t)atoi(e);
-  if (const char* e = getenv("HB_STORM")) h->storm = e[0] != '0';
+  if (const char* e = getenv("HB_STORM")) h->storm = (uint32_t)atoi(e);
   const size_t G = capacity, R = h->nmax;
   DevState& s = h->st;
   s.G = capacity;
@@ -4421,7 +4523,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
   aa.lskip = h->lskip;
   // the route's storm hand-over writes the handle's flags and lists: only when
   // the apply of the previous step is not running beside it (one stream)
-  aa.storm = (HB_ROUTE_STORM && h->nmax >= 5 && !two && !xmode && !bd.props && h->storm) ? 1u : 0u;
+  aa.storm = (HB_ROUTE_STORM && h->nmax >= 5 && !two && !xmode && !bd.props) ? h->storm : 0u;
   // n = 3, prep and apply on one stream: the route runs inside the fast
   // kernel's workgroups (k_route_fast; two-pass handles too: cfg5 0.998 ->
   // 0.931 ms/step same box)
