@@ -275,7 +275,10 @@ def cpu_baseline_wire(n, groups=100_000, W=256, budget_s=10.0, max_steps=20):
                       f"x {n}, {steps} cfg2 steps from wire records, {acks} MsgAppResp in {spent:.2f} s, one core"}
 
 
-def pmc_traffic(path, kernel, G, n, apply_us, workload=None):
+LAYOUT_RO = "role-ordered (led groups in their own partitions; --role-order)"
+
+
+def pmc_traffic(path, kernel, G, n, apply_us, workload=None, layout=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (FETCH_SIZE x 2 + WRITE_SIZE, tools/prof_summary.py).  Used only when the
     profile was taken on the same workload and its average duration agrees with
@@ -291,7 +294,8 @@ def pmc_traffic(path, kernel, G, n, apply_us, workload=None):
         except (OSError, KeyError, ValueError, StopIteration):
             continue
         if cfg.get("groups_per_gpu") == G and cfg.get("replicas") == n and "traffic_bytes" in k and \
-                (workload is None or cfg.get("workload", "").startswith(workload + ":")):
+                (workload is None or cfg.get("workload", "").startswith(workload + ":")) and \
+                cfg.get("layout") == layout:
             break
     else:
         return None, None
@@ -301,7 +305,7 @@ def pmc_traffic(path, kernel, G, n, apply_us, workload=None):
     return float(k["traffic_bytes"]), f"{src}: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, avg {k['avg_us']:.1f} us"
 
 
-def step_traffic(path, workload, G, n, ms_per_step):
+def step_traffic(path, workload, G, n, ms_per_step, layout=None):
     """Whole-step HBM bytes of an auxiliary line (cfg3 / cfg4 / tick) from the
     newest committed profile of the same workload and configuration
     (tools/profile_round.sh with WL=<workload>: FETCH_SIZE x 2 + WRITE_SIZE
@@ -316,7 +320,7 @@ def step_traffic(path, workload, G, n, ms_per_step):
         except (OSError, KeyError, ValueError, TypeError):
             continue
         if cfg.get("workload", "").startswith(workload + ":") and cfg.get("groups_per_gpu") == G and \
-                cfg.get("replicas") == n:
+                cfg.get("replicas") == n and cfg.get("layout") == layout:
             src = os.path.relpath(p, ROOT)
             if abs(bms - ms_per_step) > 0.15 * ms_per_step:
                 return None, f"{src}: profiled step {bms:.3f} ms vs live {ms_per_step:.3f} ms (stale, not used)"
@@ -437,6 +441,10 @@ def main():
                     help="groups per GPU (cfg2/cfg3/e2e: 1M, cfg5: 8M, cfg4: 4M)")
     ap.add_argument("--replicas", type=int, default=None, help="cfg2/cfg5: 3, cfg3: 5, cfg4: 7")
     ap.add_argument("--inflight", type=int, default=256, help="MaxInflightMsgs W (cfg3/cfg4)")
+    ap.add_argument("--role-order", action="store_true",
+                    help="mixed / tick: the groups laid out by role (led groups in partitions of their own), the "
+                         "layout a role-ordered slot map in the node would give; a measurement of that map, "
+                         "which libhbnode does not build (default: roles interleaved, as a node's ids fall)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-groups", type=int, default=200_000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -931,6 +939,8 @@ def run_aux(args, world, rank, local, dev, torch, dist):
                    "commit": np.ones(len(b["group"]), np.uint64)}
         else:
             g, _ = synth.mixed_groups(G, n, seed=seed, with_runs=False)
+            if args.role_order:  # led groups first (stable): whole partitions of one role
+                g = g[np.argsort(g["state"] != abi.HB_STATE_LEADER, kind="stable")]
             b, inc = synth.mixed_batch(g, 0, seed=seed)
             n_led = int((g["state"] == abi.HB_STATE_LEADER).sum())
         nmsg = len(b["group"])
@@ -976,8 +986,9 @@ def run_aux(args, world, rank, local, dev, torch, dist):
         g, _ = synth.steady_groups(G, n, seed=seed, with_runs=False)
         # half the groups lead (HeartbeatTick 1: a MsgBeat every tick), half
         # follow a leader elsewhere with ElectionTick 10 (draws past elapsed 10)
-        g["state"][1::2] = abi.HB_STATE_FOLLOWER
-        g["lead"][1::2] = 1
+        fol = slice(G // 2, None) if args.role_order else slice(1, None, 2)  # (role-ordered: leaders first)
+        g["state"][fol] = abi.HB_STATE_FOLLOWER
+        g["lead"][fol] = 1
         eng = Engine(G, max_replicas=n, max_inflight=W, max_batch=1, device=local, stream=stream)
         eng.load_groups(g)
         del g
@@ -1173,7 +1184,8 @@ def run_aux(args, world, rank, local, dev, torch, dist):
             kname = f"k_apply_lead<{n}> (X mode: LeadLane + FollowLane)"
             knames = [f"k_apply_lead<{n}, true>", f"k_apply_lead<{n}>"]
         ach_k = launch_alg / (apply_us * 1e-6) / 1e9 if apply_us > 0 else 0.0
-        tr, tsrc = pmc_traffic(args.traffic_json, knames, G, n, apply_us, workload=args.workload)
+        tr, tsrc = pmc_traffic(args.traffic_json, knames, G, n, apply_us, workload=args.workload, layout=LAYOUT_RO
+                               if args.role_order else None)
         extra = {"commits_per_s": int(st[abi.HB_STAT_COMMITS]) / sec, "entries_per_s": int(st[abi.HB_STAT_ENTRIES]) / sec,
                  "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(ach_k, 1), "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": round(ach_k / HBM_PEAK_GBS, 4), "traffic": tr,
@@ -1231,7 +1243,8 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     if args.workload in ("cfg3", "cfg4", "tick"):
         # whole-step roofline (several kernels share the step; per-kernel times: profiles/*kernel_stats.csv)
         ach = alg / (ms / args.steps * 1e-3) / args.steps / 1e9 if ms > 0 else 0.0
-        tr, tsrc = step_traffic(args.traffic_json, args.workload, G, n, ms / args.steps)
+        tr, tsrc = step_traffic(args.traffic_json, args.workload, G, n, ms / args.steps,
+                                layout=LAYOUT_RO if args.role_order and args.workload == "tick" else None)
         extra["roofline"] = {"bound": "hbm", "kernel": "hb_step (whole step)" if args.workload != "tick" else
                              "hb_tick (k_tick + finish)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr,
@@ -1241,7 +1254,8 @@ def run_aux(args, world, rank, local, dev, torch, dist):
     out = {"metric": metric, "value": val, "unit": unit, "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": ms / args.steps, "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "u64", "data": data,
-           "config": {"workload": wl, "groups_per_gpu": G, "replicas": n, "max_inflight": W},
+           "config": dict({"workload": wl, "groups_per_gpu": G, "replicas": n, "max_inflight": W},
+                          **({"layout": LAYOUT_RO} if args.role_order and args.workload in ("mixed", "tick") else {})),
            "stats": {nm: int(v) for nm, v in zip(abi.STAT_NAMES, st.tolist())}, "timing": timing,
            "parity_sanity": bool(ok), "wall_s": time.perf_counter() - t_wall, "cpu_baseline": None, **extra}
     if world > 1:

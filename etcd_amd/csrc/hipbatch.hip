@@ -2189,8 +2189,8 @@ __global__ void __launch_bounds__(PART, HB_GEN_WAVES) k_apply(ApplyArgs a) {
 #ifndef HB_ELECT_WAVES
 #define HB_ELECT_WAVES 4
 #endif
-#ifndef HB_ELECT_GRID
-#define HB_ELECT_GRID 0  // as HB_GEN_GRID
+#ifndef HB_ELECT_GRID  // persistent over the XCD-slot lists (cfg4 -9 to -11 us, cfg3 -3 to -6 us vs one
+#define HB_ELECT_GRID 1024  // workgroup per partition: an empty or short list launched 16K workgroups)
 #endif
 #ifndef HB_ELECT_EAGER
 #define HB_ELECT_EAGER 1

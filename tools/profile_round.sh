@@ -4,7 +4,7 @@
 #   2. PMC pass FETCH_SIZE  (own run, MI355X_MICROARCH.md: one counter group per pass)
 #   3. PMC pass WRITE_SIZE
 #   4. plain bench.py (the JSON line, with the traffic the passes measured)
-# WL=<workload> (default cfg2) profiles another bench line (cfg3 / cfg4 / cfg5 / tick).
+# WL=<workload> (default cfg2) profiles another bench line (cfg3 / cfg4 / cfg5 / tick); BA= adds bench args.
 # Outputs under gpurun_out/<tag>/; tools/prof_summary.py folds them into profiles/.
 set -euo pipefail
 TAG=${1:-r01}
@@ -17,6 +17,7 @@ STEPS=${STEPS:-20}
 # WL=<workload>[:<replicas>] (e.g. follow:5)
 SPEC=${WL:-cfg2}; W0=${SPEC%%:*}
 WA="--workload $W0"; [ "$SPEC" != "$W0" ] && WA="$WA --replicas ${SPEC#*:}"
+WA="$WA ${BA:-}"  # BA=<more bench args> (e.g. --role-order)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
     python3 bench.py $WA --steps "$STEPS" --warmup 5 --no-cpu-baseline > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
 echo "trace done"
