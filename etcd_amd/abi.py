@@ -124,6 +124,7 @@ HB_PHASE_GENERAL = 2
 HB_PHASE_FINISH = 3
 HB_PHASE_COUNT = 4
 HB_KERN_ROUTE_FAST = 1  # hb_step_kernels: k_route_fast ran the route and the fast lane
+HB_KERN_ROUTE_ELECT = 2  # hb_step_kernels: k_route closed storm partitions and ran the election lane
 
 STAT_NAMES = ["msgs", "appresp", "voteresp", "dropped", "commits", "won", "lost",
               "events", "faults", "entries"]

@@ -4560,7 +4560,7 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
     h->prof_n++;
   }
   h->stepped = true;
-  h->kern = fused ? HB_KERN_ROUTE_FAST : 0u;
+  h->kern = (fused ? HB_KERN_ROUTE_FAST : 0u) | (aa.storm >= 2 ? HB_KERN_ROUTE_ELECT : 0u);
   return HB_OK;
 }
 

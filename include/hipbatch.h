@@ -581,8 +581,13 @@ int  hb_phase_reset(hb_handle* h);
 /* Which apply kernels the last hb_step launched (for profiles and rooflines):
  * HB_KERN_ROUTE_FAST = the route and the n = 3 fast lane ran as one kernel
  * (k_route_fast; HB_PHASE_APPLY then brackets it), else k_route and
- * k_apply_fast / k_apply_lead separately. */
+ * k_apply_fast / k_apply_lead separately.  HB_KERN_ROUTE_ELECT = (n >= 5,
+ * batches without dense proposals) the route closed the partitions whose
+ * groups k_apply_lead would only hand over and ran the election lane there
+ * (k_route<8, false, n>; HB_STORM=0/1 at hb_create turns it off / keeps only
+ * the hand-over). */
 #define HB_KERN_ROUTE_FAST 1u
+#define HB_KERN_ROUTE_ELECT 2u
 int  hb_step_kernels(hb_handle* h, uint32_t* mask);
 
 /* ---- pinned host memory for cgo callers (Go must not hand Go memory to C

@@ -191,6 +191,7 @@ def test_cfg4_storm_repeatable_stream(n):
     for k in range(3):
         _, st, _ = pair.step(dict(b, term=synth.storm_terms(b["term"], k)), ctx=f"storm {k}")
         assert st[abi.HB_STAT_VOTERESP] == G * (n - 1) and st[abi.HB_STAT_WON] > 0
+        assert pair.eng.step_kernels() & abi.HB_KERN_ROUTE_ELECT  # (the election lane ran in the route)
     now = pair.og.groups()
     lead = np.flatnonzero((now["state"] == abi.HB_STATE_LEADER) & (np.arange(G) // 256 == 3))
     assert len(lead)
