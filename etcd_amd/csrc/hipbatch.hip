@@ -266,8 +266,30 @@ __device__ __forceinline__ uint32_t excl_scan256(uint32_t v, uint32_t* sh4, uint
 #define HB_HIST_TPB 4
 #endif
 constexpr uint32_t HIST_TPB = HB_HIST_TPB;
+// One-pass partitions take each tile's digit offsets without a scan launch
+// (HB_RDX_DIRECT): k_radix_hist also writes each workgroup's digit sums
+// (DirectSums::agg) and adds them into its superblock's (SB_HW workgroups,
+// agent-scope atomics), and the scatter sums the superblocks, aggregates and
+// tiles before its own (k_radix_scatter_d).  The superblock sums rotate over
+// three buffers: a step's hist clears the one the next step adds into (read
+// by the scatter two steps ago), as far as that one was dirtied.
+#ifndef HB_RDX_DIRECT
+#define HB_RDX_DIRECT 1
+#endif
+constexpr uint32_t SB_HW = 32;
+constexpr uint32_t SUP_BUFS = 3;
+struct DirectSums {
+  uint32_t* agg = nullptr;    // [hist workgroups][RDX_BINS]; null: k_scan_rows scans the counts
+  uint32_t* sup = nullptr;    // [superblocks][RDX_BINS] of this step (zero on entry)
+  uint32_t* clear = nullptr;  // the next step's superblock buffer: n_clear words to zero
+  uint32_t n_clear = 0;
+  uint32_t* bk_fill = nullptr;  // (k_scan_rows' clears)
+  uint32_t NBK = 0;
+  uint32_t* ctr = nullptr;
+};
 __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t G, uint32_t shift, uint32_t dbits,
-                                                           uint32_t ntiles, uint32_t* hist, uint32_t dm) {
+                                                           uint32_t ntiles, uint32_t* hist, uint32_t dm,
+                                                           DirectSums ds) {
   __shared__ uint32_t cnt[HIST_TPB][RDX_BINS];
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < HIST_TPB * RDX_BINS; i += RDX_THREADS) (&cnt[0][0])[i] = 0;
@@ -296,6 +318,22 @@ __global__ void __launch_bounds__(RDX_THREADS) k_radix_hist(RadixSrc s, uint32_t
       const uint32_t t = i >> dbits, dg = i & ((1u << dbits) - 1);
       if (t0 + t < ntiles) hist[((size_t)(t0 + t) << dbits) + dg] = cnt[t][dg];
     }
+  }
+  if (ds.agg) {  // uniform (one pass: dbits = RDX_BITS)
+    if (tid < RDX_BINS) {
+      uint32_t sum = 0;
+#pragma unroll
+      for (uint32_t t = 0; t < HIST_TPB; ++t) sum += cnt[t][tid];
+      ds.agg[(size_t)blockIdx.x * RDX_BINS + tid] = sum;
+      if (sum)
+        __hip_atomic_fetch_add(&ds.sup[(size_t)(blockIdx.x / SB_HW) * RDX_BINS + tid], sum, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint32_t gi = blockIdx.x * RDX_THREADS + tid, gs = gridDim.x * RDX_THREADS;
+    for (uint32_t i = gi; i < ds.n_clear; i += gs) ds.clear[i] = 0;
+    for (uint32_t i = gi; i < ds.NBK; i += gs) ds.bk_fill[i * CTR_STRIDE] = 0;
+    if (blockIdx.x == 0)
+      for (uint32_t i = tid; i < CTR_WORDS; i += RDX_THREADS) ds.ctr[i] = 0;
   }
 }
 
@@ -407,11 +445,17 @@ constexpr uint32_t SCAT_TPW = HB_SCAT_TPW;
 // The scatter of TPW consecutive tiles from tile0 (`first`: the workgroup that
 // writes n_valid and the one-pass bucket bounds); `off` / `totals` may be LDS.
 // off[dg * ds + tile * ts]: a tile's exclusive prefix of digit dg.
-template <bool FINAL, bool X, uint32_t TPW>
+// `pre` runs right after the first tile's loads are issued (k_radix_scatter_d
+// sums its offsets there); off's tile index counts from tbase.
+struct NoPre {
+  __device__ void operator()() const {}
+};
+template <bool FINAL, bool X, uint32_t TPW, class Pre = NoPre>
 __device__ __forceinline__ void scatter_tiles(const RadixSrc& s, const RadixDst& d, const FinalDst& f, uint32_t G,
                                               uint32_t shift, uint32_t dbits, uint32_t ntiles, uint32_t tile0,
                                               const uint32_t* off, uint32_t ds, uint32_t ts, const uint32_t* totals,
-                                              uint32_t* n_valid, bool first) {
+                                              uint32_t* n_valid, bool first, const Pre& pre = Pre{},
+                                              uint32_t tbase = 0) {
   __shared__ uint32_t s_base[RDX_BINS];  // digit base in the pass output (exclusive scan of the totals)
   __shared__ uint32_t s_off[RDX_BINS];
   __shared__ uint32_t s_wcnt[RDX_WAVES][RDX_BINS];
@@ -431,6 +475,7 @@ __device__ __forceinline__ void scatter_tiles(const RadixSrc& s, const RadixDst&
   const uint32_t n = src_n(s);
   ScatTile<X> cur, nxt;
   scat_load(s, n, G, tile0 * RDX_TILE, wave, lane, cur);
+  pre();
   {
     const uint32_t t = tid < nb ? totals[tid] : 0u;
     uint32_t all;
@@ -449,7 +494,7 @@ __device__ __forceinline__ void scatter_tiles(const RadixSrc& s, const RadixDst&
     const uint32_t tile = tile0 + j;
     if (tile >= ntiles) break;  // uniform
     // this tile's digit starts in the output; per-wave digit counters cleared
-    if (tid < nb) s_off[tid] = s_base[tid] + off[(size_t)tid * ds + (size_t)tile * ts];
+    if (tid < nb) s_off[tid] = s_base[tid] + off[(size_t)tid * ds + (size_t)(tile - tbase) * ts];
 #pragma unroll
     for (uint32_t k = 0; k < RDX_WAVES * RDX_BINS / RDX_THREADS; ++k) (&s_wcnt[0][0])[tid + k * RDX_THREADS] = 0;
     __syncthreads();
@@ -574,6 +619,94 @@ __global__ void __launch_bounds__(RDX_THREADS) __attribute__((amdgpu_waves_per_e
                                                               uint32_t ds, uint32_t ts, const uint32_t* totals, uint32_t* n_valid) {
   scatter_tiles<FINAL, X, SCAT_TPW>(s, d, f, G, shift, dbits, ntiles, blockIdx.x * SCAT_TPW, off, ds, ts, totals, n_valid,
                                     blockIdx.x == 0);
+}
+
+// One pass with direct offsets (HB_RDX_DIRECT): each tile's exclusive digit
+// prefix = the superblocks before its own + the hist workgroups before its own
+// in the superblock + the tiles before it in its hist workgroup; the digit
+// totals = every superblock.  Four lanes per digit split those loads, all
+// issued at once, while the first tile's loads are in flight.
+constexpr uint32_t DQ = RDX_THREADS / RDX_BINS;  // lanes per digit
+#ifndef HB_DIRECT_PER
+#define HB_DIRECT_PER 16  // items per lane in one round trip (more: further round trips)
+#endif
+constexpr uint32_t DIRECT_PER = HB_DIRECT_PER;
+static_assert(DQ * RDX_BINS == RDX_THREADS && SCAT_TPW <= HIST_TPB && HIST_TPB % SCAT_TPW == 0,
+              "a scatter workgroup's tiles sit in one hist workgroup");
+struct DirectPre {
+  const uint32_t* hist;  // raw tile counts [tile][RDX_BINS]
+  const uint32_t* agg;
+  const uint32_t* sup;
+  uint32_t ntiles, tile0;
+  uint32_t* l_pre;  // [DQ][RDX_BINS]
+  uint32_t* l_tsum;  // [DQ][RDX_BINS]
+  uint32_t* l_off;  // [SCAT_TPW][RDX_BINS]: exclusive prefixes of the workgroup's tiles
+  uint32_t* l_tot;  // [RDX_BINS]
+  __device__ __forceinline__ const uint32_t* item(uint32_t i, uint32_t nsb, uint32_t na, uint32_t sb,
+                                                  uint32_t hb) const {
+    return i < nsb ? sup + (size_t)i * RDX_BINS
+                   : i < nsb + na ? agg + (size_t)(sb * SB_HW + (i - nsb)) * RDX_BINS
+                                  : hist + (size_t)(hb * HIST_TPB + (i - nsb - na)) * RDX_BINS;
+  }
+  __device__ void operator()() const {
+    const uint32_t tid = threadIdx.x, dg = tid % RDX_BINS, q = tid / RDX_BINS;
+    const uint32_t hb = tile0 / HIST_TPB, sb = hb / SB_HW;
+    const uint32_t nhw = (ntiles + HIST_TPB - 1) / HIST_TPB, nsb = (nhw + SB_HW - 1) / SB_HW;
+    const uint32_t na = hb - sb * SB_HW, nt = tile0 - hb * HIST_TPB, ni = nsb + na + nt;
+    // the workgroup's own tiles but its last: their counts (lanes of quarter 0)
+    uint32_t own[SCAT_TPW > 1 ? SCAT_TPW - 1 : 1];
+#pragma unroll
+    for (uint32_t j = 0; j + 1 < SCAT_TPW; ++j)
+      own[j] = (q == 0 && tile0 + j < ntiles) ? hist[(size_t)(tile0 + j) * RDX_BINS + dg] : 0u;
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t i0 = 0; i0 < ni; i0 += DQ * DIRECT_PER) {  // (one turn up to 16 superblocks: 8M messages)
+      uint32_t v[DIRECT_PER];
+#pragma unroll
+      for (uint32_t k = 0; k < DIRECT_PER; ++k) {
+        const uint32_t i = i0 + k * DQ + q;
+        v[k] = i < ni ? item(i, nsb, na, sb, hb)[dg] : 0u;
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < DIRECT_PER; ++k) {
+        const uint32_t i = i0 + k * DQ + q;
+        if (i < nsb) {
+          tot += v[k];
+          if (i < sb) pre += v[k];
+        } else {
+          pre += v[k];
+        }
+      }
+    }
+    l_pre[q * RDX_BINS + dg] = pre;
+    l_tsum[q * RDX_BINS + dg] = tot;
+    __syncthreads();
+    if (q == 0) {
+      uint32_t p = 0, t = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < DQ; ++k) {
+        p += l_pre[k * RDX_BINS + dg];
+        t += l_tsum[k * RDX_BINS + dg];
+      }
+      l_tot[dg] = t;
+#pragma unroll
+      for (uint32_t j = 0; j < SCAT_TPW; ++j) {
+        l_off[j * RDX_BINS + dg] = p;
+        if (j + 1 < SCAT_TPW) p += own[j];
+      }
+    }
+    __syncthreads();
+  }
+};
+template <bool X>
+__global__ void __launch_bounds__(RDX_THREADS) __attribute__((amdgpu_waves_per_eu(8))) k_radix_scatter_d(
+    RadixSrc s, FinalDst f, uint32_t G, uint32_t shift, uint32_t ntiles, const uint32_t* hist, const uint32_t* agg,
+    const uint32_t* sup, uint32_t* n_valid) {
+  __shared__ uint32_t l_pre[DQ * RDX_BINS], l_tsum[DQ * RDX_BINS];
+  __shared__ uint32_t l_off[SCAT_TPW * RDX_BINS], l_tot[RDX_BINS];
+  const uint32_t tile0 = blockIdx.x * SCAT_TPW;
+  const DirectPre pre{hist, agg, sup, ntiles, tile0, l_pre, l_tsum, l_off, l_tot};
+  scatter_tiles<true, X, SCAT_TPW>(s, RadixDst{}, f, G, shift, RDX_BITS, ntiles, tile0, l_off, 1u, RDX_BINS, l_tot,
+                                   n_valid, blockIdx.x == 0, pre, tile0);
 }
 
 // One bucket (a node of at most 4,096 groups): the partition is the identity
@@ -3381,6 +3514,11 @@ struct hb_handle {
   uint32_t* hist = nullptr;       // [tiles][RDX_BINS]
   uint32_t* n_valid = nullptr;    // messages kept after pass 1 (device)
   uint32_t* totals = nullptr;     // [RDX_BINS] digit totals of the current pass
+  // one-pass direct offsets (HB_RDX_DIRECT): hist workgroup sums, rotating superblock sums
+  uint32_t* hagg = nullptr;       // [hist workgroups][RDX_BINS]
+  uint32_t* hsup = nullptr;       // [SUP_BUFS][sup_max][RDX_BINS]
+  uint32_t sup_max = 0, sup_k = 0;
+  uint32_t sup_used[SUP_BUFS] = {};  // superblocks each buffer holds non-zero (cleared by a later hist)
   RadixDst tmp[2] = {};           // intermediate passes (ping-pong)
   PrepSet set[2];
   uint32_t next_set = 0, cur = 0;  // set of the next / the last step
@@ -3731,6 +3869,14 @@ int hb_create(int device, uint32_t capacity, uint32_t max_replicas, uint32_t max
   ALLOC(h->hist, (size_t)RDX_BINS * tiles_max);
   ALLOC(h->n_valid, 4);
   ALLOC(h->totals, RDX_BINS);
+  if (h->passes == 1) {
+    const size_t nhw = (tiles_max + HIST_TPB - 1) / HIST_TPB;
+    h->sup_max = (uint32_t)((nhw + SB_HW - 1) / SB_HW);
+    ALLOC(h->hagg, nhw * RDX_BINS);
+    ALLOC(h->hsup, (size_t)SUP_BUFS * h->sup_max * RDX_BINS);
+    if (rc == HB_OK && hipMemset(h->hsup, 0, (size_t)SUP_BUFS * h->sup_max * RDX_BINS * 4) != hipSuccess)
+      rc = HB_EDEVICE;
+  }
   for (uint32_t k = 0; k + 1 < h->passes && k < 2; ++k) {  // ping-pong buffers of intermediate passes
     RadixDst& d = h->tmp[k];
     ALLOC(d.group, mb);
@@ -4448,11 +4594,30 @@ int hb_step(hb_handle* h, const hb_batch* b, uint32_t flags) {
       const uint32_t b0 = h->bk_bits / 2;
       const uint32_t dbits = h->passes == 1 ? RDX_BITS : p == 0 ? b0 : h->bk_bits - b0;
       const uint32_t dm = h->passes > 1;  // digit-major tile counts (k_scan_rows)
-      hipLaunchKernelGGL(k_radix_hist, dim3((ntiles + HIST_TPB - 1) / HIST_TPB), dim3(RDX_THREADS), 0, ps_st, src, h->G,
-                         shift, dbits, ntiles, h->hist, dm);
+      const uint32_t nhw = (ntiles + HIST_TPB - 1) / HIST_TPB;
+      const dim3 sg((ntiles + SCAT_TPW - 1) / SCAT_TPW);
+      if (HB_RDX_DIRECT && h->passes == 1) {  // hist + direct scatter: no scan launch
+        const uint32_t k = h->sup_k, kn = (k + 1) % SUP_BUFS;
+        const size_t bw = (size_t)h->sup_max * RDX_BINS;
+        DirectSums dsum{h->hagg, h->hsup + k * bw, h->hsup + kn * bw, h->sup_used[kn] * RDX_BINS,
+                        ps.bk_fill, h->NBK, ps.ctr};
+        h->sup_used[kn] = 0;
+        h->sup_used[k] = (nhw + SB_HW - 1) / SB_HW;
+        h->sup_k = kn;
+        hipLaunchKernelGGL(k_radix_hist, dim3(nhw), dim3(RDX_THREADS), 0, ps_st, src, h->G, shift, dbits, ntiles, h->hist,
+                           0u, dsum);
+        if (xmode)
+          hipLaunchKernelGGL(k_radix_scatter_d<true>, sg, dim3(RDX_THREADS), 0, ps_st, src, fin, h->G, shift, ntiles,
+                             (const uint32_t*)h->hist, (const uint32_t*)h->hagg, (const uint32_t*)dsum.sup, h->n_valid);
+        else
+          hipLaunchKernelGGL(k_radix_scatter_d<false>, sg, dim3(RDX_THREADS), 0, ps_st, src, fin, h->G, shift, ntiles,
+                             (const uint32_t*)h->hist, (const uint32_t*)h->hagg, (const uint32_t*)dsum.sup, h->n_valid);
+        break;  // (one pass)
+      }
+      hipLaunchKernelGGL(k_radix_hist, dim3(nhw), dim3(RDX_THREADS), 0, ps_st, src, h->G, shift, dbits, ntiles, h->hist,
+                         dm, DirectSums{});
       hipLaunchKernelGGL(k_scan_rows, dim3(1u << dbits), dim3(1024), 0, ps_st, h->hist, ntiles, dbits, h->totals, ps.bk_fill,
                          h->NBK, ps.ctr, dm);
-      const dim3 sg((ntiles + SCAT_TPW - 1) / SCAT_TPW);
 #define HB_SCATTER(F, X)                                                                                             \
   hipLaunchKernelGGL((k_radix_scatter<F, X>), sg, dim3(RDX_THREADS), 0, ps_st, src, dst, fin, h->G, shift, dbits, ntiles, \
                      (const uint32_t*)h->hist, dm ? ntiles : 1u, dm ? 1u : (1u << dbits), (const uint32_t*)h->totals,    \
