@@ -25,7 +25,7 @@ def test_direct_offsets_changing_batch_sizes():
     with ragged tiles and a step of messages beyond capacity."""
     G, n = 300_000, 3
     g, runs = synth.steady_groups(G, n, seed=0x5EED0011, with_runs="flat")
-    pair = Pair(g, runs, n, 256, max_batch=1 << 21, oracle_shards=16)
+    pair = Pair(g, runs, n, 256, max_batch=1 << 21)  # (one oracle: ids past capacity)
     for k, nmsg in enumerate([600_000, 20_001, 270_001, 600_000, 40_000, 599_999]):
         b = synth.random_batch(g, nmsg, seed=500 + k)
         if k == 4:  # some messages of groups beyond capacity: dropped in the partition
