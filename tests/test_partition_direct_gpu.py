@@ -1,11 +1,13 @@
-"""One-pass partitions with direct tile offsets (HB_RDX_DIRECT, r06): the
+"""Partitions with direct tile offsets (HB_RDX_DIRECT, r06): the
 histogram kernel's workgroup and superblock digit sums stand in for the
 k_scan_rows launch, and the scatter sums them before each tile.  These steps
 pin what the full-size headline tests do not reach: batch sizes that change
 from step to step (the superblock buffers rotate over three steps and each is
 cleared only as far as an earlier step dirtied it), ragged last tiles and hist
 workgroups, and batches past 8M messages, where a scatter workgroup's offset
-sums take a second round of loads.  Every event, statistic and group record
+sums take a second round of loads; and, beside them, a two-pass partition
+(1.1M groups, 5-bit digits), which keeps the scan launch, over the same
+kind of changing batches.  Every event, statistic and group record
 against the C oracle.  Reference: the per-group arrival order the partition
 keeps, raft/multinode.go:233-237.
 """
@@ -46,3 +48,19 @@ def test_direct_offsets_past_eight_million_messages():
     for k in range(2):
         b = synth.random_batch(g, 9_000_000 - k, seed=700 + k)
         pair.step(b, ctx=f"9M step {k}", check_inflights=False)
+
+
+@pytest.mark.timeout(900)
+def test_two_pass_partition_changing_batch_sizes():
+    """1.1M groups x 3: two passes (5 + 5 bits, k_scan_rows per pass: direct
+    offsets measured slower there); batch sizes change and
+    one step carries ids past capacity (dropped in the first pass)."""
+    G, n = 1_100_000, 3
+    g, runs = synth.steady_groups(G, n, seed=0x5EED0013, with_runs="flat")
+    pair = Pair(g, runs, n, 256, max_batch=1 << 22)
+    for k, nmsg in enumerate([3_000_000, 50_001, 1_500_001]):
+        b = synth.random_batch(g, nmsg, seed=900 + k)
+        if k == 1:
+            b["group"] = b["group"].copy()
+            b["group"][::31] = G + 5
+        pair.step(b, ctx=f"two-pass step {k} ({nmsg} messages)", check_inflights=False)
